@@ -1,0 +1,334 @@
+"""ctypes front-end of the C oracle (oracle/smash_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product (smash-paper_amd/).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+u8p = C.POINTER(C.c_uint8)
+i64p = C.POINTER(C.c_int64)
+
+
+class OrcText(C.Structure):
+    _fields_ = [("N", C.c_uint64), ("T", u8p), ("n_seq", C.c_uint32),
+                ("startpos", u64p), ("sizes", u64p),
+                ("names", C.POINTER(C.c_char_p))]
+
+
+class OrcIndex(C.Structure):
+    _fields_ = [("N", C.c_uint64), ("logN", C.c_uint64), ("T", u8p),
+                ("SA", u64p), ("ISA", u64p), ("LCP", u64p),
+                ("n_seq", C.c_uint32), ("startpos", u64p), ("sizes", u64p)]
+
+
+class OrcCounters(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "sa_loads", "isa_loads", "ref_loads", "lcp_loads",
+        "sa_lines", "isa_lines", "ref_lines", "lcp_lines",
+        "last_sa", "last_isa", "last_ref", "last_lcp")]
+
+
+class OrcMatch(C.Structure):
+    _fields_ = [("ref", C.c_uint64), ("query", C.c_uint64), ("len", C.c_uint64)]
+
+
+CIGAR_MAX = 160
+
+
+class OrcHit(C.Structure):
+    _fields_ = [("tid", C.c_uint32), ("rc", C.c_uint32), ("pos", C.c_int64),
+                ("qpos", C.c_int64), ("n_matches", C.c_uint32),
+                ("n_unique", C.c_uint32), ("n_matched", C.c_uint32),
+                ("hi", C.c_uint32), ("nh", C.c_uint32), ("qstart", C.c_uint32),
+                ("qend", C.c_uint32), ("first_off", C.c_uint32),
+                ("first_len", C.c_uint32), ("L0", C.c_int32), ("R0", C.c_int32),
+                ("cigar", C.c_char * CIGAR_MAX)]
+
+
+class OrcVarbinState(C.Structure):
+    _fields_ = [("total", C.c_uint64), ("dups", C.c_uint64),
+                ("kept", C.c_uint64), ("prev_pos", C.c_int64)]
+
+
+class OrcPipeline(C.Structure):
+    _fields_ = [("ix", C.POINTER(OrcIndex)), ("min_len", C.c_uint32),
+                ("tag_offsets", u32p), ("small_chr", u8p), ("major", u8p),
+                ("chrom_off", i64p), ("map", u8p), ("map_size", C.c_uint64),
+                ("bin_starts", i64p), ("nbins", C.c_uint32)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_text_from_fasta.argtypes = [C.c_char_p, C.POINTER(OrcText)]
+        L.orc_text_free.argtypes = [C.POINTER(OrcText)]
+        L.orc_build_sa.argtypes = [u8p, C.c_uint64, u64p]
+        L.orc_build_isa.argtypes = [u64p, C.c_uint64, u64p]
+        L.orc_build_lcp.argtypes = [u8p, C.c_uint64, u64p, u64p, u64p]
+        L.orc_logN.argtypes = [C.c_uint64]
+        L.orc_logN.restype = C.c_uint64
+        for fn in ("orc_mam", "orc_mem", "orc_mum"):
+            getattr(L, fn).argtypes = [C.POINTER(OrcIndex), u8p, C.c_uint32,
+                                       C.c_uint32, C.POINTER(OrcMatch),
+                                       C.c_uint32, C.POINTER(OrcCounters)]
+        L.orc_resolve.argtypes = [C.POINTER(OrcIndex), u8p, C.c_uint32,
+                                  C.POINTER(OrcMatch), C.c_uint32,
+                                  C.POINTER(OrcHit), C.c_uint32, u32p, i64p]
+        L.orc_mappability.argtypes = [C.POINTER(OrcIndex), u8p]
+        L.orc_tag.argtypes = [C.POINTER(OrcHit), u32p, u8p, C.c_uint64, C.c_int]
+        L.orc_smash_pair.argtypes = [C.POINTER(OrcHit), C.c_uint32,
+                                     C.POINTER(OrcHit), C.c_uint32, C.c_int,
+                                     C.c_int64, u32p, i64p]
+        L.orc_varbin.argtypes = [i64p, i64p, C.c_uint64, i64p, C.c_uint32,
+                                 u64p, C.POINTER(OrcVarbinState)]
+        L.orc_dedup_new.restype = C.c_void_p
+        L.orc_dedup_free.argtypes = [C.c_void_p]
+        L.orc_run_pairs.argtypes = [C.POINTER(OrcPipeline), u8p, C.c_uint32,
+                                    C.c_uint64, C.c_uint64, C.c_int, C.c_void_p,
+                                    u64p, C.POINTER(OrcVarbinState), u64p, u64p]
+        L.orc_map_only.argtypes = [C.POINTER(OrcIndex), u8p, C.c_uint32,
+                                   C.c_uint64, C.c_uint64, C.c_uint32, C.c_int,
+                                   C.POINTER(OrcCounters)]
+        L.orc_map_only.restype = C.c_uint64
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def text_from_fasta(path):
+    """(T uint8 incl. '$', startpos u64[n_seq], sizes u64[n_seq], names)."""
+    t = OrcText()
+    rc = lib().orc_text_from_fasta(path.encode(), C.byref(t))
+    if rc:
+        raise OSError("cannot read " + path)
+    T = np.ctypeslib.as_array(t.T, shape=(t.N,)).copy()
+    sp = np.ctypeslib.as_array(t.startpos, shape=(t.n_seq,)).copy()
+    sz = np.ctypeslib.as_array(t.sizes, shape=(t.n_seq,)).copy()
+    names = [t.names[i].decode() for i in range(t.n_seq)]
+    lib().orc_text_free(C.byref(t))
+    return T, sp, sz, names
+
+
+def text_from_contigs(contigs):
+    """Same layout as text_from_fasta, from [(name, ASCII uint8)] (no file)."""
+    lower = np.arange(256, dtype=np.uint8)
+    lower[ord("A"):ord("Z") + 1] += 32
+    comp = np.arange(256, dtype=np.uint8)
+    for a, b in zip(b"acgtrymkbdhvACGTRYMKBDHV", b"tgcayrkmvhdbTGCAYRKMVHDB"):
+        comp[a] = b
+    parts, sp, sz, names = [], [], [], []
+    pos = 0
+    for k, (name, s) in enumerate(contigs):
+        f = lower[s]
+        sp.append(pos); sz.append(len(f)); names.append(name)
+        parts.append(f); parts.append(np.array([ord("`")], np.uint8))
+        pos += len(f) + 1
+        sp.append(pos); sz.append(len(f)); names.append(name)
+        parts.append(comp[f[::-1]])
+        pos += len(f)
+        if k + 1 < len(contigs):
+            parts.append(np.array([ord("`")], np.uint8))
+            pos += 1
+    parts.append(np.array([ord("$")], np.uint8))
+    T = np.concatenate(parts)
+    return T, np.array(sp, np.uint64), np.array(sz, np.uint64), names
+
+
+def build_index(T):
+    N = len(T)
+    Tp = np.zeros(N + 64, np.uint8)
+    Tp[:N] = T
+    SA = np.empty(N, np.uint64)
+    ISA = np.empty(N, np.uint64)
+    LCP = np.empty(N, np.uint64)
+    L = lib()
+    if L.orc_build_sa(_p(Tp, u8p), N, _p(SA, u64p)):
+        raise MemoryError
+    L.orc_build_isa(_p(SA, u64p), N, _p(ISA, u64p))
+    L.orc_build_lcp(_p(Tp, u8p), N, _p(SA, u64p), _p(ISA, u64p), _p(LCP, u64p))
+    return SA, ISA, LCP
+
+
+class Index:
+    """Host index (text + SA/ISA/LCP as uint64) wrapped for the C oracle."""
+
+    def __init__(self, T, startpos, sizes, names, SA=None, ISA=None, LCP=None):
+        N = len(T)
+        self.T = np.zeros(N + 64, np.uint8)
+        self.T[:N] = T
+        self.N = N
+        if SA is None:
+            SA, ISA, LCP = build_index(T)
+        self.SA = np.ascontiguousarray(SA, dtype=np.uint64)
+        self.ISA = np.ascontiguousarray(ISA, dtype=np.uint64)
+        self.LCP = np.ascontiguousarray(LCP, dtype=np.uint64)
+        self.startpos = np.ascontiguousarray(startpos, dtype=np.uint64)
+        self.sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+        self.names = list(names)
+        self.contigs = [names[i] for i in range(0, len(names), 2)]
+        self.c = OrcIndex(N, lib().orc_logN(N), _p(self.T, u8p), _p(self.SA, u64p),
+                          _p(self.ISA, u64p), _p(self.LCP, u64p),
+                          len(self.startpos), _p(self.startpos, u64p),
+                          _p(self.sizes, u64p))
+
+    @classmethod
+    def from_fasta(cls, path):
+        T, sp, sz, names = text_from_fasta(path)
+        return cls(T, sp, sz, names)
+
+    def search(self, read: bytes, mode="MAM", min_len=20, counters=None):
+        P = np.frombuffer(read, np.uint8)
+        fn = {"MAM": lib().orc_mam, "MEM": lib().orc_mem, "MUM": lib().orc_mum}[mode]
+        cap = 512
+        while True:
+            out = (OrcMatch * cap)()
+            n = fn(C.byref(self.c), _p(P, u8p), len(P), min_len, out, cap,
+                   C.byref(counters) if counters is not None else None)
+            if n <= cap:
+                break
+            cap = n
+        return [(out[i].ref, out[i].query, out[i].len) for i in range(n)]
+
+    def resolve(self, read: bytes, matches):
+        P = np.frombuffer(read, np.uint8)
+        m = (OrcMatch * max(1, len(matches)))()
+        for i, (r, q, l) in enumerate(matches):
+            m[i].ref, m[i].query, m[i].len = r, q, l
+        hits = (OrcHit * 64)()
+        bt = C.c_uint32()
+        bp = C.c_int64()
+        n = lib().orc_resolve(C.byref(self.c), _p(P, u8p), len(P), m, len(matches),
+                              hits, 64, C.byref(bt), C.byref(bp))
+        best = None if bt.value == 0xFFFFFFFF else (bt.value, bp.value)
+        return [hits[i] for i in range(n)], best
+
+    def mappability(self):
+        total = int(sum(self.sizes[0::2]))
+        out = np.zeros(2 + 2 * total, np.uint8)
+        if lib().orc_mappability(C.byref(self.c), _p(out, u8p)):
+            raise MemoryError
+        return out
+
+
+def lower_read(seq: bytes) -> bytes:
+    """NewQuery::extend (query.cpp:125-144): drop spaces, lowercase; the
+    fastqs_to_sam replaceN step (fastqs_to_sam.cpp:289) turns N into Z
+    first, so reads' Ns become 'z'."""
+    return seq.replace(b" ", b"").replace(b"N", b"Z").lower()
+
+
+def tag(hit, offsets, mapbin, small):
+    off = np.ascontiguousarray(offsets, dtype=np.uint32)
+    return lib().orc_tag(C.byref(hit), _p(off, u32p), _p(mapbin, u8p),
+                         len(mapbin), int(small))
+
+
+def smash_pair(h1, h2, min_excess=4, window=10000):
+    a = (OrcHit * max(1, len(h1)))(*h1)
+    b = (OrcHit * max(1, len(h2)))(*h2)
+    tid = np.zeros(128, np.uint32)
+    pos = np.zeros(128, np.int64)
+    n = lib().orc_smash_pair(a, len(h1), b, len(h2), min_excess, window,
+                             _p(tid, u32p), _p(pos, i64p))
+    if n < 0:
+        return None
+    return list(zip(tid[:n].tolist(), pos[:n].tolist()))
+
+
+def varbin(pos0, abspos, bin_starts, state=None, counts=None):
+    pos0 = np.ascontiguousarray(pos0, np.int64)
+    abspos = np.ascontiguousarray(abspos, np.int64)
+    bs = np.ascontiguousarray(bin_starts, np.int64)
+    if counts is None:
+        counts = np.zeros(len(bs), np.uint64)
+    if state is None:
+        state = OrcVarbinState(0, 0, 0, -1)
+    lib().orc_varbin(_p(pos0, i64p), _p(abspos, i64p), len(pos0), _p(bs, i64p),
+                     len(bs), _p(counts, u64p), C.byref(state))
+    return counts, state
+
+
+MAJOR_RE = None
+
+
+def major_flags(names, chrom_sizes_names):
+    """perl filter ^chr(\\d+|[XY]) \\d+$ (smash_mapping.sh:29) and varbin's
+    chromosome filter (varbin.py:38-49)."""
+    import re
+    rx = re.compile(r"^chr(\d+|[XY])$")
+    return np.array([1 if (rx.match(n) and "_" not in n and n != "chrM"
+                           and n in chrom_sizes_names) else 0 for n in names],
+                    np.uint8)
+
+
+class Pipeline:
+    """Whole-chain oracle: map -> resolve -> tag -> smash -> dedup -> varbin."""
+
+    def __init__(self, ix: Index, mapbin, chrom_sizes, bin_starts, min_len=20):
+        self.ix = ix
+        names = ix.contigs
+        sizes = [int(s) for s in ix.sizes[0::2]]
+        self.tag_off = np.array(np.cumsum([0] + sizes[:-1]), dtype=np.uint32)
+        self.small = np.array([1 if ("_gl000" in n or "chrM" in n) else 0
+                               for n in names], np.uint8)
+        self.major = major_flags(names, chrom_sizes)
+        self.chrom_off = np.array([chrom_sizes.get(n, 0) for n in names], np.int64)
+        self.mapbin = np.ascontiguousarray(mapbin, np.uint8)
+        self.bin_starts = np.ascontiguousarray(bin_starts, np.int64)
+        self.c = OrcPipeline(C.pointer(ix.c), min_len, _p(self.tag_off, u32p),
+                             _p(self.small, u8p), _p(self.major, u8p),
+                             _p(self.chrom_off, i64p), _p(self.mapbin, u8p),
+                             len(self.mapbin), _p(self.bin_starts, i64p),
+                             len(self.bin_starts))
+        self.dedup = lib().orc_dedup_new()
+        self.counts = np.zeros(len(self.bin_starts), np.uint64)
+        self.state = OrcVarbinState(0, 0, 0, -1)
+        self.n_dupe = C.c_uint64(0)
+        self.n_pos = C.c_uint64(0)
+
+    def run(self, reads: np.ndarray, threads=1):
+        """reads: uint8 [2*n_pairs, L] lowercased (N->z), mates interleaved."""
+        reads = np.ascontiguousarray(reads, np.uint8)
+        n_pairs = reads.shape[0] // 2
+        err = lib().orc_run_pairs(C.byref(self.c), _p(reads, u8p), reads.shape[1],
+                                  reads.shape[1], n_pairs, threads, self.dedup,
+                                  _p(self.counts, u64p), C.byref(self.state),
+                                  C.byref(self.n_dupe), C.byref(self.n_pos))
+        return err
+
+    def __del__(self):
+        try:
+            lib().orc_dedup_free(self.dedup)
+        except Exception:
+            pass
+
+
+def map_only(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=False):
+    reads = np.ascontiguousarray(reads, np.uint8)
+    ctr = OrcCounters() if count else None
+    n = lib().orc_map_only(C.byref(ix.c), _p(reads, u8p), reads.shape[1],
+                           reads.shape[1], reads.shape[0], min_len, threads,
+                           C.byref(ctr) if ctr is not None else None)
+    return n, ctr
