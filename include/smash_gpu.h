@@ -1,0 +1,209 @@
+/*
+ * include/smash_gpu.h -- C ABI of the MI355X-native SMASH read -> bin-count
+ * path (libsmashgpu.so, built from the HIP sources in smash-paper_amd/csrc/
+ * for gfx950).
+ *
+ * The reference has no FFI: its seams are in-process C++ calls and files.
+ * Each entry point below names the reference interface it replaces.
+ *
+ * Conventions: plain pointers and sizes; `d_` = device pointer (HBM of the
+ * handle's device), `h_` = host pointer; int status codes (SMASH_OK = 0),
+ * never exceptions across the ABI; caller-owned output buffers; one handle
+ * per device; an index is immutable after creation; streams are
+ * hipStream_t passed as void* (0 = default stream); no global state.
+ */
+#ifndef SMASH_GPU_H_
+#define SMASH_GPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------- */
+#define SMASH_OK 0
+#define SMASH_ERR_ARG (-1)       /* bad argument / shape */
+#define SMASH_ERR_HIP (-2)       /* HIP runtime error (message: smash_last_error) */
+#define SMASH_ERR_IO (-3)        /* file missing / unreadable / inconsistent */
+#define SMASH_ERR_NOMEM (-4)     /* device allocation failed */
+#define SMASH_ERR_UNSUPPORTED (-5)
+/* pipeline data errors (positive), reported by smash_pipeline_stats:        */
+#define SMASH_ERR_TAG_LEFT 1     /* "left mappability too big"  mappability_tag.cpp:107-111 */
+#define SMASH_ERR_TAG_RIGHT 2    /* "right mappability too big" mappability_tag.cpp:112-113 */
+
+const char *smash_last_error(void);   /* thread-local text of the last error */
+
+/* ---- reference text (Sequence::Sequence, fasta.cpp:133-285) -------------- */
+/* Parses a FASTA exactly like the reference with -rcref (lowercase, '`'
+ * separators, reverse complements, final '$') into malloc'd host arrays:
+ * text[N], startpos/sizes[n_seq], names[n_seq] (2 entries per contig).
+ * Free with smash_text_free. */
+int smash_text_from_fasta(const char *path, uint8_t **text, uint64_t *N,
+                          uint32_t *n_seq, uint64_t **startpos,
+                          uint64_t **sizes, char ***names);
+void smash_text_free(uint8_t *text, uint32_t n_seq, uint64_t *startpos,
+                     uint64_t *sizes, char **names);
+
+/* ---- search modes (query.h:126 mum_t) ------------------------------------ */
+#define SMASH_MODE_MAM 1         /* -mumreference / default (longSA.cpp:503) */
+
+/* ========================================================================== */
+/* Index: replaces longSA::longSA (longSA.cpp:94-210) + Sequence (fasta.cpp)  */
+/* ========================================================================== */
+typedef struct smash_index smash_index;
+
+/* Build the whole index ON THE DEVICE from the doubled text (layout of
+ * fasta.cpp:189-247: c1 ` rc(c1) ` c2 ... rc(cn) $): suffix array (GPU prefix
+ * doubling, byte-identical to qsufsort's since the SA of a '$'-terminated
+ * text is unique), ISA, LCP (u8 saturated + exact overflow table, as
+ * vec_uchar longSA.h:18-61) and map.bin (longSA::show, longSA.cpp:612-690).
+ * startpos/sizes/names: 2 entries per contig (forward, reverse complement);
+ * names may be NULL (only smash_index_save writes them). */
+int smash_index_create(const uint8_t *h_text, uint64_t N, uint32_t n_seq,
+                       const uint64_t *h_startpos, const uint64_t *h_sizes,
+                       const char *const *names, int device,
+                       smash_index **out);
+
+/* Load the reference's on-disk cache <fasta>.bin/rc1.ref.{bin,seq.bin} and
+ * rc1.i{4,8}.index.{bin,sa.bin,isa.bin,lcp.vec.bin,lcp.m.bin} (longSA.cpp:
+ * 100-136, fasta.cpp:150-181) and, if present, <fasta>.bin/map.bin; the
+ * map is computed on the device otherwise.  Replaces the mmap path of
+ * util.cpp:100-125. */
+int smash_index_load(const char *fasta_path, int device, smash_index **out);
+
+/* Write the reference's on-disk cache (rc1.i4 when N <= INT32_MAX-100000 as
+ * `mummer` would, else rc1.i8, mummer.cpp:156-183) + map.bin
+ * (index_setup.sh:19-22).  fasta_size is stored in the headers
+ * (longSA.cpp:182, fasta.cpp:265). */
+int smash_index_save(const smash_index *ix, const char *fasta_path,
+                     uint64_t fasta_size);
+
+void smash_index_free(smash_index *ix);
+
+typedef struct {
+  uint64_t N;              /* doubled text length incl. '$' */
+  uint64_t logN;           /* ceil(log2 N) (longSA.cpp:97) */
+  uint32_t idx_bytes;      /* 4 or 8: SA/ISA element width in HBM */
+  uint32_t n_seq;
+  uint64_t n_lcp_overflow; /* entries with LCP >= 255 */
+  uint64_t map_bytes;      /* 2 + 2 * sum(forward contig sizes) */
+  const uint8_t *d_text;   /* N + 64 bytes (zero padded) */
+  const void *d_sa;        /* N x idx_bytes */
+  const void *d_isa;       /* N x idx_bytes */
+  const uint8_t *d_lcp8;   /* N, min(LCP,255) */
+  const uint64_t *d_lcp_ovf; /* n_lcp_overflow x {idx, val} sorted by idx */
+  const uint8_t *d_map;    /* map.bin image */
+  uint64_t device_bytes;   /* total HBM held by the index */
+  double build_seconds;    /* wall time of create/load */
+} smash_index_info;
+int smash_index_query(const smash_index *ix, smash_index_info *out);
+
+/* ========================================================================== */
+/* Search: replaces longSA::MAM(Aligner&) (longSA.cpp:503-536) for a batch.   */
+/* Each read's matches go to slots [i*cap_per_read, ...) as packed u64:       */
+/*   bits 0-47 ref (text position), 48-55 query offset, 56-63 length          */
+/* (match_t, longSA.h:78-92; reads <= 255 bp), in emission order (ascending   */
+/* query offset, as process_match receives them, query.cpp:436-438).          */
+/* d_n_out[i] = number of matches (written up to cap_per_read).               */
+/* Reads: d_seqs + i*stride, length d_lens[i] (or `len` when d_lens==NULL),   */
+/* already lowercased as NewQuery::extend does (query.cpp:125-144).           */
+/* ========================================================================== */
+int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len,
+                    const uint8_t *d_seqs, uint64_t stride,
+                    const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                    uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out,
+                    void *stream);
+
+/* ========================================================================== */
+/* Pipeline: prepare_matches (query.cpp:231-306) + mappability_tag           */
+/* (mappability_tag.cpp:93-124) + smashMEM.py filters & global pair de-dup   */
+/* (smashMEM.py:154-228) + varbin.py (varbin.py:52-92), fused per batch.      */
+/* ========================================================================== */
+typedef struct smash_pipeline smash_pipeline;
+
+typedef struct {
+  uint32_t min_len;          /* MAM minimum length (query.h:129: 20) */
+  uint32_t read_len;         /* fixed mate length of the batches (<= 255) */
+  uint64_t max_pairs;        /* batch capacity */
+  uint32_t n_contig;         /* forward contigs = n_seq / 2 */
+  const uint32_t *h_tag_offsets; /* [n_contig] sam_header.txt offsets (u32, chromosomes.h:169-196) */
+  const uint8_t *h_small_chr;    /* [n_contig] name has "_gl000" or "chrM" (mappability_tag.cpp:82) */
+  const int64_t *h_chrom_off;    /* [n_contig] chrom_sizes.txt col 3, or -1 = not binned
+                                    (perl ^chr(\d+|[XY])$ smash_mapping.sh:29 + varbin.py:38-49) */
+  uint32_t nbins;
+  const int64_t *h_bin_starts;   /* [nbins] bins.txt col 3 (start abspos), ascending */
+  int32_t min_excess;        /* smashMEM arg 5 (smash_mapping.sh:25: 4) */
+  int64_t hit_window;        /* smashMEM arg 4 (10000) */
+  uint64_t dedup_capacity;   /* distinct pair keys the persistent set holds */
+} smash_pipeline_cfg;
+
+int smash_pipeline_create(const smash_index *ix, const smash_pipeline_cfg *cfg,
+                          smash_pipeline **out);
+void smash_pipeline_free(smash_pipeline *p);
+
+/* One batch of n_pairs pairs: d_reads holds 2*n_pairs mates of cfg->read_len
+ * bytes, mate 2q = read 1, 2q+1 = read 2 of pair q (Pair::run alternation,
+ * query.cpp:486-505), pairs in name order (samtools sort -n).  Runs map ->
+ * resolve -> tag -> filter -> de-dup (first wins, against every earlier
+ * batch) -> adjacent de-dup (carried across batches) -> bin, adding into
+ * d_counts[nbins] (u64).  Asynchronous on `stream`. */
+int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
+                      uint64_t n_pairs, uint64_t *d_counts, void *stream);
+
+/* Multi-GPU phases (one rank per GPU; the caller runs the collectives):
+ *  1. smash_phase_map      -- map/resolve/tag/filter/hash + in-batch first-wins
+ *  2. smash_phase_export   -- (key hash, global pair index) of in-batch-first
+ *                             keys into d_send[n][3] grouped by owner rank
+ *                             (hash % world); h_send_counts[world] filled
+ *                             (synchronises the stream)
+ *     caller: all_to_all(d_send) -> d_recv
+ *  3. smash_dedup_owner    -- owner side: for received entries decide
+ *                             first-wins against the persistent set (global
+ *                             index order), insert winners, write one byte
+ *                             per entry (1 = keep) into d_flags
+ *     caller: all_to_all(d_flags) back, in d_send order
+ *  4. smash_phase_import   -- apply the returned flags
+ *  5. smash_phase_positions-- emit kept positions; d_tail[2] = {count, last
+ *                             pos0 or -1} for the adjacent-dup boundary
+ *     caller: all_gather(d_tail) -> previous rank's last pos (d_prev)
+ *  6. smash_phase_bin      -- adjacent de-dup against *d_prev, bin, add. */
+int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                    void *stream);
+int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
+                       uint64_t *d_send, int64_t *h_send_counts, void *stream);
+int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint64_t n_recv,
+                      uint8_t *d_flags, void *stream);
+int smash_phase_import(smash_pipeline *p, const uint8_t *d_flags_back,
+                       void *stream);
+int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *stream);
+int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev, uint64_t *d_counts,
+                    void *stream);
+
+typedef struct {
+  uint64_t pairs;          /* pairs processed */
+  uint64_t key_pairs;      /* pairs that produced a key (smashMEM.py:162) */
+  uint64_t dupe_pairs;     /* "N dupes" (smashMEM.py:227-230) */
+  uint64_t positions;      /* lines reaching varbin (TotalReads) */
+  uint64_t dups;           /* DupsRemoved (varbin.py:56-58) */
+  uint64_t kept;           /* ReadsKept */
+  uint64_t matches;        /* MAM matches */
+  int32_t error;           /* first data error (SMASH_ERR_TAG_*), 0 = none */
+} smash_stats;
+/* Synchronises the pipeline's last stream. */
+int smash_pipeline_stats(smash_pipeline *p, smash_stats *out);
+
+/* Start a new run: clears the pair-key set, the carried adjacent-dup state
+ * and the stats (a fresh smashMEM.py + varbin.py invocation). */
+int smash_pipeline_reset(smash_pipeline *p, void *stream);
+
+/* Debug/test view of the last batch's per-pair filter output: for pair q,
+ * h_nk[q] = kept hits (-1 = no key), h_keep[q] = survives de-dup, hits as
+ * (tid << 48 | pos0) in h_hits[q*2*slots ...]. slots = read_len - min_len + 1. */
+int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_keep,
+                        uint64_t *h_hits, uint64_t *h_hash);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

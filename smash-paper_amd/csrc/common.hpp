@@ -1,0 +1,102 @@
+// smash-paper_amd/csrc/common.hpp -- shared internals of libsmashgpu (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/smash_gpu.h"
+
+namespace smash {
+
+void set_error(const std::string &msg);
+
+#define SMASH_HIP(call)                                                      \
+  do {                                                                       \
+    hipError_t e_ = (call);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      ::smash::set_error(std::string(#call) + ": " + hipGetErrorString(e_)); \
+      return SMASH_ERR_HIP;                                                  \
+    }                                                                        \
+  } while (0)
+
+// Throwing variant for internal helpers; converted to a status at the ABI.
+struct hip_failure {
+  std::string what;
+};
+#define SMASH_HIPX(call)                                                       \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess)                                                      \
+      throw ::smash::hip_failure{std::string(#call) + ": " +                   \
+                                 hipGetErrorString(e_)};                       \
+  } while (0)
+
+template <class T>
+T *dalloc(size_t n) {
+  void *p = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e != hipSuccess)
+    throw hip_failure{"hipMalloc(" + std::to_string(n * sizeof(T)) +
+                      " B): " + hipGetErrorString(e)};
+  return static_cast<T *>(p);
+}
+inline void dfree(void *p) {
+  if (p) (void)hipFree(p);
+}
+
+inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 1u << 20) {
+  uint64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<unsigned>(g);
+}
+
+inline uint64_t ceil_log2(uint64_t n) {
+  uint64_t b = 0;
+  while ((1ull << b) < n && b < 63) ++b;
+  return b;
+}
+
+// Packed match (smash_gpu.h): ref 48 | qoff 8 | len 8
+__host__ __device__ inline uint64_t pack_match(uint64_t ref, uint32_t q,
+                                               uint32_t len) {
+  return (ref & 0xFFFFFFFFFFFFull) | (uint64_t(q & 0xFF) << 48) |
+         (uint64_t(len & 0xFF) << 56);
+}
+
+}  // namespace smash
+
+// The device index (smash_gpu.h: smash_index).  SA/ISA width is 4 bytes when
+// N < 2^32, else 8 (the reference's ANINT, size.h:24-38).
+struct smash_index {
+  int device = 0;
+  uint64_t N = 0, logN = 0;
+  uint32_t idx_bytes = 4;
+  uint32_t n_seq = 0;
+  std::vector<uint64_t> startpos, sizes;
+  std::vector<std::string> names;
+  uint8_t *d_text = nullptr;     // N + 64 (zero pad)
+  void *d_sa = nullptr;
+  void *d_isa = nullptr;
+  uint8_t *d_lcp8 = nullptr;     // min(LCP,255)
+  uint64_t *d_ovf = nullptr;     // {idx,val} for LCP >= 255, sorted
+  uint64_t n_ovf = 0;
+  uint8_t *d_map = nullptr;
+  uint64_t map_bytes = 0;
+  uint64_t *d_startpos = nullptr;
+  uint64_t *d_sizes = nullptr;
+  double build_seconds = 0;
+  uint64_t device_bytes = 0;
+};
+
+namespace smash {
+// sa_build.hip
+void build_sa_isa(smash_index *ix, hipStream_t s);       // fills d_sa, d_isa
+uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, saturating)
+void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
+void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
+}  // namespace smash

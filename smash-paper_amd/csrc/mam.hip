@@ -1,0 +1,105 @@
+// smash-paper_amd/csrc/mam.hip -- per-read MAM search on gfx950.
+//
+// Replaces longSA::MAM (longSA.cpp:503-536) with traverse/top_down_faster
+// (:297-380), the inline suffix link + expand_link (longSA.h:158-174) and
+// is_leftmaximal (:540-546).  One read per lane; the read is staged in LDS;
+// the SA interval lives in registers.  The work is chains of dependent
+// random loads into the HBM-resident SA / ISA / text / LCP (no MFMA).
+//
+// Results are identical to the reference because the match set is a pure
+// function of (read, index): the same probe sequence is executed.  LCP is
+// read from the u8 array saturated at 255: expand_link only asks
+// LCP >= depth with depth <= read length <= 255, for which
+// min(LCP,255) >= depth <=> LCP >= depth, so the reference's overflow
+// lower_bound (longSA.h:34-39) is never needed on this path.
+#include "common.hpp"
+#include "mam_device.hpp"
+
+namespace smash {
+namespace {
+
+template <class IdxT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_mam(
+    DevIndex<IdxT> x, const uint8_t *__restrict__ seqs, uint64_t stride,
+    const uint16_t *__restrict__ lens, uint32_t len0, uint64_t n_reads,
+    uint32_t min_len, uint64_t *__restrict__ out, uint32_t cap,
+    uint32_t *__restrict__ n_out, uint32_t row) {
+  extern __shared__ uint8_t lds[];
+  const uint64_t r0 = uint64_t(blockIdx.x) * BLOCK;
+  const uint32_t nr = uint32_t(n_reads - r0 < BLOCK ? n_reads - r0 : BLOCK);
+  // stage this block's reads (coalesced byte copy)
+  for (uint32_t rr = 0; rr < nr; ++rr) {
+    const uint32_t L = lens ? lens[r0 + rr] : len0;
+    const uint8_t *src = seqs + (r0 + rr) * stride;
+    for (uint32_t k = threadIdx.x; k < L; k += BLOCK) lds[rr * row + k] = src[k];
+  }
+  __syncthreads();
+  if (threadIdx.x >= nr) return;
+  const uint64_t r = r0 + threadIdx.x;
+  const uint32_t L = lens ? lens[r] : len0;
+  const uint8_t *P = lds + threadIdx.x * row;
+  MatchSink sink{out + r * cap, cap, 0};
+  mam_read(x, P, L, min_len, sink);
+  n_out[r] = sink.n;
+}
+
+template <class IdxT>
+int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
+           uint64_t stride, const uint16_t *lens, uint32_t len,
+           uint64_t n_reads, uint64_t *out, uint32_t cap, uint32_t *n_out,
+           hipStream_t s) {
+  constexpr int B = 128;
+  uint32_t maxL = lens ? 255 : len;
+  uint32_t row = (maxL + 3) / 4;
+  if ((row & 1) == 0) ++row;   // odd word stride: conflict-free LDS rows
+  row *= 4;
+  const size_t lds = size_t(B) * row;
+  const uint64_t blocks = (n_reads + B - 1) / B;
+  DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
+  for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
+    const uint64_t nb = blocks - b0 < (1u << 30) ? blocks - b0 : (1u << 30);
+    const uint64_t off = b0 * B;
+    k_mam<IdxT, B><<<unsigned(nb), B, lds, s>>>(
+        x, seqs + off * stride, stride, lens ? lens + off : nullptr, len,
+        n_reads - off, min_len, out + off * cap, cap, n_out + off, row);
+  }
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+}  // namespace
+}  // namespace smash
+
+using namespace smash;
+
+extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len,
+                               const uint8_t *d_seqs, uint64_t stride,
+                               const uint16_t *d_lens, uint32_t len,
+                               uint64_t n_reads, uint64_t *d_out,
+                               uint32_t cap_per_read, uint32_t *d_n_out,
+                               void *stream) {
+  if (!ix || !d_seqs || !d_out || !d_n_out || cap_per_read == 0) {
+    set_error("smash_map_batch: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  if (mode != SMASH_MODE_MAM) {
+    set_error("smash_map_batch: only SMASH_MODE_MAM (the SMASH default) runs on the device");
+    return SMASH_ERR_UNSUPPORTED;
+  }
+  if (!d_lens && (len == 0 || len > 255)) {
+    set_error("smash_map_batch: read length must be 1..255");
+    return SMASH_ERR_ARG;
+  }
+  if (min_len < 2) {   // "NOTE: min_len must be > 1" (longSA.h:194)
+    set_error("smash_map_batch: min_len must be > 1");
+    return SMASH_ERR_ARG;
+  }
+  if (n_reads == 0) return SMASH_OK;
+  SMASH_HIP(hipSetDevice(ix->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return ix->idx_bytes == 4
+             ? launch<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
+                                d_out, cap_per_read, d_n_out, s)
+             : launch<uint64_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
+                                d_out, cap_per_read, d_n_out, s);
+}

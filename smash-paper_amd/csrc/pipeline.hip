@@ -1,0 +1,829 @@
+// smash-paper_amd/csrc/pipeline.hip -- the read -> bin-count chain per batch.
+//
+//   k_mam        longSA::MAM per mate                        (mam_device.hpp)
+//   k_post       per pair: Aligner::prepare_matches           query.cpp:231-306
+//                + mappability_tag L/R                         mappability_tag.cpp:93-124
+//                + smashMEM filters, key                       smashMEM.py:84-92,154-217
+//   dedup        global first-wins pair key set               smashMEM.py:149,217-228
+//   k_emit       awk/perl extraction of major-chromosome hits smash_mapping.sh:29
+//   k_bin        varbin adjacent de-dup + bisect + count      varbin.py:52-92
+//
+// All per-pair state lives in HBM; the host only launches.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "common.hpp"
+#include "mam_device.hpp"
+
+namespace {
+constexpr int MAXA = 48;        // alignments per mate kept on chip
+constexpr int kB = 256;
+enum Stat { S_PAIRS, S_KEYPAIRS, S_DUPEPAIRS, S_POS, S_DUPS, S_KEPT, S_MATCHES, S_ERR, S_N };
+}  // namespace
+
+struct smash_pipeline {
+  const smash_index *ix = nullptr;
+  int device = 0;
+  uint32_t read_len = 0, min_len = 20, slots = 0, n_contig = 0, nbins = 0;
+  int32_t min_excess = 4;
+  int64_t hit_window = 10000;
+  uint64_t max_pairs = 0;
+  uint32_t *d_tag_off = nullptr;
+  uint8_t *d_small = nullptr;
+  int64_t *d_chrom_off = nullptr;
+  int64_t *d_bins = nullptr;
+  uint64_t *d_match = nullptr;
+  uint32_t *d_nmatch = nullptr;
+  int32_t *d_nk = nullptr;
+  uint32_t *d_nmajor = nullptr;
+  uint64_t *d_hits = nullptr;
+  uint64_t *d_hash = nullptr;   // [2*max_pairs] hi, lo
+  uint8_t *d_keep = nullptr;
+  uint8_t *d_first = nullptr;
+  uint64_t *d_k[2] = {nullptr, nullptr};
+  uint32_t *d_v[2] = {nullptr, nullptr};
+  void *d_temp = nullptr;
+  size_t temp_bytes = 0;
+  uint64_t *d_table = nullptr;
+  uint64_t table_mask = 0;
+  uint32_t *d_posoff = nullptr;   // [max_pairs + 1]
+  uint32_t *d_cnt = nullptr;      // [max_pairs]
+  int64_t *d_pos0 = nullptr, *d_abs = nullptr;
+  int64_t *d_prev = nullptr;      // [2] carried {last pos0 or -1, -}
+  unsigned long long *d_stats = nullptr;
+  uint32_t *d_send_q = nullptr;   // exported slot -> pair
+  unsigned long long *d_owner = nullptr;  // per-owner counters (<= 64 ranks)
+  uint64_t n_pairs = 0, n_export = 0;
+  hipStream_t last = nullptr;
+};
+
+namespace smash {
+namespace {
+
+struct PostCfg {
+  const uint64_t *startpos, *sizes;
+  uint32_t n_seq, L, slots;
+  const uint32_t *tag_off;
+  const uint8_t *small;
+  const int64_t *chrom_off;
+  const uint8_t *map;
+  uint64_t map_bytes;
+  int32_t min_excess;
+  int64_t window;
+};
+
+struct Aln {
+  int64_t pos, qpos;
+  uint32_t seq;
+  uint16_t prefix, len, suffix;
+  uint8_t rc, pad;
+};
+
+struct Hit {
+  int64_t pos;
+  uint32_t tid, qstart, qend;
+  int32_t L0, R0;
+  int64_t qkey;   // qpos for to_print
+  uint8_t rc;
+};
+
+__device__ inline bool merge_less(const Aln &a, const Aln &b) {   // to_merge
+  if (a.rc != b.rc) return a.rc < b.rc;
+  if (a.seq != b.seq) return a.seq < b.seq;
+  if (a.pos != b.pos) return a.pos < b.pos;
+  return a.prefix < b.prefix;
+}
+
+__device__ inline unsigned mapb(const PostCfg &c, uint64_t at) {
+  return at < c.map_bytes ? c.map[at] : 0u;
+}
+
+// resolve + merge + to_print order + tags for one mate; returns #hits
+__device__ int mate_hits(const PostCfg &c, const uint64_t *m, uint32_t n,
+                         Hit *hits, int32_t &err) {
+  Aln a[MAXA];
+  int na = 0;
+  const uint32_t L = c.L;
+  for (uint32_t k = 0; k < n && k < MAXA; ++k) {
+    const uint64_t w = m[k];
+    const uint64_t ref = w & 0xFFFFFFFFFFFFull;
+    const uint32_t q = uint32_t((w >> 48) & 0xFF), len = uint32_t(w >> 56);
+    uint32_t lo = 0, hi = c.n_seq;          // upper_bound(startpos, ref)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (c.startpos[mid] <= ref) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t si = lo - 1;
+    const uint64_t rcpos = ref - q;
+    int64_t pos = int64_t(rcpos - c.startpos[si]);
+    const uint32_t extra = L - len - q;
+    Aln x;
+    x.qpos = q;
+    x.len = uint16_t(len);
+    if (si & 1) {
+      x.seq = si - 1;
+      pos = int64_t(c.sizes[si - 1] - uint64_t(pos)) - int64_t(L);
+      x.prefix = uint16_t(extra);
+      x.suffix = uint16_t(q);
+      x.rc = 1;
+    } else {
+      x.seq = si;
+      x.prefix = uint16_t(q);
+      x.suffix = uint16_t(extra);
+      x.rc = 0;
+    }
+    x.pos = pos;
+    if (pos >= 0) a[na++] = x;            // erase pos < 0 (query.cpp:239-246)
+  }
+  if (n > MAXA) err = SMASH_ERR_UNSUPPORTED;
+  // insertion sort by to_merge (distinct keys: no ties)
+  for (int i = 1; i < na; ++i) {
+    Aln t = a[i];
+    int j = i - 1;
+    while (j >= 0 && merge_less(t, a[j])) { a[j + 1] = a[j]; --j; }
+    a[j + 1] = t;
+  }
+  int nh = 0;
+  int g0 = 0;
+  for (int i = 0; i < na; ++i) {
+    const bool endg = (i + 1 == na) || a[i + 1].pos != a[i].pos ||
+                      a[i + 1].seq != a[i].seq || a[i + 1].rc != a[i].rc;
+    if (!endg) continue;
+    Hit h;
+    h.tid = a[i].seq >> 1;
+    h.rc = a[i].rc;
+    h.pos = a[i].pos;
+    h.qstart = a[g0].prefix;                 // leading S (query.cpp:260-263)
+    h.qend = L - a[i].suffix;                // trailing S (:267-268)
+    int64_t qmin = a[g0].qpos;
+    for (int k = g0 + 1; k <= i; ++k) qmin = a[k].qpos < qmin ? a[k].qpos : qmin;
+    h.qkey = qmin;
+    // mappability_tag on every '=' block; block k starts at offset prefix_k
+    const uint32_t abspos = c.tag_off[h.tid] + uint32_t(h.pos + 1);
+    const bool small = c.small[h.tid] != 0;
+    for (int k = g0; k <= i; ++k) {
+      const uint32_t cnt = a[k].len;
+      const uint32_t li = abspos + uint32_t(a[k].prefix) + cnt - 1;
+      const uint32_t ri = abspos + uint32_t(a[k].prefix) - 1;
+      const unsigned lm = mapb(c, 2 + uint64_t(li) * 2);
+      const unsigned left = lm ? lm - 1 : 255;
+      const unsigned rm = mapb(c, 2 + uint64_t(ri) * 2 + 1);
+      const unsigned right = rm ? rm : 255;
+      if (k == g0) { h.L0 = int32_t(left); h.R0 = int32_t(right); }
+      if (!small && err == 0) {
+        if (left > cnt) err = SMASH_ERR_TAG_LEFT;
+        else if (right > cnt) err = SMASH_ERR_TAG_RIGHT;
+      }
+    }
+    // to_print order: insert by (qpos, rc)
+    int j = nh - 1;
+    while (j >= 0 && (h.qkey < hits[j].qkey || (h.qkey == hits[j].qkey && h.rc < hits[j].rc))) {
+      hits[j + 1] = hits[j];
+      --j;
+    }
+    hits[j + 1] = h;
+    ++nh;
+    g0 = i + 1;
+  }
+  return nh;
+}
+
+__device__ inline uint64_t mix64(uint64_t z) {
+  z ^= z >> 33; z *= 0xff51afd7ed558ccdull;
+  z ^= z >> 33; z *= 0xc4ceb9fe1a85ec53ull;
+  z ^= z >> 33;
+  return z;
+}
+
+__global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restrict__ match,
+                                             const uint32_t *__restrict__ nmatch,
+                                             uint64_t n_pairs, int32_t *nk_out,
+                                             uint32_t *nmajor_out, uint64_t *hits_out,
+                                             uint64_t *hash_out,
+                                             unsigned long long *stats) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  int32_t err = 0;
+  unsigned long long nm = 0;
+  if (q < n_pairs) {
+    Hit h1[MAXA], h2[MAXA];
+    const uint32_t n1 = nmatch[2 * q], n2 = nmatch[2 * q + 1];
+    nm = n1 + n2;
+    const int k1 = mate_hits(c, match + (2 * q) * c.slots, n1 < c.slots ? n1 : c.slots, h1, err);
+    const int k2 = mate_hits(c, match + (2 * q + 1) * c.slots, n2 < c.slots ? n2 : c.slots, h2, err);
+    if (n1 > c.slots || n2 > c.slots) err = SMASH_ERR_UNSUPPORTED;
+    // smashMEM excess-mappability filter (smashMEM.py:84-92)
+    int m1 = 0, m2 = 0;
+    for (int i = 0; i < k1; ++i) {
+      const int mx = h1[i].L0 > h1[i].R0 ? h1[i].L0 : h1[i].R0;
+      if (int(h1[i].qend) - int(h1[i].qstart) - mx >= c.min_excess) h1[m1++] = h1[i];
+    }
+    for (int i = 0; i < k2; ++i) {
+      const int mx = h2[i].L0 > h2[i].R0 ? h2[i].L0 : h2[i].R0;
+      if (int(h2[i].qend) - int(h2[i].qstart) - mx >= c.min_excess) h2[m2++] = h2[i];
+    }
+    uint64_t *ho = hits_out + q * (2 * uint64_t(c.slots));
+    int32_t nk = -1;
+    uint32_t nmaj = 0;
+    uint64_t hh = 0x9E3779B97F4A7C15ull, hl = 0xD1B54A32D192ED03ull;
+    if (m1 > 0 || m2 > 0) {                  // smashMEM.py:162
+      nk = 0;
+      auto put = [&](uint32_t tid, int64_t pos) {
+        ho[nk++] = (uint64_t(tid) << 48) | (uint64_t(pos) & 0xFFFFFFFFFFFFull);
+        const uint64_t w = (uint64_t(tid) << 48) ^ uint64_t(pos);
+        hh = mix64(hh ^ w) + 0x632BE59BD9B4E019ull;
+        hl = mix64(hl + w * 0x9E3779B97F4A7C15ull) ^ (hl >> 29);
+        if (c.chrom_off[tid] >= 0) ++nmaj;
+      };
+      for (int i = 0; i < m1; ++i) put(h1[i].tid, h1[i].pos);
+      for (int b = 0; b < m2; ++b) {         // hit window (smashMEM.py:193-200)
+        bool close = false;
+        for (int i = 0; i < m1; ++i) {
+          int64_t d = h1[i].pos - h2[b].pos;
+          d = d < 0 ? -d : d;
+          if (h1[i].tid == h2[b].tid && d < c.window) { close = true; break; }
+        }
+        if (!close) put(h2[b].tid, h2[b].pos);
+      }
+      hh = mix64(hh ^ uint64_t(nk)) | 1;
+      hl = mix64(hl + uint64_t(nk)) | 1;
+    }
+    nk_out[q] = nk;
+    nmajor_out[q] = nmaj;
+    hash_out[2 * q] = hh;
+    hash_out[2 * q + 1] = hl;
+  }
+  // block-aggregated stats
+  __shared__ unsigned long long s_nm, s_pairs;
+  __shared__ int s_err;
+  if (threadIdx.x == 0) { s_nm = 0; s_pairs = 0; s_err = 0; }
+  __syncthreads();
+  if (q < n_pairs) {
+    atomicAdd(&s_nm, nm);
+    atomicAdd(&s_pairs, 1ull);
+    if (err) atomicCAS(&s_err, 0, err);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_pairs) {
+      atomicAdd(&stats[S_MATCHES], s_nm);
+      atomicAdd(&stats[S_PAIRS], s_pairs);
+    }
+    if (s_err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)s_err);
+  }
+}
+
+__global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n,
+                             uint64_t *key, uint32_t *val) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  key[q] = nk[q] >= 0 ? hash[2 * q] : ~0ull;
+  val[q] = uint32_t(q);
+}
+
+// 128-bit key set, open addressing, slot = {hi, lo}, 0 = empty.
+// returns true if the key was already present; inserts it otherwise.
+__device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi,
+                                uint64_t lo, bool insert, bool *full) {
+  uint64_t i = (hi ^ (hi >> 31)) & mask;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
+    unsigned long long cur = __hip_atomic_load(sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == 0) {
+      if (!insert) return false;
+      const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
+      if (prev == 0) {
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * i + 1]),
+                           (unsigned long long)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+      cur = prev;
+    }
+    if (cur == hi) {
+      const unsigned long long l = __hip_atomic_load(
+          reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT);
+      if (l == lo) return true;
+    }
+    i = (i + 1) & mask;
+  }
+  *full = true;
+  return false;
+}
+
+// mode 0: single GPU (test+insert the persistent set); mode 1: mark
+// in-batch first occurrences only (multi-GPU export)
+__global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
+                              uint64_t n, const int32_t *nk, const uint64_t *hash,
+                              uint64_t *table, uint64_t mask, int mode, uint8_t *keep,
+                              uint8_t *first, unsigned long long *stats) {
+  const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  unsigned long long kp = 0, dp = 0;
+  bool full = false;
+  if (s < n) {
+    const uint32_t q = val[s];
+    if (nk[q] < 0) {
+      keep[q] = 0;
+      first[q] = 0;
+    } else {
+      kp = 1;
+      bool f = true;
+      const uint64_t lo = hash[2 * q + 1];
+      for (uint64_t t = s; t-- > 0 && key[t] == key[s];) {
+        const uint32_t q2 = val[t];
+        if (hash[2 * q2 + 1] == lo) { f = false; break; }
+      }
+      first[q] = f ? 1 : 0;
+      if (mode == 0) {
+        bool k = f && !set_test_insert(table, mask, key[s], lo, true, &full);
+        keep[q] = k ? 1 : 0;
+        dp = k ? 0 : 1;
+      }
+    }
+  }
+  __shared__ unsigned long long a, b;
+  __shared__ int fl;
+  if (threadIdx.x == 0) { a = 0; b = 0; fl = 0; }
+  __syncthreads();
+  if (kp) atomicAdd(&a, kp);
+  if (dp) atomicAdd(&b, dp);
+  if (full) fl = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a) atomicAdd(&stats[S_KEYPAIRS], a);
+    if (b) atomicAdd(&stats[S_DUPEPAIRS], b);
+    if (fl) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
+  }
+}
+
+__global__ void k_count(const uint8_t *keep, const uint32_t *nmajor, uint64_t n,
+                        uint32_t *cnt) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q < n) cnt[q] = keep[q] ? nmajor[q] : 0;
+}
+
+__global__ void k_emit(const uint8_t *keep, const int32_t *nk,
+                       const uint64_t *hits, const uint32_t *off, uint64_t n,
+                       uint32_t slots, const int64_t *chrom_off, int64_t *pos0,
+                       int64_t *absp) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= n || !keep[q]) return;
+  const uint64_t *h = hits + q * 2 * uint64_t(slots);
+  uint64_t o = off[q];
+  for (int32_t i = 0; i < nk[q]; ++i) {
+    const uint32_t tid = uint32_t(h[i] >> 48);
+    const int64_t p = int64_t(h[i] & 0xFFFFFFFFFFFFull);
+    const int64_t co = chrom_off[tid];
+    if (co < 0) continue;
+    pos0[o] = p;
+    absp[o] = p + co;
+    ++o;
+  }
+}
+
+// varbin: adjacent de-dup on the pos string (== pos0), bisect_right, count.
+__global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
+                                            const int64_t *__restrict__ absp,
+                                            const uint32_t *npos_p, const int64_t *prev_p,
+                                            const int64_t *__restrict__ bins, uint32_t nbins,
+                                            unsigned long long *counts,
+                                            unsigned long long *stats) {
+  const uint64_t n = *npos_p;
+  const int64_t prev0 = *prev_p;
+  unsigned long long d = 0, k = 0, t = 0;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t p = pos0[i];
+    const int64_t pr = i ? pos0[i - 1] : prev0;
+    ++t;
+    if (pr >= 0 && pr == p) { ++d; continue; }
+    const int64_t a = absp[i];
+    uint32_t lo = 0, hi = nbins;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a < bins[mid]) hi = mid; else lo = mid + 1;
+    }
+    atomicAdd(&counts[lo == 0 ? nbins - 1 : lo - 1], 1ull);
+    ++k;
+  }
+  __shared__ unsigned long long sd, sk, st;
+  if (threadIdx.x == 0) { sd = 0; sk = 0; st = 0; }
+  __syncthreads();
+  if (t) { atomicAdd(&st, t); atomicAdd(&sd, d); atomicAdd(&sk, k); }
+  __syncthreads();
+  if (threadIdx.x == 0 && st) {
+    atomicAdd(&stats[S_POS], st);
+    atomicAdd(&stats[S_DUPS], sd);
+    atomicAdd(&stats[S_KEPT], sk);
+  }
+}
+
+__global__ void k_tail(const uint32_t *npos_p, const int64_t *pos0, int64_t *prev,
+                       int64_t *tail) {
+  const uint32_t n = *npos_p;
+  const int64_t last = n ? pos0[n - 1] : -1;
+  if (tail) { tail[0] = int64_t(n); tail[1] = last; }
+  if (prev && n) prev[0] = last;
+}
+
+int check_pipe(smash_pipeline *p, uint64_t n_pairs) {
+  if (!p) { set_error("null pipeline"); return SMASH_ERR_ARG; }
+  if (n_pairs > p->max_pairs) {
+    set_error("batch larger than cfg.max_pairs");
+    return SMASH_ERR_ARG;
+  }
+  return SMASH_OK;
+}
+
+PostCfg post_cfg(const smash_pipeline *p) {
+  PostCfg c;
+  c.startpos = p->ix->d_startpos;
+  c.sizes = p->ix->d_sizes;
+  c.n_seq = p->ix->n_seq;
+  c.L = p->read_len;
+  c.slots = p->slots;
+  c.tag_off = p->d_tag_off;
+  c.small = p->d_small;
+  c.chrom_off = p->d_chrom_off;
+  c.map = p->ix->d_map;
+  c.map_bytes = p->ix->map_bytes;
+  c.min_excess = p->min_excess;
+  c.window = p->hit_window;
+  return c;
+}
+
+}  // namespace
+}  // namespace smash
+
+using namespace smash;
+
+extern "C" int smash_pipeline_create(const smash_index *ix,
+                                     const smash_pipeline_cfg *cfg,
+                                     smash_pipeline **out) {
+  if (!ix || !cfg || !out || cfg->read_len == 0 || cfg->read_len > 255 ||
+      cfg->min_len < 2 || cfg->read_len < cfg->min_len || cfg->max_pairs == 0 ||
+      cfg->max_pairs > 0xFFFFFFFFull || cfg->n_contig * 2 != ix->n_seq ||
+      !cfg->h_tag_offsets || !cfg->h_small_chr || !cfg->h_chrom_off ||
+      !cfg->h_bin_starts || cfg->nbins == 0) {
+    set_error("smash_pipeline_create: bad configuration");
+    return SMASH_ERR_ARG;
+  }
+  if (!ix->d_map) {
+    set_error("smash_pipeline_create: index has no map.bin");
+    return SMASH_ERR_ARG;
+  }
+  auto *p = new smash_pipeline;
+  try {
+    SMASH_HIPX(hipSetDevice(ix->device));
+    p->ix = ix;
+    p->device = ix->device;
+    p->read_len = cfg->read_len;
+    p->min_len = cfg->min_len;
+    p->slots = cfg->read_len - cfg->min_len + 1;
+    p->n_contig = cfg->n_contig;
+    p->nbins = cfg->nbins;
+    p->min_excess = cfg->min_excess;
+    p->hit_window = cfg->hit_window;
+    p->max_pairs = cfg->max_pairs;
+    const uint64_t P = cfg->max_pairs;
+    p->d_tag_off = dalloc<uint32_t>(p->n_contig);
+    p->d_small = dalloc<uint8_t>(p->n_contig);
+    p->d_chrom_off = dalloc<int64_t>(p->n_contig);
+    p->d_bins = dalloc<int64_t>(p->nbins);
+    SMASH_HIPX(hipMemcpy(p->d_tag_off, cfg->h_tag_offsets, 4 * p->n_contig, hipMemcpyHostToDevice));
+    SMASH_HIPX(hipMemcpy(p->d_small, cfg->h_small_chr, p->n_contig, hipMemcpyHostToDevice));
+    SMASH_HIPX(hipMemcpy(p->d_chrom_off, cfg->h_chrom_off, 8 * p->n_contig, hipMemcpyHostToDevice));
+    SMASH_HIPX(hipMemcpy(p->d_bins, cfg->h_bin_starts, 8 * p->nbins, hipMemcpyHostToDevice));
+    p->d_match = dalloc<uint64_t>(2 * P * p->slots);
+    p->d_nmatch = dalloc<uint32_t>(2 * P);
+    p->d_nk = dalloc<int32_t>(P);
+    p->d_nmajor = dalloc<uint32_t>(P);
+    p->d_hits = dalloc<uint64_t>(P * 2 * p->slots);
+    p->d_hash = dalloc<uint64_t>(2 * P);
+    p->d_keep = dalloc<uint8_t>(P);
+    p->d_first = dalloc<uint8_t>(P);
+    for (int i = 0; i < 2; ++i) {
+      p->d_k[i] = dalloc<uint64_t>(P);
+      p->d_v[i] = dalloc<uint32_t>(P);
+    }
+    size_t a = 0, b = 0;
+    {
+      hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
+      hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
+      SMASH_HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, a, kb, vb, P));
+    }
+    p->d_posoff = dalloc<uint32_t>(P + 1);
+    p->d_cnt = dalloc<uint32_t>(P);
+    SMASH_HIPX(hipcub::DeviceScan::InclusiveSum(nullptr, b, p->d_cnt, p->d_posoff + 1, P));
+    p->temp_bytes = std::max(a, b);
+    p->d_temp = dalloc<uint8_t>(p->temp_bytes);
+    uint64_t cap = 2 * std::max<uint64_t>(cfg->dedup_capacity, P);
+    uint64_t pw = 1;
+    while (pw < cap) pw <<= 1;
+    p->table_mask = pw - 1;
+    p->d_table = dalloc<uint64_t>(2 * pw);
+    SMASH_HIPX(hipMemset(p->d_table, 0, 16 * pw));
+    p->d_pos0 = dalloc<int64_t>(P * 2 * p->slots);
+    p->d_abs = dalloc<int64_t>(P * 2 * p->slots);
+    p->d_prev = dalloc<int64_t>(2);
+    int64_t init[2] = {-1, -1};
+    SMASH_HIPX(hipMemcpy(p->d_prev, init, 16, hipMemcpyHostToDevice));
+    p->d_stats = dalloc<unsigned long long>(S_N);
+    SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * S_N));
+    p->d_send_q = dalloc<uint32_t>(P);
+    p->d_owner = dalloc<unsigned long long>(2 * 64);
+    SMASH_HIPX(hipMemset(p->d_posoff, 0, 4));
+  } catch (hip_failure &f) {
+    set_error(f.what);
+    smash_pipeline_free(p);
+    return SMASH_ERR_NOMEM;
+  }
+  *out = p;
+  return SMASH_OK;
+}
+
+extern "C" void smash_pipeline_free(smash_pipeline *p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
+                  (void *)p->d_bins, (void *)p->d_match, (void *)p->d_nmatch,
+                  (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
+                  (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_first,
+                  (void *)p->d_k[0], (void *)p->d_k[1], (void *)p->d_v[0],
+                  (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
+                  (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
+                  (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
+                  (void *)p->d_send_q, (void *)p->d_owner})
+    dfree(q);
+  delete p;
+}
+
+extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
+                               uint64_t n_pairs, void *stream) {
+  int rc = check_pipe(p, n_pairs);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  p->last = s;
+  p->n_pairs = n_pairs;
+  if (!n_pairs) return SMASH_OK;
+  SMASH_HIP(hipSetDevice(p->device));
+  rc = smash_map_batch(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len,
+                       nullptr, p->read_len, 2 * n_pairs, p->d_match, p->slots,
+                       p->d_nmatch, stream);
+  if (rc) return rc;
+  k_post<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
+      post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_nk, p->d_nmajor,
+      p->d_hits, p->d_hash, p->d_stats);
+  SMASH_HIP(hipGetLastError());
+  // in-batch ordering for de-dup: stable radix sort of key hi, value = pair
+  k_dedup_keys<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_nk, p->d_hash, n_pairs,
+                                                             p->d_k[0], p->d_v[0]);
+  hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
+  hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
+  size_t tb = p->temp_bytes;
+  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_pairs, 0, 64, s));
+  if (kb.Current() != p->d_k[0]) {   // keep sorted data in slot 0
+    std::swap(p->d_k[0], p->d_k[1]);
+    std::swap(p->d_v[0], p->d_v[1]);
+  }
+  return SMASH_OK;
+}
+
+static int dedup_local(smash_pipeline *p, hipStream_t s) {
+  if (!p->n_pairs) return SMASH_OK;
+  k_dedup_first<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, s>>>(
+      p->d_k[0], p->d_v[0], p->n_pairs, p->d_nk, p->d_hash, p->d_table,
+      p->table_mask, 0, p->d_keep, p->d_first, p->d_stats);
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+extern "C" int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *stream) {
+  if (!p) return SMASH_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  p->last = s;
+  const uint64_t n = p->n_pairs;
+  if (n) {
+    k_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, n, p->d_cnt);
+    size_t tb = p->temp_bytes;
+    SMASH_HIP(hipcub::DeviceScan::InclusiveSum(p->d_temp, tb, p->d_cnt, p->d_posoff + 1, n, s));
+    k_emit<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nk, p->d_hits,
+                                                    p->d_posoff, n, p->slots,
+                                                    p->d_chrom_off, p->d_pos0, p->d_abs);
+  }
+  k_tail<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_pos0, nullptr, d_tail);
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
+                               uint64_t *d_counts, void *stream) {
+  if (!p || !d_counts) return SMASH_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  p->last = s;
+  const uint64_t n = p->n_pairs;
+  const int64_t *prev = d_prev ? d_prev : p->d_prev;
+  k_bin<<<2048, kB, 0, s>>>(p->d_pos0, p->d_abs, p->d_posoff + n, prev, p->d_bins,
+                            p->nbins, reinterpret_cast<unsigned long long *>(d_counts),
+                            p->d_stats);
+  // carry the adjacent-dup state across batches (single-GPU use)
+  k_tail<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_pos0, p->d_prev, nullptr);
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+extern "C" int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
+                                 uint64_t n_pairs, uint64_t *d_counts, void *stream) {
+  int rc = smash_phase_map(p, d_reads, n_pairs, stream);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if ((rc = dedup_local(p, s))) return rc;
+  if ((rc = smash_phase_positions(p, nullptr, stream))) return rc;
+  return smash_phase_bin(p, nullptr, d_counts, stream);
+}
+
+// ---- multi-GPU de-dup exchange ------------------------------------------------
+namespace smash {
+namespace {
+__global__ void k_export_count(const uint8_t *first, const int32_t *nk,
+                               const uint64_t *hash, uint64_t n, int world,
+                               unsigned long long *cnt) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q < n && nk[q] >= 0 && first[q]) atomicAdd(&cnt[hash[2 * q] % uint64_t(world)], 1ull);
+}
+__global__ void k_export_fill(const uint8_t *first, const int32_t *nk,
+                              const uint64_t *hash, uint64_t n, int world,
+                              uint64_t gbase, unsigned long long *cursor,
+                              uint64_t *send, uint32_t *send_q) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= n || nk[q] < 0 || !first[q]) return;
+  const uint64_t o = atomicAdd(&cursor[hash[2 * q] % uint64_t(world)], 1ull);
+  send[3 * o] = hash[2 * q];
+  send[3 * o + 1] = hash[2 * q + 1];
+  send[3 * o + 2] = gbase + q;
+  send_q[o] = uint32_t(q);
+}
+__global__ void k_owner_keys(const uint64_t *recv, uint64_t n, uint64_t *key, uint32_t *val) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j < n) { key[j] = recv[3 * j]; val[j] = uint32_t(j); }
+}
+__global__ void k_owner_decide(const uint64_t *key, const uint32_t *val, const uint64_t *recv,
+                               uint64_t n, uint64_t *table, uint64_t mask, uint8_t *flags,
+                               unsigned long long *stats) {
+  const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint32_t j = val[s];
+  const uint64_t lo = recv[3 * j + 1], g = recv[3 * j + 2];
+  bool win = true;
+  for (uint64_t t = s; t-- > 0 && key[t] == key[s];) {
+    const uint32_t j2 = val[t];
+    if (recv[3 * j2 + 1] == lo && recv[3 * j2 + 2] < g) { win = false; break; }
+  }
+  for (uint64_t t = s + 1; win && t < n && key[t] == key[s]; ++t) {
+    const uint32_t j2 = val[t];
+    if (recv[3 * j2 + 1] == lo && recv[3 * j2 + 2] < g) win = false;
+  }
+  bool full = false;
+  const bool keep = win && !set_test_insert(table, mask, key[s], lo, true, &full);
+  flags[j] = keep ? 1 : 0;
+  if (full) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
+}
+__global__ void k_import(const uint8_t *flags, const uint32_t *send_q, uint64_t n_export,
+                         uint8_t *keep) {
+  const uint64_t o = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (o < n_export) keep[send_q[o]] = flags[o];
+}
+__global__ void k_import_stats(const uint8_t *keep, const int32_t *nk, uint64_t n,
+                               unsigned long long *stats) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q < n && nk[q] >= 0) {
+    atomicAdd(&stats[S_KEYPAIRS], 1ull);
+    if (!keep[q]) atomicAdd(&stats[S_DUPEPAIRS], 1ull);
+  }
+}
+}  // namespace
+}  // namespace smash
+
+extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
+                                  uint64_t *d_send, int64_t *h_send_counts,
+                                  void *stream) {
+  if (!p || world < 1 || world > 64 || !d_send || !h_send_counts) {
+    set_error("smash_phase_export: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  p->last = s;
+  const uint64_t n = p->n_pairs;
+  SMASH_HIP(hipMemsetAsync(p->d_keep, 0, n ? n : 1, s));
+  if (n) {
+    // in-batch first occurrences (mode 1: no persistent-set probe)
+    k_dedup_first<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
+        p->d_k[0], p->d_v[0], n, p->d_nk, p->d_hash, p->d_table, p->table_mask, 1,
+        p->d_keep, p->d_first, p->d_stats);
+  }
+  SMASH_HIP(hipMemsetAsync(p->d_owner, 0, 2 * 64 * 8, s));
+  if (n)
+    k_export_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_first, p->d_nk, p->d_hash, n,
+                                                           world, p->d_owner);
+  unsigned long long cnt[64];
+  SMASH_HIP(hipMemcpyAsync(cnt, p->d_owner, 8 * world, hipMemcpyDeviceToHost, s));
+  SMASH_HIP(hipStreamSynchronize(s));
+  unsigned long long off[64];
+  uint64_t tot = 0;
+  for (int r = 0; r < world; ++r) {
+    off[r] = tot;
+    tot += cnt[r];
+    h_send_counts[r] = int64_t(cnt[r]);
+  }
+  p->n_export = tot;
+  SMASH_HIP(hipMemcpyAsync(p->d_owner + 64, off, 8 * world, hipMemcpyHostToDevice, s));
+  if (n)
+    k_export_fill<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_first, p->d_nk, p->d_hash, n,
+                                                          world, global_base, p->d_owner + 64,
+                                                          d_send, p->d_send_q);
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv,
+                                 uint64_t n_recv, uint8_t *d_flags, void *stream) {
+  if (!p || (n_recv && (!d_recv || !d_flags))) return SMASH_ERR_ARG;
+  if (n_recv > p->max_pairs) {
+    set_error("smash_dedup_owner: more keys than cfg.max_pairs");
+    return SMASH_ERR_ARG;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  p->last = s;
+  if (!n_recv) return SMASH_OK;
+  // reuse the sort buffers (phase_map's sorted keys are no longer needed)
+  k_owner_keys<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(d_recv, n_recv, p->d_k[0], p->d_v[0]);
+  hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
+  hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
+  size_t tb = p->temp_bytes;
+  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_recv, 0, 64, s));
+  k_owner_decide<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(
+      kb.Current(), vb.Current(), d_recv, n_recv, p->d_table, p->table_mask, d_flags,
+      p->d_stats);
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+extern "C" int smash_phase_import(smash_pipeline *p, const uint8_t *d_flags_back,
+                                  void *stream) {
+  if (!p) return SMASH_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  p->last = s;
+  if (p->n_export)
+    k_import<<<grid_for(p->n_export, kB, 1u << 30), kB, 0, s>>>(d_flags_back, p->d_send_q,
+                                                               p->n_export, p->d_keep);
+  if (p->n_pairs)
+    k_import_stats<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nk,
+                                                                    p->n_pairs, p->d_stats);
+  SMASH_HIP(hipGetLastError());
+  return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_stats(smash_pipeline *p, smash_stats *o) {
+  if (!p || !o) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  if (p->last) SMASH_HIP(hipStreamSynchronize(p->last));
+  SMASH_HIP(hipDeviceSynchronize());
+  unsigned long long st[S_N];
+  SMASH_HIP(hipMemcpy(st, p->d_stats, sizeof(st), hipMemcpyDeviceToHost));
+  o->pairs = st[S_PAIRS];
+  o->key_pairs = st[S_KEYPAIRS];
+  o->dupe_pairs = st[S_DUPEPAIRS];
+  o->positions = st[S_POS];
+  o->dups = st[S_DUPS];
+  o->kept = st[S_KEPT];
+  o->matches = st[S_MATCHES];
+  o->error = int32_t(st[S_ERR]);
+  return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_keep,
+                                   uint64_t *h_hits, uint64_t *h_hash) {
+  if (!p) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  SMASH_HIP(hipDeviceSynchronize());
+  const uint64_t n = p->n_pairs;
+  if (!n) return SMASH_OK;
+  if (h_nk) SMASH_HIP(hipMemcpy(h_nk, p->d_nk, 4 * n, hipMemcpyDeviceToHost));
+  if (h_keep) SMASH_HIP(hipMemcpy(h_keep, p->d_keep, n, hipMemcpyDeviceToHost));
+  if (h_hits) SMASH_HIP(hipMemcpy(h_hits, p->d_hits, 8 * n * 2 * p->slots, hipMemcpyDeviceToHost));
+  if (h_hash) SMASH_HIP(hipMemcpy(h_hash, p->d_hash, 16 * n, hipMemcpyDeviceToHost));
+  return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
+  if (!p) return SMASH_ERR_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SMASH_HIP(hipSetDevice(p->device));
+  SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * (p->table_mask + 1), s));
+  SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * S_N, s));
+  static const int64_t init[2] = {-1, -1};
+  SMASH_HIP(hipMemcpyAsync(p->d_prev, init, 16, hipMemcpyHostToDevice, s));
+  SMASH_HIP(hipStreamSynchronize(s));
+  return SMASH_OK;
+}

@@ -1,0 +1,421 @@
+"""smashgpu -- Python host side of the MI355X SMASH read -> bin-count path.
+
+Mirrors the reference's driver layer (index_setup.sh / smash_mapping.sh /
+binning.sh glue around mummer, mappability_tag, smashMEM.py and varbin.py)
+over the C ABI of libsmashgpu.so (include/smash_gpu.h).  PyTorch is used only
+for device memory, streams and torch.distributed; every computation runs in
+the HIP kernels of smash-paper_amd/csrc.  There is no CPU fallback: if the
+library is missing this module raises on import of the library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsmashgpu.so")
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+u8p = C.POINTER(C.c_uint8)
+i64p = C.POINTER(C.c_int64)
+i32p = C.POINTER(C.c_int32)
+vp = C.c_void_p
+
+SMASH_MODE_MAM = 1
+ERRORS = {1: "left mappability too big (mappability_tag.cpp:110)",
+          2: "right mappability too big (mappability_tag.cpp:113)",
+          -4: "out of device memory / key set full",
+          -5: "unsupported (more matches per read than on-chip slots)"}
+
+EXPORTS = [
+    "smash_last_error", "smash_text_from_fasta", "smash_text_free",
+    "smash_index_create", "smash_index_load", "smash_index_save",
+    "smash_index_free", "smash_index_query", "smash_map_batch",
+    "smash_pipeline_create", "smash_pipeline_free", "smash_count_batch",
+    "smash_phase_map", "smash_phase_export", "smash_dedup_owner",
+    "smash_phase_import", "smash_phase_positions", "smash_phase_bin",
+    "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_peek",
+]
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [("N", C.c_uint64), ("logN", C.c_uint64), ("idx_bytes", C.c_uint32),
+                ("n_seq", C.c_uint32), ("n_lcp_overflow", C.c_uint64),
+                ("map_bytes", C.c_uint64), ("d_text", vp), ("d_sa", vp),
+                ("d_isa", vp), ("d_lcp8", vp), ("d_lcp_ovf", vp), ("d_map", vp),
+                ("device_bytes", C.c_uint64), ("build_seconds", C.c_double)]
+
+
+class PipelineCfg(C.Structure):
+    _fields_ = [("min_len", C.c_uint32), ("read_len", C.c_uint32),
+                ("max_pairs", C.c_uint64), ("n_contig", C.c_uint32),
+                ("h_tag_offsets", u32p), ("h_small_chr", u8p),
+                ("h_chrom_off", i64p), ("nbins", C.c_uint32),
+                ("h_bin_starts", i64p), ("min_excess", C.c_int32),
+                ("hit_window", C.c_int64), ("dedup_capacity", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("pairs", C.c_uint64), ("key_pairs", C.c_uint64),
+                ("dupe_pairs", C.c_uint64), ("positions", C.c_uint64),
+                ("dups", C.c_uint64), ("kept", C.c_uint64),
+                ("matches", C.c_uint64), ("error", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class SmashError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def lib():
+    """Load libsmashgpu.so (raises if it was not built: no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise SmashError("libsmashgpu.so not built (run `make -C smash-paper_amd` "
+                         "or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    L.smash_last_error.restype = C.c_char_p
+    L.smash_text_from_fasta.argtypes = [C.c_char_p, C.POINTER(u8p), u64p, u32p,
+                                        C.POINTER(u64p), C.POINTER(u64p),
+                                        C.POINTER(C.POINTER(C.c_char_p))]
+    L.smash_text_free.argtypes = [u8p, C.c_uint32, u64p, u64p, C.POINTER(C.c_char_p)]
+    L.smash_text_free.restype = None
+    L.smash_index_create.argtypes = [u8p, C.c_uint64, C.c_uint32, u64p, u64p,
+                                     C.POINTER(C.c_char_p), C.c_int, C.POINTER(vp)]
+    L.smash_index_load.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+    L.smash_index_save.argtypes = [vp, C.c_char_p, C.c_uint64]
+    L.smash_index_free.argtypes = [vp]
+    L.smash_index_free.restype = None
+    L.smash_index_query.argtypes = [vp, C.POINTER(IndexInfo)]
+    L.smash_map_batch.argtypes = [vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp,
+                                  C.c_uint32, C.c_uint64, vp, C.c_uint32, vp, vp]
+    L.smash_pipeline_create.argtypes = [vp, C.POINTER(PipelineCfg), C.POINTER(vp)]
+    L.smash_pipeline_free.argtypes = [vp]
+    L.smash_pipeline_free.restype = None
+    L.smash_count_batch.argtypes = [vp, vp, C.c_uint64, vp, vp]
+    L.smash_phase_map.argtypes = [vp, vp, C.c_uint64, vp]
+    L.smash_phase_export.argtypes = [vp, C.c_int, C.c_uint64, vp, i64p, vp]
+    L.smash_dedup_owner.argtypes = [vp, vp, C.c_uint64, vp, vp]
+    L.smash_phase_import.argtypes = [vp, vp, vp]
+    L.smash_phase_positions.argtypes = [vp, vp, vp]
+    L.smash_phase_bin.argtypes = [vp, vp, vp, vp]
+    L.smash_pipeline_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.smash_pipeline_reset.argtypes = [vp, vp]
+    L.smash_pipeline_peek.argtypes = [vp, i32p, u8p, u64p, u64p]
+    _LIB = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().smash_last_error().decode(errors="replace")
+        raise SmashError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return int(stream)
+
+
+# ---------------------------------------------------------------------------
+# reference text
+# ---------------------------------------------------------------------------
+_LOWER = np.arange(256, dtype=np.uint8)
+_LOWER[ord("A"):ord("Z") + 1] += 32
+_COMP = np.arange(256, dtype=np.uint8)
+for _a, _b in zip(b"acgtrymkbdhvACGTRYMKBDHV", b"tgcayrkmvhdbTGCAYRKMVHDB"):
+    _COMP[_a] = _b
+
+
+def text_from_fasta(path):
+    """Sequence::Sequence with -rcref (fasta.cpp:133-285), in the library."""
+    L = lib()
+    t = u8p()
+    N = C.c_uint64()
+    ns = C.c_uint32()
+    sp = u64p()
+    sz = u64p()
+    nm = C.POINTER(C.c_char_p)()
+    check(L.smash_text_from_fasta(path.encode(), C.byref(t), C.byref(N), C.byref(ns),
+                                  C.byref(sp), C.byref(sz), C.byref(nm)),
+          "smash_text_from_fasta")
+    T = np.ctypeslib.as_array(t, shape=(N.value,)).copy()
+    startpos = np.ctypeslib.as_array(sp, shape=(ns.value,)).copy()
+    sizes = np.ctypeslib.as_array(sz, shape=(ns.value,)).copy()
+    names = [nm[i].decode() for i in range(ns.value)]
+    L.smash_text_free(t, ns, sp, sz, nm)
+    return T, startpos, sizes, names
+
+
+def text_from_contigs(contigs):
+    """The same text layout from in-memory contigs [(name, ASCII uint8)]."""
+    parts, sp, sz, names = [], [], [], []
+    pos = 0
+    for k, (name, s) in enumerate(contigs):
+        f = _LOWER[s]
+        sp.append(pos); sz.append(len(f)); names.append(name)
+        parts.append(f)
+        parts.append(np.array([ord("`")], np.uint8))
+        pos += len(f) + 1
+        sp.append(pos); sz.append(len(f)); names.append(name)
+        parts.append(_COMP[f[::-1]])
+        pos += len(f)
+        if k + 1 < len(contigs):
+            parts.append(np.array([ord("`")], np.uint8))
+            pos += 1
+    parts.append(np.array([ord("$")], np.uint8))
+    return (np.concatenate(parts), np.array(sp, np.uint64), np.array(sz, np.uint64),
+            names)
+
+
+def prepare_reads(seqs) -> np.ndarray:
+    """fastqs_to_sam replaceN (N->Z, fastqs_to_sam.cpp:289) + NewQuery::extend
+    lowercasing (query.cpp:125-144).  seqs: uint8 [n, L] ASCII."""
+    a = np.asarray(seqs, np.uint8).copy()
+    a[a == ord("N")] = ord("Z")
+    return _LOWER[a]
+
+
+# ---------------------------------------------------------------------------
+# index
+# ---------------------------------------------------------------------------
+class Index:
+    """HBM-resident SA/ISA/LCP/text/map.bin (replaces longSA, longSA.cpp:94)."""
+
+    def __init__(self, handle, names, sizes):
+        self.h = vp(handle)
+        self.info = IndexInfo()
+        check(lib().smash_index_query(self.h, C.byref(self.info)), "smash_index_query")
+        self.names = list(names)
+        self.sizes = [int(x) for x in sizes]
+        self.contigs = [self.names[i] for i in range(0, len(self.names), 2)]
+        self.contig_sizes = self.sizes[0::2]
+
+    @classmethod
+    def create(cls, T, startpos, sizes, names, device=0):
+        T = np.ascontiguousarray(T, np.uint8)
+        sp = np.ascontiguousarray(startpos, np.uint64)
+        sz = np.ascontiguousarray(sizes, np.uint64)
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        h = vp()
+        check(lib().smash_index_create(_p(T, u8p), len(T), len(sp), _p(sp, u64p),
+                                       _p(sz, u64p), arr, device, C.byref(h)),
+              "smash_index_create")
+        return cls(h.value, names, sz)
+
+    @classmethod
+    def from_fasta(cls, path, device=0):
+        return cls.create(*text_from_fasta(path), device=device)
+
+    @classmethod
+    def from_contigs(cls, contigs, device=0):
+        return cls.create(*text_from_contigs(contigs), device=device)
+
+    @classmethod
+    def load(cls, fasta_path, device=0):
+        """Load the reference's <fasta>.bin/ cache (longSA.cpp:100-136)."""
+        h = vp()
+        check(lib().smash_index_load(fasta_path.encode(), device, C.byref(h)),
+              "smash_index_load")
+        names, sizes = [], []
+        with open(fasta_path + ".bin/rc1.ref.bin", "rb") as f:
+            b = f.read()
+        n = int.from_bytes(b[16:24], "little")
+        off = 24
+        for _ in range(n):
+            sizes.append(int.from_bytes(b[off + 8:off + 16], "little"))
+            L = int.from_bytes(b[off + 16:off + 24], "little")
+            names.append(b[off + 24:off + 24 + L].decode())
+            off += 24 + L
+        return cls(h.value, names, sizes)
+
+    def save(self, fasta_path, fasta_size=None):
+        if fasta_size is None:
+            fasta_size = os.path.getsize(fasta_path)
+        check(lib().smash_index_save(self.h, fasta_path.encode(), fasta_size),
+              "smash_index_save")
+
+    @property
+    def N(self):
+        return self.info.N
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().smash_index_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------
+# read -> bin-count pipeline
+# ---------------------------------------------------------------------------
+MAJOR = re.compile(r"^chr(\d+|[XY])$")
+
+
+def contig_tables(contigs, sizes, chrom_sizes):
+    """Host-side per-contig tables of the reference glue:
+    tag offsets = cumulative sam_header.txt lengths (chromosomes.h:169-196,
+    index_setup.sh:31); small = '_gl000'/'chrM' (mappability_tag.cpp:82);
+    chrom_off = chrom_sizes.txt offset when the perl filter
+    ^chr(\\d+|[XY]) \\d+$ (smash_mapping.sh:29) and varbin's filters
+    (varbin.py:38-49) keep the contig, else -1."""
+    tag = np.cumsum([0] + [int(s) for s in sizes[:-1]]).astype(np.uint32)
+    small = np.array([1 if ("_gl000" in c or "chrM" in c) else 0 for c in contigs], np.uint8)
+    off = np.array([chrom_sizes[c] if (MAJOR.match(c) and "_" not in c and c != "chrM"
+                                       and c in chrom_sizes) else -1 for c in contigs],
+                   np.int64)
+    return tag, small, off
+
+
+def read_chrom_sizes(path):
+    out = {}
+    for line in open(path):
+        c = line.rstrip("\n").split("\t")
+        if c[0] in out:
+            continue    # fileToDictionary keeps the first (varbin.py:131-146)
+        out[c[0]] = int(c[2])
+    return out
+
+
+def read_bins(path):
+    rows = [line.rstrip("\n").split("\t") for line in open(path)]
+    return rows, np.array([int(r[2]) for r in rows], np.int64)
+
+
+class Pipeline:
+    """prepare_matches + mappability_tag + smashMEM + varbin on the device."""
+
+    def __init__(self, index: Index, chrom_sizes: dict, bin_starts, read_len,
+                 max_pairs, min_len=20, min_excess=4, hit_window=10000,
+                 dedup_capacity=None):
+        self.index = index
+        sizes = index.contig_sizes
+        self.tag, self.small, self.off = contig_tables(index.contigs, sizes, chrom_sizes)
+        self.bins = np.ascontiguousarray(bin_starts, np.int64)
+        self.cfg = PipelineCfg(min_len, read_len, max_pairs, len(index.contigs),
+                               _p(self.tag, u32p), _p(self.small, u8p),
+                               _p(self.off, i64p), len(self.bins), _p(self.bins, i64p),
+                               min_excess, hit_window,
+                               dedup_capacity or max_pairs)
+        h = vp()
+        check(lib().smash_pipeline_create(index.h, C.byref(self.cfg), C.byref(h)),
+              "smash_pipeline_create")
+        self.h = h
+        self.read_len = read_len
+        self.max_pairs = max_pairs
+        self.slots = read_len - min_len + 1
+
+    def count_batch(self, d_reads, n_pairs, d_counts, stream=None):
+        """d_reads: device uint8 [2*n_pairs, read_len] (torch tensor or ptr)."""
+        check(lib().smash_count_batch(self.h, _ptr(d_reads), n_pairs, _ptr(d_counts),
+                                      vp(_stream(stream))), "smash_count_batch")
+
+    def phase_map(self, d_reads, n_pairs, stream=None):
+        check(lib().smash_phase_map(self.h, _ptr(d_reads), n_pairs, vp(_stream(stream))),
+              "smash_phase_map")
+
+    def phase_export(self, world, global_base, d_send, stream=None):
+        counts = np.zeros(world, np.int64)
+        check(lib().smash_phase_export(self.h, world, global_base, _ptr(d_send),
+                                       _p(counts, i64p), vp(_stream(stream))),
+              "smash_phase_export")
+        return counts
+
+    def dedup_owner(self, d_recv, n_recv, d_flags, stream=None):
+        check(lib().smash_dedup_owner(self.h, _ptr(d_recv), n_recv, _ptr(d_flags),
+                                      vp(_stream(stream))), "smash_dedup_owner")
+
+    def phase_import(self, d_flags_back, stream=None):
+        check(lib().smash_phase_import(self.h, _ptr(d_flags_back), vp(_stream(stream))),
+              "smash_phase_import")
+
+    def phase_positions(self, d_tail, stream=None):
+        check(lib().smash_phase_positions(self.h, _ptr(d_tail), vp(_stream(stream))),
+              "smash_phase_positions")
+
+    def phase_bin(self, d_prev, d_counts, stream=None):
+        check(lib().smash_phase_bin(self.h, _ptr(d_prev), _ptr(d_counts),
+                                    vp(_stream(stream))), "smash_phase_bin")
+
+    def reset(self, stream=None):
+        check(lib().smash_pipeline_reset(self.h, vp(_stream(stream))), "smash_pipeline_reset")
+
+    def stats(self):
+        s = Stats()
+        check(lib().smash_pipeline_stats(self.h, C.byref(s)), "smash_pipeline_stats")
+        return s
+
+    def peek(self, n_pairs):
+        nk = np.zeros(n_pairs, np.int32)
+        keep = np.zeros(n_pairs, np.uint8)
+        hits = np.zeros(n_pairs * 2 * self.slots, np.uint64)
+        check(lib().smash_pipeline_peek(self.h, _p(nk, i32p), _p(keep, u8p),
+                                        _p(hits, u64p), None), "smash_pipeline_peek")
+        return nk, keep, hits.reshape(n_pairs, 2 * self.slots)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().smash_pipeline_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return vp(x)
+    return vp(x.data_ptr())
+
+
+def map_batch(index: Index, d_reads, n_reads, read_len, d_out, cap, d_n, min_len=20,
+              stream=None):
+    """longSA::MAM over a batch (smash_map_batch)."""
+    check(lib().smash_map_batch(index.h, SMASH_MODE_MAM, min_len, _ptr(d_reads),
+                                read_len, None, read_len, n_reads, _ptr(d_out), cap,
+                                _ptr(d_n), vp(_stream(stream))), "smash_map_batch")
+
+
+def unpack_matches(words, n):
+    """packed u64 (ref 48 | qoff 8 | len 8) -> [(ref, qoff, len)]"""
+    w = np.asarray(words[:n], np.uint64)
+    return [(int(x & 0xFFFFFFFFFFFF), int((x >> 48) & 0xFF), int(x >> 56)) for x in w]
+
+
+_HIP = None
+
+
+def download(dptr, nbytes, dtype=np.uint8):
+    """Device -> host copy of raw device memory (tests / index export)."""
+    global _HIP
+    if _HIP is None:
+        _HIP = C.CDLL("libamdhip64.so")
+        _HIP.hipMemcpy.argtypes = [vp, vp, C.c_size_t, C.c_int]
+        _HIP.hipDeviceSynchronize.argtypes = []
+    out = np.empty(nbytes, np.uint8)
+    _HIP.hipDeviceSynchronize()
+    rc = _HIP.hipMemcpy(out.ctypes.data_as(vp), vp(dptr), nbytes, 2)
+    if rc != 0:
+        raise SmashError("hipMemcpy D2H failed (%d)" % rc)
+    return out.view(dtype)

@@ -1,0 +1,223 @@
+"""Device parity: every HIP kernel against the oracle / reference goldens.
+
+Marked `gpu` (MI355X).  Index build (SA/ISA/LCP/map.bin), index save/load in
+the reference's on-disk format, per-read MAM triples, and the whole
+read -> bin-count pipeline (counts + varbin stats) incl. multi-batch state.
+"""
+import hashlib
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from conftest import gold, interleaved_reads, load_bins, load_chrom_sizes, read_gz_lines
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import smashgpu as S  # noqa: E402
+import oracle as O  # noqa: E402
+
+
+def _sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def sums():
+    return {l.split()[0]: (l.split()[1], int(l.split()[2])) for l in open(gold("tiny_index.sha256"))}
+
+
+@pytest.fixture(scope="module")
+def gix(tiny_fa):
+    assert torch.cuda.is_available()
+    return S.Index.from_fasta(tiny_fa)
+
+
+def _arrays(ix):
+    i = ix.info
+    N = i.N
+    dt = np.uint32 if i.idx_bytes == 4 else np.uint64
+    SA = S.download(i.d_sa, N * i.idx_bytes, dt)
+    ISA = S.download(i.d_isa, N * i.idx_bytes, dt)
+    L8 = S.download(i.d_lcp8, N)
+    ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
+    mp = S.download(i.d_map, i.map_bytes)
+    T = S.download(i.d_text, N)
+    return T, SA, ISA, L8, ovf, mp
+
+
+def test_device_index_matches_reference(gix, tiny_ix, sums):
+    T, SA, ISA, L8, ovf, mp = _arrays(gix)
+    assert gix.info.idx_bytes == 4
+    assert _sha(T.tobytes()) == sums["rc1.ref.seq.bin"][0]
+    assert _sha(SA.tobytes()) == sums["rc1.i4.index.sa.bin"][0]
+    assert _sha(ISA.tobytes()) == sums["rc1.i4.index.isa.bin"][0]
+    assert _sha(L8.tobytes()) == sums["rc1.i4.index.lcp.vec.bin"][0]
+    assert _sha(ovf.tobytes()) == sums["rc1.i4.index.lcp.m.bin:masked"][0]
+    assert _sha(mp[2:].tobytes()) == sums["map.bin[2:]"][0]
+    assert gix.info.logN == O.lib().orc_logN(gix.info.N)
+
+
+def test_index_save_load_roundtrip(gix, tiny_fa, tmp_path, sums):
+    fa = str(tmp_path / "tiny.fa")
+    shutil.copy(tiny_fa, fa)
+    gix.save(fa)
+    d = fa + ".bin/"
+    for name in ("rc1.ref.seq.bin", "rc1.ref.bin", "rc1.i4.index.bin", "rc1.i4.index.sa.bin",
+                 "rc1.i4.index.isa.bin", "rc1.i4.index.lcp.vec.bin"):
+        assert _sha(open(d + name, "rb").read()) == sums[name][0], name
+    m = np.fromfile(d + "rc1.i4.index.lcp.m.bin", np.uint64).reshape(-1, 2)
+    assert _sha(m.tobytes()) == sums["rc1.i4.index.lcp.m.bin:masked"][0]
+    assert _sha(open(d + "map.bin", "rb").read()[2:]) == sums["map.bin[2:]"][0]
+    ix2 = S.Index.load(fa)
+    a, b = _arrays(gix), _arrays(ix2)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    # without map.bin the loader recomputes it on the device
+    os.remove(d + "map.bin")
+    ix3 = S.Index.load(fa)
+    assert np.array_equal(_arrays(ix3)[5][2:], a[5][2:])
+
+
+def _device_reads(reads):
+    return torch.from_numpy(np.ascontiguousarray(reads)).cuda()
+
+
+def run_map(ix, reads, min_len=20):
+    n, L = reads.shape
+    cap = L - min_len + 1
+    d = _device_reads(reads)
+    out = torch.zeros(n * cap, dtype=torch.int64, device="cuda")
+    nn = torch.zeros(n, dtype=torch.int32, device="cuda")
+    S.map_batch(ix, d, n, L, out, cap, nn, min_len=min_len)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().view(np.uint64).reshape(n, cap)
+    k = nn.cpu().numpy()
+    return [S.unpack_matches(o[i], k[i]) for i in range(n)]
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_mam_matches_reference(gix, s):
+    reads = interleaved_reads(s)
+    exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+           for l in read_gz_lines("%s_MAM.txt.gz" % s)]
+    got = run_map(gix, reads)
+    assert len(got) == len(exp)
+    bad = [i for i in range(len(exp)) if got[i] != exp[i]]
+    assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)
+
+
+def make_pipe(ix, L, max_pairs, bins_path=None, cs_path=None):
+    _, starts = load_bins(bins_path or gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(cs_path or gold("tiny_chrom_sizes.txt"))
+    return S.Pipeline(ix, cs, starts, L, max_pairs), starts
+
+
+def run_pipeline(pipe, reads, nbins, batch=None):
+    n_pairs = reads.shape[0] // 2
+    batch = batch or n_pairs
+    counts = torch.zeros(nbins, dtype=torch.int64, device="cuda")
+    pipe.reset()
+    for b0 in range(0, n_pairs, batch):
+        b1 = min(n_pairs, b0 + batch)
+        d = _device_reads(reads[2 * b0:2 * b1])
+        pipe.count_batch(d, b1 - b0, counts)
+    st = pipe.stats()
+    return counts.cpu().numpy().astype(np.uint64), st
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_pipeline_matches_reference_varbin(gix, s):
+    reads = interleaved_reads(s)
+    pipe, starts = make_pipe(gix, reads.shape[1], reads.shape[0] // 2)
+    counts, st = run_pipeline(pipe, reads, len(starts))
+    assert st.error == 0
+    exp = [int(l.split("\t")[3]) for l in open(gold("%s_varbin.txt" % s))]
+    assert counts.tolist() == exp
+    g = open(gold("%s_varbin_stats_partial.txt" % s)).read().split("\n")[1].split("\t")
+    assert (st.positions, st.dups, st.kept) == (int(g[0]), int(g[1]), int(g[2]))
+    assert st.pairs == reads.shape[0] // 2
+
+
+@pytest.mark.parametrize("batch", [1, 7, 137, 1000])
+def test_pipeline_batches_equal_one_pass(gix, batch):
+    reads = interleaved_reads("s100")
+    pipe, starts = make_pipe(gix, reads.shape[1], 1000)
+    c1, s1 = run_pipeline(pipe, reads, len(starts), batch=1000)
+    c2, s2 = run_pipeline(pipe, reads, len(starts), batch=batch)
+    assert c1.tolist() == c2.tolist()
+    assert s1.as_dict() == s2.as_dict()
+
+
+def test_pipeline_matches_oracle_per_pair(gix, tiny_ix):
+    """Per-pair kept hit lists (smashMEM output before de-dup) == oracle."""
+    reads = interleaved_reads("s150")
+    n = reads.shape[0] // 2
+    pipe, starts = make_pipe(gix, reads.shape[1], n)
+    run_pipeline(pipe, reads, len(starts))
+    nk, keep, hits = pipe.peek(n)
+    mapbin = tiny_ix.mappability()
+    offs = np.cumsum([0] + [int(x) for x in tiny_ix.sizes[0::2]][:-1]).astype(np.uint32)
+    small = [1 if ("_gl000" in c or "chrM" in c) else 0 for c in tiny_ix.contigs]
+    for q in range(n):
+        hs = []
+        for m in (0, 1):
+            P = reads[2 * q + m].tobytes()
+            h, _ = tiny_ix.resolve(P, tiny_ix.search(P))
+            for x in h:
+                O.tag(x, offs, mapbin, small[x.tid])
+            hs.append(h)
+        exp = O.smash_pair(hs[0], hs[1])
+        if exp is None:
+            assert nk[q] == -1
+            continue
+        assert nk[q] == len(exp), q
+        got = [(int(w >> 48), int(w & 0xFFFFFFFFFFFF)) for w in hits[q, :nk[q]]]
+        assert got == exp, q
+
+
+@pytest.fixture(scope="module")
+def mid():
+    import synth
+    g = synth.make_genome("mid")
+    T, sp, sz, names = O.text_from_contigs(g)
+    oix = O.Index(T, sp, sz, names)
+    dix = S.Index.create(T, sp, sz, names)
+    return g, oix, dix
+
+
+def test_mid_genome_index_equals_oracle(mid):
+    g, oix, dix = mid
+    T, SA, ISA, L8, ovf, mp = _arrays(dix)
+    assert np.array_equal(SA.astype(np.uint64), oix.SA)
+    assert np.array_equal(ISA.astype(np.uint64), oix.ISA)
+    assert np.array_equal(L8, np.minimum(oix.LCP, 255).astype(np.uint8))
+    big = np.nonzero(oix.LCP >= 255)[0]
+    assert np.array_equal(ovf[:, 0], big) and np.array_equal(ovf[:, 1], oix.LCP[big])
+    assert np.array_equal(mp[2:], oix.mappability()[2:])
+
+
+def test_mid_genome_pipeline_equals_oracle(mid, tmp_path):
+    import synth
+    g, oix, dix = mid
+    r1, r2 = synth.make_reads(g, 6000, 150, seed=33)
+    reads = np.empty((12000, 150), np.uint8)
+    reads[0::2], reads[1::2] = r1, r2
+    reads = S.prepare_reads(reads)
+    # MAM on every read
+    got = run_map(dix, reads)
+    for i in range(0, len(reads), 7):
+        assert got[i] == oix.search(reads[i].tobytes()), i
+    bins_path = str(tmp_path / "bins.txt")
+    synth.make_bins(g, 16, bins_path)
+    synth.write_index_side_files(str(tmp_path), g)
+    cs_path = str(tmp_path / "chrom_sizes.txt")
+    pipe, starts = make_pipe(dix, 150, 2500, bins_path, cs_path)
+    counts, st = run_pipeline(pipe, reads, len(starts), batch=2500)
+    op = O.Pipeline(oix, oix.mappability(), load_chrom_sizes(cs_path), starts)
+    assert op.run(reads, threads=8) == 0
+    assert counts.tolist() == op.counts.tolist()
+    assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
+    assert st.dupe_pairs == op.n_dupe.value

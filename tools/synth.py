@@ -156,6 +156,21 @@ def make_genome(kind: str = "tiny", seed: int | None = None):
         pal = np.concatenate([half, revcomp(half)])
         contigs[0][1][30000:30120] = pal
         return contigs
+    if kind == "mid":
+        # ~3.2 Mbp, for device-vs-oracle parity at a size the C oracle
+        # indexes in seconds
+        seed = 5 if seed is None else seed
+        rng = np.random.default_rng(seed)
+        spec = [("chr1", 1400000), ("chr2", 1000000), ("chr3", 600000),
+                ("chrX", 200000), ("chrM", 16571), ("chr4_gl000193_random", 30000)]
+        contigs = [(n, ACGT[rng.integers(0, 4, size=L)]) for n, L in spec]
+        nmask = [np.zeros(len(s), bool) for _, s in contigs]
+        for ci, a, b in [(0, 0, 10000), (0, 700000, 760000), (1, 300000, 301000),
+                         (2, 590000, 600000)]:
+            contigs[ci][1][a:b] = ord("N")
+            nmask[ci][a:b] = True
+        _inject_repeats(rng, contigs, nmask, scale=10.0)
+        return contigs
     if kind == "chr21":
         seed = 21 if seed is None else seed
         rng = np.random.default_rng(seed)
