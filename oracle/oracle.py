@@ -28,7 +28,8 @@ class OrcText(C.Structure):
 
 class OrcIndex(C.Structure):
     _fields_ = [("N", C.c_uint64), ("logN", C.c_uint64), ("T", u8p),
-                ("SA", u64p), ("ISA", u64p), ("LCP", u64p),
+                ("SA", C.c_void_p), ("ISA", C.c_void_p), ("idx_bytes", C.c_uint32),
+                ("L8", u8p), ("ovf", u64p), ("n_ovf", C.c_uint64),
                 ("n_seq", C.c_uint32), ("startpos", u64p), ("sizes", u64p)]
 
 
@@ -36,7 +37,7 @@ class OrcCounters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "sa_loads", "isa_loads", "ref_loads", "lcp_loads",
         "sa_lines", "isa_lines", "ref_lines", "lcp_lines",
-        "last_sa", "last_isa", "last_ref", "last_lcp")]
+        "last_sa", "last_isa", "last_ref", "last_lcp", "ovf_lookups")]
 
 
 class OrcMatch(C.Structure):
@@ -172,26 +173,52 @@ def build_index(T):
 
 
 class Index:
-    """Host index (text + SA/ISA/LCP as uint64) wrapped for the C oracle."""
+    """Host index wrapped for the C oracle: text, SA/ISA (u32 when N < 2^32,
+    else u64, like the reference's ANINT) and the vec_uchar LCP (u8 + sorted
+    {idx,val} overflow, longSA.h:18-61).  Built by the oracle's own builder
+    unless arrays are given (e.g. downloaded from the device)."""
 
-    def __init__(self, T, startpos, sizes, names, SA=None, ISA=None, LCP=None):
-        N = len(T)
-        self.T = np.zeros(N + 64, np.uint8)
-        self.T[:N] = T
+    def __init__(self, T, startpos, sizes, names, SA=None, ISA=None, LCP=None,
+                 L8=None, ovf=None, padded_text=False):
+        N = len(T) - (64 if padded_text else 0)
+        if padded_text:
+            self.T = T
+        else:
+            self.T = np.zeros(N + 64, np.uint8)
+            self.T[:N] = T
         self.N = N
         if SA is None:
-            SA, ISA, LCP = build_index(T)
-        self.SA = np.ascontiguousarray(SA, dtype=np.uint64)
-        self.ISA = np.ascontiguousarray(ISA, dtype=np.uint64)
-        self.LCP = np.ascontiguousarray(LCP, dtype=np.uint64)
+            SA, ISA, LCP = build_index(self.T[:N])
+        it = np.uint32 if N <= 0xFFFFFFFF else np.uint64
+        self.SA = np.ascontiguousarray(SA, dtype=it)
+        self.ISA = np.ascontiguousarray(ISA, dtype=it)
+        if L8 is None:
+            LCP = np.asarray(LCP, np.uint64)
+            L8 = np.minimum(LCP, 255).astype(np.uint8)
+            big = np.nonzero(LCP >= 255)[0]
+            ovf = np.empty((len(big), 2), np.uint64)
+            ovf[:, 0] = big
+            ovf[:, 1] = LCP[big]
+        self.L8 = np.ascontiguousarray(L8, np.uint8)
+        self.ovf = np.ascontiguousarray(np.asarray(ovf, np.uint64).reshape(-1, 2))
         self.startpos = np.ascontiguousarray(startpos, dtype=np.uint64)
         self.sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
         self.names = list(names)
         self.contigs = [names[i] for i in range(0, len(names), 2)]
-        self.c = OrcIndex(N, lib().orc_logN(N), _p(self.T, u8p), _p(self.SA, u64p),
-                          _p(self.ISA, u64p), _p(self.LCP, u64p),
-                          len(self.startpos), _p(self.startpos, u64p),
-                          _p(self.sizes, u64p))
+        self.c = OrcIndex(N, lib().orc_logN(N), _p(self.T, u8p),
+                          self.SA.ctypes.data, self.ISA.ctypes.data,
+                          self.SA.itemsize, _p(self.L8, u8p),
+                          _p(self.ovf, u64p) if len(self.ovf) else None,
+                          len(self.ovf), len(self.startpos),
+                          _p(self.startpos, u64p), _p(self.sizes, u64p))
+
+    @property
+    def LCP(self):
+        """Exact LCP (u64) rebuilt from the vec_uchar layout (tests)."""
+        out = self.L8.astype(np.uint64)
+        if len(self.ovf):
+            out[self.ovf[:, 0].astype(np.int64)] = self.ovf[:, 1]
+        return out
 
     @classmethod
     def from_fasta(cls, path):

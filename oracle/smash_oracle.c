@@ -224,8 +224,25 @@ uint64_t orc_logN(uint64_t N) {
 typedef struct {
   const orc_index *ix;
   orc_counters *c;
-  uint32_t isz;      /* element bytes of SA/ISA in the device layout */
+  uint32_t isz;      /* element bytes of SA/ISA */
 } ctx_t;
+
+static inline uint64_t idx_at(const void *a, uint32_t isz, uint64_t k) {
+  return isz == 4 ? ((const uint32_t *)a)[k] : ((const uint64_t *)a)[k];
+}
+
+/* vec_uchar::operator[] (longSA.h:34-39) */
+static uint64_t lcp_exact(const orc_index *ix, uint64_t k, orc_counters *c) {
+  const uint8_t v = ix->L8[k];
+  if (v != 255) return v;
+  if (c) c->ovf_lookups++;
+  uint64_t lo = 0, hi = ix->n_ovf;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) / 2;
+    if (ix->ovf[2 * mid] < k) lo = mid + 1; else hi = mid;
+  }
+  return ix->ovf[2 * lo + 1];
+}
 
 static inline void tick(uint64_t *loads, uint64_t *lines, uint64_t *last,
                         uint64_t byte_addr) {
@@ -235,11 +252,11 @@ static inline void tick(uint64_t *loads, uint64_t *lines, uint64_t *last,
 }
 static inline uint64_t SAat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->sa_loads, &x->c->sa_lines, &x->c->last_sa, k * x->isz);
-  return x->ix->SA[k];
+  return idx_at(x->ix->SA, x->isz, k);
 }
 static inline uint64_t ISAat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->isa_loads, &x->c->isa_lines, &x->c->last_isa, k * x->isz);
-  return x->ix->ISA[k];
+  return idx_at(x->ix->ISA, x->isz, k);
 }
 static inline int64_t Tat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->ref_loads, &x->c->ref_lines, &x->c->last_ref, k);
@@ -247,7 +264,7 @@ static inline int64_t Tat(const ctx_t *x, uint64_t k) {
 }
 static inline uint64_t LCPat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->lcp_loads, &x->c->lcp_lines, &x->c->last_lcp, k);
-  return x->ix->LCP[k];
+  return lcp_exact(x->ix, k, x->c);
 }
 
 typedef struct { uint64_t depth, start, end; } ival_t;   /* longSA.h:64-75 */
@@ -347,7 +364,7 @@ static void emit(sink_t *s, uint64_t ref, uint64_t q, uint64_t len) {
 static ctx_t mkctx(const orc_index *ix, orc_counters *c) {
   ctx_t x;
   x.ix = ix; x.c = c;
-  x.isz = ix->N <= 0xFFFFFFFFull ? 4 : 8;
+  x.isz = ix->idx_bytes == 4 ? 4 : 8;
   return x;
 }
 
@@ -670,7 +687,7 @@ int orc_mappability(const orc_index *ix, uint8_t *out) {
   uint64_t *ml = (uint64_t *)malloc(N * 8);
   if (!ml) return -1;
   for (uint64_t i = 0; i < N; ++i) {
-    ml[i] = ix->LCP[i] + 1;
+    ml[i] = lcp_exact(ix, i, NULL) + 1;
     if (i && ml[i - 1] < ml[i]) ml[i - 1] = ml[i];
   }
   out[0] = 0; out[1] = 0;          /* 2 junk bytes (longSA.cpp:617) */
@@ -678,8 +695,8 @@ int orc_mappability(const orc_index *ix, uint8_t *out) {
   for (uint32_t chrom = 0; chrom < ix->n_seq; chrom += 2) {
     const uint64_t sp = ix->startpos[chrom], sz = ix->sizes[chrom];
     for (uint64_t i = 0; i < sz; ++i) {
-      const uint64_t sapos = ix->ISA[i + sp];
-      const uint64_t rcsapos = ix->ISA[sp + 2 * sz - i];
+      const uint64_t sapos = idx_at(ix->ISA, ix->idx_bytes, i + sp);
+      const uint64_t rcsapos = idx_at(ix->ISA, ix->idx_bytes, sp + 2 * sz - i);
       if (ml[sapos] + i >= sz) ml[sapos] = 0;
       if (ml[rcsapos] >= i) ml[rcsapos] = 0;
       out[w++] = (uint8_t)(ml[rcsapos] < 255 ? ml[rcsapos] : 255);
@@ -987,6 +1004,7 @@ uint64_t orc_map_only(const orc_index *ix, const uint8_t *reads, uint32_t L,
       ctr->isa_loads += jobs[t].ctr.isa_loads; ctr->isa_lines += jobs[t].ctr.isa_lines;
       ctr->ref_loads += jobs[t].ctr.ref_loads; ctr->ref_lines += jobs[t].ctr.ref_lines;
       ctr->lcp_loads += jobs[t].ctr.lcp_loads; ctr->lcp_lines += jobs[t].ctr.lcp_lines;
+      ctr->ovf_lookups += jobs[t].ctr.ovf_lookups;
     }
   }
   free(jobs);

@@ -53,7 +53,13 @@ void orc_build_lcp(const uint8_t *T, uint64_t N, const uint64_t *SA,
 typedef struct {
   uint64_t N, logN;
   const uint8_t *T;
-  const uint64_t *SA, *ISA, *LCP;  /* LCP exact (vec_uchar::operator[]) */
+  const void *SA, *ISA;   /* idx_bytes-wide elements (ANINT, size.h:33-38) */
+  uint32_t idx_bytes;     /* 4 or 8 */
+  /* vec_uchar (longSA.h:18-61): u8 vector, 255 -> lower_bound in the
+   * {idx, val} overflow table sorted by idx */
+  const uint8_t *L8;
+  const uint64_t *ovf;
+  uint64_t n_ovf;
   uint32_t n_seq;
   const uint64_t *startpos, *sizes;
 } orc_index;
@@ -66,6 +72,8 @@ typedef struct {
   uint64_t sa_loads, isa_loads, ref_loads, lcp_loads;
   uint64_t sa_lines, isa_lines, ref_lines, lcp_lines;
   uint64_t last_sa, last_isa, last_ref, last_lcp;
+  uint64_t ovf_lookups;   /* vec_uchar overflow lower_bounds (not on the
+                             device path: it compares min(LCP,255)) */
 } orc_counters;
 
 typedef struct { uint64_t ref, query, len; } orc_match;  /* longSA.h:78-92 */

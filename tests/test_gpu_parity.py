@@ -214,8 +214,34 @@ def test_mid_genome_pipeline_equals_oracle(mid, tmp_path):
     synth.make_bins(g, 16, bins_path)
     synth.write_index_side_files(str(tmp_path), g)
     cs_path = str(tmp_path / "chrom_sizes.txt")
-    pipe, starts = make_pipe(dix, 150, 2500, bins_path, cs_path)
+    pipe, starts = make_pipe(dix, 150, 6000, bins_path, cs_path)
+    # per-pair smashMEM output and first-wins keep flags vs the oracle
+    counts, st = run_pipeline(pipe, reads, len(starts), batch=6000)
+    nk, keep, hits = pipe.peek(6000)
+    mapbin = oix.mappability()
+    offs = np.cumsum([0] + [int(x) for x in oix.sizes[0::2]][:-1]).astype(np.uint32)
+    small = [1 if ("_gl000" in c or "chrM" in c) else 0 for c in oix.contigs]
+    seen = set()
+    for q in range(6000):
+        hs = []
+        for m in (0, 1):
+            P = reads[2 * q + m].tobytes()
+            h, _ = oix.resolve(P, oix.search(P))
+            for x in h:
+                O.tag(x, offs, mapbin, small[x.tid])
+            hs.append(h)
+        exp = O.smash_pair(hs[0], hs[1])
+        if exp is None:
+            assert nk[q] == -1, q
+            continue
+        got = [(int(w >> 48), int(w & 0xFFFFFFFFFFFF)) for w in hits[q, :max(nk[q], 0)]]
+        assert got == exp, (q, got, exp)
+        k = tuple(exp)
+        assert keep[q] == (k not in seen), (q, exp, keep[q])
+        seen.add(k)
+    c1 = counts
     counts, st = run_pipeline(pipe, reads, len(starts), batch=2500)
+    assert counts.tolist() == c1.tolist()
     op = O.Pipeline(oix, oix.mappability(), load_chrom_sizes(cs_path), starts)
     assert op.run(reads, threads=8) == 0
     assert counts.tolist() == op.counts.tolist()
