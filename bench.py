@@ -1,0 +1,291 @@
+#!/usr/bin/env python
+"""bench.py -- reads/s mapped + binned on MI355X (BASELINE.json metric).
+
+Workload (default --config c3, the 1-GPU configuration BASELINE.json's metric
+is quoted on: "hg19, 150 bp", sample_bins/50000): the hg19-shaped synthetic
+genome (tools/synth.py: hg19 contig lengths, N runs over the assembly gaps,
+repeats; 3.1 Gbp, doubled text N = 6.19e9, 64-bit SA/ISA) is indexed ON THE
+DEVICE and kept resident in HBM; every rank holds its own batch of synthetic
+150 bp SMASH read pairs in HBM.  One step = one complete independent run of
+the hot path over that batch (fresh pair-key set and adjacent-dup state):
+MAM search -> resolve -> mappability tag -> smashMEM filters -> global pair
+de-dup -> varbin adjacent de-dup -> bin counts (+ the multi-GPU exchanges and
+the RCCL all-reduce of the count vector when N > 1).  value = reads (mates)
+processed by all ranks / max-over-ranks wall time of the K timed steps.
+
+Also reported: `roofline` of the dominant kernel (k_mam: algorithmic bytes =
+64 B x distinct line transitions per read, counted by the oracle on a sample
+of the same reads, over the HIP-event-timed kernel duration) and
+`cpu_baseline` (the C oracle of the whole chain on the host cores, rank 0,
+N = 1, bounded sample).  The bench also checks that the device's bin counts on
+that sample are identical to the oracle's.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in ("smash-paper_amd", "tools", "oracle"):
+    sys.path.insert(0, os.path.join(ROOT, _p))
+
+import numpy as np  # noqa: E402
+
+METRIC = ("reads/sec mapped+binned (hg19, 150 bp) at 1/2/4/8 MI355X; "
+          "bit-exact bin counts")
+
+CONFIGS = {
+    # BASELINE.json configs[2]: hg19, 150 bp, sample_bins/50000 (metric's config)
+    "c3": dict(genome="hg19", read_len=150, pairs=2_000_000, bins="50000", seed=3,
+               workload="C3 hg19-shaped 150 bp SMASH reads, sample_bins/50000"),
+    # configs[1]: hg19 1M x 100 bp, sample_bins/100000 (synthesized 2-way split)
+    "c2": dict(genome="hg19", read_len=100, pairs=500_000, bins="100000", seed=2,
+               workload="C2 hg19-shaped 1M x 100 bp SMASH reads, sample_bins/100000"),
+    # configs[0]-like plumbing on the chr21-sized genome (bins split 10-way)
+    "c1": dict(genome="chr21", read_len=100, pairs=500_000, bins="500000", seed=1,
+               workload="C1-shaped chr21-sized genome, 100 bp, sample_bins/500000"),
+    # quick functional run
+    "mid": dict(genome="mid", read_len=150, pairs=200_000, bins="synthetic", seed=2,
+                workload="3.2 Mbp synthetic genome, 150 bp (functional check)"),
+}
+
+
+def log(*a):
+    print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
+
+
+def chrom_sizes_of(contigs):
+    out, n = {}, 0
+    for name, s in contigs:
+        if "_" in name:
+            continue
+        out[name] = n
+        n += len(s)
+    return out
+
+
+def bin_starts_for(cfg, contigs, tmpdir):
+    import synth
+    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    if cfg["bins"] == "50000":
+        path = src
+    elif cfg["bins"] in ("100000", "500000"):
+        path = os.path.join(tmpdir, "bins_%s.txt" % cfg["bins"])
+        synth.split_bins(src, 2 if cfg["bins"] == "100000" else 10, path)
+    else:
+        path = os.path.join(tmpdir, "bins_syn.txt")
+        synth.make_bins(contigs, 64, path)
+    return np.array([int(l.split("\t")[2]) for l in open(path)], np.int64)
+
+
+def chrom_sizes_for(cfg, contigs):
+    cs = chrom_sizes_of(contigs)
+    if cfg["genome"] == "chr21":    # hg19 offset so that hg19 bins apply (§8d C1)
+        cs = {"chr21": 2781598825}
+    return cs
+
+
+def make_reads(contigs, cfg, n_pairs, seed):
+    import smashgpu as S
+    import synth
+    r1, r2 = synth.make_reads(contigs, n_pairs, cfg["read_len"], seed=seed)
+    reads = np.empty((2 * n_pairs, cfg["read_len"]), np.uint8)
+    reads[0::2] = r1
+    reads[1::2] = r2
+    return S.prepare_reads(reads)
+
+
+def host_index(S, O, dix, T, sp, sz, names):
+    """Download the device index into the oracle's host layout (cpu leg)."""
+    i = dix.info
+    N = i.N
+    dt = np.uint32 if i.idx_bytes == 4 else np.uint64
+    SA = S.download(i.d_sa, N * i.idx_bytes, dt)
+    ISA = S.download(i.d_isa, N * i.idx_bytes, dt)
+    L8 = S.download(i.d_lcp8, N)
+    ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
+    mp = S.download(i.d_map, i.map_bytes)
+    return O.Index(T, sp, sz, names, SA=SA, ISA=ISA, L8=L8, ovf=ovf), mp
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--pairs", type=int, default=0, help="pairs per rank per step")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.pairs:
+        cfg["pairs"] = args.pairs
+
+    import torch
+    import smashgpu as S
+    import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    t0 = time.time()
+    contigs = synth.make_genome(cfg["genome"])
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    log("genome %s: %.3f Gbp, N=%d (%.1fs)" % (cfg["genome"], sum(len(s) for _, s in contigs) / 1e9,
+                                               len(T), time.time() - t0))
+    dix = S.Index.create(T, sp, sz, names, device=local)
+    log("device index: %.1f s, %.1f GB in HBM, idx_bytes=%d, lcp overflow %d"
+        % (dix.info.build_seconds, dix.info.device_bytes / 1e9, dix.info.idx_bytes,
+           dix.info.n_lcp_overflow))
+    tmpdir = tempfile.mkdtemp()
+    starts = bin_starts_for(cfg, contigs, tmpdir)
+    cs = chrom_sizes_for(cfg, contigs)
+    P = cfg["pairs"]
+    L = cfg["read_len"]
+    reads_h = make_reads(contigs, cfg, P, cfg["seed"] * 1000 + rank)
+    d_reads = torch.from_numpy(reads_h).to(dev)
+    log("reads: %d pairs x %d bp per rank (%.1fs since start)" % (P, L, time.time() - t0))
+    pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P)
+    counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+
+    if world > 1:
+        from dist import ShardedCounter
+        sc = ShardedCounter(pipe, rank, world, dev)
+
+    def step(i):
+        counts.zero_()
+        if world == 1:
+            pipe.reset()
+            pipe.count_batch(d_reads, P, counts)
+        else:
+            sc.reset()
+            sc.step(d_reads, P, 0, counts)
+            dist.all_reduce(counts)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ref_counts = counts.cpu().numpy().copy()
+    st0 = pipe.stats()
+    if st0.error:
+        raise SystemExit("pipeline data error: %s" % S.ERRORS.get(st0.error, st0.error))
+    pipe.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    mam_ms, launches, mam_reads = pipe.profile_read()
+    pipe.profile(False)
+    st = pipe.stats()
+    same = bool(np.array_equal(counts.cpu().numpy(), ref_counts)) if args.warmup else True
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_reads = 2 * P * world * args.steps
+    value = total_reads / el
+    log("timed %d steps: %.3f s -> %.3e reads/s; k_mam %.1f ms/launch; stats %s; "
+        "deterministic=%s" % (args.steps, el, value, mam_ms / max(launches, 1),
+                              st.as_dict(), same))
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "reads/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64 (integer)",
+        "data": "synthetic (tools/synth.py genome + SMASH reads, seeded)",
+        "config": {"workload": cfg["workload"], "genome": cfg["genome"],
+                   "genome_bp": int(sum(len(s) for _, s in contigs)),
+                   "text_N": int(dix.info.N), "pairs_per_rank": P, "read_len": L,
+                   "reads_per_step": 2 * P * world, "bins": int(len(starts)),
+                   "parallelism": "dp%d: pair shards, all_to_all key de-dup, "
+                                  "all_gather tails, all_reduce counts" % world
+                   if world > 1 else "single GPU",
+                   "index_build_s": round(dix.info.build_seconds, 2),
+                   "index_hbm_gb": round(dix.info.device_bytes / 1e9, 2)},
+    }
+
+    # ---- roofline + cpu baseline (rank 0) -------------------------------------
+    avg_ms = mam_ms / max(launches, 1)
+    reads_per_launch = mam_reads / max(launches, 1)
+    roof = None
+    cpu = None
+    if rank == 0:
+        import oracle as O
+        t2 = time.time()
+        oix, mp = host_index(S, O, dix, T, sp, sz, names)
+        log("host copy of the index for the oracle: %.1fs" % (time.time() - t2))
+        # algorithmic bytes per read: 64 B x line transitions (same algorithm)
+        ns = min(4000, 2 * P)
+        _, ctr = O.map_only(oix, reads_h[:ns], threads=min(16, os.cpu_count() or 1), count=True)
+        lines = ctr.sa_lines + ctr.isa_lines + ctr.ref_lines + ctr.lcp_lines
+        b_read = 64.0 * lines / ns
+        achieved = reads_per_launch * b_read / (avg_ms / 1e3) / 1e9
+        roof = {"bound": "hbm", "kernel": "k_mam", "achieved": round(achieved, 2),
+                "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
+                "traffic": None, "bytes_per_read": round(b_read, 1),
+                "avg_kernel_ms": round(avg_ms, 3), "reads_per_launch": int(reads_per_launch),
+                "lines_per_read": {"sa": ctr.sa_lines / ns, "isa": ctr.isa_lines / ns,
+                                   "ref": ctr.ref_lines / ns, "lcp": ctr.lcp_lines / ns}}
+        pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
+        if os.path.exists(pmc):
+            try:
+                roof["traffic"] = json.load(open(pmc)).get("k_mam_bytes_per_launch")
+                roof["traffic_source"] = os.path.relpath(pmc, ROOT)
+            except Exception:
+                pass
+        if world == 1 and not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            op = O.Pipeline(oix, mp, cs, starts)
+            # calibrate, then a bounded sample of ~cpu_seconds
+            n0 = min(P, 256 * threads)
+            t3 = time.perf_counter()
+            op.run(reads_h[:2 * n0], threads=threads)
+            dt0 = time.perf_counter() - t3
+            n1 = int(min(P, max(n0, n0 * args.cpu_seconds / max(dt0, 1e-3))))
+            op = O.Pipeline(oix, mp, cs, starts)
+            t3 = time.perf_counter()
+            err = op.run(reads_h[:2 * n1], threads=threads)
+            dt = time.perf_counter() - t3
+            # device on the same sample must give the same counts
+            pipe.reset()
+            c2 = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+            pipe.count_batch(d_reads[:2 * n1], n1, c2)
+            dev_counts = c2.cpu().numpy().astype(np.uint64)
+            exact = bool(err == 0 and np.array_equal(dev_counts, op.counts))
+            cpu = {"value": 2 * n1 / dt, "unit": "reads/s", "cores": threads,
+                   "kind": "port",
+                   "sample": "%d pairs (%d reads) of the same batch, whole chain "
+                             "(oracle/smash_oracle.c orc_run_pairs), %.1f s" % (n1, 2 * n1, dt),
+                   "bin_counts_identical_to_device": exact}
+            log("cpu baseline: %.3e reads/s on %d threads; device==oracle counts: %s"
+                % (cpu["value"], threads, exact))
+    out["roofline"] = roof
+    out["cpu_baseline"] = cpu
+    out["deterministic_counts"] = same
+    out["stats_last_step"] = st.as_dict()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -193,6 +193,14 @@ typedef struct {
 /* Synchronises the pipeline's last stream. */
 int smash_pipeline_stats(smash_pipeline *p, smash_stats *out);
 
+/* Kernel timing for the roofline: when enabled, HIP events are recorded on
+ * the launch stream around the search kernel (k_mam) of every phase_map /
+ * count_batch; _read synchronises and returns the summed milliseconds, the
+ * number of launches and of reads searched since the last enable. */
+int smash_pipeline_profile(smash_pipeline *p, int enable);
+int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
+                                uint64_t *launches, uint64_t *reads);
+
 /* Start a new run: clears the pair-key set, the carried adjacent-dup state
  * and the stats (a fresh smashMEM.py + varbin.py invocation). */
 int smash_pipeline_reset(smash_pipeline *p, void *stream);

@@ -530,23 +530,34 @@ typedef struct {
   uint8_t nb; uint16_t boff[16], blen[16];
 } aln_t;
 
-static const aln_t *g_cmp_base;
-static int to_merge_cmp(const void *pa, const void *pb) {
-  const aln_t *a = g_cmp_base + *(const uint32_t *)pa;
-  const aln_t *b = g_cmp_base + *(const uint32_t *)pb;
+/* comparators take the alignment base explicitly (thread-safe; the worker
+ * threads of orc_run_pairs resolve concurrently) */
+static int to_merge_cmp(const aln_t *base, uint32_t ia, uint32_t ib) {
+  const aln_t *a = base + ia;
+  const aln_t *b = base + ib;
   if (a->rc != b->rc) return a->rc < b->rc ? -1 : 1;
   if (a->seq_index != b->seq_index) return a->seq_index < b->seq_index ? -1 : 1;
   if (a->pos != b->pos) return a->pos < b->pos ? -1 : 1;
   if (a->prefix != b->prefix) return a->prefix < b->prefix ? -1 : 1;
   return 0;
 }
-static int to_print_cmp(const void *pa, const void *pb) {
-  const aln_t *a = g_cmp_base + *(const uint32_t *)pa;
-  const aln_t *b = g_cmp_base + *(const uint32_t *)pb;
+static int to_print_cmp(const aln_t *base, uint32_t ia, uint32_t ib) {
+  const aln_t *a = base + ia;
+  const aln_t *b = base + ib;
   if (a->qpos != b->qpos) return a->qpos < b->qpos ? -1 : 1;
   if (a->rc != b->rc) return a->rc < b->rc ? -1 : 1;
   /* ties only between members of one diagonal group: equal seq/pos */
   return (a->n_matches > b->n_matches) ? -1 : (a->n_matches < b->n_matches);
+}
+
+static void isort(uint32_t *idx, uint32_t n, const aln_t *base,
+                  int (*cmp)(const aln_t *, uint32_t, uint32_t)) {
+  for (uint32_t i = 1; i < n; ++i) {
+    uint32_t t = idx[i];
+    uint32_t j = i;
+    while (j > 0 && cmp(base, t, idx[j - 1]) < 0) { idx[j] = idx[j - 1]; --j; }
+    idx[j] = t;
+  }
 }
 
 int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
@@ -590,8 +601,7 @@ int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
   }
   if (na == 0) return 0;
   for (uint32_t i = 0; i < na; ++i) idx[i] = i;
-  g_cmp_base = al;
-  qsort(idx, na, sizeof(uint32_t), to_merge_cmp);
+  isort(idx, na, al, to_merge_cmp);
   /* merge equal diagonals into one CIGAR (query.cpp:252-289) */
   uint32_t gstart = 0;
   char cig[ORC_CIGAR_MAX];
@@ -643,8 +653,7 @@ int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
   }
   /* to_print order (query.cpp:290-303) */
   for (uint32_t i = 0; i < na; ++i) idx[i] = i;
-  g_cmp_base = al;
-  qsort(idx, na, sizeof(uint32_t), to_print_cmp);
+  isort(idx, na, al, to_print_cmp);
   *best_tid = (uint32_t)(al[idx[0]].seq_index / 2);
   *best_pos = al[idx[0]].pos;
   uint32_t nh = 0;

@@ -57,6 +57,10 @@ struct smash_pipeline {
   unsigned long long *d_owner = nullptr;  // per-owner counters (<= 64 ranks)
   uint64_t n_pairs = 0, n_export = 0;
   hipStream_t last = nullptr;
+  // profiling (smash_pipeline_profile)
+  bool prof = false;
+  std::vector<hipEvent_t> ev;     // pairs: [2i] before, [2i+1] after k_mam
+  uint64_t n_ev = 0, prof_reads = 0;
 };
 
 namespace smash {
@@ -351,7 +355,7 @@ __global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *
   if (full) fl = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (a) atomicAdd(&stats[S_KEYPAIRS], a);
+    if (a && mode == 0) atomicAdd(&stats[S_KEYPAIRS], a);
     if (b) atomicAdd(&stats[S_DUPEPAIRS], b);
     if (fl) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
   }
@@ -503,15 +507,17 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_hash = dalloc<uint64_t>(2 * P);
     p->d_keep = dalloc<uint8_t>(P);
     p->d_first = dalloc<uint8_t>(P);
+    // sort buffers also serve the owner side of the multi-GPU de-dup,
+    // which may receive more keys than one batch holds
     for (int i = 0; i < 2; ++i) {
-      p->d_k[i] = dalloc<uint64_t>(P);
-      p->d_v[i] = dalloc<uint32_t>(P);
+      p->d_k[i] = dalloc<uint64_t>(2 * P);
+      p->d_v[i] = dalloc<uint32_t>(2 * P);
     }
     size_t a = 0, b = 0;
     {
       hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
       hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
-      SMASH_HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, a, kb, vb, P));
+      SMASH_HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, a, kb, vb, 2 * P));
     }
     p->d_posoff = dalloc<uint32_t>(P + 1);
     p->d_cnt = dalloc<uint32_t>(P);
@@ -546,6 +552,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
 extern "C" void smash_pipeline_free(smash_pipeline *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
+  for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
                   (void *)p->d_bins, (void *)p->d_match, (void *)p->d_nmatch,
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
@@ -568,10 +575,25 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
   p->n_pairs = n_pairs;
   if (!n_pairs) return SMASH_OK;
   SMASH_HIP(hipSetDevice(p->device));
+  if (p->prof) {
+    if (2 * p->n_ev + 2 > p->ev.size()) {
+      for (int k = 0; k < 64; ++k) {
+        hipEvent_t e;
+        SMASH_HIP(hipEventCreate(&e));
+        p->ev.push_back(e);
+      }
+    }
+    SMASH_HIP(hipEventRecord(p->ev[2 * p->n_ev], s));
+  }
   rc = smash_map_batch(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len,
                        nullptr, p->read_len, 2 * n_pairs, p->d_match, p->slots,
                        p->d_nmatch, stream);
   if (rc) return rc;
+  if (p->prof) {
+    SMASH_HIP(hipEventRecord(p->ev[2 * p->n_ev + 1], s));
+    ++p->n_ev;
+    p->prof_reads += 2 * n_pairs;
+  }
   k_post<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
       post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_nk, p->d_nmajor,
       p->d_hits, p->d_hash, p->d_stats);
@@ -749,8 +771,8 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
 extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv,
                                  uint64_t n_recv, uint8_t *d_flags, void *stream) {
   if (!p || (n_recv && (!d_recv || !d_flags))) return SMASH_ERR_ARG;
-  if (n_recv > p->max_pairs) {
-    set_error("smash_dedup_owner: more keys than cfg.max_pairs");
+  if (n_recv > 2 * p->max_pairs) {
+    set_error("smash_dedup_owner: more keys than 2 * cfg.max_pairs");
     return SMASH_ERR_ARG;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -825,5 +847,30 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   static const int64_t init[2] = {-1, -1};
   SMASH_HIP(hipMemcpyAsync(p->d_prev, init, 16, hipMemcpyHostToDevice, s));
   SMASH_HIP(hipStreamSynchronize(s));
+  return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_profile(smash_pipeline *p, int enable) {
+  if (!p) return SMASH_ERR_ARG;
+  p->prof = enable != 0;
+  p->n_ev = 0;
+  p->prof_reads = 0;
+  return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
+                                           uint64_t *launches, uint64_t *reads) {
+  if (!p) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  double ms = 0;
+  for (uint64_t i = 0; i < p->n_ev; ++i) {
+    SMASH_HIP(hipEventSynchronize(p->ev[2 * i + 1]));
+    float t = 0;
+    SMASH_HIP(hipEventElapsedTime(&t, p->ev[2 * i], p->ev[2 * i + 1]));
+    ms += t;
+  }
+  if (search_ms) *search_ms = ms;
+  if (launches) *launches = p->n_ev;
+  if (reads) *reads = p->prof_reads;
   return SMASH_OK;
 }

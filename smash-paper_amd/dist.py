@@ -1,0 +1,82 @@
+"""Multi-GPU driver of one read -> bin-count batch (one process per GPU).
+
+Reads shard by contiguous pair ranges: in every step rank r owns global pairs
+[base + r*B, base + (r+1)*B), so the global name order (samtools sort -n,
+SURVEY.md Appendix A.11) is (step, rank, pair).  Everything is per-rank except
+the two dependencies the reference's sequential scripts carry:
+
+* smashMEM.py's global first-wins pair de-dup (smashMEM.py:149,217-228): the
+  in-batch-first keys are sent to owner rank = hash % world (all_to_all), the
+  owner decides first-wins by global pair index against its persistent key set
+  and returns one flag per key (all_to_all back);
+* varbin.py's adjacent de-dup (varbin.py:56-58) compares with the previous
+  emitted position: all_gather of every rank's {count, last pos0} gives each
+  rank the last position emitted before its shard.
+
+Bin counts stay per rank until the caller's all_reduce.
+`pipe` is a smashgpu.Pipeline (device tensors, RCCL) or any object with the
+same phase_* methods (the CPU tests drive this code over gloo with an
+oracle-backed stand-in).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class ShardedCounter:
+    def __init__(self, pipe, rank, world, device, group=None):
+        self.pipe = pipe
+        self.rank = rank
+        self.world = world
+        self.device = device
+        self.group = group
+        self.carried = torch.full((1,), -1, dtype=torch.int64, device=device)
+        self.max_pairs = pipe.max_pairs
+
+    def reset(self):
+        self.pipe.reset()
+        self.carried.fill_(-1)
+
+    def step(self, d_reads, n_pairs, step_base, d_counts):
+        """One batch: this rank's n_pairs pairs start at global index
+        step_base + rank * n_pairs (every rank passes the same n_pairs)."""
+        dev, W, r = self.device, self.world, self.rank
+        p = self.pipe
+        p.phase_map(d_reads, n_pairs)
+        send = torch.empty((max(n_pairs, 1), 3), dtype=torch.int64, device=dev)
+        cnt = p.phase_export(W, step_base + r * n_pairs, send)
+        sc = torch.as_tensor(cnt, dtype=torch.int64).to(dev)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        rcv = rc.cpu().tolist()
+        snd = [int(x) for x in cnt]
+        n_recv = sum(rcv)
+        recv = torch.empty((max(n_recv, 1), 3), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv[:n_recv], send[:sum(snd)], output_split_sizes=rcv,
+                               input_split_sizes=snd, group=self.group)
+        flags = torch.empty(max(n_recv, 1), dtype=torch.uint8, device=dev)
+        p.dedup_owner(recv, n_recv, flags)
+        back = torch.empty(max(sum(snd), 1), dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(back[:sum(snd)], flags[:n_recv], output_split_sizes=snd,
+                               input_split_sizes=rcv, group=self.group)
+        p.phase_import(back)
+        tail = torch.empty(2, dtype=torch.int64, device=dev)
+        p.phase_positions(tail)
+        tails = torch.empty((W, 2), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(tails, tail, group=self.group)
+        prev = self._prev(tails[:r], self.carried)
+        p.phase_bin(prev, d_counts)
+        self.carried = self._prev(tails, self.carried)
+
+    @staticmethod
+    def _prev(tails, carried):
+        """last pos0 of the latest non-empty shard among `tails` (rank order),
+        else the carried value -- on the device, no host sync."""
+        if tails.shape[0] == 0:
+            return carried.clone()
+        nonempty = tails[:, 0] > 0
+        idx = torch.arange(tails.shape[0], device=tails.device)
+        last = torch.where(nonempty, idx, torch.full_like(idx, -1)).max()
+        pick = tails[last.clamp(min=0), 1].reshape(1)
+        return torch.where(last >= 0, pick, carried)

@@ -39,6 +39,7 @@ EXPORTS = [
     "smash_phase_map", "smash_phase_export", "smash_dedup_owner",
     "smash_phase_import", "smash_phase_positions", "smash_phase_bin",
     "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_peek",
+    "smash_pipeline_profile", "smash_pipeline_profile_read",
 ]
 
 
@@ -113,6 +114,8 @@ def lib():
     L.smash_pipeline_stats.argtypes = [vp, C.POINTER(Stats)]
     L.smash_pipeline_reset.argtypes = [vp, vp]
     L.smash_pipeline_peek.argtypes = [vp, i32p, u8p, u64p, u64p]
+    L.smash_pipeline_profile.argtypes = [vp, C.c_int]
+    L.smash_pipeline_profile_read.argtypes = [vp, C.POINTER(C.c_double), u64p, u64p]
     _LIB = L
     return L
 
@@ -363,6 +366,18 @@ class Pipeline:
         s = Stats()
         check(lib().smash_pipeline_stats(self.h, C.byref(s)), "smash_pipeline_stats")
         return s
+
+    def profile(self, enable=True):
+        check(lib().smash_pipeline_profile(self.h, int(enable)), "smash_pipeline_profile")
+
+    def profile_read(self):
+        """(summed k_mam milliseconds, launches, reads searched)"""
+        ms = C.c_double()
+        n = C.c_uint64()
+        r = C.c_uint64()
+        check(lib().smash_pipeline_profile_read(self.h, C.byref(ms), C.byref(n), C.byref(r)),
+              "smash_pipeline_profile_read")
+        return ms.value, n.value, r.value
 
     def peek(self, n_pairs):
         nk = np.zeros(n_pairs, np.int32)
