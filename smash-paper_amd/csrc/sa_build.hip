@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -28,6 +29,20 @@ namespace smash {
 namespace {
 
 constexpr int kBlock = 256;
+
+double wall() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+// SMASH_VERBOSE=1: per-phase timings of the device index build on stderr
+void vlog(const char *fmt, double t0, uint64_t a = 0, uint64_t b = 0) {
+  static const bool on = getenv("SMASH_VERBOSE") && getenv("SMASH_VERBOSE")[0] == '1';
+  if (!on) return;
+  fprintf(stderr, "[smash-index %7.2fs] ", wall() - t0);
+  fprintf(stderr, fmt, (unsigned long long)a, (unsigned long long)b);
+  fprintf(stderr, "\n");
+  fflush(stderr);
+}
 
 __global__ void k_hist256(const uint8_t *__restrict__ T, uint64_t N,
                           unsigned long long *cnt) {
@@ -283,6 +298,8 @@ template <class IdxT>
 void build_sa_isa_t(smash_index *ix, hipStream_t s) {
   const uint64_t N = ix->N;
   const uint8_t *T = ix->d_text;
+  const double t0 = wall();
+  vlog("suffix sort: N=%llu idx_bytes=%llu", t0, N, sizeof(IdxT));
   // alphabet
   unsigned long long *d_cnt = dalloc<unsigned long long>(256);
   SMASH_HIPX(hipMemsetAsync(d_cnt, 0, 256 * 8, s));
@@ -322,6 +339,7 @@ void build_sa_isa_t(smash_index *ix, hipStream_t s) {
   }
   SMASH_HIPX(hipMemcpyAsync(d_cnt, boff, 64 * 8, hipMemcpyHostToDevice, s));
   k_bucket_scatter<IdxT><<<gb, kBlock, 0, s>>>(T, N, cmap, base, nb, d_cnt, SA);
+  vlog("buckets: %llu (largest %llu)", t0, nb, maxb);
 
   // 2. per-bucket sort by the next kchars characters
   {
@@ -350,6 +368,7 @@ void build_sa_isa_t(smash_index *ix, hipStream_t s) {
     }
     SMASH_HIPX(hipStreamSynchronize(s));
     dfree(k0); dfree(k1); dfree(v0); dfree(v1); dfree(hd); dfree(st); dfree(temp);
+    vlog("bucket sorts done (%llu chars/key)", t0, uint64_t(kchars));
   }
 
   // 3. prefix doubling over tied suffixes
@@ -428,6 +447,7 @@ void build_sa_isa_t(smash_index *ix, hipStream_t s) {
         SMASH_HIPX(hipMemcpyAsync(&nn, d_nsel, 8, hipMemcpyDeviceToHost, s));
         SMASH_HIPX(hipStreamSynchronize(s));
         std::swap(P, P2);
+        vlog("doubling h=%llu: %llu suffixes still tied", t0, h, nn);
         n_a = nn;
         h *= 2;
       }
@@ -449,10 +469,15 @@ uint32_t *build_lcp32_t(smash_index *ix, hipStream_t s) {
   uint64_t chunk = N / 262144;
   chunk = std::min<uint64_t>(std::max<uint64_t>(chunk, 64), 65536);
   const uint64_t threads = (N + chunk - 1) / chunk;
+  const double t0 = wall();
   k_kasai<IdxT><<<unsigned((threads + 127) / 128), 128, 0, s>>>(
       ix->d_text, N, static_cast<const IdxT *>(ix->d_sa),
       static_cast<const IdxT *>(ix->d_isa), lcp, chunk);
   SMASH_HIPX(hipGetLastError());
+  if (getenv("SMASH_VERBOSE")) {
+    SMASH_HIPX(hipStreamSynchronize(s));
+    vlog("LCP (Kasai, %llu-position chunks)", t0, chunk);
+  }
   return lcp;
 }
 

@@ -63,8 +63,9 @@ class ShardedCounter:
         p.phase_import(back)
         tail = torch.empty(2, dtype=torch.int64, device=dev)
         p.phase_positions(tail)
-        tails = torch.empty((W, 2), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(tails, tail, group=self.group)
+        parts = [torch.empty(2, dtype=torch.int64, device=dev) for _ in range(W)]
+        dist.all_gather(parts, tail, group=self.group)
+        tails = torch.stack(parts)
         prev = self._prev(tails[:r], self.carried)
         p.phase_bin(prev, d_counts)
         self.carried = self._prev(tails, self.carried)

@@ -1,0 +1,95 @@
+"""world_size-2 run of the multi-GPU exchange (smash-paper_amd/dist.py) over
+torch.distributed/gloo on the CPU: the pair-key all_to_all, the tail
+all_gather and the count all_reduce must reproduce the single-process
+chain exactly (global name order = step, rank, pair)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT, gold, interleaved_reads, load_bins, load_chrom_sizes
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, per_rank, steps, out_q):
+    import sys
+    for p in ("oracle", "tools", "tests", "smash-paper_amd"):
+        sys.path.insert(0, os.path.join(ROOT, p))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gzip, tempfile
+    import oracle as O
+    from mock_pipeline import OraclePhasePipeline
+    from dist import ShardedCounter
+    d = tempfile.mkdtemp()
+    fa = os.path.join(d, "tiny.fa")
+    with gzip.open(gold("tiny.fa.gz"), "rb") as f, open(fa, "wb") as g:
+        g.write(f.read())
+    oix = O.Index.from_fasta(fa)
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    pipe = OraclePhasePipeline(oix, oix.mappability(), cs, starts, per_rank)
+    sc = ShardedCounter(pipe, rank, world, torch.device("cpu"))
+    reads = interleaved_reads("s100")
+    counts = torch.zeros(len(starts), dtype=torch.int64)
+    sc.reset()
+    for s in range(steps):
+        base = s * world * per_rank
+        lo = base + rank * per_rank
+        d_reads = torch.from_numpy(reads[2 * lo:2 * (lo + per_rank)].copy())
+        sc.step(d_reads, per_rank, base, counts)
+    dist.all_reduce(counts)
+    st = torch.tensor([pipe.total, pipe.dups, pipe.kept], dtype=torch.int64)
+    dist.all_reduce(st)
+    if rank == 0:
+        out_q.put((counts.numpy().tolist(), st.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,per_rank,steps", [(2, 250, 2), (2, 97, 3)])
+def test_two_rank_exchange_matches_single_process(world, per_rank, steps, tiny_ix):
+    import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per_rank, steps, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue as _queue
+    res = None
+    for _ in range(600):
+        try:
+            res = q.get(timeout=1)
+            break
+        except _queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        if res is None:
+            p.terminate()
+    assert res is not None, [p.exitcode for p in procs]
+    got_counts, got_stats = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = world * per_rank * steps
+    reads = interleaved_reads("s100")[:2 * n]
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    op = O.Pipeline(tiny_ix, tiny_ix.mappability(), cs, starts)
+    assert op.run(reads, threads=4) == 0
+    assert got_counts == op.counts.tolist()
+    assert got_stats == [op.state.total, op.state.dups, op.state.kept]
