@@ -47,6 +47,8 @@ void smash_text_free(uint8_t *text, uint32_t n_seq, uint64_t *startpos,
 
 /* ---- search modes (query.h:126 mum_t) ------------------------------------ */
 #define SMASH_MODE_MAM 1         /* -mumreference / default (longSA.cpp:503) */
+#define SMASH_MODE_MAM_PLAIN 2   /* same matches, the reference's probe
+                                    sequence without the accelerators (A/B) */
 
 /* ========================================================================== */
 /* Index: replaces longSA::longSA (longSA.cpp:94-210) + Sequence (fasta.cpp)  */
@@ -96,6 +98,10 @@ typedef struct {
   const uint8_t *d_map;    /* map.bin image */
   uint64_t device_bytes;   /* total HBM held by the index */
   double build_seconds;    /* wall time of create/load */
+  /* search accelerators (results-preserving):           */
+  uint32_t kmer_k;         /* k of the k-mer -> SA-interval table */
+  const uint8_t *d_uniq;   /* U[x] = min(255, max(LCP[ISA[x]], LCP[ISA[x]+1])) */
+  const uint64_t *d_kmer;  /* 4^k x {lo, hi}; lo > hi = absent */
 } smash_index_info;
 int smash_index_query(const smash_index *ix, smash_index_info *out);
 

@@ -37,7 +37,16 @@ class OrcCounters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "sa_loads", "isa_loads", "ref_loads", "lcp_loads",
         "sa_lines", "isa_lines", "ref_lines", "lcp_lines",
-        "last_sa", "last_isa", "last_ref", "last_lcp", "ovf_lookups")]
+        "last_sa", "last_isa", "last_ref", "last_lcp", "ovf_lookups",
+        "kt_lines", "u_lines", "last_kt", "last_u")]
+
+    def lines(self):
+        return (self.sa_lines + self.isa_lines + self.ref_lines + self.lcp_lines
+                + self.kt_lines + self.u_lines)
+
+
+class OrcAccel(C.Structure):
+    _fields_ = [("U", u8p), ("KT", u64p), ("K", C.c_uint32)]
 
 
 class OrcMatch(C.Structure):
@@ -110,6 +119,16 @@ def lib():
                                    C.c_uint64, C.c_uint64, C.c_uint32, C.c_int,
                                    C.POINTER(OrcCounters)]
         L.orc_map_only.restype = C.c_uint64
+        L.orc_accel_k.argtypes = [C.c_uint64]
+        L.orc_accel_k.restype = C.c_uint32
+        L.orc_build_accel.argtypes = [C.POINTER(OrcIndex), C.c_uint32, u8p, u64p]
+        L.orc_mam_fast.argtypes = [C.POINTER(OrcIndex), C.POINTER(OrcAccel), u8p,
+                                   C.c_uint32, C.c_uint32, C.POINTER(OrcMatch),
+                                   C.c_uint32, C.POINTER(OrcCounters)]
+        L.orc_map_only_fast.argtypes = [C.POINTER(OrcIndex), C.POINTER(OrcAccel), u8p,
+                                        C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
+                                        C.c_int, C.POINTER(OrcCounters)]
+        L.orc_map_only_fast.restype = C.c_uint64
         _LIB = L
     return _LIB
 
@@ -238,6 +257,26 @@ class Index:
             cap = n
         return [(out[i].ref, out[i].query, out[i].len) for i in range(n)]
 
+    def accel(self, U=None, KT=None, K=None):
+        """Search accelerators (built here, or given, e.g. from the device)."""
+        if U is None:
+            K = lib().orc_accel_k(self.N)
+            U = np.zeros(self.N + 64, np.uint8)
+            KT = np.zeros(2 << (2 * K), np.uint64)
+            lib().orc_build_accel(C.byref(self.c), K, _p(U, u8p), _p(KT, u64p))
+        self._U = np.ascontiguousarray(U, np.uint8)
+        self._KT = np.ascontiguousarray(KT, np.uint64)
+        self.acc = OrcAccel(_p(self._U, u8p), _p(self._KT, u64p), int(K))
+        return self._U, self._KT, int(K)
+
+    def search_fast(self, read: bytes, min_len=20, counters=None):
+        P = np.frombuffer(read, np.uint8)
+        out = (OrcMatch * 512)()
+        n = lib().orc_mam_fast(C.byref(self.c), C.byref(self.acc), _p(P, u8p), len(P),
+                               min_len, out, 512,
+                               C.byref(counters) if counters is not None else None)
+        return [(out[i].ref, out[i].query, out[i].len) for i in range(min(n, 512))]
+
     def resolve(self, read: bytes, matches):
         P = np.frombuffer(read, np.uint8)
         m = (OrcMatch * max(1, len(matches)))()
@@ -350,6 +389,16 @@ class Pipeline:
             lib().orc_dedup_free(self.dedup)
         except Exception:
             pass
+
+
+def map_only_fast(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=False):
+    """Accelerated search (device algorithm) on the CPU; counters = its lines."""
+    reads = np.ascontiguousarray(reads, np.uint8)
+    ctr = OrcCounters() if count else None
+    n = lib().orc_map_only_fast(C.byref(ix.c), C.byref(ix.acc), _p(reads, u8p),
+                                reads.shape[1], reads.shape[1], reads.shape[0], min_len,
+                                threads, C.byref(ctr) if ctr is not None else None)
+    return n, ctr
 
 
 def map_only(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=False):

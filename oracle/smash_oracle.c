@@ -982,6 +982,7 @@ static void *map_worker(void *arg) {
   orc_match m[256];
   memset(&j->ctr, 0, sizeof(j->ctr));
   j->ctr.last_sa = j->ctr.last_isa = j->ctr.last_ref = j->ctr.last_lcp = ~0ull;
+  j->ctr.last_kt = j->ctr.last_u = ~0ull;
   for (uint64_t q = j->begin; q < j->end; ++q)
     j->total += (uint64_t)orc_mam(j->ix, j->reads + q * j->stride, j->L,
                                   j->min_len, m, 256, j->count ? &j->ctr : NULL);
@@ -1014,6 +1015,191 @@ uint64_t orc_map_only(const orc_index *ix, const uint8_t *reads, uint32_t L,
       ctr->ref_loads += jobs[t].ctr.ref_loads; ctr->ref_lines += jobs[t].ctr.ref_lines;
       ctr->lcp_loads += jobs[t].ctr.lcp_loads; ctr->lcp_lines += jobs[t].ctr.lcp_lines;
       ctr->ovf_lookups += jobs[t].ctr.ovf_lookups;
+    }
+  }
+  free(jobs);
+  return total;
+}
+
+/* ======================================================================== */
+/* accelerated search (device SMASH_MODE_MAM), restated for checking        */
+/* ======================================================================== */
+
+uint32_t orc_accel_k(uint64_t N) {
+  uint32_t K = 4;
+  while (K < 14 && (1ull << (2 * (K + 2))) <= N) ++K;
+  return K;
+}
+
+static int acgt(uint8_t c) {
+  return c == 'a' ? 0 : c == 'c' ? 1 : c == 'g' ? 2 : c == 't' ? 3 : -1;
+}
+
+void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT) {
+  const uint64_t N = ix->N;
+  const uint32_t isz = ix->idx_bytes == 4 ? 4 : 8;
+  for (uint64_t x = 0; x < N; ++x) {
+    const uint64_t r = idx_at(ix->ISA, isz, x);
+    const uint8_t a = ix->L8[r], b = r + 1 < N ? ix->L8[r + 1] : 0;
+    U[x] = a > b ? a : b;
+  }
+  memset(U + N, 0, 64);
+  const uint64_t nk = 1ull << (2 * K);
+  for (uint64_t w = 0; w < nk; ++w) { KT[2 * w] = 1; KT[2 * w + 1] = 0; }
+  uint64_t prev = ~0ull;
+  for (uint64_t r = 0; r < N; ++r) {
+    const uint64_t x = idx_at(ix->SA, isz, r);
+    uint64_t code = 0;
+    int ok = x + K <= N;
+    for (uint32_t k = 0; ok && k < K; ++k) {
+      int v = acgt(ix->T[x + k]);
+      if (v < 0) ok = 0;
+      code = (code << 2) | (uint64_t)(v & 3);
+    }
+    if (!ok) { prev = ~0ull; continue; }
+    if (code != prev) KT[2 * code] = r;
+    KT[2 * code + 1] = r;
+    prev = code;
+  }
+}
+
+int orc_mam_fast(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
+                 uint32_t L, uint32_t min_len, orc_match *out, uint32_t cap,
+                 orc_counters *ctr) {
+  ctx_t x = mkctx(ix, ctr);
+  sink_t s = {out, cap, 0};
+  const uint64_t N = ix->N;
+  const uint32_t K = acc->K;
+  ival_t cur = {0, 0, N - 1};
+  uint64_t prefix = 0, pos = 0;
+  int have_pos = 0;
+  while (prefix < L) {
+    if (cur.depth == 0 && prefix + K <= L) {                 /* (C) */
+      uint64_t w = 0;
+      int ok = 1;
+      for (uint32_t k = 0; k < K; ++k) {
+        int v = acgt(P[prefix + k]);
+        if (v < 0) ok = 0;
+        w = (w << 2) | (uint64_t)(v & 3);
+      }
+      if (ok) {
+        if (ctr) tick(&ctr->sa_loads, &ctr->kt_lines, &ctr->last_kt, 16 * w);
+        const uint64_t lo = acc->KT[2 * w], hi = acc->KT[2 * w + 1];
+        if (lo <= hi) { cur.depth = K; cur.start = lo; cur.end = hi; have_pos = 0; }
+      }
+    }
+    if (cur.depth < L) {
+      while (prefix + cur.depth < L) {
+        if (cur.start == cur.end) {                          /* (A) */
+          if (!have_pos) { pos = SAat(&x, cur.start); have_pos = 1; }
+          while (prefix + cur.depth < L) {
+            if (ctr) tick(&ctr->ref_loads, &ctr->ref_lines, &ctr->last_ref, pos + cur.depth);
+            const uint64_t rem = L - prefix - cur.depth;
+            const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
+            uint32_t k = 0;
+            while (k < lim && P[prefix + cur.depth + k] == ix->T[pos + cur.depth + k]) ++k;
+            cur.depth += k;
+            if (k < lim) break;
+          }
+          break;
+        }
+        uint64_t st = cur.start, en = cur.end;
+        if (!td_faster(&x, (int64_t)(int8_t)P[prefix + cur.depth], cur.depth, &st, &en)) break;
+        cur.depth += 1; cur.start = st; cur.end = en; have_pos = 0;
+        if (cur.depth == L) break;
+      }
+    }
+    if (cur.depth <= 1) {
+      cur.depth = 0; cur.start = 0; cur.end = N - 1; have_pos = 0;
+      ++prefix;
+      continue;
+    }
+    if (cur.start == cur.end) {
+      if (!have_pos) { pos = SAat(&x, cur.start); have_pos = 1; }
+      if (cur.depth >= min_len) {
+        int lm = (prefix == 0 || pos == 0) ? 1
+                 : ((int64_t)(int8_t)P[prefix - 1] != Tat(&x, pos - 1));
+        if (lm) emit(&s, pos, prefix, cur.depth);
+      }
+      const uint64_t d = cur.depth;                          /* (B) */
+      uint64_t j = 1;
+      int hit = 0;
+      while (j < d) {
+        if (ctr) tick(&ctr->lcp_loads, &ctr->u_lines, &ctr->last_u, pos + j);
+        const uint64_t rem = d - j;
+        const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
+        uint32_t k = 0;
+        while (k < lim && (uint64_t)acc->U[pos + j + k] < d - j - k) ++k;
+        if (k < lim) { j += k; hit = 1; break; }
+        j += lim;
+      }
+      prefix += j;
+      if (!hit) { cur.depth = 0; cur.start = 0; cur.end = N - 1; have_pos = 0; continue; }
+      cur.depth = d - j;
+      cur.start = cur.end = ISAat(&x, pos + j);
+      have_pos = 0;
+      if (!expand_link(&x, &cur)) { cur.depth = 0; cur.start = 0; cur.end = N - 1; }
+      continue;
+    }
+    cur.depth -= 1;
+    cur.start = ISAat(&x, SAat(&x, cur.start) + 1);
+    cur.end = ISAat(&x, SAat(&x, cur.end) + 1);
+    ++prefix;
+    have_pos = 0;
+    if (cur.depth == 0 || !expand_link(&x, &cur)) { cur.depth = 0; cur.start = 0; cur.end = N - 1; }
+  }
+  return (int)s.n;
+}
+
+typedef struct {
+  const orc_index *ix;
+  const orc_accel *acc;
+  const uint8_t *reads;
+  uint32_t L, min_len;
+  uint64_t stride, begin, end, total;
+  orc_counters ctr;
+  int count;
+} fjob_t;
+
+static void *fast_worker(void *arg) {
+  fjob_t *j = (fjob_t *)arg;
+  orc_match m[256];
+  memset(&j->ctr, 0, sizeof(j->ctr));
+  j->ctr.last_sa = j->ctr.last_isa = j->ctr.last_ref = j->ctr.last_lcp = ~0ull;
+  j->ctr.last_kt = j->ctr.last_u = ~0ull;
+  for (uint64_t q = j->begin; q < j->end; ++q)
+    j->total += (uint64_t)orc_mam_fast(j->ix, j->acc, j->reads + q * j->stride, j->L,
+                                       j->min_len, m, 256, j->count ? &j->ctr : NULL);
+  return NULL;
+}
+
+uint64_t orc_map_only_fast(const orc_index *ix, const orc_accel *acc,
+                           const uint8_t *reads, uint32_t L, uint64_t stride,
+                           uint64_t n, uint32_t min_len, int threads,
+                           orc_counters *ctr) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  fjob_t *jobs = (fjob_t *)calloc((size_t)threads, sizeof(fjob_t));
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].ix = ix; jobs[t].acc = acc; jobs[t].reads = reads; jobs[t].L = L;
+    jobs[t].min_len = min_len; jobs[t].stride = stride;
+    jobs[t].begin = n * (uint64_t)t / (uint64_t)threads;
+    jobs[t].end = n * (uint64_t)(t + 1) / (uint64_t)threads;
+    jobs[t].count = ctr != NULL;
+    pthread_create(&th[t], NULL, fast_worker, &jobs[t]);
+  }
+  uint64_t total = 0;
+  if (ctr) memset(ctr, 0, sizeof(*ctr));
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    total += jobs[t].total;
+    if (ctr) {
+      ctr->sa_lines += jobs[t].ctr.sa_lines; ctr->isa_lines += jobs[t].ctr.isa_lines;
+      ctr->ref_lines += jobs[t].ctr.ref_lines; ctr->lcp_lines += jobs[t].ctr.lcp_lines;
+      ctr->kt_lines += jobs[t].ctr.kt_lines; ctr->u_lines += jobs[t].ctr.u_lines;
+      ctr->sa_loads += jobs[t].ctr.sa_loads; ctr->isa_loads += jobs[t].ctr.isa_loads;
+      ctr->ref_loads += jobs[t].ctr.ref_loads; ctr->lcp_loads += jobs[t].ctr.lcp_loads;
     }
   }
   free(jobs);

@@ -66,6 +66,8 @@ typedef struct {
 /* logN = ceil(log(N)/log(2.0)) (longSA.cpp:97) */
 uint64_t orc_logN(uint64_t N);
 
+typedef struct { uint64_t ref, query, len; } orc_match;  /* longSA.h:78-92 */
+
 /* Access accounting for the roofline: distinct 64-B line transitions per
  * array (BASELINE.md "B_read"), counted on the algorithm as run. */
 typedef struct {
@@ -74,9 +76,31 @@ typedef struct {
   uint64_t last_sa, last_isa, last_ref, last_lcp;
   uint64_t ovf_lookups;   /* vec_uchar overflow lower_bounds (not on the
                              device path: it compares min(LCP,255)) */
+  uint64_t kt_lines, u_lines;       /* accelerated path only */
+  uint64_t last_kt, last_u;
 } orc_counters;
 
-typedef struct { uint64_t ref, query, len; } orc_match;  /* longSA.h:78-92 */
+/* Search accelerators of the device path (smash-paper_amd/csrc/
+ * aux_build.hip), restated here so that the accelerated algorithm can be
+ * checked on the CPU (it must emit exactly orc_mam's matches) and so that its
+ * line transitions can be counted for the roofline:
+ *   U[x]  = min(255, max(LCP[ISA[x]], LCP[ISA[x]+1]))    (N + 64 bytes)
+ *   KT[w] = {lo, hi} SA interval of ACGT k-mer w, lo > hi if absent. */
+typedef struct {
+  const uint8_t *U;
+  const uint64_t *KT;
+  uint32_t K;
+} orc_accel;
+uint32_t orc_accel_k(uint64_t N);
+void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT);
+int orc_mam_fast(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
+                 uint32_t L, uint32_t min_len, orc_match *out, uint32_t cap,
+                 orc_counters *ctr);
+uint64_t orc_map_only_fast(const orc_index *ix, const orc_accel *acc,
+                           const uint8_t *reads, uint32_t L, uint64_t stride,
+                           uint64_t n, uint32_t min_len, int threads,
+                           orc_counters *ctr);
+
 
 /* longSA::MAM (longSA.cpp:503-536).  P: lowercased read.  Returns the number
  * of matches (written up to cap). */

@@ -1,0 +1,107 @@
+// smash-paper_amd/csrc/aux_build.hip -- search accelerators derived from the
+// index (results-preserving; see mam_device.hpp):
+//
+//  U[x]  (u8, one per text position) = min(255, max(LCP[ISA[x]], LCP[ISA[x]+1]))
+//        The suffix at x is alone in its SA interval at depth d iff U[x] < d
+//        (d <= 255).  This is what the reference's suffix-link chain
+//        (longSA.cpp:523-534 + expand_link, longSA.h:158-174) tests one step
+//        at a time with two random LCP loads; the device scans U[pos+1..]
+//        sequentially instead.  Same quantity as map.bin's `right` before the
+//        edge rules (longSA.cpp:628-641, 666).
+//  KT[w] ({lo, hi} u64 pair per ACGT k-mer w, 2 bits/char, first char most
+//        significant) = the SA interval of the suffixes starting with w, or
+//        lo > hi when w does not occur.  It replaces the first k narrowing
+//        steps of top_down_faster from the root (longSA.cpp:322-380).
+#include "common.hpp"
+
+namespace smash {
+namespace {
+
+template <class IdxT>
+__global__ void k_uniq(const IdxT *__restrict__ ISA, const uint8_t *__restrict__ L8,
+                       uint64_t N, uint8_t *U) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x < N; x += stride) {
+    const uint64_t r = ISA[x];
+    const uint8_t a = L8[r];
+    const uint8_t b = r + 1 < N ? L8[r + 1] : 0;
+    U[x] = a > b ? a : b;
+  }
+}
+
+__device__ inline int acgt2(uint8_t c) {
+  switch (c) {
+    case 'a': return 0;
+    case 'c': return 1;
+    case 'g': return 2;
+    case 't': return 3;
+    default: return -1;
+  }
+}
+
+template <class IdxT>
+__global__ void k_kcode(const IdxT *__restrict__ SA, const uint8_t *__restrict__ T,
+                        uint64_t N, int K, uint32_t *code) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < N; r += stride) {
+    const uint64_t x = SA[r];
+    uint32_t c = 0;
+    bool ok = x + K <= N;
+    for (int k = 0; ok && k < K; ++k) {
+      const int v = acgt2(T[x + k]);
+      if (v < 0) ok = false;
+      c = (c << 2) | uint32_t(v);
+    }
+    code[r] = ok ? c : 0xFFFFFFFFu;
+  }
+}
+
+__global__ void k_kfill(uint64_t *kt, uint64_t n) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w < n; w += stride) {
+    kt[2 * w] = 1;       // empty: lo > hi
+    kt[2 * w + 1] = 0;
+  }
+}
+
+__global__ void k_kbounds(const uint32_t *__restrict__ code, uint64_t N, uint64_t *kt) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < N; r += stride) {
+    const uint32_t c = code[r];
+    if (c == 0xFFFFFFFFu) continue;
+    if (r == 0 || code[r - 1] != c) kt[2 * uint64_t(c)] = r;
+    if (r + 1 == N || code[r + 1] != c) kt[2 * uint64_t(c) + 1] = r;
+  }
+}
+
+template <class IdxT>
+void build_aux_t(smash_index *ix, hipStream_t s) {
+  const uint64_t N = ix->N;
+  if (!ix->d_uniq) ix->d_uniq = dalloc<uint8_t>(N + 64);
+  SMASH_HIPX(hipMemsetAsync(ix->d_uniq + N, 0, 64, s));
+  k_uniq<IdxT><<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
+      static_cast<const IdxT *>(ix->d_isa), ix->d_lcp8, N, ix->d_uniq);
+  // k: about log4(N) - 2 characters (a few tens of suffixes per k-mer), <= 14
+  int K = 4;
+  while (K < 14 && (1ull << (2 * (K + 2))) <= N) ++K;
+  ix->kmer_k = uint32_t(K);
+  const uint64_t nk = 1ull << (2 * K);
+  if (!ix->d_kmer) ix->d_kmer = dalloc<uint64_t>(2 * nk);
+  k_kfill<<<grid_for(nk, 256, 1u << 20), 256, 0, s>>>(ix->d_kmer, nk);
+  uint32_t *code = dalloc<uint32_t>(N);
+  k_kcode<IdxT><<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
+      static_cast<const IdxT *>(ix->d_sa), ix->d_text, N, K, code);
+  k_kbounds<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(code, N, ix->d_kmer);
+  SMASH_HIPX(hipStreamSynchronize(s));
+  dfree(code);
+  SMASH_HIPX(hipGetLastError());
+}
+
+}  // namespace
+
+void build_aux(smash_index *ix, hipStream_t s) {
+  if (ix->idx_bytes == 4) build_aux_t<uint32_t>(ix, s);
+  else build_aux_t<uint64_t>(ix, s);
+}
+
+}  // namespace smash

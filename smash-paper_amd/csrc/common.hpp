@@ -87,6 +87,9 @@ struct smash_index {
   uint64_t n_ovf = 0;
   uint8_t *d_map = nullptr;
   uint64_t map_bytes = 0;
+  uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
+  uint64_t *d_kmer = nullptr;    // {lo,hi} per k-mer
+  uint32_t kmer_k = 0;
   uint64_t *d_startpos = nullptr;
   uint64_t *d_sizes = nullptr;
   double build_seconds = 0;
@@ -99,4 +102,5 @@ void build_sa_isa(smash_index *ix, hipStream_t s);       // fills d_sa, d_isa
 uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, saturating)
 void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
 void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
+void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
 }  // namespace smash

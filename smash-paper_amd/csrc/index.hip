@@ -36,6 +36,7 @@ void free_index(smash_index *ix) {
   (void)hipSetDevice(ix->device);
   dfree(ix->d_text); dfree(ix->d_sa); dfree(ix->d_isa); dfree(ix->d_lcp8);
   dfree(ix->d_ovf); dfree(ix->d_map); dfree(ix->d_startpos); dfree(ix->d_sizes);
+  dfree(ix->d_uniq); dfree(ix->d_kmer);
   (void)hipSetDevice(cur);
   delete ix;
 }
@@ -52,7 +53,8 @@ void upload_tables(smash_index *ix, hipStream_t s) {
 void account(smash_index *ix) {
   const uint64_t N = ix->N;
   ix->device_bytes = (N + 64) + 2 * N * ix->idx_bytes + N + 16 * ix->n_ovf +
-                     ix->map_bytes + 16 * ix->n_seq;
+                     ix->map_bytes + 16 * ix->n_seq + (N + 64) +
+                     (ix->kmer_k ? 16ull << (2 * ix->kmer_k) : 0);
 }
 
 // u32 exact LCP from lcp8 + overflow (used when map.bin must be computed
@@ -142,6 +144,8 @@ extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N,
     build_map(ix.get(), lcp, s);
     SMASH_HIPX(hipStreamSynchronize(s));
     dfree(lcp);
+    build_aux(ix.get(), s);
+    SMASH_HIPX(hipStreamSynchronize(s));
     SMASH_HIPX(hipStreamDestroy(s));
     ix->build_seconds = now_s() - t0;
     account(ix.get());
@@ -261,6 +265,8 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
       dfree(lcp);
     }
     SMASH_HIPX(hipStreamSynchronize(s));
+    build_aux(ix.get(), s);
+    SMASH_HIPX(hipStreamSynchronize(s));
     SMASH_HIPX(hipStreamDestroy(s));
     ix->build_seconds = now_s() - t0;
     account(ix.get());
@@ -368,5 +374,8 @@ extern "C" int smash_index_query(const smash_index *ix, smash_index_info *o) {
   o->d_map = ix->d_map;
   o->device_bytes = ix->device_bytes;
   o->build_seconds = ix->build_seconds;
+  o->kmer_k = ix->kmer_k;
+  o->d_uniq = ix->d_uniq;
+  o->d_kmer = ix->d_kmer;
   return SMASH_OK;
 }

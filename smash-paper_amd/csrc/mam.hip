@@ -18,7 +18,7 @@
 namespace smash {
 namespace {
 
-template <class IdxT, int BLOCK>
+template <class IdxT, int BLOCK, bool PLAIN>
 __global__ __launch_bounds__(BLOCK) void k_mam(
     DevIndex<IdxT> x, const uint8_t *__restrict__ seqs, uint64_t stride,
     const uint16_t *__restrict__ lens, uint32_t len0, uint64_t n_reads,
@@ -39,11 +39,12 @@ __global__ __launch_bounds__(BLOCK) void k_mam(
   const uint32_t L = lens ? lens[r] : len0;
   const uint8_t *P = lds + threadIdx.x * row;
   MatchSink sink{out + r * cap, cap, 0};
-  mam_read(x, P, L, min_len, sink);
+  if (PLAIN) mam_read_plain(x, P, L, min_len, sink);
+  else mam_read(x, P, L, min_len, sink);
   n_out[r] = sink.n;
 }
 
-template <class IdxT>
+template <class IdxT, bool PLAIN>
 int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
            uint64_t stride, const uint16_t *lens, uint32_t len,
            uint64_t n_reads, uint64_t *out, uint32_t cap, uint32_t *n_out,
@@ -59,7 +60,7 @@ int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
     const uint64_t nb = blocks - b0 < (1u << 30) ? blocks - b0 : (1u << 30);
     const uint64_t off = b0 * B;
-    k_mam<IdxT, B><<<unsigned(nb), B, lds, s>>>(
+    k_mam<IdxT, B, PLAIN><<<unsigned(nb), B, lds, s>>>(
         x, seqs + off * stride, stride, lens ? lens + off : nullptr, len,
         n_reads - off, min_len, out + off * cap, cap, n_out + off, row);
   }
@@ -82,8 +83,16 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
     set_error("smash_map_batch: bad arguments");
     return SMASH_ERR_ARG;
   }
-  if (mode != SMASH_MODE_MAM) {
-    set_error("smash_map_batch: only SMASH_MODE_MAM (the SMASH default) runs on the device");
+  if (mode != SMASH_MODE_MAM && mode != SMASH_MODE_MAM_PLAIN) {
+    set_error("smash_map_batch: only the MAM modes (the SMASH default) run on the device");
+    return SMASH_ERR_UNSUPPORTED;
+  }
+  if (mode == SMASH_MODE_MAM && (!ix->d_uniq || !ix->d_kmer)) {
+    set_error("smash_map_batch: index lacks the search accelerators");
+    return SMASH_ERR_ARG;
+  }
+  if (!d_lens && len > 255) {
+    set_error("smash_map_batch: reads longer than 255 need the exact LCP path");
     return SMASH_ERR_UNSUPPORTED;
   }
   if (!d_lens && (len == 0 || len > 255)) {
@@ -97,9 +106,14 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
   if (n_reads == 0) return SMASH_OK;
   SMASH_HIP(hipSetDevice(ix->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  return ix->idx_bytes == 4
-             ? launch<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
-                                d_out, cap_per_read, d_n_out, s)
-             : launch<uint64_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
-                                d_out, cap_per_read, d_n_out, s);
+  const bool plain = mode == SMASH_MODE_MAM_PLAIN;
+  if (ix->idx_bytes == 4)
+    return plain ? launch<uint32_t, true>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
+                                          d_out, cap_per_read, d_n_out, s)
+                 : launch<uint32_t, false>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
+                                           d_out, cap_per_read, d_n_out, s);
+  return plain ? launch<uint64_t, true>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
+                                        d_out, cap_per_read, d_n_out, s)
+               : launch<uint64_t, false>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
+                                         d_out, cap_per_read, d_n_out, s);
 }

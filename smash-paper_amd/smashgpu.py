@@ -26,6 +26,7 @@ i32p = C.POINTER(C.c_int32)
 vp = C.c_void_p
 
 SMASH_MODE_MAM = 1
+SMASH_MODE_MAM_PLAIN = 2
 ERRORS = {1: "left mappability too big (mappability_tag.cpp:110)",
           2: "right mappability too big (mappability_tag.cpp:113)",
           -4: "out of device memory / key set full",
@@ -48,7 +49,8 @@ class IndexInfo(C.Structure):
                 ("n_seq", C.c_uint32), ("n_lcp_overflow", C.c_uint64),
                 ("map_bytes", C.c_uint64), ("d_text", vp), ("d_sa", vp),
                 ("d_isa", vp), ("d_lcp8", vp), ("d_lcp_ovf", vp), ("d_map", vp),
-                ("device_bytes", C.c_uint64), ("build_seconds", C.c_double)]
+                ("device_bytes", C.c_uint64), ("build_seconds", C.c_double),
+                ("kmer_k", C.c_uint32), ("d_uniq", vp), ("d_kmer", vp)]
 
 
 class PipelineCfg(C.Structure):
@@ -405,9 +407,9 @@ def _ptr(x):
 
 
 def map_batch(index: Index, d_reads, n_reads, read_len, d_out, cap, d_n, min_len=20,
-              stream=None):
+              stream=None, mode=SMASH_MODE_MAM):
     """longSA::MAM over a batch (smash_map_batch)."""
-    check(lib().smash_map_batch(index.h, SMASH_MODE_MAM, min_len, _ptr(d_reads),
+    check(lib().smash_map_batch(index.h, mode, min_len, _ptr(d_reads),
                                 read_len, None, read_len, n_reads, _ptr(d_out), cap,
                                 _ptr(d_n), vp(_stream(stream))), "smash_map_batch")
 

@@ -85,25 +85,36 @@ def _device_reads(reads):
     return torch.from_numpy(np.ascontiguousarray(reads)).cuda()
 
 
-def run_map(ix, reads, min_len=20):
+def run_map(ix, reads, min_len=20, mode=S.SMASH_MODE_MAM):
     n, L = reads.shape
     cap = L - min_len + 1
     d = _device_reads(reads)
     out = torch.zeros(n * cap, dtype=torch.int64, device="cuda")
     nn = torch.zeros(n, dtype=torch.int32, device="cuda")
-    S.map_batch(ix, d, n, L, out, cap, nn, min_len=min_len)
+    S.map_batch(ix, d, n, L, out, cap, nn, min_len=min_len, mode=mode)
     torch.cuda.synchronize()
     o = out.cpu().numpy().view(np.uint64).reshape(n, cap)
     k = nn.cpu().numpy()
     return [S.unpack_matches(o[i], k[i]) for i in range(n)]
 
 
+def test_device_accelerators_equal_oracle(gix, tiny_ix):
+    i = gix.info
+    U = S.download(i.d_uniq, i.N + 64)
+    KT = S.download(i.d_kmer, 16 << (2 * i.kmer_k), np.uint64)
+    U2, KT2, K2 = tiny_ix.accel()
+    assert i.kmer_k == K2
+    assert np.array_equal(U[:i.N], U2[:i.N])
+    assert np.array_equal(KT, KT2)
+
+
 @pytest.mark.parametrize("s", ["s100", "s150"])
-def test_mam_matches_reference(gix, s):
+@pytest.mark.parametrize("mode", [S.SMASH_MODE_MAM, S.SMASH_MODE_MAM_PLAIN])
+def test_mam_matches_reference(gix, s, mode):
     reads = interleaved_reads(s)
     exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
            for l in read_gz_lines("%s_MAM.txt.gz" % s)]
-    got = run_map(gix, reads)
+    got = run_map(gix, reads, mode=mode)
     assert len(got) == len(exp)
     bad = [i for i in range(len(exp)) if got[i] != exp[i]]
     assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)
@@ -206,8 +217,9 @@ def test_mid_genome_pipeline_equals_oracle(mid, tmp_path):
     reads = np.empty((12000, 150), np.uint8)
     reads[0::2], reads[1::2] = r1, r2
     reads = S.prepare_reads(reads)
-    # MAM on every read
+    # MAM on every read, both device modes
     got = run_map(dix, reads)
+    assert got == run_map(dix, reads, mode=S.SMASH_MODE_MAM_PLAIN)
     for i in range(0, len(reads), 7):
         assert got[i] == oix.search(reads[i].tobytes()), i
     bins_path = str(tmp_path / "bins.txt")

@@ -1,0 +1,40 @@
+"""The accelerated search (device SMASH_MODE_MAM, restated in the oracle as
+orc_mam_fast) must emit exactly the reference's MAM triples: checked against
+the golden vectors and against orc_mam on a larger synthetic genome (CPU)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import interleaved_reads, read_gz_lines
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_fast_search_matches_reference_goldens(tiny_ix, s):
+    tiny_ix.accel()
+    exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+           for l in read_gz_lines("%s_MAM.txt.gz" % s)]
+    reads = interleaved_reads(s)
+    for i, e in enumerate(exp):
+        assert tiny_ix.search_fast(reads[i].tobytes()) == e, i
+
+
+def test_fast_search_equals_plain_on_mid_genome():
+    import synth
+    g = synth.make_genome("mid")
+    ix = O.Index(*O.text_from_contigs(g))
+    U, KT, K = ix.accel()
+    assert K == O.lib().orc_accel_k(ix.N)
+    r1, r2 = synth.make_reads(g, 3000, 150, seed=44)
+    reads = np.empty((6000, 150), np.uint8)
+    reads[0::2], reads[1::2] = r1, r2
+    reads[reads == ord("N")] = ord("Z")
+    lo = np.arange(256, dtype=np.uint8); lo[65:91] += 32
+    reads = lo[reads]
+    c1, c2 = O.OrcCounters(), O.OrcCounters()
+    for i in range(len(reads)):
+        P = reads[i].tobytes()
+        assert ix.search_fast(P) == ix.search(P), i
+    n1, k1 = O.map_only(ix, reads, threads=4, count=True)
+    n2, k2 = O.map_only_fast(ix, reads, threads=4, count=True)
+    assert n1 == n2
+    assert k2.lines() < k1.lines()     # the point of the accelerators
