@@ -110,7 +110,9 @@ def host_index(S, O, dix, T, sp, sz, names):
     oix = O.Index(T, sp, sz, names, SA=SA, ISA=ISA, L8=L8, ovf=ovf)
     U = S.download(i.d_uniq, N + 64)
     KT = S.download(i.d_kmer, 16 << (2 * i.kmer_k), np.uint64)
-    oix.accel(U, KT, i.kmer_k)
+    BM = S.download(i.d_bitmap, 8 * ((1 << (2 * i.bitmap_b)) // 64 + 1), np.uint64)
+    it = np.array([(i.in_text[c >> 6] >> (c & 63)) & 1 for c in range(256)], np.uint8)
+    oix.accel(U, KT, i.kmer_k, BM, i.bitmap_b, it)
     return oix, mp
 
 
@@ -239,8 +241,8 @@ def main():
         # algorithmic bytes per read: 64 B x line transitions of the algorithm
         # the kernel runs (orc_mam_fast = the device's accelerated search)
         ns = min(4000, 2 * P)
-        _, ctr = O.map_only_fast(oix, reads_h[:ns], threads=min(16, os.cpu_count() or 1),
-                                 count=True)
+        _, ctr = O.map_only_v3(oix, reads_h[:ns], threads=min(16, os.cpu_count() or 1),
+                               count=True)
         lines = ctr.lines()
         b_read = 64.0 * lines / ns
         achieved = reads_per_launch * b_read / (avg_ms / 1e3) / 1e9
@@ -250,7 +252,8 @@ def main():
                 "avg_kernel_ms": round(avg_ms, 3), "reads_per_launch": int(reads_per_launch),
                 "lines_per_read": {"sa": ctr.sa_lines / ns, "isa": ctr.isa_lines / ns,
                                    "ref": ctr.ref_lines / ns, "lcp": ctr.lcp_lines / ns,
-                                   "kmer": ctr.kt_lines / ns, "uniq": ctr.u_lines / ns}}
+                                   "kmer": ctr.kt_lines / ns, "uniq": ctr.u_lines / ns,
+                                   "bitmap": ctr.bm_lines / ns}}
         pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
         if os.path.exists(pmc):
             try:

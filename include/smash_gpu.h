@@ -102,6 +102,9 @@ typedef struct {
   uint32_t kmer_k;         /* k of the k-mer -> SA-interval table */
   const uint8_t *d_uniq;   /* U[x] = min(255, max(LCP[ISA[x]], LCP[ISA[x]+1])) */
   const uint64_t *d_kmer;  /* 4^k x {lo, hi}; lo > hi = absent */
+  uint32_t bitmap_b;       /* B of the B-mer presence bitmap */
+  const uint64_t *d_bitmap;/* 4^B bits: ACGT B-mer occurs in the text */
+  uint64_t in_text[4];     /* 256-bit set of bytes occurring in the text */
 } smash_index_info;
 int smash_index_query(const smash_index *ix, smash_index_info *out);
 

@@ -38,15 +38,16 @@ class OrcCounters(C.Structure):
         "sa_loads", "isa_loads", "ref_loads", "lcp_loads",
         "sa_lines", "isa_lines", "ref_lines", "lcp_lines",
         "last_sa", "last_isa", "last_ref", "last_lcp", "ovf_lookups",
-        "kt_lines", "u_lines", "last_kt", "last_u")]
+        "kt_lines", "u_lines", "last_kt", "last_u", "bm_lines", "last_bm")]
 
     def lines(self):
         return (self.sa_lines + self.isa_lines + self.ref_lines + self.lcp_lines
-                + self.kt_lines + self.u_lines)
+                + self.kt_lines + self.u_lines + self.bm_lines)
 
 
 class OrcAccel(C.Structure):
-    _fields_ = [("U", u8p), ("KT", u64p), ("K", C.c_uint32)]
+    _fields_ = [("U", u8p), ("KT", u64p), ("K", C.c_uint32), ("BM", u64p),
+                ("B", C.c_uint32), ("in_text", C.c_uint8 * 256)]
 
 
 class OrcMatch(C.Structure):
@@ -129,6 +130,12 @@ def lib():
                                         C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
                                         C.c_int, C.POINTER(OrcCounters)]
         L.orc_map_only_fast.restype = C.c_uint64
+        L.orc_accel_b.argtypes = [C.c_uint64]
+        L.orc_accel_b.restype = C.c_uint32
+        L.orc_build_bitmap.argtypes = [C.POINTER(OrcIndex), C.c_uint32, u64p, u8p]
+        L.orc_mam_v3.argtypes = L.orc_mam_fast.argtypes
+        L.orc_map_only_v3.argtypes = L.orc_map_only_fast.argtypes
+        L.orc_map_only_v3.restype = C.c_uint64
         _LIB = L
     return _LIB
 
@@ -257,17 +264,33 @@ class Index:
             cap = n
         return [(out[i].ref, out[i].query, out[i].len) for i in range(n)]
 
-    def accel(self, U=None, KT=None, K=None):
+    def accel(self, U=None, KT=None, K=None, BM=None, B=None, in_text=None):
         """Search accelerators (built here, or given, e.g. from the device)."""
         if U is None:
             K = lib().orc_accel_k(self.N)
             U = np.zeros(self.N + 64, np.uint8)
             KT = np.zeros(2 << (2 * K), np.uint64)
             lib().orc_build_accel(C.byref(self.c), K, _p(U, u8p), _p(KT, u64p))
+        if BM is None:
+            B = lib().orc_accel_b(self.N)
+            BM = np.zeros((1 << (2 * B)) // 64 + 1, np.uint64)
+            in_text = np.zeros(256, np.uint8)
+            lib().orc_build_bitmap(C.byref(self.c), B, _p(BM, u64p), _p(in_text, u8p))
         self._U = np.ascontiguousarray(U, np.uint8)
         self._KT = np.ascontiguousarray(KT, np.uint64)
-        self.acc = OrcAccel(_p(self._U, u8p), _p(self._KT, u64p), int(K))
+        self._BM = np.ascontiguousarray(BM, np.uint64)
+        self.acc = OrcAccel(_p(self._U, u8p), _p(self._KT, u64p), int(K),
+                            _p(self._BM, u64p), int(B),
+                            (C.c_uint8 * 256)(*[int(v) for v in in_text]))
         return self._U, self._KT, int(K)
+
+    def search_v3(self, read: bytes, min_len=20, counters=None):
+        P = np.frombuffer(read, np.uint8)
+        out = (OrcMatch * 512)()
+        n = lib().orc_mam_v3(C.byref(self.c), C.byref(self.acc), _p(P, u8p), len(P),
+                             min_len, out, 512,
+                             C.byref(counters) if counters is not None else None)
+        return [(out[i].ref, out[i].query, out[i].len) for i in range(min(n, 512))]
 
     def search_fast(self, read: bytes, min_len=20, counters=None):
         P = np.frombuffer(read, np.uint8)
@@ -398,6 +421,15 @@ def map_only_fast(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=Fal
     n = lib().orc_map_only_fast(C.byref(ix.c), C.byref(ix.acc), _p(reads, u8p),
                                 reads.shape[1], reads.shape[1], reads.shape[0], min_len,
                                 threads, C.byref(ctr) if ctr is not None else None)
+    return n, ctr
+
+
+def map_only_v3(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=False):
+    reads = np.ascontiguousarray(reads, np.uint8)
+    ctr = OrcCounters() if count else None
+    n = lib().orc_map_only_v3(C.byref(ix.c), C.byref(ix.acc), _p(reads, u8p),
+                              reads.shape[1], reads.shape[1], reads.shape[0], min_len,
+                              threads, C.byref(ctr) if ctr is not None else None)
     return n, ctr
 
 

@@ -982,7 +982,7 @@ static void *map_worker(void *arg) {
   orc_match m[256];
   memset(&j->ctr, 0, sizeof(j->ctr));
   j->ctr.last_sa = j->ctr.last_isa = j->ctr.last_ref = j->ctr.last_lcp = ~0ull;
-  j->ctr.last_kt = j->ctr.last_u = ~0ull;
+  j->ctr.last_kt = j->ctr.last_u = j->ctr.last_bm = ~0ull;
   for (uint64_t q = j->begin; q < j->end; ++q)
     j->total += (uint64_t)orc_mam(j->ix, j->reads + q * j->stride, j->L,
                                   j->min_len, m, 256, j->count ? &j->ctr : NULL);
@@ -1166,7 +1166,7 @@ static void *fast_worker(void *arg) {
   orc_match m[256];
   memset(&j->ctr, 0, sizeof(j->ctr));
   j->ctr.last_sa = j->ctr.last_isa = j->ctr.last_ref = j->ctr.last_lcp = ~0ull;
-  j->ctr.last_kt = j->ctr.last_u = ~0ull;
+  j->ctr.last_kt = j->ctr.last_u = j->ctr.last_bm = ~0ull;
   for (uint64_t q = j->begin; q < j->end; ++q)
     j->total += (uint64_t)orc_mam_fast(j->ix, j->acc, j->reads + q * j->stride, j->L,
                                        j->min_len, m, 256, j->count ? &j->ctr : NULL);
@@ -1200,6 +1200,243 @@ uint64_t orc_map_only_fast(const orc_index *ix, const orc_accel *acc,
       ctr->kt_lines += jobs[t].ctr.kt_lines; ctr->u_lines += jobs[t].ctr.u_lines;
       ctr->sa_loads += jobs[t].ctr.sa_loads; ctr->isa_loads += jobs[t].ctr.isa_loads;
       ctr->ref_loads += jobs[t].ctr.ref_loads; ctr->lcp_loads += jobs[t].ctr.lcp_loads;
+    }
+  }
+  free(jobs);
+  return total;
+}
+
+/* ======================================================================== */
+/* v3: per-position evaluation                                              */
+/* ======================================================================== */
+
+uint32_t orc_accel_b(uint64_t N) {
+  uint32_t B = 8;
+  while (B < 18 && (1ull << (2 * (B - 1))) <= N) ++B;
+  return B;
+}
+
+void orc_build_bitmap(const orc_index *ix, uint32_t B, uint64_t *BM, uint8_t *in_text) {
+  const uint64_t N = ix->N;
+  memset(BM, 0, ((1ull << (2 * B)) / 64 + 1) * 8);
+  memset(in_text, 0, 256);
+  uint64_t code = 0, mask = (1ull << (2 * B)) - 1;
+  uint32_t run = 0;    /* consecutive ACGT chars ending at x */
+  for (uint64_t x = 0; x < N; ++x) {
+    in_text[ix->T[x]] = 1;
+    int v = acgt(ix->T[x]);
+    if (v < 0) { run = 0; code = 0; continue; }
+    code = ((code << 2) | (uint64_t)v) & mask;
+    if (++run >= B) BM[code >> 6] |= 1ull << (code & 63);
+  }
+}
+
+#define V3_SCAN 32
+
+/* window filter: can P[p .. p+min_len) occur in the text at all?  0 = no
+ * (then ms(p) < min_len and p cannot emit). */
+static int v3_window(const orc_accel *acc, const uint8_t *P, uint64_t p,
+                     uint32_t min_len, orc_counters *ctr, uint64_t *next_p) {
+  *next_p = p + 1;
+  for (uint64_t k = p + min_len; k-- > p;)
+    if (!acc->in_text[P[k]]) { *next_p = k + 1; return 0; }
+  const uint32_t B = acc->B;
+  if (B > min_len) return 1;
+  const uint64_t bmask = (1ull << (2 * B)) - 1;
+  for (int end = 0; end < 2; ++end) {
+    const uint64_t q = end ? p + min_len - B : p;
+    uint64_t code = 0;
+    for (uint32_t k = 0; k < B; ++k) {
+      int v = acgt(P[q + k]);
+      if (v < 0) return 1;          /* non-ACGT text byte: no bitmap verdict */
+      code = ((code << 2) | (uint64_t)v) & bmask;
+    }
+    if (ctr) tick(&ctr->sa_loads, &ctr->bm_lines, &ctr->last_bm, code >> 3);
+    if (!((acc->BM[code >> 6] >> (code & 63)) & 1)) return 0;
+  }
+  return 1;
+}
+
+/* final state of a traverse over a small interval: each candidate suffix is
+ * compared with P directly (independent loads); the suffixes sharing the
+ * longest match form the new interval (contiguous in SA order). */
+static void v3_scan(const ctx_t *x, const uint8_t *P, uint64_t L, uint64_t p,
+                    ival_t *cur, uint64_t *pos) {
+  int64_t best = -1;
+  uint64_t bl = cur->start, bh = cur->start, bpos = 0;
+  const uint64_t d = cur->depth, rem = L - p - d;
+  for (uint64_t m = cur->start; m <= cur->end; ++m) {
+    const uint64_t sp = SAat(x, m);
+    uint64_t l = 0;
+    while (l < rem) {
+      if (x->c) tick(&x->c->ref_loads, &x->c->ref_lines, &x->c->last_ref, sp + d + l);
+      uint32_t k = 0;
+      const uint32_t lim = rem - l < 8 ? (uint32_t)(rem - l) : 8u;
+      while (k < lim && P[p + d + l + k] == x->ix->T[sp + d + l + k]) ++k;
+      l += k;
+      if (k < lim) break;
+    }
+    if ((int64_t)l > best) { best = (int64_t)l; bl = bh = m; bpos = sp; }
+    else if ((int64_t)l == best) bh = m;
+  }
+  cur->depth = d + (uint64_t)best;
+  cur->start = bl;
+  cur->end = bh;
+  *pos = bpos;
+}
+
+int orc_mam_v3(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
+               uint32_t L, uint32_t min_len, orc_match *out, uint32_t cap,
+               orc_counters *ctr) {
+  ctx_t x = mkctx(ix, ctr);
+  sink_t s = {out, cap, 0};
+  const uint64_t N = ix->N;
+  const uint32_t K = acc->K;
+  ival_t cur = {0, 0, N - 1};
+  uint64_t prefix = 0, pos = 0;
+  int have_pos = 0;
+  while (prefix < L) {
+    /* (F) a shallow state can be dropped at any prefix whose min_len window
+     * does not occur: ms(prefix) < min_len, nothing is emitted there */
+    if (cur.depth < min_len) {
+      if (prefix + min_len > L) break;
+      uint64_t nxt;
+      if (!v3_window(acc, P, prefix, min_len, ctr, &nxt)) {
+        cur.depth = 0; cur.start = 0; cur.end = N - 1; have_pos = 0;
+        prefix = nxt;
+        continue;
+      }
+    }
+    if (cur.depth == 0 && prefix + K <= L) {                 /* (C) */
+      uint64_t w = 0;
+      int ok = 1;
+      for (uint32_t k = 0; k < K; ++k) {
+        int v = acgt(P[prefix + k]);
+        if (v < 0) ok = 0;
+        w = (w << 2) | (uint64_t)(v & 3);
+      }
+      if (ok) {
+        if (ctr) tick(&ctr->sa_loads, &ctr->kt_lines, &ctr->last_kt, 16 * w);
+        const uint64_t lo = acc->KT[2 * w], hi = acc->KT[2 * w + 1];
+        if (lo <= hi) { cur.depth = K; cur.start = lo; cur.end = hi; have_pos = 0; }
+      }
+    }
+    if (cur.depth < L) {
+      while (prefix + cur.depth < L) {
+        if (cur.start == cur.end) {                          /* (A) */
+          if (!have_pos) { pos = SAat(&x, cur.start); have_pos = 1; }
+          while (prefix + cur.depth < L) {
+            if (ctr) tick(&ctr->ref_loads, &ctr->ref_lines, &ctr->last_ref, pos + cur.depth);
+            const uint64_t rem = L - prefix - cur.depth;
+            const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
+            uint32_t k = 0;
+            while (k < lim && P[prefix + cur.depth + k] == ix->T[pos + cur.depth + k]) ++k;
+            cur.depth += k;
+            if (k < lim) break;
+          }
+          break;
+        }
+        if (cur.end - cur.start + 1 <= V3_SCAN) {            /* (S) */
+          v3_scan(&x, P, L, prefix, &cur, &pos);
+          have_pos = cur.start == cur.end;
+          break;
+        }
+        uint64_t st = cur.start, en = cur.end;
+        if (!td_faster(&x, (int64_t)(int8_t)P[prefix + cur.depth], cur.depth, &st, &en)) break;
+        cur.depth += 1; cur.start = st; cur.end = en; have_pos = 0;
+        if (cur.depth == L) break;
+      }
+    }
+    if (cur.depth <= 1) {
+      cur.depth = 0; cur.start = 0; cur.end = N - 1; have_pos = 0;
+      ++prefix;
+      continue;
+    }
+    if (cur.start == cur.end) {
+      if (!have_pos) { pos = SAat(&x, cur.start); have_pos = 1; }
+      if (cur.depth >= min_len) {
+        int lm = (prefix == 0 || pos == 0) ? 1
+                 : ((int64_t)(int8_t)P[prefix - 1] != Tat(&x, pos - 1));
+        if (lm) emit(&s, pos, prefix, cur.depth);
+      }
+      const uint64_t d = cur.depth;                          /* (B) */
+      uint64_t j = 1;
+      int hit = 0;
+      while (j < d) {
+        if (ctr) tick(&ctr->lcp_loads, &ctr->u_lines, &ctr->last_u, pos + j);
+        const uint64_t rem = d - j;
+        const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
+        uint32_t k = 0;
+        while (k < lim && (uint64_t)acc->U[pos + j + k] < d - j - k) ++k;
+        if (k < lim) { j += k; hit = 1; break; }
+        j += lim;
+      }
+      prefix += j;
+      if (!hit) { cur.depth = 0; cur.start = 0; cur.end = N - 1; have_pos = 0; continue; }
+      cur.depth = d - j;
+      cur.start = cur.end = ISAat(&x, pos + j);
+      have_pos = 0;
+      if (!expand_link(&x, &cur)) { cur.depth = 0; cur.start = 0; cur.end = N - 1; }
+      continue;
+    }
+    cur.depth -= 1;
+    cur.start = ISAat(&x, SAat(&x, cur.start) + 1);
+    cur.end = ISAat(&x, SAat(&x, cur.end) + 1);
+    ++prefix;
+    have_pos = 0;
+    if (cur.depth == 0 || !expand_link(&x, &cur)) { cur.depth = 0; cur.start = 0; cur.end = N - 1; }
+  }
+  return (int)s.n;
+}
+
+typedef struct {
+  const orc_index *ix;
+  const orc_accel *acc;
+  const uint8_t *reads;
+  uint32_t L, min_len;
+  uint64_t stride, begin, end, total;
+  orc_counters ctr;
+  int count;
+} v3job_t;
+
+static void *v3_worker(void *arg) {
+  v3job_t *j = (v3job_t *)arg;
+  orc_match m[256];
+  memset(&j->ctr, 0, sizeof(j->ctr));
+  j->ctr.last_sa = j->ctr.last_isa = j->ctr.last_ref = j->ctr.last_lcp = ~0ull;
+  j->ctr.last_kt = j->ctr.last_u = j->ctr.last_bm = ~0ull;
+  for (uint64_t q = j->begin; q < j->end; ++q)
+    j->total += (uint64_t)orc_mam_v3(j->ix, j->acc, j->reads + q * j->stride, j->L,
+                                     j->min_len, m, 256, j->count ? &j->ctr : NULL);
+  return NULL;
+}
+
+uint64_t orc_map_only_v3(const orc_index *ix, const orc_accel *acc,
+                         const uint8_t *reads, uint32_t L, uint64_t stride,
+                         uint64_t n, uint32_t min_len, int threads,
+                         orc_counters *ctr) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  v3job_t *jobs = (v3job_t *)calloc((size_t)threads, sizeof(v3job_t));
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].ix = ix; jobs[t].acc = acc; jobs[t].reads = reads; jobs[t].L = L;
+    jobs[t].min_len = min_len; jobs[t].stride = stride;
+    jobs[t].begin = n * (uint64_t)t / (uint64_t)threads;
+    jobs[t].end = n * (uint64_t)(t + 1) / (uint64_t)threads;
+    jobs[t].count = ctr != NULL;
+    pthread_create(&th[t], NULL, v3_worker, &jobs[t]);
+  }
+  uint64_t total = 0;
+  if (ctr) memset(ctr, 0, sizeof(*ctr));
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    total += jobs[t].total;
+    if (ctr) {
+      ctr->sa_lines += jobs[t].ctr.sa_lines; ctr->isa_lines += jobs[t].ctr.isa_lines;
+      ctr->ref_lines += jobs[t].ctr.ref_lines; ctr->lcp_lines += jobs[t].ctr.lcp_lines;
+      ctr->kt_lines += jobs[t].ctr.kt_lines; ctr->u_lines += jobs[t].ctr.u_lines;
+      ctr->bm_lines += jobs[t].ctr.bm_lines;
     }
   }
   free(jobs);

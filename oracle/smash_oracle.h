@@ -78,6 +78,7 @@ typedef struct {
                              device path: it compares min(LCP,255)) */
   uint64_t kt_lines, u_lines;       /* accelerated path only */
   uint64_t last_kt, last_u;
+  uint64_t bm_lines, last_bm;       /* v3 bitmap */
 } orc_counters;
 
 /* Search accelerators of the device path (smash-paper_amd/csrc/
@@ -90,7 +91,25 @@ typedef struct {
   const uint8_t *U;
   const uint64_t *KT;
   uint32_t K;
+  /* v3: presence bitmap of every ACGT B-mer of the text (bit code(w)), and
+   * the set of bytes occurring in the text */
+  const uint64_t *BM;
+  uint32_t B;
+  uint8_t in_text[256];
 } orc_accel;
+uint32_t orc_accel_b(uint64_t N);
+/* BM must hold 4^B bits (zeroed by the callee) */
+void orc_build_bitmap(const orc_index *ix, uint32_t B, uint64_t *BM, uint8_t *in_text);
+/* v3 search: positions evaluated independently (MAM output is a function of
+ * the per-position matching statistics); same matches as
+ * orc_mam. */
+int orc_mam_v3(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
+               uint32_t L, uint32_t min_len, orc_match *out, uint32_t cap,
+               orc_counters *ctr);
+uint64_t orc_map_only_v3(const orc_index *ix, const orc_accel *acc,
+                         const uint8_t *reads, uint32_t L, uint64_t stride,
+                         uint64_t n, uint32_t min_len, int threads,
+                         orc_counters *ctr);
 uint32_t orc_accel_k(uint64_t N);
 void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT);
 int orc_mam_fast(const orc_index *ix, const orc_accel *acc, const uint8_t *P,

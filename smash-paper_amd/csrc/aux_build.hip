@@ -74,6 +74,35 @@ __global__ void k_kbounds(const uint32_t *__restrict__ code, uint64_t N, uint64_
   }
 }
 
+// presence bitmap of every ACGT B-mer of the text (bit = 2-bit code)
+__global__ void k_bitmap(const uint8_t *__restrict__ T, uint64_t N, int B,
+                         unsigned long long *bm) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const uint64_t mask = (1ull << (2 * B)) - 1;
+  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x + B <= N; x += stride) {
+    uint64_t c = 0;
+    bool ok = true;
+    for (int k = 0; k < B; ++k) {
+      const int v = acgt2(T[x + k]);
+      ok = ok && v >= 0;
+      c = ((c << 2) | uint64_t(v & 3)) & mask;
+    }
+    if (ok) atomicOr(&bm[c >> 6], 1ull << (c & 63));
+  }
+}
+
+__global__ void k_present(const uint8_t *__restrict__ T, uint64_t N, unsigned int *present) {
+  __shared__ unsigned int h[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += stride)
+    h[T[i]] = 1;
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += blockDim.x)
+    if (h[i]) present[i] = 1;
+}
+
 template <class IdxT>
 void build_aux_t(smash_index *ix, hipStream_t s) {
   const uint64_t N = ix->N;
@@ -94,6 +123,25 @@ void build_aux_t(smash_index *ix, hipStream_t s) {
   k_kbounds<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(code, N, ix->d_kmer);
   SMASH_HIPX(hipStreamSynchronize(s));
   dfree(code);
+  // B-mer presence bitmap: about log4(N)+1 characters (sparse: 1-10 % set)
+  int B = 8;
+  while (B < 18 && (1ull << (2 * (B - 1))) <= N) ++B;
+  ix->bitmap_b = uint32_t(B);
+  const uint64_t words = ((1ull << (2 * B)) >> 6) + 1;
+  if (!ix->d_bitmap) ix->d_bitmap = dalloc<uint64_t>(words);
+  SMASH_HIPX(hipMemsetAsync(ix->d_bitmap, 0, 8 * words, s));
+  k_bitmap<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
+      ix->d_text, N, B, reinterpret_cast<unsigned long long *>(ix->d_bitmap));
+  unsigned int *pres = dalloc<unsigned int>(256);
+  SMASH_HIPX(hipMemsetAsync(pres, 0, 1024, s));
+  k_present<<<grid_for(N, 256, 4096), 256, 0, s>>>(ix->d_text, N, pres);
+  unsigned int hp[256];
+  SMASH_HIPX(hipMemcpyAsync(hp, pres, 1024, hipMemcpyDeviceToHost, s));
+  SMASH_HIPX(hipStreamSynchronize(s));
+  dfree(pres);
+  for (int i = 0; i < 4; ++i) ix->in_text[i] = 0;
+  for (int c = 0; c < 256; ++c)
+    if (hp[c]) ix->in_text[c >> 6] |= 1ull << (c & 63);
   SMASH_HIPX(hipGetLastError());
 }
 

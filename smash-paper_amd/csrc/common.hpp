@@ -90,6 +90,9 @@ struct smash_index {
   uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
   uint64_t *d_kmer = nullptr;    // {lo,hi} per k-mer
   uint32_t kmer_k = 0;
+  uint64_t *d_bitmap = nullptr;  // B-mer presence bits (aux_build.hip)
+  uint32_t bitmap_b = 0;
+  uint64_t in_text[4] = {0, 0, 0, 0};   // bytes occurring in the text
   uint64_t *d_startpos = nullptr;
   uint64_t *d_sizes = nullptr;
   double build_seconds = 0;

@@ -36,7 +36,7 @@ void free_index(smash_index *ix) {
   (void)hipSetDevice(ix->device);
   dfree(ix->d_text); dfree(ix->d_sa); dfree(ix->d_isa); dfree(ix->d_lcp8);
   dfree(ix->d_ovf); dfree(ix->d_map); dfree(ix->d_startpos); dfree(ix->d_sizes);
-  dfree(ix->d_uniq); dfree(ix->d_kmer);
+  dfree(ix->d_uniq); dfree(ix->d_kmer); dfree(ix->d_bitmap);
   (void)hipSetDevice(cur);
   delete ix;
 }
@@ -54,7 +54,8 @@ void account(smash_index *ix) {
   const uint64_t N = ix->N;
   ix->device_bytes = (N + 64) + 2 * N * ix->idx_bytes + N + 16 * ix->n_ovf +
                      ix->map_bytes + 16 * ix->n_seq + (N + 64) +
-                     (ix->kmer_k ? 16ull << (2 * ix->kmer_k) : 0);
+                     (ix->kmer_k ? 16ull << (2 * ix->kmer_k) : 0) +
+                     (ix->bitmap_b ? (1ull << (2 * ix->bitmap_b)) / 8 : 0);
 }
 
 // u32 exact LCP from lcp8 + overflow (used when map.bin must be computed
@@ -377,5 +378,8 @@ extern "C" int smash_index_query(const smash_index *ix, smash_index_info *o) {
   o->kmer_k = ix->kmer_k;
   o->d_uniq = ix->d_uniq;
   o->d_kmer = ix->d_kmer;
+  o->bitmap_b = ix->bitmap_b;
+  o->d_bitmap = ix->d_bitmap;
+  for (int k = 0; k < 4; ++k) o->in_text[k] = ix->in_text[k];
   return SMASH_OK;
 }

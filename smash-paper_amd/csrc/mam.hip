@@ -40,7 +40,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam(
   const uint8_t *P = lds + threadIdx.x * row;
   MatchSink sink{out + r * cap, cap, 0};
   if (PLAIN) mam_read_plain(x, P, L, min_len, sink);
-  else mam_read(x, P, L, min_len, sink);
+  else mam_read_v3(x, P, L, min_len, sink);
   n_out[r] = sink.n;
 }
 
@@ -51,10 +51,10 @@ int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
            hipStream_t s) {
   constexpr int B = 128;
   uint32_t maxL = lens ? 255 : len;
-  uint32_t row = (maxL + 3) / 4;
+  uint32_t row = (maxL + 3) / 4 + 1;   // +1 word: lds_load8 over-read
   if ((row & 1) == 0) ++row;   // odd word stride: conflict-free LDS rows
   row *= 4;
-  const size_t lds = size_t(B) * row;
+  const size_t lds = size_t(B) * row + 16;
   const uint64_t blocks = (n_reads + B - 1) / B;
   DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
   for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
@@ -87,7 +87,7 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
     set_error("smash_map_batch: only the MAM modes (the SMASH default) run on the device");
     return SMASH_ERR_UNSUPPORTED;
   }
-  if (mode == SMASH_MODE_MAM && (!ix->d_uniq || !ix->d_kmer)) {
+  if (mode == SMASH_MODE_MAM && (!ix->d_uniq || !ix->d_kmer || !ix->d_bitmap)) {
     set_error("smash_map_batch: index lacks the search accelerators");
     return SMASH_ERR_ARG;
   }

@@ -17,8 +17,10 @@ struct DevIndex {
   const uint8_t *L8;    // min(LCP,255)
   const uint8_t *U;     // per-position unique-length bytes (aux_build.hip)
   const uint64_t *KT;   // k-mer -> {lo, hi}
+  const uint64_t *BM;   // B-mer presence bitmap
   uint64_t N, logN;
-  int K;
+  int K, B;
+  uint64_t in_text[4];  // bytes that occur in the text
 };
 
 template <class IdxT>
@@ -33,6 +35,9 @@ inline DevIndex<IdxT> make_dev_index(const smash_index *ix) {
   x.N = ix->N;
   x.logN = ix->logN;
   x.K = int(ix->kmer_k);
+  x.BM = ix->d_bitmap;
+  x.B = int(ix->bitmap_b);
+  for (int k = 0; k < 4; ++k) x.in_text[k] = ix->in_text[k];
   return x;
 }
 
@@ -297,6 +302,207 @@ __device__ void mam_read(const DevIndex<IdxT> &x, const uint8_t *P, uint32_t L,
     if (depth == 0 || !expand_link(x, depth, start, end)) {
       depth = 0; start = 0; end = N - 1;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v3 (SMASH_MODE_MAM): the MAM output is a function of the per-position
+// matching statistics -- p emits iff ms(p) >= min_len, the ms(p)-prefix occurs
+// once, and p is left-maximal -- so the streaming state may be dropped at any
+// prefix that provably cannot emit.  On top of (A), (B), (C):
+//  (F) while the state is shallow (depth < min_len), a prefix whose min_len
+//      window holds a byte absent from the text, or whose first/last B-mer is
+//      absent from the presence bitmap, cannot reach min_len: skip it with a
+//      reset (the reference would walk the suffix links down instead);
+//  (S) an interval of <= 32 suffixes finishes its traverse by comparing
+//      every candidate with the read (independent loads instead of the
+//      2*log2(n) dependent probes per character of top_down_faster); the
+//      suffixes sharing the longest match are the traverse's final interval.
+// ---------------------------------------------------------------------------
+constexpr int kScan = 32;
+
+// 8 read bytes at byte offset `off` of an LDS row (row 4-byte aligned and
+// padded; bytes past the read are masked by the callers)
+__device__ __forceinline__ uint64_t lds_load8(const uint8_t *P, uint64_t off) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(P);
+  const uint64_t q = off >> 2, sh = (off & 3) * 8;
+  const uint64_t lo = uint64_t(w[q]) | (uint64_t(w[q + 1]) << 32);
+  if (sh == 0) return lo;
+  return (lo >> sh) | (uint64_t(w[q + 2]) << (64 - sh));
+}
+
+// bytes of agreement of two 8-byte words, capped at lim (<= 8)
+__device__ __forceinline__ uint32_t agree8(uint64_t a, uint64_t b, uint32_t lim) {
+  const uint64_t d = a ^ b;
+  const uint32_t k = d ? uint32_t(__builtin_ctzll(d) >> 3) : 8u;
+  return k < lim ? k : lim;
+}
+
+template <class IdxT>
+__device__ __forceinline__ bool in_text(const DevIndex<IdxT> &x, uint8_t b) {
+  return (x.in_text[b >> 6] >> (b & 63)) & 1ull;
+}
+
+// lcp of P[off .. off+rem) with T[t ...]
+template <class IdxT>
+__device__ __forceinline__ uint64_t lcp_read_text(const DevIndex<IdxT> &x, const uint8_t *P,
+                                                  uint64_t off, uint64_t rem, uint64_t t,
+                                                  uint64_t first_word) {
+  uint64_t l = 0;
+  uint64_t tw = first_word;
+  for (;;) {
+    const uint32_t lim = rem - l < 8 ? uint32_t(rem - l) : 8u;
+    const uint32_t k = agree8(tw, lds_load8(P, off + l), lim);
+    l += k;
+    if (k < 8 || l >= rem) return l;
+    tw = load8(x.T, t + l);
+  }
+}
+
+// (F): can P[p .. p+min_len) occur?  next_p: where to resume when not
+template <class IdxT>
+__device__ bool window_ok(const DevIndex<IdxT> &x, const uint8_t *P, uint64_t p,
+                          uint32_t min_len, uint64_t &next_p) {
+  next_p = p + 1;
+  for (uint64_t k = p + min_len; k-- > p;)
+    if (!in_text(x, P[k])) { next_p = k + 1; return false; }
+  const int B = x.B;
+  if (B <= 0 || uint32_t(B) > min_len) return true;
+  const uint64_t mask = (1ull << (2 * B)) - 1;
+  uint64_t c0 = 0, c1 = 0;
+  const uint64_t q1 = p + min_len - B;
+  for (int k = 0; k < B; ++k) {
+    const int v0 = acgt_code(P[p + k]), v1 = acgt_code(P[q1 + k]);
+    if (v0 < 0 || v1 < 0) return true;     // no bitmap verdict
+    c0 = ((c0 << 2) | uint64_t(v0)) & mask;
+    c1 = ((c1 << 2) | uint64_t(v1)) & mask;
+  }
+  const uint64_t w0 = x.BM[c0 >> 6], w1 = x.BM[c1 >> 6];
+  return ((w0 >> (c0 & 63)) & (w1 >> (c1 & 63)) & 1ull) != 0;
+}
+
+// (S): final traverse state over a small interval
+template <class IdxT>
+__device__ void scan_small(const DevIndex<IdxT> &x, const uint8_t *P, uint64_t L,
+                           uint64_t p, uint64_t &depth, uint64_t &start, uint64_t &end,
+                           uint64_t &pos) {
+  const uint64_t d = depth, rem = L - p - d;
+  const uint64_t pw = lds_load8(P, p + d);
+  const uint32_t lim0 = rem < 8 ? uint32_t(rem) : 8u;
+  int64_t best = -1;
+  uint64_t bl = start, bh = start, bpos = 0;
+  for (uint64_t m0 = start; m0 <= end; m0 += 4) {
+    uint64_t sp[4], tw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sp[k] = m0 + k <= end ? uint64_t(x.SA[m0 + k]) : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tw[k] = m0 + k <= end ? load8(x.T, sp[k] + d) : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (m0 + k > end) break;
+      uint64_t l = agree8(tw[k], pw, lim0);
+      if (l == 8 && rem > 8)
+        l = 8 + lcp_read_text(x, P, p + d + 8, rem - 8, sp[k] + d + 8, load8(x.T, sp[k] + d + 8));
+      if (int64_t(l) > best) { best = int64_t(l); bl = bh = m0 + k; bpos = sp[k]; }
+      else if (int64_t(l) == best) bh = m0 + k;
+    }
+  }
+  depth = d + uint64_t(best);
+  start = bl;
+  end = bh;
+  pos = bpos;
+}
+
+template <class IdxT>
+__device__ void mam_read_v3(const DevIndex<IdxT> &x, const uint8_t *P, uint32_t L,
+                            uint32_t min_len, MatchSink &sink) {
+  const uint64_t N = x.N;
+  uint64_t depth = 0, start = 0, end = N - 1;
+  uint64_t prefix = 0, pos = 0;
+  bool have_pos = false;
+  while (prefix < L) {
+    if (depth < min_len) {                                   // (F)
+      if (prefix + min_len > L) break;
+      uint64_t nxt;
+      if (!window_ok(x, P, prefix, min_len, nxt)) {
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        prefix = nxt;
+        continue;
+      }
+    }
+    if (depth == 0 && prefix + uint64_t(x.K) <= L) {         // (C)
+      uint32_t w = 0;
+      bool ok = true;
+      for (int k = 0; k < x.K; ++k) {
+        const int v = acgt_code(P[prefix + k]);
+        ok = ok && v >= 0;
+        w = (w << 2) | uint32_t(v & 3);
+      }
+      if (ok) {
+        const uint64_t lo = x.KT[2 * uint64_t(w)], hi = x.KT[2 * uint64_t(w) + 1];
+        if (lo <= hi) { depth = uint64_t(x.K); start = lo; end = hi; have_pos = false; }
+      }
+    }
+    if (depth < L) {
+      while (prefix + depth < L) {
+        if (start == end) {                                  // (A)
+          if (!have_pos) { pos = x.SA[start]; have_pos = true; }
+          depth += lcp_read_text(x, P, prefix + depth, L - prefix - depth, pos + depth,
+                                 load8(x.T, pos + depth));
+          break;
+        }
+        if (end - start + 1 <= uint64_t(kScan)) {           // (S)
+          scan_small(x, P, L, prefix, depth, start, end, pos);
+          have_pos = start == end;
+          break;
+        }
+        uint64_t s = start, e = end;
+        if (!td_faster(x, sch(P[prefix + depth]), depth, s, e)) break;
+        depth += 1;
+        start = s;
+        end = e;
+        have_pos = false;
+        if (depth == L) break;
+      }
+    }
+    if (depth <= 1) {
+      depth = 0; start = 0; end = N - 1; have_pos = false;
+      ++prefix;
+      continue;
+    }
+    if (end == start) {
+      if (!have_pos) { pos = x.SA[start]; have_pos = true; }
+      if (depth >= min_len) {
+        const bool lm = (prefix == 0 || pos == 0) ? true
+                        : (sch(P[prefix - 1]) != sch(x.T[pos - 1]));
+        if (lm) sink.emit(pos, prefix, depth);
+      }
+      const uint64_t d = depth;                              // (B)
+      uint64_t j = 1;
+      bool hit = false;
+      while (j < d) {
+        const uint64_t u = load8(x.U, pos + j);
+        const uint64_t rem = d - j;
+        const uint32_t lim = rem < 8 ? uint32_t(rem) : 8u;
+        uint32_t k = 0;
+        while (k < lim && uint64_t(uint8_t(u >> (8 * k))) < d - j - k) ++k;
+        if (k < lim) { j += k; hit = true; break; }
+        j += lim;
+      }
+      prefix += j;
+      if (!hit) { depth = 0; start = 0; end = N - 1; have_pos = false; continue; }
+      depth = d - j;
+      start = end = x.ISA[pos + j];
+      have_pos = false;
+      if (!expand_link(x, depth, start, end)) { depth = 0; start = 0; end = N - 1; }
+      continue;
+    }
+    depth = depth - 1;
+    start = x.ISA[uint64_t(x.SA[start]) + 1];
+    end = x.ISA[uint64_t(x.SA[end]) + 1];
+    ++prefix;
+    have_pos = false;
+    if (depth == 0 || !expand_link(x, depth, start, end)) { depth = 0; start = 0; end = N - 1; }
   }
 }
 

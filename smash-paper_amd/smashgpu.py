@@ -50,7 +50,8 @@ class IndexInfo(C.Structure):
                 ("map_bytes", C.c_uint64), ("d_text", vp), ("d_sa", vp),
                 ("d_isa", vp), ("d_lcp8", vp), ("d_lcp_ovf", vp), ("d_map", vp),
                 ("device_bytes", C.c_uint64), ("build_seconds", C.c_double),
-                ("kmer_k", C.c_uint32), ("d_uniq", vp), ("d_kmer", vp)]
+                ("kmer_k", C.c_uint32), ("d_uniq", vp), ("d_kmer", vp),
+                ("bitmap_b", C.c_uint32), ("d_bitmap", vp), ("in_text", C.c_uint64 * 4)]
 
 
 class PipelineCfg(C.Structure):

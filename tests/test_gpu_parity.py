@@ -106,6 +106,11 @@ def test_device_accelerators_equal_oracle(gix, tiny_ix):
     assert i.kmer_k == K2
     assert np.array_equal(U[:i.N], U2[:i.N])
     assert np.array_equal(KT, KT2)
+    assert i.bitmap_b == tiny_ix.acc.B
+    BM = S.download(i.d_bitmap, 8 * ((1 << (2 * i.bitmap_b)) // 64 + 1), np.uint64)
+    assert np.array_equal(BM, tiny_ix._BM)
+    it = [(i.in_text[c >> 6] >> (c & 63)) & 1 for c in range(256)]
+    assert it == list(tiny_ix.acc.in_text)
 
 
 @pytest.mark.parametrize("s", ["s100", "s150"])

@@ -16,6 +16,26 @@ def test_fast_search_matches_reference_goldens(tiny_ix, s):
     reads = interleaved_reads(s)
     for i, e in enumerate(exp):
         assert tiny_ix.search_fast(reads[i].tobytes()) == e, i
+        assert tiny_ix.search_v3(reads[i].tobytes()) == e, i
+
+
+def test_v3_on_edge_reads(tiny_ix):
+    """reads with bytes absent from the text, 'n' (present in the text),
+    all-N, min_len windows at the read end, a palindrome."""
+    tiny_ix.accel()
+    T = tiny_ix.T[:tiny_ix.N]
+    rng = np.random.default_rng(5)
+    cases = []
+    for _ in range(300):
+        p = int(rng.integers(0, tiny_ix.N - 200))
+        r = bytearray(T[p:p + 120].tobytes())
+        for _k in range(int(rng.integers(0, 4))):
+            r[int(rng.integers(0, 120))] = int(rng.choice(list(b"acgtnz`$N")))
+        cases.append(bytes(r))
+    cases += [b"z" * 100, b"n" * 100, b"a" * 100, b"acgt" * 30]
+    for P in cases:
+        for ml in (20, 12, 30):
+            assert tiny_ix.search_v3(P, min_len=ml) == tiny_ix.search(P, min_len=ml)
 
 
 def test_fast_search_equals_plain_on_mid_genome():
@@ -33,8 +53,11 @@ def test_fast_search_equals_plain_on_mid_genome():
     c1, c2 = O.OrcCounters(), O.OrcCounters()
     for i in range(len(reads)):
         P = reads[i].tobytes()
-        assert ix.search_fast(P) == ix.search(P), i
+        exp = ix.search(P)
+        assert ix.search_fast(P) == exp, i
+        assert ix.search_v3(P) == exp, i
     n1, k1 = O.map_only(ix, reads, threads=4, count=True)
     n2, k2 = O.map_only_fast(ix, reads, threads=4, count=True)
-    assert n1 == n2
-    assert k2.lines() < k1.lines()     # the point of the accelerators
+    n3, k3 = O.map_only_v3(ix, reads, threads=4, count=True)
+    assert n1 == n2 == n3
+    assert k3.lines() < k2.lines() < k1.lines()     # the point of the accelerators
