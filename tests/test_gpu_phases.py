@@ -1,0 +1,90 @@
+"""Multi-GPU phase API on one device: W pipelines ("ranks") share one index;
+the collectives of smash-paper_amd/dist.py (all_to_all of keys and flags,
+all_gather of tails, all_reduce of counts) are emulated in-process with
+tensor slicing.  The result must equal one pipeline over the same pairs in
+global order (step, rank, pair).  (dist.py itself is run over real
+torch.distributed collectives in tests/test_dist_gloo.py.)"""
+import numpy as np
+import pytest
+
+from conftest import gold, interleaved_reads, load_bins, load_chrom_sizes
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+import smashgpu as S  # noqa: E402
+from dist import ShardedCounter  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def gix(tiny_fa):
+    return S.Index.from_fasta(tiny_fa)
+
+
+def _prev(tails, carried):
+    return ShardedCounter._prev(tails, carried)
+
+
+def run_emulated(ix, reads, W, per_rank, steps, starts, cs):
+    dev = torch.device("cuda")
+    pipes = [S.Pipeline(ix, cs, starts, reads.shape[1], per_rank) for _ in range(W)]
+    for p in pipes:
+        p.reset()
+    counts = [torch.zeros(len(starts), dtype=torch.int64, device=dev) for _ in range(W)]
+    carried = torch.full((1,), -1, dtype=torch.int64, device=dev)
+    for s in range(steps):
+        base = s * W * per_rank
+        sends, cnts = [], []
+        for r in range(W):
+            lo = base + r * per_rank
+            d = torch.from_numpy(np.ascontiguousarray(reads[2 * lo:2 * (lo + per_rank)])).to(dev)
+            pipes[r].phase_map(d, per_rank)
+            send = torch.empty((per_rank, 3), dtype=torch.int64, device=dev)
+            cnt = pipes[r].phase_export(W, base + r * per_rank, send)
+            sends.append(send)
+            cnts.append([int(c) for c in cnt])
+        offs = [np.cumsum([0] + c) for c in cnts]
+        # all_to_all: owner o receives segment o of every rank, rank order
+        flags_back = [[None] * W for _ in range(W)]
+        for o in range(W):
+            parts = [sends[r][offs[r][o]:offs[r][o + 1]] for r in range(W)]
+            recv = torch.cat(parts) if parts else torch.empty((0, 3), dtype=torch.int64, device=dev)
+            n = recv.shape[0]
+            flags = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+            pipes[o].dedup_owner(recv if n else torch.empty((1, 3), dtype=torch.int64, device=dev),
+                                 n, flags)
+            k = 0
+            for r in range(W):
+                m = cnts[r][o]
+                flags_back[r][o] = flags[k:k + m]
+                k += m
+        tails = []
+        for r in range(W):
+            back = torch.cat(flags_back[r]) if sum(cnts[r]) else torch.zeros(1, dtype=torch.uint8, device=dev)
+            pipes[r].phase_import(back)
+            tail = torch.empty(2, dtype=torch.int64, device=dev)
+            pipes[r].phase_positions(tail)
+            tails.append(tail)
+        T = torch.stack(tails)
+        for r in range(W):
+            pipes[r].phase_bin(_prev(T[:r], carried), counts[r])
+        carried = _prev(T, carried)
+    total = sum(c.cpu().numpy().astype(np.uint64) for c in counts)
+    st = [p.stats() for p in pipes]
+    return total, (sum(x.positions for x in st), sum(x.dups for x in st),
+                   sum(x.kept for x in st), sum(x.dupe_pairs for x in st))
+
+
+@pytest.mark.parametrize("W,per_rank,steps", [(2, 500, 2), (3, 111, 3), (4, 250, 1)])
+def test_phases_equal_single_pipeline(gix, W, per_rank, steps):
+    reads = interleaved_reads("s100")
+    n = W * per_rank * steps
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    one = S.Pipeline(gix, cs, starts, reads.shape[1], n)
+    one.reset()
+    c1 = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    one.count_batch(torch.from_numpy(np.ascontiguousarray(reads[:2 * n])).cuda(), n, c1)
+    s1 = one.stats()
+    total, st = run_emulated(gix, reads, W, per_rank, steps, starts, cs)
+    assert total.tolist() == c1.cpu().numpy().astype(np.uint64).tolist()
+    assert st == (s1.positions, s1.dups, s1.kept, s1.dupe_pairs)
