@@ -93,6 +93,7 @@ struct smash_index {
   uint64_t *d_bitmap = nullptr;  // B-mer presence bits (aux_build.hip)
   uint32_t bitmap_b = 0;
   uint64_t in_text[4] = {0, 0, 0, 0};   // bytes occurring in the text
+  uint64_t *d_work = nullptr;    // k_mam work counter (stream-ordered use)
   uint64_t *d_startpos = nullptr;
   uint64_t *d_sizes = nullptr;
   double build_seconds = 0;

@@ -36,12 +36,13 @@ void free_index(smash_index *ix) {
   (void)hipSetDevice(ix->device);
   dfree(ix->d_text); dfree(ix->d_sa); dfree(ix->d_isa); dfree(ix->d_lcp8);
   dfree(ix->d_ovf); dfree(ix->d_map); dfree(ix->d_startpos); dfree(ix->d_sizes);
-  dfree(ix->d_uniq); dfree(ix->d_kmer); dfree(ix->d_bitmap);
+  dfree(ix->d_uniq); dfree(ix->d_kmer); dfree(ix->d_bitmap); dfree(ix->d_work);
   (void)hipSetDevice(cur);
   delete ix;
 }
 
 void upload_tables(smash_index *ix, hipStream_t s) {
+  if (!ix->d_work) ix->d_work = dalloc<uint64_t>(1);
   ix->d_startpos = dalloc<uint64_t>(ix->n_seq);
   ix->d_sizes = dalloc<uint64_t>(ix->n_seq);
   SMASH_HIPX(hipMemcpyAsync(ix->d_startpos, ix->startpos.data(), 8 * ix->n_seq,

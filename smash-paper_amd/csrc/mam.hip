@@ -18,30 +18,41 @@
 namespace smash {
 namespace {
 
+// Persistent grid sized to the resident capacity; each lane pulls the next
+// read from a device work counter as soon as its previous read is done, so a
+// slow read (repeats: large intervals) delays only its own lane instead of a
+// whole block.  The read is copied into the lane's LDS row.
 template <class IdxT, int BLOCK, bool PLAIN>
 __global__ __launch_bounds__(BLOCK) void k_mam(
     DevIndex<IdxT> x, const uint8_t *__restrict__ seqs, uint64_t stride,
     const uint16_t *__restrict__ lens, uint32_t len0, uint64_t n_reads,
     uint32_t min_len, uint64_t *__restrict__ out, uint32_t cap,
-    uint32_t *__restrict__ n_out, uint32_t row) {
+    uint32_t *__restrict__ n_out, uint32_t row, unsigned long long *work) {
   extern __shared__ uint8_t lds[];
-  const uint64_t r0 = uint64_t(blockIdx.x) * BLOCK;
-  const uint32_t nr = uint32_t(n_reads - r0 < BLOCK ? n_reads - r0 : BLOCK);
-  // stage this block's reads (coalesced byte copy)
-  for (uint32_t rr = 0; rr < nr; ++rr) {
-    const uint32_t L = lens ? lens[r0 + rr] : len0;
-    const uint8_t *src = seqs + (r0 + rr) * stride;
-    for (uint32_t k = threadIdx.x; k < L; k += BLOCK) lds[rr * row + k] = src[k];
+  uint8_t *P = lds + threadIdx.x * row;
+  for (;;) {
+    const uint64_t r = atomicAdd(work, 1ull);
+    if (r >= n_reads) break;
+    const uint32_t L = lens ? lens[r] : len0;
+    // lane-private copy with aligned 4-byte global loads
+    const uint8_t *src = seqs + r * stride;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+    const uint32_t sh = uint32_t(a & 3);
+    const uint32_t nw = (L + sh + 3) >> 2;
+    for (uint32_t k = 0; k < nw; ++k) {
+      const uint32_t v = w[k];
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const int32_t o = int32_t(4 * k + b) - int32_t(sh);
+        if (o >= 0 && uint32_t(o) < L) P[o] = uint8_t(v >> (8 * b));
+      }
+    }
+    MatchSink sink{out + r * cap, cap, 0};
+    if (PLAIN) mam_read_plain(x, P, L, min_len, sink);
+    else mam_read_v3(x, P, L, min_len, sink);
+    n_out[r] = sink.n;
   }
-  __syncthreads();
-  if (threadIdx.x >= nr) return;
-  const uint64_t r = r0 + threadIdx.x;
-  const uint32_t L = lens ? lens[r] : len0;
-  const uint8_t *P = lds + threadIdx.x * row;
-  MatchSink sink{out + r * cap, cap, 0};
-  if (PLAIN) mam_read_plain(x, P, L, min_len, sink);
-  else mam_read_v3(x, P, L, min_len, sink);
-  n_out[r] = sink.n;
 }
 
 template <class IdxT, bool PLAIN>
@@ -55,15 +66,19 @@ int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   if ((row & 1) == 0) ++row;   // odd word stride: conflict-free LDS rows
   row *= 4;
   const size_t lds = size_t(B) * row + 16;
-  const uint64_t blocks = (n_reads + B - 1) / B;
+  int per_cu = 0, cus = 0;
+  SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void *>(k_mam<IdxT, B, PLAIN>), B, lds));
+  SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
+  if (per_cu < 1) per_cu = 1;
+  uint64_t blocks = uint64_t(per_cu) * uint64_t(cus);
+  const uint64_t need = (n_reads + B - 1) / B;
+  if (blocks > need) blocks = need;
   DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
-  for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
-    const uint64_t nb = blocks - b0 < (1u << 30) ? blocks - b0 : (1u << 30);
-    const uint64_t off = b0 * B;
-    k_mam<IdxT, B, PLAIN><<<unsigned(nb), B, lds, s>>>(
-        x, seqs + off * stride, stride, lens ? lens + off : nullptr, len,
-        n_reads - off, min_len, out + off * cap, cap, n_out + off, row);
-  }
+  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
+  k_mam<IdxT, B, PLAIN><<<unsigned(blocks), B, lds, s>>>(
+      x, seqs, stride, lens, len, n_reads, min_len, out, cap, n_out, row,
+      reinterpret_cast<unsigned long long *>(ix->d_work));
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }
