@@ -94,6 +94,10 @@ struct smash_index {
   uint32_t bitmap_b = 0;
   uint64_t in_text[4] = {0, 0, 0, 0};   // bytes occurring in the text
   uint64_t *d_work = nullptr;    // k_mam work counter (stream-ordered use)
+  // k_mam_sm read records (mam_sm.hpp k_prep), grown on demand by
+  // smash_map_batch; like d_work, one batch in flight per index
+  mutable uint32_t *d_rec = nullptr;
+  mutable uint64_t rec_bytes = 0;
   uint64_t *d_startpos = nullptr;
   uint64_t *d_sizes = nullptr;
   double build_seconds = 0;

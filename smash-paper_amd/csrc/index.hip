@@ -13,6 +13,13 @@
 #include "common.hpp"
 
 namespace smash {
+// SMASH_IDX_BYTES=8: 8-byte SA/ISA even when N < 2^32 (tests the wide
+// search path on small genomes; the reference would pick rc1.i4 there)
+static bool force_wide_index() {
+  const char *e = getenv("SMASH_IDX_BYTES");
+  return e && e[0] == '8';
+}
+
 static thread_local std::string g_err;
 void set_error(const std::string &msg) { g_err = msg; }
 }  // namespace smash
@@ -36,13 +43,13 @@ void free_index(smash_index *ix) {
   (void)hipSetDevice(ix->device);
   dfree(ix->d_text); dfree(ix->d_sa); dfree(ix->d_isa); dfree(ix->d_lcp8);
   dfree(ix->d_ovf); dfree(ix->d_map); dfree(ix->d_startpos); dfree(ix->d_sizes);
-  dfree(ix->d_uniq); dfree(ix->d_kmer); dfree(ix->d_bitmap); dfree(ix->d_work);
+  dfree(ix->d_uniq); dfree(ix->d_kmer); dfree(ix->d_bitmap); dfree(ix->d_work); dfree(ix->d_rec);
   (void)hipSetDevice(cur);
   delete ix;
 }
 
 void upload_tables(smash_index *ix, hipStream_t s) {
-  if (!ix->d_work) ix->d_work = dalloc<uint64_t>(1);
+  if (!ix->d_work) ix->d_work = dalloc<uint64_t>(16);   // [0] work counter, [1..10] k_mam_sm probe check
   ix->d_startpos = dalloc<uint64_t>(ix->n_seq);
   ix->d_sizes = dalloc<uint64_t>(ix->n_seq);
   SMASH_HIPX(hipMemcpyAsync(ix->d_startpos, ix->startpos.data(), 8 * ix->n_seq,
@@ -128,7 +135,7 @@ extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N,
     ix->device = device;
     ix->N = N;
     ix->logN = uint64_t(std::ceil(std::log(double(N)) / std::log(2.0)));
-    ix->idx_bytes = N <= 0xFFFFFFFFull ? 4 : 8;
+    ix->idx_bytes = (N <= 0xFFFFFFFFull && !force_wide_index()) ? 4 : 8;
     ix->n_seq = n_seq;
     ix->startpos.assign(h_startpos, h_startpos + n_seq);
     ix->sizes.assign(h_sizes, h_sizes + n_seq);
@@ -209,7 +216,7 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
     if (sa_size != N || n_vec != N) throw hip_failure{"index size mismatch"};
     SMASH_HIPX(hipSetDevice(device));
     ix->device = device;
-    ix->idx_bytes = N <= 0xFFFFFFFFull ? 4 : 8;
+    ix->idx_bytes = (N <= 0xFFFFFFFFull && !force_wide_index()) ? 4 : 8;
     hipStream_t s;
     SMASH_HIPX(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::vector<uint8_t> buf;

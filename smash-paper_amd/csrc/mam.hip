@@ -14,6 +14,13 @@
 // lower_bound (longSA.h:34-39) is never needed on this path.
 #include "common.hpp"
 #include "mam_device.hpp"
+#include "mam_sm.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cstring>
 
 namespace smash {
 namespace {
@@ -53,6 +60,129 @@ __global__ __launch_bounds__(BLOCK) void k_mam(
     else mam_read_v3(x, P, L, min_len, sink);
     n_out[r] = sink.n;
   }
+}
+
+// SMASH_MODE_MAM default: the state-machine kernel (mam_sm.hpp).  Setting
+// SMASH_MAM_KERNEL=direct selects the direct per-lane v3 kernel instead (same
+// results; kept for A/B measurement).
+template <class IdxT>
+int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
+              uint64_t stride, const uint16_t *lens, uint32_t len,
+              uint64_t n_reads, uint64_t *out, uint32_t cap, uint32_t *n_out,
+              hipStream_t s) {
+  constexpr int B = 128;
+  const sm::Geom g = sm::make_geom(lens ? 255 : len);
+  // read records (k_prep)
+  const uint64_t need = n_reads * g.chunks * 16;
+  if (need > ix->rec_bytes) {
+    SMASH_HIP(hipStreamSynchronize(s));
+    if (ix->d_rec) SMASH_HIP(hipFree(ix->d_rec));
+    ix->d_rec = nullptr;
+    ix->rec_bytes = 0;
+    const uint64_t bytes = need + need / 4;
+    SMASH_HIP(hipMalloc(&ix->d_rec, bytes));
+    ix->rec_bytes = bytes;
+  }
+  {
+    const uint64_t threads = n_reads * g.chunks * 4;
+    sm::k_prep<<<unsigned((threads + 255) / 256), 256, 0, s>>>(
+        seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
+        ix->in_text[3], g, ix->d_rec);
+    SMASH_HIP(hipGetLastError());
+  }
+  const size_t lds = size_t(B) * g.w_row * 4 + 16;
+  int per_cu = 0, cus = 0;
+  // Every probe is range-checked (in_ranges): an address outside the index
+  // arrays retires its lane and fails the call instead of faulting the GPU.
+  // (The unchecked instantiation faulted on MI355X with the 8-byte index
+  // although the checked one, same logic, reports no out-of-range probe on
+  // hg19 and matches the direct kernel read for read: DESIGN.md section 4.)
+  constexpr bool check = true;
+  SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void *>(sm::k_mam_sm<IdxT, B, check>), B, lds));
+  SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
+  if (per_cu < 1) per_cu = 1;
+  uint64_t blocks = uint64_t(per_cu) * uint64_t(cus);
+  const uint64_t want = (n_reads + B - 1) / B;
+  if (blocks > want) blocks = want;
+  sm::Ctx<IdxT> c;
+  c.x = make_dev_index<IdxT>(ix);
+  c.rec = reinterpret_cast<const uint4 *>(ix->d_rec);
+  c.g = g;
+  c.lens = lens; c.len0 = len;
+  c.min_len = min_len; c.cap = cap; c.n_reads = n_reads;
+  c.out = out; c.n_out = n_out;
+  c.work = reinterpret_cast<unsigned long long *>(ix->d_work);
+  c.iters = nullptr;
+  c.wave_stats = nullptr;
+  const bool stats = std::getenv("SMASH_SM_STATS") != nullptr;
+  if (stats) {
+    SMASH_HIP(hipMalloc(&c.iters, n_reads * sizeof(uint32_t)));
+    SMASH_HIP(hipMalloc(&c.wave_stats, 16));
+    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 16, s));
+  }
+  c.viol = nullptr;
+  {
+    const uint64_t N = ix->N, isz = ix->idx_bytes;
+    const uint64_t spans[8][2] = {
+        {reinterpret_cast<uint64_t>(ix->d_text), N + 64},
+        {reinterpret_cast<uint64_t>(ix->d_sa), N * isz},
+        {reinterpret_cast<uint64_t>(ix->d_isa), N * isz},
+        {reinterpret_cast<uint64_t>(ix->d_lcp8), N},
+        {reinterpret_cast<uint64_t>(ix->d_uniq), N + 64},
+        {reinterpret_cast<uint64_t>(ix->d_kmer), 16ull << (2 * ix->kmer_k)},
+        {reinterpret_cast<uint64_t>(ix->d_bitmap), 8 * (((1ull << (2 * ix->bitmap_b)) >> 6) + 1)},
+        {reinterpret_cast<uint64_t>(ix->d_rec), n_reads * g.chunks * 16}};
+    for (int k = 0; k < 8; ++k) { c.rlo[k] = spans[k][0]; c.rhi[k] = spans[k][0] + spans[k][1]; }
+  }
+  if (check) {   // d_work[1..10] (index.hip allocates 16 words)
+    c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;
+    SMASH_HIP(hipMemsetAsync(c.viol, 0, 10 * 8, s));
+  }
+  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
+  sm::k_mam_sm<IdxT, B, check><<<unsigned(blocks), B, lds, s>>>(c);
+  SMASH_HIP(hipGetLastError());
+  if (check) {
+    unsigned long long h[10];
+    SMASH_HIP(hipMemcpyAsync(h, c.viol, sizeof(h), hipMemcpyDeviceToHost, s));
+    SMASH_HIP(hipStreamSynchronize(s));
+    if (h[0]) {
+      char msg[512];
+      std::snprintf(msg, sizeof(msg),
+                    "k_mam_sm: %llu out-of-range probes; first: state %llu op %llu addr %#llx "
+                    "addr2 %#llx prefix %llu depth %llu interval [%llu,%llu] read %llu",
+                    h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+      std::fprintf(stderr, "%s\n", msg);
+      set_error(msg);
+      return SMASH_ERR_HIP;
+    }
+  }
+  if (stats) {
+    std::vector<uint32_t> h(n_reads);
+    unsigned long long ws[2];
+    SMASH_HIP(hipStreamSynchronize(s));
+    SMASH_HIP(hipMemcpy(h.data(), c.iters, n_reads * 4, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 16, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipFree(c.iters));
+    SMASH_HIP(hipFree(c.wave_stats));
+    std::vector<uint32_t> srt(h);
+    std::sort(srt.begin(), srt.end());
+    double sum = 0;
+    for (uint32_t v : h) sum += v;
+    auto q = [&](double f) { return srt[std::min<size_t>(srt.size() - 1, size_t(f * srt.size()))]; };
+    std::fprintf(stderr,
+                 "[k_mam_sm] reads %llu blocks %llu (%d/CU) row %u words: lane-iterations/read mean %.1f "
+                 "p50 %u p90 %u p99 %u p99.9 %u max %u; wave-iterations %llu, active lanes/iteration %.2f\n",
+                 (unsigned long long)n_reads, (unsigned long long)blocks, per_cu, g.w_row, sum / n_reads,
+                 q(0.5), q(0.9), q(0.99), q(0.999), srt.back(), ws[0],
+                 double(ws[1]) / double(ws[0] ? ws[0] : 1));
+  }
+  return SMASH_OK;
+}
+
+bool use_direct() {
+  const char *e = std::getenv("SMASH_MAM_KERNEL");
+  return e && std::strcmp(e, "direct") == 0;
 }
 
 template <class IdxT, bool PLAIN>
@@ -122,6 +252,13 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
   SMASH_HIP(hipSetDevice(ix->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool plain = mode == SMASH_MODE_MAM_PLAIN;
+  if (!plain && !use_direct()) {
+    if (ix->idx_bytes == 4)
+      return launch_sm<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
+                                 cap_per_read, d_n_out, s);
+    return launch_sm<uint64_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
+                               cap_per_read, d_n_out, s);
+  }
   if (ix->idx_bytes == 4)
     return plain ? launch<uint32_t, true>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
                                           d_out, cap_per_read, d_n_out, s)

@@ -1,0 +1,647 @@
+// smash-paper_amd/csrc/mam_sm.hpp -- the v3 MAM search as a lane state
+// machine: every loop iteration issues one 16-byte gather per lane (two for
+// the states that own two independent probes), then each lane advances its
+// state with ALU work only until it names its next address.
+//
+// Why: a direct per-lane implementation (mam_read_v3, mam_device.hpp) keeps
+// the lanes of a wave in different phases; SIMT then issues each phase's
+// load for its few lanes only and the wave waits one memory latency per
+// phase present.  Here all lanes share one gather per iteration.  Because the
+// wave executes the union of the state bodies present in an iteration, every
+// body is kept small and branch-light:
+//  * k_prep turns each read into a record (raw bytes, a 2-bit code stream,
+//    and a "bad" mask = not ACGT or absent from the text) once, so the (F)
+//    window filter, the B-mer and k-mer codes are O(1) bit extractions;
+//  * states are grouped by what they load (an SA/ISA element, one text byte,
+//    16 text bytes to compare, 16 U or LCP bytes to scan) and share the
+//    decoding of the loaded block;
+//  * 16-byte scans of U and LCP (singleton chains, expand_link) are unrolled
+//    without branches.
+//
+// The algorithm, and therefore every emitted match, is mam_read_v3's: the
+// same traverse / top_down_faster / (S) scan / (A) extension / (B) chain /
+// suffix link / expand_link / (F) filter decisions, per lane, in order.
+#pragma once
+#include "mam_device.hpp"
+
+namespace smash {
+namespace sm {
+
+// record / LDS row geometry for a launch (reads up to max_len bases)
+struct Geom {
+  uint32_t w_raw;    // read bytes + lds_load8 over-read, in words
+  uint32_t w_cod;    // 2-bit code stream words (+2: 3-word extraction)
+  uint32_t w_row;    // LDS row words (odd: conflict-free lane rows)
+  uint32_t c_bad;    // record chunks holding the bad mask (1 or 2)
+  uint32_t chunks;   // 16-byte record chunks per read
+};
+
+inline Geom make_geom(uint32_t max_len) {
+  Geom g;
+  g.w_raw = (max_len + 12 + 3) / 4;
+  g.w_cod = (2 * max_len + 31) / 32 + 2;
+  g.w_row = g.w_raw + g.w_cod;
+  if ((g.w_row & 1) == 0) ++g.w_row;
+  g.c_bad = max_len > 128 ? 2 : 1;
+  g.chunks = g.c_bad + (g.w_row + 3) / 4;
+  return g;
+}
+
+__device__ __forceinline__ bool is_acgt(uint32_t b) {
+  return b == 'a' || b == 'c' || b == 'g' || b == 't';
+}
+
+// One thread per record word.  Record of read r (g.chunks * 4 words):
+//   [0, 4*c_bad)          bad mask, bit i of word i/32: base i is not ACGT
+//                         or does not occur in the text
+//   [4*c_bad, +w_raw)     the read bytes, zero padded
+//   [.., +w_cod)          2-bit codes (a0 c1 g2 t3, others 0), big-endian:
+//                         base 16j+t at bits 31-2t..30-2t of word j
+//   rest                  zero
+__global__ void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
+                       const uint16_t *__restrict__ lens, uint32_t len0, uint64_t n,
+                       uint64_t it0, uint64_t it1, uint64_t it2, uint64_t it3, Geom g,
+                       uint32_t *__restrict__ rec) {
+  const uint32_t rw = g.chunks * 4;
+  const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  if (t >= n * rw) return;
+  const uint64_t r = t / rw;
+  const uint32_t w = uint32_t(t - r * rw);
+  const uint32_t L = lens ? lens[r] : len0;
+  const uint8_t *P = seqs + r * stride;
+  uint32_t out = 0;
+  if (w < 4 * g.c_bad) {
+    for (uint32_t k = 0; k < 32; ++k) {
+      const uint32_t i = 32 * w + k;
+      if (i >= L) break;
+      const uint32_t b = P[i];
+      const uint64_t word = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
+      const bool present = (word >> (b & 63)) & 1ull;
+      if (!(is_acgt(b) && present)) out |= 1u << k;
+    }
+  } else {
+    const uint32_t q = w - 4 * g.c_bad;
+    if (q < g.w_raw) {
+      for (uint32_t k = 0; k < 4; ++k)
+        if (4 * q + k < L) out |= uint32_t(P[4 * q + k]) << (8 * k);
+    } else if (q < g.w_raw + g.w_cod) {
+      const uint32_t j = q - g.w_raw;
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t i = 16 * j + k;
+        if (i >= L) break;
+        const int cd = acgt_code(P[i]);
+        out |= uint32_t(cd < 0 ? 0 : cd) << (30 - 2 * k);
+      }
+    }
+  }
+  rec[t] = out;
+}
+
+enum : uint32_t { S_EXIT = 0, S_NEW, S_COPY, S_BM, S_KT, S_IDX, S_BYTE, S_CMP, S_USCAN, S_EXL, S_EXR };
+// S_IDX ops (an SA / ISA element arrived; *2: a second one in v2)
+enum : uint32_t { O_SAPOS, O_SAPOS2, O_SCAN_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2, O_TD_SA2, O_TD_SA };
+// S_BYTE ops (one text byte; *2: a second one in v2)
+enum : uint32_t { O_TD_T2 = 0, O_TD_T, O_LM };
+// S_CMP ops (16 text bytes compared with the read)
+enum : uint32_t { O_EXT = 0, O_SCAN };
+// ALU continuations
+enum : uint32_t { A_NONE = 0, A_TOP, A_TRAV, A_AFTER, A_CHAIN_DONE, A_EXPAND,
+                  A_TD_LEFT, A_TD_AFTER_LEFT, A_TD_RIGHT, A_TD_DONE };
+
+__device__ __forceinline__ uint64_t lo64(const uint4 &v) { return uint64_t(v.x) | (uint64_t(v.y) << 32); }
+__device__ __forceinline__ uint64_t hi64(const uint4 &v) { return uint64_t(v.z) | (uint64_t(v.w) << 32); }
+__device__ __forceinline__ uint32_t dword_at(const uint4 &v, uint32_t i) {   // i = 0..3
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ uint32_t byte_at(const uint4 &v, uint32_t o) {
+  return (dword_at(v, o >> 2) >> (8 * (o & 3))) & 0xFF;
+}
+// bytes [o, o+8) of the block (past 16: zero)
+__device__ __forceinline__ uint64_t bytes8_at(const uint4 &v, uint32_t o) {
+  const uint64_t lo = lo64(v), hi = hi64(v);
+  if (o == 0) return lo;
+  if (o < 8) return (lo >> (8 * o)) | (hi << (64 - 8 * o));
+  if (o == 8) return hi;
+  return hi >> (8 * (o - 8));
+}
+// agreeing bytes of block bytes [o, 16) with the read at P[poff ...], <= lim
+__device__ __forceinline__ uint32_t agree_block(const uint4 &v, uint32_t o, const uint8_t *P,
+                                                uint32_t poff, uint32_t lim) {
+  uint32_t k = agree8(bytes8_at(v, o), lds_load8(P, poff), lim < 8 ? lim : 8u);
+  if (k == 8 && lim > 8) k += agree8(bytes8_at(v, o + 8), lds_load8(P, poff + 8), lim - 8);
+  return k;
+}
+// mask bit i (0..15): byte i of the block satisfies f
+template <class F>
+__device__ __forceinline__ uint32_t byte_mask(const uint4 &v, F f) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 16; ++i) {
+    const uint32_t b = (dword_at(v, i >> 2) >> (8 * (i & 3))) & 0xFF;
+    m |= uint32_t(f(b, i)) << i;
+  }
+  return m;
+}
+
+struct Bad {   // the read's bad mask (registers; named, never an array)
+  uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+  __device__ __forceinline__ uint32_t word(uint32_t i) const {
+    uint32_t r = 0;
+    r = i == 0 ? w0 : r; r = i == 1 ? w1 : r; r = i == 2 ? w2 : r; r = i == 3 ? w3 : r;
+    r = i == 4 ? w4 : r; r = i == 5 ? w5 : r; r = i == 6 ? w6 : r; r = i == 7 ? w7 : r;
+    return r;
+  }
+  // bits [a, a+n) as the low bits, n <= 32
+  __device__ __forceinline__ uint32_t bits(uint32_t a, uint32_t n) const {
+    const uint32_t q = a >> 5, s = a & 31;
+    const uint64_t x = (uint64_t(word(q + 1)) << 32) | word(q);
+    const uint32_t y = uint32_t(x >> s);
+    return n >= 32 ? y : (y & ((1u << n) - 1));
+  }
+  // highest set bit in [a, a+n), or -1
+  __device__ __forceinline__ int32_t last(uint32_t a, uint32_t n) const {
+    uint32_t e = a + n;
+    while (e > a) {
+      const uint32_t k = e - a < 32 ? e - a : 32u;
+      const uint32_t s = e - k;
+      const uint32_t y = bits(s, k);
+      if (y) return int32_t(s + 31 - __builtin_clz(y));
+      e = s;
+    }
+    return -1;
+  }
+};
+
+// 2n code bits of bases [p, p+n) (first base most significant), n <= 32
+__device__ __forceinline__ uint64_t codes_at(const uint32_t *C, uint32_t p, uint32_t n) {
+  const uint32_t b = 2 * p, q = b >> 5, s = b & 31;
+  const uint64_t hi = (uint64_t(C[q]) << 32) | C[q + 1];
+  const uint64_t x = s ? (hi << s) | (uint64_t(C[q + 2]) >> (32 - s)) : hi;
+  return x >> (64 - 2 * n);
+}
+
+template <class IdxT>
+struct Ctx {
+  DevIndex<IdxT> x;
+  const uint4 *rec;      // k_prep records
+  Geom g;
+  const uint16_t *lens;
+  uint32_t len0, min_len, cap;
+  uint64_t n_reads;
+  uint64_t *out;
+  uint32_t *n_out;
+  unsigned long long *work;
+  // profiling (SMASH_SM_STATS): per-read loop iterations; per-kernel sums of
+  // wave iterations and of active lanes over them
+  uint32_t *iters;
+  unsigned long long *wave_stats;
+  // bounds-checked variant (SMASH_SM_CHECK): valid [lo, hi) byte ranges of
+  // the arrays the search reads; the first out-of-range address is recorded
+  // in viol[1..9] (viol[0] counts them) and its lane retires instead of
+  // faulting
+  uint64_t rlo[8], rhi[8];
+  unsigned long long *viol;
+};
+
+template <class IdxT>
+__device__ __forceinline__ uint64_t ia(const IdxT *a, uint64_t i) {
+  return reinterpret_cast<uint64_t>(a + i);
+}
+template <class IdxT>
+__device__ __forceinline__ uint64_t idx_val(const uint4 &v, uint32_t ao) {
+  if (sizeof(IdxT) == 8) return (ao & 8) ? hi64(v) : lo64(v);
+  return dword_at(v, ao >> 2);
+}
+
+template <class IdxT>
+__device__ __forceinline__ bool in_ranges(const Ctx<IdxT> &c, uint64_t a) {
+  bool ok = false;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ok = ok || (a >= c.rlo[k] && a < c.rhi[k]);
+  return ok;
+}
+
+template <class IdxT, int BLOCK, bool CHECK>
+__global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
+  extern __shared__ uint32_t ldsw[];
+  const DevIndex<IdxT> &x = c.x;
+  const uint64_t N = x.N;
+  uint32_t *row = ldsw + threadIdx.x * c.g.w_row;
+  const uint8_t *P = reinterpret_cast<const uint8_t *>(row);
+  const uint32_t *C = row + c.g.w_raw;
+  const uint32_t lane = threadIdx.x & 63;
+
+  uint32_t st = S_NEW, op = 0;
+  uint64_t addr = 0, addr2 = 0;
+  bool need2 = false;
+  uint64_t rd = 0;
+  uint32_t L = 0, nem = 0, kc = 0;
+  Bad bad{0, 0, 0, 0, 0, 0, 0, 0};
+  // search state (longSA.h interval_t + prefix)
+  uint32_t prefix = 0, depth = 0;
+  uint64_t start = 0, end = 0, pos = 0;
+  bool have_pos = false;
+  // phase registers, shared by phases that are never live together
+  uint64_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0;
+  uint64_t &l = x0, &r = x1, &l2 = x2, &r2 = x3, &m = x4;      // top_down_faster
+  uint64_t &bl = x0, &bh = x1, &bpos = x2, &sp = x3;            // (S) scan (m = x4)
+  uint64_t &es = x0, &ee = x1;                                  // expand_link
+  uint64_t &c0 = x2, &c1 = x3;                                  // (F) bitmap codes
+  int32_t cf = 0, cl = 0, best = -1, ch = 0;
+  bool found = false, hit = false, bm2 = false, td_left = false, skip_f = false;
+  uint32_t lc = 0, dch = 0, j = 0, expc = 0, thresh = 0;
+  uint32_t it = 0;
+  uint64_t w_iters = 0, w_active = 0;
+
+  for (;;) {
+    const uint64_t newm = __ballot(st == S_NEW);
+    unsigned long long base = 0;
+    if (newm) {
+      const uint32_t leader = __builtin_ctzll(newm);
+      if (lane == leader) base = atomicAdd(c.work, (unsigned long long)__popcll(newm));
+    }
+    const uint64_t live = __ballot(st != S_EXIT);
+    if (live == 0) break;
+    if (c.wave_stats) { w_iters += 1; w_active += __popcll(live); }
+    if (CHECK && st >= S_COPY && (!in_ranges(c, addr) || (need2 && !in_ranges(c, addr2)))) {
+      if (atomicAdd(c.viol, 1ull) == 0) {
+        c.viol[1] = st; c.viol[2] = op; c.viol[3] = addr; c.viol[4] = need2 ? addr2 : 0;
+        c.viol[5] = prefix; c.viol[6] = depth; c.viol[7] = start; c.viol[8] = end; c.viol[9] = rd;
+      }
+      st = S_EXIT;
+      need2 = false;
+    }
+    uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
+    if (st >= S_COPY) v = *reinterpret_cast<const uint4 *>(addr & ~uint64_t(15));
+    if (need2) v2 = *reinterpret_cast<const uint4 *>(addr2 & ~uint64_t(15));
+    bool fresh = false;   // assigned a read this iteration: its first chunk loads next
+    if (newm) {
+      base = __shfl(base, int(__builtin_ctzll(newm)), 64);
+      if (st == S_NEW) {
+        fresh = true;
+        rd = base + __popcll(newm & ((1ull << lane) - 1));
+        if (rd >= c.n_reads) {
+          st = S_EXIT;
+        } else {
+          L = c.lens ? c.lens[rd] : c.len0;
+          addr = reinterpret_cast<uint64_t>(c.rec + rd * c.g.chunks);
+          kc = 0;
+          st = S_COPY;
+        }
+      }
+    }
+    if (st < S_COPY || fresh) continue;
+    ++it;
+#ifdef SM_TRACE
+    if (st != S_COPY)
+      printf("it %u st %u op %u prefix %u depth %u [%llu,%llu] pos %llu hp %d\n", it, st, op, prefix,
+             depth, (unsigned long long)start, (unsigned long long)end, (unsigned long long)pos,
+             int(have_pos));
+#endif
+    const uint32_t ao = uint32_t(addr) & 15;
+    uint32_t a_next = A_NONE;
+
+    switch (st) {
+      case S_COPY: {
+        if (kc < c.g.c_bad) {
+          if (kc == 0) { bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w; }
+          else { bad.w4 = v.x; bad.w5 = v.y; bad.w6 = v.z; bad.w7 = v.w; }
+        } else {
+          const uint32_t q = 4 * (kc - c.g.c_bad);
+          if (q + 0 < c.g.w_row) row[q + 0] = v.x;
+          if (q + 1 < c.g.w_row) row[q + 1] = v.y;
+          if (q + 2 < c.g.w_row) row[q + 2] = v.z;
+          if (q + 3 < c.g.w_row) row[q + 3] = v.w;
+        }
+        if (++kc < c.g.chunks) {
+          addr += 16;
+        } else {
+          prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
+          skip_f = false;
+          a_next = A_TOP;
+        }
+        break;
+      }
+      case S_BM: {                                   // (F) B-mer presence
+        const uint64_t cc = bm2 ? c1 : c0;
+        if (!((((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull)) {
+          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a_next = A_TOP;
+        } else if (!bm2) {
+          bm2 = true;
+          addr = reinterpret_cast<uint64_t>(x.BM + (c1 >> 6));
+        } else {
+          skip_f = true;                              // window passed: go on at (C)
+          a_next = A_TOP;
+        }
+        break;
+      }
+      case S_KT: {                                   // (C)
+        const uint64_t lo = lo64(v), hi = hi64(v);
+        if (lo <= hi) { depth = uint32_t(x.K); start = lo; end = hi; have_pos = false; }
+        a_next = A_TRAV;
+        break;
+      }
+      case S_IDX: {
+        const uint64_t iv = idx_val<IdxT>(v, ao);
+        const uint64_t iv2 = idx_val<IdxT>(v2, uint32_t(addr2) & 15);
+        if (op == O_SAPOS || op == O_SAPOS2) {
+          pos = iv; have_pos = true;
+          a_next = op == O_SAPOS ? A_TRAV : A_AFTER;
+        } else if (op == O_SCAN_SA) {
+          sp = iv; lc = 0;
+          addr = reinterpret_cast<uint64_t>(x.T + sp + depth);
+          st = S_CMP; op = O_SCAN;
+        } else if (op == O_ISAJ) {
+          start = end = iv; have_pos = false;
+          a_next = A_EXPAND;
+        } else if (op == O_NS_SA2) {                  // suffix link, both ends
+          addr = ia(x.ISA, iv + 1); addr2 = ia(x.ISA, iv2 + 1);
+          op = O_NS_ISA2;
+        } else if (op == O_NS_ISA2) {
+          start = iv; end = iv2; need2 = false;
+          ++prefix; have_pos = false;
+          if (depth == 0) { start = 0; end = N - 1; a_next = A_TOP; }
+          else a_next = A_EXPAND;
+        } else if (op == O_TD_SA2) {                  // top_down_faster: both ends
+          addr = reinterpret_cast<uint64_t>(x.T + iv + depth);
+          addr2 = reinterpret_cast<uint64_t>(x.T + iv2 + depth);
+          st = S_BYTE; op = O_TD_T2;
+        } else {                                      // O_TD_SA: a bisection probe
+          addr = reinterpret_cast<uint64_t>(x.T + iv + depth);
+          st = S_BYTE; op = O_TD_T;
+        }
+        break;
+      }
+      case S_BYTE: {
+        const int32_t tb = int32_t(int8_t(byte_at(v, ao)));
+        if (op == O_TD_T2) {
+          cf = ch - tb;
+          cl = ch - int32_t(int8_t(byte_at(v2, uint32_t(addr2) & 15)));
+          need2 = false;
+          if (cf < 0 || cl > 0) { a_next = A_AFTER; break; }   // no occurrence
+          l = start; r = end; found = false; l2 = start; r2 = end;
+          if (cf == 0) { found = true; a_next = A_TD_AFTER_LEFT; }
+          else a_next = A_TD_LEFT;
+        } else if (op == O_TD_T) {
+          const int32_t vg = ch - tb;
+          if (td_left) {
+            if (vg <= 0) {
+              if (!found && vg == 0) { found = true; l2 = m; r2 = r; }
+              r = m;
+            } else {
+              l = m;
+            }
+            a_next = A_TD_LEFT;
+          } else {
+            if (vg < 0) r2 = m; else l2 = m;
+            a_next = A_TD_RIGHT;
+          }
+        } else {                                      // O_LM: is_leftmaximal
+          if (P[prefix - 1] != uint8_t(tb)) {
+            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
+            ++nem;
+          }
+          dch = depth; j = 1;
+          addr = reinterpret_cast<uint64_t>(x.U + pos + 1);
+          st = S_USCAN;
+        }
+        break;
+      }
+      case S_CMP: {                                  // (A) extension / (S) candidate
+        const uint32_t off = prefix + depth + lc;
+        const uint32_t rem = L - off;
+        const uint32_t lim = rem < 16 - ao ? rem : 16 - ao;
+        const uint32_t k = agree_block(v, ao, P, off, lim);
+        lc += k;
+        if (k == lim && k < rem) {
+          addr += k;
+        } else if (op == O_EXT) {
+          depth += lc; lc = 0;
+          a_next = A_AFTER;
+        } else {
+          if (int32_t(lc) > best) { best = int32_t(lc); bl = bh = m; bpos = sp; }
+          else if (int32_t(lc) == best) bh = m;
+          if (++m <= end) {
+            addr = ia(x.SA, m);
+            st = S_IDX; op = O_SCAN_SA;
+          } else {
+            depth += uint32_t(best); start = bl; end = bh; pos = bpos;
+            have_pos = start == end;
+            a_next = A_AFTER;
+          }
+        }
+        break;
+      }
+      case S_USCAN: {                                // (B) first j with U[pos+j] >= d-j
+        const uint32_t D = dch - j;
+        const uint32_t lim = D < 16 - ao ? D : 16 - ao;
+        const uint32_t inr = ((1u << lim) - 1) << ao;
+        const uint32_t hm = byte_mask(v, [&](uint32_t b, uint32_t i) { return b + i >= D + ao; }) & inr;
+        if (hm) {
+          j += uint32_t(__builtin_ctz(hm)) - ao; hit = true;
+          a_next = A_CHAIN_DONE;
+        } else {
+          j += lim;
+          if (j < dch) addr += lim;
+          else { hit = false; a_next = A_CHAIN_DONE; }
+        }
+        break;
+      }
+      case S_EXL: {                                  // expand_link, left side
+        const uint32_t sm = byte_mask(v, [&](uint32_t b, uint32_t) { return b < depth; }) &
+                            ((2u << ao) - 1);
+        const uint32_t k = sm ? ao - (31 - __builtin_clz(sm)) : ao + 1;
+        if (k && expc + k >= thresh) {
+          depth = 0; start = 0; end = N - 1; have_pos = false; a_next = A_TOP;
+        } else {
+          expc += k; es -= k;
+          if (!sm) {
+            addr = reinterpret_cast<uint64_t>(x.L8 + es);
+          } else if (ee < N - 1) {
+            addr = reinterpret_cast<uint64_t>(x.L8 + ee + 1);
+            st = S_EXR;
+          } else {
+            start = es; end = ee; a_next = A_TOP;
+          }
+        }
+        break;
+      }
+      case S_EXR: {                                  // expand_link, right side
+        const uint64_t room = N - 1 - ee;
+        const uint32_t lim = room < uint64_t(16 - ao) ? uint32_t(room) : 16 - ao;
+        const uint32_t sm = byte_mask(v, [&](uint32_t b, uint32_t) { return b < depth; }) &
+                            (((1u << lim) - 1) << ao);
+        const uint32_t k = sm ? uint32_t(__builtin_ctz(sm)) - ao : lim;
+        if (k && expc + k >= thresh) {
+          depth = 0; start = 0; end = N - 1; have_pos = false; a_next = A_TOP;
+        } else {
+          expc += k; ee += k;
+          if (!sm && ee < N - 1) addr += lim;
+          else { start = es; end = ee; a_next = A_TOP; }
+        }
+        break;
+      }
+      default:
+        break;
+    }
+
+    // ---- ALU continuations, in the order the common chains run ----
+    while (a_next != A_NONE) {
+      if (a_next == A_TD_LEFT) {
+        if (r > l + 1) {
+          m = (l + r) >> 1;
+          addr = ia(x.SA, m);
+          st = S_IDX; op = O_TD_SA; td_left = true;
+          a_next = A_NONE;
+        } else {
+          l = r;
+          a_next = A_TD_AFTER_LEFT;
+        }
+      }
+      if (a_next == A_TD_AFTER_LEFT) {
+        if (!found) l2 = l - 1;
+        if (cl == 0) { l2 = end; a_next = A_TD_DONE; }
+        else a_next = A_TD_RIGHT;
+      }
+      if (a_next == A_TD_RIGHT) {
+        if (r2 > l2 + 1) {
+          m = (l2 + r2) >> 1;
+          addr = ia(x.SA, m);
+          st = S_IDX; op = O_TD_SA; td_left = false;
+          a_next = A_NONE;
+        } else {
+          a_next = A_TD_DONE;
+        }
+      }
+      if (a_next == A_TD_DONE) {
+        if (l <= l2) {
+          start = l; end = l2; ++depth; have_pos = false;
+          a_next = depth == L ? A_AFTER : A_TRAV;
+        } else {
+          a_next = A_AFTER;
+        }
+      }
+      if (a_next == A_CHAIN_DONE) {
+        prefix += j;
+        if (!hit) {
+          depth = 0; start = 0; end = N - 1; have_pos = false;
+          a_next = A_TOP;
+        } else {
+          depth = dch - j;
+          addr = ia(x.ISA, pos + j);
+          st = S_IDX; op = O_ISAJ;
+          a_next = A_NONE;
+        }
+      }
+      if (a_next == A_EXPAND) {
+        thresh = uint32_t(2ull * depth * x.logN);
+        expc = 0;
+        es = start; ee = end;
+        addr = reinterpret_cast<uint64_t>(x.L8 + es);
+        st = S_EXL;
+        a_next = A_NONE;
+      }
+      if (a_next == A_AFTER) {
+        if (depth <= 1) {
+          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
+          a_next = A_TOP;
+        } else if (start == end) {
+          if (!have_pos) {
+            addr = ia(x.SA, start);
+            st = S_IDX; op = O_SAPOS2;
+          } else if (depth >= c.min_len && prefix != 0 && pos != 0) {
+            addr = reinterpret_cast<uint64_t>(x.T + pos - 1);
+            st = S_BYTE; op = O_LM;
+          } else {
+            if (depth >= c.min_len) {
+              if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
+              ++nem;
+            }
+            dch = depth; j = 1;
+            addr = reinterpret_cast<uint64_t>(x.U + pos + 1);
+            st = S_USCAN;
+          }
+          a_next = A_NONE;
+        } else {                                     // non-singleton suffix link
+          --depth;
+          addr = ia(x.SA, start); addr2 = ia(x.SA, end); need2 = true;
+          st = S_IDX; op = O_NS_SA2;
+          a_next = A_NONE;
+        }
+      }
+      if (a_next == A_TOP) {
+        if (prefix >= L) goto read_done;
+        if (depth < c.min_len && !skip_f) {                        // (F)
+          if (prefix + c.min_len > L) goto read_done;
+          int32_t kb = bad.last(prefix, c.min_len);
+
+          while (kb >= 0 && in_text(x, P[kb])) kb = bad.last(prefix, uint32_t(kb) - prefix);
+          if (kb >= 0) {
+            depth = 0; start = 0; end = N - 1; have_pos = false;
+            prefix = uint32_t(kb) + 1;
+            continue;                                               // A_TOP again
+          }
+          const uint32_t B = uint32_t(x.B);
+          if (B > 0 && B <= c.min_len) {
+            const uint32_t q1 = prefix + c.min_len - B;
+            if (bad.bits(prefix, B) == 0 && bad.bits(q1, B) == 0) {
+              c0 = codes_at(C, prefix, B);
+              c1 = codes_at(C, q1, B);
+              addr = reinterpret_cast<uint64_t>(x.BM + (c0 >> 6));
+              st = S_BM; bm2 = false;
+              a_next = A_NONE;
+              break;
+            }
+          }
+        }
+        skip_f = false;
+        // (C) from the root
+        if (depth == 0 && prefix + uint32_t(x.K) <= L && bad.bits(prefix, uint32_t(x.K)) == 0) {
+          addr = reinterpret_cast<uint64_t>(x.KT + 2 * codes_at(C, prefix, uint32_t(x.K)));
+          st = S_KT;
+          a_next = A_NONE;
+          break;
+        }
+        a_next = A_TRAV;
+      }
+      if (a_next == A_TRAV) {
+        if (depth >= L || prefix + depth >= L) {
+          a_next = A_AFTER;
+          continue;
+        }
+        if (start == end) {
+          if (!have_pos) {
+            addr = ia(x.SA, start);
+            st = S_IDX; op = O_SAPOS;
+          } else {
+            addr = reinterpret_cast<uint64_t>(x.T + pos + depth);
+            st = S_CMP; op = O_EXT; lc = 0;
+          }
+        } else if (end - start + 1 <= uint64_t(kScan)) {
+          m = start; best = -1; bl = bh = start; bpos = 0;
+          addr = ia(x.SA, m);
+          st = S_IDX; op = O_SCAN_SA;
+        } else {
+          ch = int32_t(int8_t(P[prefix + depth]));
+          addr = ia(x.SA, start); addr2 = ia(x.SA, end); need2 = true;
+          st = S_IDX; op = O_TD_SA2;
+        }
+        a_next = A_NONE;
+      }
+      continue;
+    read_done:
+      c.n_out[rd] = nem;
+      if (c.iters) c.iters[rd] = it;
+      it = 0;
+      st = S_NEW;
+      break;
+    }
+  }
+  if (c.wave_stats && lane == 0) {
+    atomicAdd(c.wave_stats, (unsigned long long)w_iters);
+    atomicAdd(c.wave_stats + 1, (unsigned long long)w_active);
+  }
+}
+
+}  // namespace sm
+}  // namespace smash

@@ -1,0 +1,77 @@
+"""The device MAM state machine (smash-paper_amd/csrc/mam_sm.hpp: k_prep +
+k_mam_sm) compiled for the host as a single-lane emulation (tools/sm_emu) and
+checked on the CPU: against the reference's MAM goldens, against the oracle's
+restatement of longSA::MAM on edge reads and read lengths, for both SA/ISA
+widths.  The GPU tests (test_gpu_parity.py) run the same kernel on MI355X;
+this suite pins its control flow without a GPU."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import interleaved_reads, read_gz_lines
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools", "sm_emu"))
+import sm_emu  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def emu(tiny_ix):
+    tiny_ix.accel()
+    return sm_emu.Emu(tiny_ix), sm_emu.Emu(tiny_ix, wide=True)
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+@pytest.mark.parametrize("wide", [False, True])
+def test_state_machine_matches_reference_goldens(emu, s, wide):
+    exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+           for l in read_gz_lines("%s_MAM.txt.gz" % s)]
+    got, iters = emu[int(wide)].map(interleaved_reads(s))
+    bad = [i for i in range(len(exp)) if got[i] != exp[i]]
+    assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)
+    assert iters.min() > 0
+
+
+def _edge_reads(ix, L, n, rng):
+    T = ix.T[:ix.N]
+    out = np.empty((n, L), np.uint8)
+    for i in range(n):
+        p = int(rng.integers(0, ix.N - L - 1))
+        r = bytearray(T[p:p + L].tobytes())
+        for _k in range(int(rng.integers(0, 5))):
+            r[int(rng.integers(0, L))] = int(rng.choice(list(b"acgtnz`$N")))
+        out[i] = np.frombuffer(bytes(r), np.uint8)
+    return out
+
+
+@pytest.mark.parametrize("L", [15, 32, 33, 100, 128, 129, 150, 255])
+def test_state_machine_edge_reads(emu, tiny_ix, L):
+    """bytes absent from the text, 'n' (present), windows at the read end,
+    homopolymers; read lengths around the record/bad-mask boundaries."""
+    rng = np.random.default_rng(L)
+    reads = _edge_reads(tiny_ix, L, 120, rng)
+    extra = [b"z" * L, b"n" * L, b"a" * L, (b"acgt" * 64)[:L], (b"c" * (L // 2) + b"z" + b"c" * L)[:L]]
+    reads = np.concatenate([reads, np.array([np.frombuffer(x, np.uint8) for x in extra])])
+    for ml in (20, 12, 30):
+        got, _ = emu[0].map(reads, min_len=ml)
+        for i in range(len(reads)):
+            assert got[i] == tiny_ix.search(reads[i].tobytes(), min_len=ml), (ml, i)
+
+
+def test_state_machine_on_mid_genome():
+    import oracle as O
+    import synth
+    g = synth.make_genome("mid")
+    ix = O.Index(*O.text_from_contigs(g))
+    ix.accel()
+    r1, r2 = synth.make_reads(g, 1500, 150, seed=45)
+    reads = np.empty((3000, 150), np.uint8)
+    reads[0::2], reads[1::2] = r1, r2
+    reads[reads == ord("N")] = ord("Z")
+    lo = np.arange(256, dtype=np.uint8)
+    lo[65:91] += 32
+    reads = lo[reads]
+    got, _ = sm_emu.Emu(ix).map(reads)
+    for i in range(len(reads)):
+        assert got[i] == ix.search(reads[i].tobytes()), i

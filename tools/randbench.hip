@@ -1,0 +1,86 @@
+// tools/randbench.hip -- ceiling of dependent random 16-byte loads on MI355X
+// as a function of the footprint (the access pattern of the MAM search:
+// every lane follows its own chain of dependent probes into a ~144 GB index).
+//
+//   randbench <GiB list...>
+// For each footprint: lanes = waves_per_simd * 4 * CUs * 64 chains, each doing
+// `steps` dependent 16-byte loads at hashed addresses; prints loads/s and the
+// 64-B-line rate.  Also an "ilp" variant with 4 independent chains per lane.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+  std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); std::exit(1); } } while (0)
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return x;
+}
+
+template <int ILP>
+__global__ __launch_bounds__(256) void k_chase(const uint4 *buf, uint64_t n16, int steps,
+                                               uint64_t *sink, uint64_t seed) {
+  const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  uint64_t h[ILP];
+#pragma unroll
+  for (int k = 0; k < ILP; ++k) h[k] = mix(t * ILP + k + seed);
+  uint64_t acc = 0;
+  for (int s = 0; s < steps; ++s) {
+    uint4 v[ILP];
+#pragma unroll
+    for (int k = 0; k < ILP; ++k) v[k] = buf[h[k] % n16];
+#pragma unroll
+    for (int k = 0; k < ILP; ++k) {
+      acc += v[k].x;
+      h[k] = mix(h[k] + v[k].x + 1);   // dependent on the loaded value
+    }
+  }
+  if (acc == 0x123456789ull) sink[0] = acc;
+}
+
+int main(int argc, char **argv) {
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  std::vector<double> gib;
+  for (int i = 1; i < argc; ++i) gib.push_back(std::atof(argv[i]));
+  if (gib.empty()) gib = {0.25, 4, 32, 128};
+  uint64_t *sink;
+  CK(hipMalloc(&sink, 8));
+  for (double g : gib) {
+    const uint64_t bytes = uint64_t(g * (1ull << 30)) & ~uint64_t(255);
+    void *buf = nullptr;
+    CK(hipMalloc(&buf, bytes));
+    CK(hipMemset(buf, 0, bytes));
+    const uint64_t n16 = bytes / 16;
+    for (int wps : {4, 8}) {
+      for (int ilp : {1, 4}) {
+        const uint64_t threads = uint64_t(wps) * 4 * cus * 64;
+        const int steps = 64;
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+        auto launch = [&](uint64_t seed) {
+          if (ilp == 1) k_chase<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
+          else k_chase<4><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
+        };
+        launch(1);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        for (int r = 0; r < 3; ++r) launch(100 + r);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        const double loads = 3.0 * threads * steps * ilp;
+        const double rate = loads / (ms * 1e-3);
+        std::printf("footprint %8.2f GiB  waves/SIMD %d  ilp %d : %.3f G loads/s  (%.0f GB/s of 64-B lines)  avg latency %.2f us\n",
+                    g, wps, ilp, rate * 1e-9, rate * 64e-9, (ms * 1e-3 / 3.0 / steps) * 1e6);
+        std::fflush(stdout);
+        CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
+      }
+    }
+    CK(hipFree(buf));
+  }
+  return 0;
+}

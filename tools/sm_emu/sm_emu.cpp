@@ -1,0 +1,64 @@
+// tools/sm_emu/sm_emu.cpp -- runs the device MAM state machine
+// (smash-paper_amd/csrc/mam_sm.hpp: k_prep + k_mam_sm) on the host as a single
+// lane, over host copies of the index arrays.  Test tooling only: it lets the
+// CPU suite check the device kernel's control flow against the goldens and the
+// oracle (tests/test_sm_emu.py), and it is the debugger for that kernel
+// (rocgdb is not available on the GPU pool).  Not linked into the product.
+#include "hip/hip_runtime.h"
+#include "../../smash-paper_amd/csrc/mam_sm.hpp"
+
+thread_local dim3 threadIdx, blockIdx, blockDim;
+namespace smash { namespace sm { uint32_t ldsw[1 << 12]; } }
+
+using namespace smash;
+
+template <class IdxT>
+static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t *L8,
+               const uint8_t *U, const uint64_t *KT, int K, const uint64_t *BM, int B,
+               const uint64_t *in_text, uint64_t N, uint64_t logN, const uint8_t *reads,
+               uint64_t stride, uint32_t L, uint64_t n, uint32_t min_len, uint64_t *out,
+               uint32_t cap, uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
+               uint64_t *viol) {
+  const sm::Geom g = sm::make_geom(L);
+  if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
+  std::vector<uint4> rec(n * g.chunks);
+  blockIdx.x = 0; blockDim.x = 1;
+  for (uint64_t t = 0; t < n * g.chunks * 4; ++t) {
+    threadIdx.x = unsigned(t);
+    sm::k_prep(reads, stride, nullptr, L, n, in_text[0], in_text[1], in_text[2], in_text[3], g,
+               reinterpret_cast<uint32_t *>(rec.data()) + 0 * t);
+  }
+  threadIdx.x = 0;
+  sm::Ctx<IdxT> c;
+  c.x.T = T; c.x.SA = static_cast<const IdxT *>(SA); c.x.ISA = static_cast<const IdxT *>(ISA);
+  c.x.L8 = L8; c.x.U = U; c.x.KT = KT; c.x.BM = BM;
+  c.x.N = N; c.x.logN = logN; c.x.K = K; c.x.B = B;
+  for (int k = 0; k < 4; ++k) c.x.in_text[k] = in_text[k];
+  c.rec = rec.data(); c.g = g; c.lens = nullptr; c.len0 = L; c.min_len = min_len; c.cap = cap;
+  c.n_reads = n; c.out = out; c.n_out = n_out;
+  unsigned long long work = 0;
+  c.work = &work;
+  c.iters = iters; c.wave_stats = nullptr;
+  for (int k = 0; k < 7; ++k) { c.rlo[k] = spans[2 * k]; c.rhi[k] = spans[2 * k + 1]; }
+  c.rlo[7] = reinterpret_cast<uint64_t>(rec.data());
+  c.rhi[7] = c.rlo[7] + rec.size() * sizeof(uint4);
+  unsigned long long v[10] = {0};
+  c.viol = v;
+  sm::k_mam_sm<IdxT, 1, true>(c);
+  for (int k = 0; k < 10; ++k) viol[k] = v[k];
+  return 0;
+}
+
+extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int idx_bytes,
+                          const uint8_t *L8, const uint8_t *U, const uint64_t *KT, int K,
+                          const uint64_t *BM, int B, const uint64_t *in_text, uint64_t N,
+                          uint64_t logN, const uint8_t *reads, uint64_t stride, uint32_t L,
+                          uint64_t n, uint32_t min_len, uint64_t *out, uint32_t cap,
+                          uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
+                          uint64_t *viol) {
+  if (idx_bytes == 4)
+    return run<uint32_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
+                         min_len, out, cap, n_out, iters, spans, viol);
+  return run<uint64_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
+                       min_len, out, cap, n_out, iters, spans, viol);
+}

@@ -1,0 +1,108 @@
+"""tools/sm_emu/sm_emu.py -- ctypes wrapper of the single-lane host emulation
+of the device MAM state machine (sm_emu.cpp).  Test tooling only."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libsmemu.so")
+_lib = None
+
+
+def build():
+    srcs = [os.path.join(HERE, f) for f in ("sm_emu.cpp", "hip/hip_runtime.h")] + [
+        os.path.join(HERE, "..", "..", "smash-paper_amd", "csrc", f)
+        for f in ("mam_sm.hpp", "mam_device.hpp", "common.hpp")]
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs):
+        return LIB
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", HERE,
+                           "-I", os.path.join(HERE, "..", "..", "include"),
+                           "-o", LIB, os.path.join(HERE, "sm_emu.cpp")])
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = C.CDLL(build())
+        _lib.sm_emu_map.restype = C.c_int
+    return _lib
+
+
+def _padded(a, dtype):
+    """16-byte block loads may touch up to 15 bytes past an element: copy into
+    a 64-byte aligned buffer with 64 bytes of zero padding."""
+    a = np.ascontiguousarray(a, dtype)
+    raw = np.zeros(a.nbytes + 128, np.uint8)
+    off = (-raw.ctypes.data) % 64
+    buf = raw[off:off + a.nbytes + 64]
+    buf[:a.nbytes] = a.view(np.uint8).reshape(-1)
+    return buf, raw
+
+
+def in_text_words(in_text):
+    w = np.zeros(4, np.uint64)
+    for b in range(256):
+        if in_text[b]:
+            w[b >> 6] |= np.uint64(1) << np.uint64(b & 63)
+    return w
+
+
+class Emu:
+    def __init__(self, ix, wide=False):
+        """ix: oracle.Index with accel() built; wide: run the 8-byte SA/ISA
+        instantiation (the device uses it when N >= 2^32)."""
+        self.ix = ix
+        self.keep = []
+
+        self.spans = []
+
+        def P(a, dt):
+            buf, raw = _padded(a, dt)
+            self.keep.append(raw)
+            nb = np.ascontiguousarray(a, dt).nbytes
+            self.spans += [buf.ctypes.data, buf.ctypes.data + nb]
+            return buf.ctypes.data
+        self.T = P(ix.T, np.uint8)
+        it = np.uint64 if wide else ix.SA.dtype
+        self.SA = P(ix.SA, it)
+        self.ISA = P(ix.ISA, it)
+        self.L8 = P(ix.L8, np.uint8)
+        self.U = P(ix._U, np.uint8)
+        self.KT = P(ix._KT, np.uint64)
+        self.BM = P(ix._BM, np.uint64)
+        self.K = ix.acc.K
+        self.B = ix.acc.B
+        self.it = in_text_words(list(ix.acc.in_text))
+        self.isz = np.dtype(it).itemsize
+
+    def map(self, reads, min_len=20, cap=512):
+        """reads: uint8 [n, L].  Returns (list of [(ref, q, len)], iterations)."""
+        reads = np.ascontiguousarray(reads, np.uint8)
+        n, L = reads.shape
+        out = np.zeros(n * cap, np.uint64)
+        nout = np.zeros(n, np.uint32)
+        iters = np.zeros(n, np.uint32)
+        spans = np.array(self.spans, np.uint64)   # T SA ISA L8 U KT BM
+        viol = np.zeros(10, np.uint64)
+        from oracle import lib as olib
+        logN = olib().orc_logN(C.c_uint64(self.ix.N))
+        rc = lib().sm_emu_map(
+            C.c_void_p(self.T), C.c_void_p(self.SA), C.c_void_p(self.ISA), self.isz,
+            C.c_void_p(self.L8), C.c_void_p(self.U), C.c_void_p(self.KT), self.K,
+            C.c_void_p(self.BM), self.B, self.it.ctypes.data_as(C.c_void_p),
+            C.c_uint64(self.ix.N), C.c_uint64(logN), reads.ctypes.data_as(C.c_void_p),
+            C.c_uint64(L), C.c_uint32(L), C.c_uint64(n), C.c_uint32(min_len),
+            out.ctypes.data_as(C.c_void_p), C.c_uint32(cap),
+            nout.ctypes.data_as(C.c_void_p), iters.ctypes.data_as(C.c_void_p),
+            spans.ctypes.data_as(C.c_void_p), viol.ctypes.data_as(C.c_void_p))
+        assert rc == 0
+        assert viol[0] == 0, ("out-of-range probe", viol.tolist())
+        res = []
+        for i in range(n):
+            k = min(int(nout[i]), cap)
+            w = out[i * cap:i * cap + k]
+            res.append([(int(x & 0xFFFFFFFFFFFF), int((x >> 48) & 0xFF), int(x >> 56)) for x in w])
+        return res, iters
