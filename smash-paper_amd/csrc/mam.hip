@@ -65,6 +65,69 @@ __global__ __launch_bounds__(BLOCK) void k_mam(
 // SMASH_MODE_MAM default: the state-machine kernel (mam_sm.hpp).  Setting
 // SMASH_MAM_KERNEL=direct selects the direct per-lane v3 kernel instead (same
 // results; kept for A/B measurement).
+template <class IdxT, bool STATS>
+int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, size_t lds,
+           hipStream_t s) {
+  constexpr int B = 128;
+  // Every probe is checked against the span of the index arrays and the
+  // records: a wild address retires its lane and fails the call instead of
+  // faulting the GPU.
+  constexpr bool CHECK = true;
+  auto kern = sm::k_mam_sm<IdxT, B, CHECK, STATS>;
+  int per_cu = 0, cus = 0;
+  SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void *>(kern), B, lds));
+  SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
+  if (per_cu < 1) per_cu = 1;
+  uint64_t blocks = uint64_t(per_cu) * uint64_t(cus);
+  const uint64_t want = (n_reads + B - 1) / B;
+  if (blocks > want) blocks = want;
+  sm::Ctx<IdxT> c = c0;
+  std::vector<uint32_t> h_iters;
+  if (STATS) {
+    SMASH_HIP(hipMalloc(&c.iters, n_reads * sizeof(uint32_t)));
+    SMASH_HIP(hipMalloc(&c.wave_stats, 16));
+    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 16, s));
+  }
+  c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;   // d_work[1..10]
+  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 11 * 8, s));
+  kern<<<unsigned(blocks), B, lds, s>>>(c);
+  SMASH_HIP(hipGetLastError());
+  unsigned long long h[10];
+  SMASH_HIP(hipMemcpyAsync(h, c.viol, sizeof(h), hipMemcpyDeviceToHost, s));
+  SMASH_HIP(hipStreamSynchronize(s));
+  if (h[0]) {
+    char msg[512];
+    std::snprintf(msg, sizeof(msg),
+                  "k_mam_sm: %llu probes outside the index; first: state %llu op %llu addr %#llx "
+                  "addr2 %#llx prefix %llu depth %llu interval [%llu,%llu] read %llu",
+                  h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+    std::fprintf(stderr, "%s\n", msg);
+    set_error(msg);
+    return SMASH_ERR_HIP;
+  }
+  if (STATS) {
+    std::vector<uint32_t> hv(n_reads);
+    unsigned long long ws[2];
+    SMASH_HIP(hipMemcpy(hv.data(), c.iters, n_reads * 4, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 16, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipFree(c.iters));
+    SMASH_HIP(hipFree(c.wave_stats));
+    std::vector<uint32_t> srt(hv);
+    std::sort(srt.begin(), srt.end());
+    double sum = 0;
+    for (uint32_t v : hv) sum += v;
+    auto q = [&](double f) { return srt[std::min<size_t>(srt.size() - 1, size_t(f * srt.size()))]; };
+    std::fprintf(stderr,
+                 "[k_mam_sm] reads %llu blocks %llu (%d/CU) row %u words: lane-iterations/read mean %.1f "
+                 "p50 %u p90 %u p99 %u p99.9 %u max %u; wave-iterations %llu, active lanes/iteration %.2f\n",
+                 (unsigned long long)n_reads, (unsigned long long)blocks, per_cu, c.w_row, sum / n_reads,
+                 q(0.5), q(0.9), q(0.99), q(0.999), srt.back(), ws[0],
+                 double(ws[1]) / double(ws[0] ? ws[0] : 1));
+  }
+  return SMASH_OK;
+}
+
 template <class IdxT>
 int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
               uint64_t stride, const uint16_t *lens, uint32_t len,
@@ -90,38 +153,19 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
         ix->in_text[3], g, ix->d_rec);
     SMASH_HIP(hipGetLastError());
   }
-  const size_t lds = size_t(B) * g.w_row * 4 + 16;
-  int per_cu = 0, cus = 0;
-  // Every probe is range-checked (in_ranges): an address outside the index
-  // arrays retires its lane and fails the call instead of faulting the GPU.
-  // (The unchecked instantiation faulted on MI355X with the 8-byte index
-  // although the checked one, same logic, reports no out-of-range probe on
-  // hg19 and matches the direct kernel read for read: DESIGN.md section 4.)
-  constexpr bool check = true;
-  SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, reinterpret_cast<const void *>(sm::k_mam_sm<IdxT, B, check>), B, lds));
-  SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
-  if (per_cu < 1) per_cu = 1;
-  uint64_t blocks = uint64_t(per_cu) * uint64_t(cus);
-  const uint64_t want = (n_reads + B - 1) / B;
-  if (blocks > want) blocks = want;
   sm::Ctx<IdxT> c;
-  c.x = make_dev_index<IdxT>(ix);
+  const DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
+  c.T = x.T; c.SA = x.SA; c.ISA = x.ISA; c.L8 = x.L8; c.U = x.U; c.KT = x.KT; c.BM = x.BM;
+  c.N = x.N; c.logN = uint32_t(x.logN); c.K = uint32_t(x.K); c.B = uint32_t(x.B);
+  c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(ix->d_rec);
-  c.g = g;
-  c.lens = lens; c.len0 = len;
-  c.min_len = min_len; c.cap = cap; c.n_reads = n_reads;
+  c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
+  c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
   c.out = out; c.n_out = n_out;
   c.work = reinterpret_cast<unsigned long long *>(ix->d_work);
+  for (int k = 0; k < 4; ++k) c.in_text[k] = ix->in_text[k];
   c.iters = nullptr;
   c.wave_stats = nullptr;
-  const bool stats = std::getenv("SMASH_SM_STATS") != nullptr;
-  if (stats) {
-    SMASH_HIP(hipMalloc(&c.iters, n_reads * sizeof(uint32_t)));
-    SMASH_HIP(hipMalloc(&c.wave_stats, 16));
-    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 16, s));
-  }
-  c.viol = nullptr;
   {
     const uint64_t N = ix->N, isz = ix->idx_bytes;
     const uint64_t spans[8][2] = {
@@ -133,51 +177,15 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
         {reinterpret_cast<uint64_t>(ix->d_kmer), 16ull << (2 * ix->kmer_k)},
         {reinterpret_cast<uint64_t>(ix->d_bitmap), 8 * (((1ull << (2 * ix->bitmap_b)) >> 6) + 1)},
         {reinterpret_cast<uint64_t>(ix->d_rec), n_reads * g.chunks * 16}};
-    for (int k = 0; k < 8; ++k) { c.rlo[k] = spans[k][0]; c.rhi[k] = spans[k][0] + spans[k][1]; }
-  }
-  if (check) {   // d_work[1..10] (index.hip allocates 16 words)
-    c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;
-    SMASH_HIP(hipMemsetAsync(c.viol, 0, 10 * 8, s));
-  }
-  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
-  sm::k_mam_sm<IdxT, B, check><<<unsigned(blocks), B, lds, s>>>(c);
-  SMASH_HIP(hipGetLastError());
-  if (check) {
-    unsigned long long h[10];
-    SMASH_HIP(hipMemcpyAsync(h, c.viol, sizeof(h), hipMemcpyDeviceToHost, s));
-    SMASH_HIP(hipStreamSynchronize(s));
-    if (h[0]) {
-      char msg[512];
-      std::snprintf(msg, sizeof(msg),
-                    "k_mam_sm: %llu out-of-range probes; first: state %llu op %llu addr %#llx "
-                    "addr2 %#llx prefix %llu depth %llu interval [%llu,%llu] read %llu",
-                    h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
-      std::fprintf(stderr, "%s\n", msg);
-      set_error(msg);
-      return SMASH_ERR_HIP;
+    c.lo = ~0ull; c.hi = 0;
+    for (int k = 0; k < 8; ++k) {
+      c.lo = std::min<uint64_t>(c.lo, spans[k][0]);
+      c.hi = std::max<uint64_t>(c.hi, spans[k][0] + spans[k][1]);
     }
   }
-  if (stats) {
-    std::vector<uint32_t> h(n_reads);
-    unsigned long long ws[2];
-    SMASH_HIP(hipStreamSynchronize(s));
-    SMASH_HIP(hipMemcpy(h.data(), c.iters, n_reads * 4, hipMemcpyDeviceToHost));
-    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 16, hipMemcpyDeviceToHost));
-    SMASH_HIP(hipFree(c.iters));
-    SMASH_HIP(hipFree(c.wave_stats));
-    std::vector<uint32_t> srt(h);
-    std::sort(srt.begin(), srt.end());
-    double sum = 0;
-    for (uint32_t v : h) sum += v;
-    auto q = [&](double f) { return srt[std::min<size_t>(srt.size() - 1, size_t(f * srt.size()))]; };
-    std::fprintf(stderr,
-                 "[k_mam_sm] reads %llu blocks %llu (%d/CU) row %u words: lane-iterations/read mean %.1f "
-                 "p50 %u p90 %u p99 %u p99.9 %u max %u; wave-iterations %llu, active lanes/iteration %.2f\n",
-                 (unsigned long long)n_reads, (unsigned long long)blocks, per_cu, g.w_row, sum / n_reads,
-                 q(0.5), q(0.9), q(0.99), q(0.999), srt.back(), ws[0],
-                 double(ws[1]) / double(ws[0] ? ws[0] : 1));
-  }
-  return SMASH_OK;
+  const size_t lds = size_t(B) * g.w_row * 4 + 16;
+  if (std::getenv("SMASH_SM_STATS")) return run_sm<IdxT, true>(ix, c, n_reads, lds, s);
+  return run_sm<IdxT, false>(ix, c, n_reads, lds, s);
 }
 
 bool use_direct() {

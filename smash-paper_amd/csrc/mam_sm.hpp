@@ -24,6 +24,12 @@
 #pragma once
 #include "mam_device.hpp"
 
+// the 16-byte probe (the host emulation, tools/sm_emu, substitutes a checked
+// load here)
+#ifndef SM_LOAD16
+#define SM_LOAD16(a) (*reinterpret_cast<const uint4 *>((a) & ~uint64_t(15)))
+#endif
+
 namespace smash {
 namespace sm {
 
@@ -97,16 +103,18 @@ __global__ void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
   rec[t] = out;
 }
 
-enum : uint32_t { S_EXIT = 0, S_NEW, S_COPY, S_BM, S_KT, S_IDX, S_BYTE, S_CMP, S_USCAN, S_EXL, S_EXR };
+// lane states: S_COPY and above own a pending 16-byte probe at `addr`
+enum : uint32_t { S_EXIT = 0, S_NEW, S_ALU, S_COPY, S_BM, S_KT, S_IDX, S_BYTE, S_CMP, S_USCAN,
+                  S_EXL, S_EXR };
 // S_IDX ops (an SA / ISA element arrived; *2: a second one in v2)
 enum : uint32_t { O_SAPOS, O_SAPOS2, O_SCAN_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2, O_TD_SA2, O_TD_SA };
 // S_BYTE ops (one text byte; *2: a second one in v2)
 enum : uint32_t { O_TD_T2 = 0, O_TD_T, O_LM };
 // S_CMP ops (16 text bytes compared with the read)
 enum : uint32_t { O_EXT = 0, O_SCAN };
-// ALU continuations
-enum : uint32_t { A_NONE = 0, A_TOP, A_TRAV, A_AFTER, A_CHAIN_DONE, A_EXPAND,
-                  A_TD_LEFT, A_TD_AFTER_LEFT, A_TD_RIGHT, A_TD_DONE };
+// ALU continuations, in the order the decide chain runs them
+enum : uint32_t { A_NONE = 0, A_TD_LEFT, A_TD_AFTER_LEFT, A_TD_RIGHT, A_TD_DONE, A_CHAIN_DONE,
+                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE };
 
 __device__ __forceinline__ uint64_t lo64(const uint4 &v) { return uint64_t(v.x) | (uint64_t(v.y) << 32); }
 __device__ __forceinline__ uint64_t hi64(const uint4 &v) { return uint64_t(v.z) | (uint64_t(v.w) << 32); }
@@ -182,25 +190,32 @@ __device__ __forceinline__ uint64_t codes_at(const uint32_t *C, uint32_t p, uint
 
 template <class IdxT>
 struct Ctx {
-  DevIndex<IdxT> x;
-  const uint4 *rec;      // k_prep records
-  Geom g;
+  // the index (DevIndex fields, flattened: every field is a live SGPR)
+  const uint8_t *T;
+  const IdxT *SA, *ISA;
+  const uint8_t *L8, *U;
+  const uint64_t *KT, *BM;
+  uint64_t N;
+  uint32_t logN, K, B, min_len;
+  // k_prep records and the LDS row geometry
+  const uint4 *rec;
+  uint32_t chunks, c_bad, w_row, w_raw;
   const uint16_t *lens;
-  uint32_t len0, min_len, cap;
+  uint32_t len0, cap;
   uint64_t n_reads;
   uint64_t *out;
   uint32_t *n_out;
   unsigned long long *work;
-  // profiling (SMASH_SM_STATS): per-read loop iterations; per-kernel sums of
-  // wave iterations and of active lanes over them
+  // probe check: every probe address must lie in [lo, hi) (the span of the
+  // index arrays and the records); a lane that names another address records
+  // it in viol[1..9] (viol[0] counts) and retires instead of faulting
+  uint64_t lo, hi;
+  unsigned long long *viol;
+  uint64_t in_text[4];    // bytes occurring in the text (copied to LDS)
+  // STATS builds only: per-read loop iterations; per-kernel sums of wave
+  // iterations and of active lanes over them
   uint32_t *iters;
   unsigned long long *wave_stats;
-  // bounds-checked variant (SMASH_SM_CHECK): valid [lo, hi) byte ranges of
-  // the arrays the search reads; the first out-of-range address is recorded
-  // in viol[1..9] (viol[0] counts them) and its lane retires instead of
-  // faulting
-  uint64_t rlo[8], rhi[8];
-  unsigned long long *viol;
 };
 
 template <class IdxT>
@@ -213,25 +228,26 @@ __device__ __forceinline__ uint64_t idx_val(const uint4 &v, uint32_t ao) {
   return dword_at(v, ao >> 2);
 }
 
-template <class IdxT>
-__device__ __forceinline__ bool in_ranges(const Ctx<IdxT> &c, uint64_t a) {
-  bool ok = false;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ok = ok || (a >= c.rlo[k] && a < c.rhi[k]);
-  return ok;
-}
-
-template <class IdxT, int BLOCK, bool CHECK>
-__global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
+// One lane = one read at a time.  Each iteration: (1) the lanes with a
+// pending probe load 16 bytes (two blocks when need2); (2) "consume": the
+// loaded block advances the lane's state; (3) "decide": a fixed chain of ALU
+// continuations names the next probe.  The chain has no loops: the two rare
+// transitions that go backwards in it (end of read inside traverse ->
+// after-traverse; a window filter skip -> the next window) park the lane in
+// S_ALU for one iteration.
+template <class IdxT, int BLOCK, bool CHECK, bool STATS>
+__global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   extern __shared__ uint32_t ldsw[];
-  const DevIndex<IdxT> &x = c.x;
-  const uint64_t N = x.N;
-  uint32_t *row = ldsw + threadIdx.x * c.g.w_row;
+  __shared__ uint64_t s_in_text[4];
+  for (uint32_t k = threadIdx.x; k < 4; k += blockDim.x) s_in_text[k] = c.in_text[k];
+  __syncthreads();
+  const uint64_t N = c.N;
+  uint32_t *row = ldsw + threadIdx.x * c.w_row;
   const uint8_t *P = reinterpret_cast<const uint8_t *>(row);
-  const uint32_t *C = row + c.g.w_raw;
+  const uint32_t *C = row + c.w_raw;
   const uint32_t lane = threadIdx.x & 63;
 
-  uint32_t st = S_NEW, op = 0;
+  uint32_t st = S_NEW, op = 0, pend = A_NONE;
   uint64_t addr = 0, addr2 = 0;
   bool need2 = false;
   uint64_t rd = 0;
@@ -257,13 +273,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
     const uint64_t newm = __ballot(st == S_NEW);
     unsigned long long base = 0;
     if (newm) {
-      const uint32_t leader = __builtin_ctzll(newm);
-      if (lane == leader) base = atomicAdd(c.work, (unsigned long long)__popcll(newm));
+      if (lane == uint32_t(__builtin_ctzll(newm)))
+        base = atomicAdd(c.work, (unsigned long long)__popcll(newm));
     }
     const uint64_t live = __ballot(st != S_EXIT);
     if (live == 0) break;
-    if (c.wave_stats) { w_iters += 1; w_active += __popcll(live); }
-    if (CHECK && st >= S_COPY && (!in_ranges(c, addr) || (need2 && !in_ranges(c, addr2)))) {
+    if (STATS) { w_iters += 1; w_active += __popcll(live); }
+    if (CHECK && st >= S_COPY &&
+        (addr < c.lo || addr >= c.hi || (need2 && (addr2 < c.lo || addr2 >= c.hi)))) {
       if (atomicAdd(c.viol, 1ull) == 0) {
         c.viol[1] = st; c.viol[2] = op; c.viol[3] = addr; c.viol[4] = need2 ? addr2 : 0;
         c.viol[5] = prefix; c.viol[6] = depth; c.viol[7] = start; c.viol[8] = end; c.viol[9] = rd;
@@ -272,8 +289,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
       need2 = false;
     }
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
-    if (st >= S_COPY) v = *reinterpret_cast<const uint4 *>(addr & ~uint64_t(15));
-    if (need2) v2 = *reinterpret_cast<const uint4 *>(addr2 & ~uint64_t(15));
+    if (st >= S_COPY) v = SM_LOAD16(addr);
+    if (need2) v2 = SM_LOAD16(addr2);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
     if (newm) {
       base = __shfl(base, int(__builtin_ctzll(newm)), 64);
@@ -284,14 +301,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
           st = S_EXIT;
         } else {
           L = c.lens ? c.lens[rd] : c.len0;
-          addr = reinterpret_cast<uint64_t>(c.rec + rd * c.g.chunks);
+          addr = reinterpret_cast<uint64_t>(c.rec + rd * c.chunks);
           kc = 0;
           st = S_COPY;
         }
       }
     }
-    if (st < S_COPY || fresh) continue;
-    ++it;
+    if (st < S_ALU || fresh) continue;
+    if (STATS) ++it;
 #ifdef SM_TRACE
     if (st != S_COPY)
       printf("it %u st %u op %u prefix %u depth %u [%llu,%llu] pos %llu hp %d\n", it, st, op, prefix,
@@ -299,46 +316,50 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
              int(have_pos));
 #endif
     const uint32_t ao = uint32_t(addr) & 15;
-    uint32_t a_next = A_NONE;
+    uint32_t a = A_NONE;
 
+    // ---------------- consume ----------------
     switch (st) {
+      case S_ALU:
+        a = pend;
+        break;
       case S_COPY: {
-        if (kc < c.g.c_bad) {
+        if (kc < c.c_bad) {
           if (kc == 0) { bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w; }
           else { bad.w4 = v.x; bad.w5 = v.y; bad.w6 = v.z; bad.w7 = v.w; }
         } else {
-          const uint32_t q = 4 * (kc - c.g.c_bad);
-          if (q + 0 < c.g.w_row) row[q + 0] = v.x;
-          if (q + 1 < c.g.w_row) row[q + 1] = v.y;
-          if (q + 2 < c.g.w_row) row[q + 2] = v.z;
-          if (q + 3 < c.g.w_row) row[q + 3] = v.w;
+          const uint32_t q = 4 * (kc - c.c_bad);
+          if (q + 0 < c.w_row) row[q + 0] = v.x;
+          if (q + 1 < c.w_row) row[q + 1] = v.y;
+          if (q + 2 < c.w_row) row[q + 2] = v.z;
+          if (q + 3 < c.w_row) row[q + 3] = v.w;
         }
-        if (++kc < c.g.chunks) {
+        if (++kc < c.chunks) {
           addr += 16;
         } else {
           prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
           skip_f = false;
-          a_next = A_TOP;
+          a = A_TOP;
         }
         break;
       }
       case S_BM: {                                   // (F) B-mer presence
         const uint64_t cc = bm2 ? c1 : c0;
         if (!((((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull)) {
-          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a_next = A_TOP;
+          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
         } else if (!bm2) {
           bm2 = true;
-          addr = reinterpret_cast<uint64_t>(x.BM + (c1 >> 6));
+          addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
         } else {
           skip_f = true;                              // window passed: go on at (C)
-          a_next = A_TOP;
+          a = A_TOP;
         }
         break;
       }
       case S_KT: {                                   // (C)
         const uint64_t lo = lo64(v), hi = hi64(v);
-        if (lo <= hi) { depth = uint32_t(x.K); start = lo; end = hi; have_pos = false; }
-        a_next = A_TRAV;
+        if (lo <= hi) { depth = c.K; start = lo; end = hi; have_pos = false; }
+        a = A_TRAV;
         break;
       }
       case S_IDX: {
@@ -346,43 +367,44 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
         const uint64_t iv2 = idx_val<IdxT>(v2, uint32_t(addr2) & 15);
         if (op == O_SAPOS || op == O_SAPOS2) {
           pos = iv; have_pos = true;
-          a_next = op == O_SAPOS ? A_TRAV : A_AFTER;
+          a = op == O_SAPOS ? A_TRAV : A_AFTER;
         } else if (op == O_SCAN_SA) {
           sp = iv; lc = 0;
-          addr = reinterpret_cast<uint64_t>(x.T + sp + depth);
+          addr = reinterpret_cast<uint64_t>(c.T + sp + depth);
           st = S_CMP; op = O_SCAN;
         } else if (op == O_ISAJ) {
           start = end = iv; have_pos = false;
-          a_next = A_EXPAND;
+          a = A_EXPAND;
         } else if (op == O_NS_SA2) {                  // suffix link, both ends
-          addr = ia(x.ISA, iv + 1); addr2 = ia(x.ISA, iv2 + 1);
+          addr = ia(c.ISA, iv + 1); addr2 = ia(c.ISA, iv2 + 1);
           op = O_NS_ISA2;
         } else if (op == O_NS_ISA2) {
           start = iv; end = iv2; need2 = false;
           ++prefix; have_pos = false;
-          if (depth == 0) { start = 0; end = N - 1; a_next = A_TOP; }
-          else a_next = A_EXPAND;
-        } else if (op == O_TD_SA2) {                  // top_down_faster: both ends
-          addr = reinterpret_cast<uint64_t>(x.T + iv + depth);
-          addr2 = reinterpret_cast<uint64_t>(x.T + iv2 + depth);
-          st = S_BYTE; op = O_TD_T2;
-        } else {                                      // O_TD_SA: a bisection probe
-          addr = reinterpret_cast<uint64_t>(x.T + iv + depth);
-          st = S_BYTE; op = O_TD_T;
+          if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
+          else a = A_EXPAND;
+        } else {                                      // top_down_faster probes
+          addr = reinterpret_cast<uint64_t>(c.T + iv + depth);
+          if (op == O_TD_SA2) addr2 = reinterpret_cast<uint64_t>(c.T + iv2 + depth);
+          op = op == O_TD_SA2 ? O_TD_T2 : O_TD_T;
+          st = S_BYTE;
         }
         break;
       }
       case S_BYTE: {
         const int32_t tb = int32_t(int8_t(byte_at(v, ao)));
-        if (op == O_TD_T2) {
+        if (op == O_TD_T2) {                          // both ends of the interval
           cf = ch - tb;
           cl = ch - int32_t(int8_t(byte_at(v2, uint32_t(addr2) & 15)));
           need2 = false;
-          if (cf < 0 || cl > 0) { a_next = A_AFTER; break; }   // no occurrence
-          l = start; r = end; found = false; l2 = start; r2 = end;
-          if (cf == 0) { found = true; a_next = A_TD_AFTER_LEFT; }
-          else a_next = A_TD_LEFT;
-        } else if (op == O_TD_T) {
+          if (cf < 0 || cl > 0) {
+            a = A_AFTER;                              // no occurrence: traverse ends
+          } else {
+            l = start; r = end; found = false; l2 = start; r2 = end;
+            if (cf == 0) found = true;
+            a = cf == 0 ? A_TD_AFTER_LEFT : A_TD_LEFT;
+          }
+        } else if (op == O_TD_T) {                    // a bisection probe
           const int32_t vg = ch - tb;
           if (td_left) {
             if (vg <= 0) {
@@ -391,18 +413,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
             } else {
               l = m;
             }
-            a_next = A_TD_LEFT;
           } else {
             if (vg < 0) r2 = m; else l2 = m;
-            a_next = A_TD_RIGHT;
           }
+          a = td_left ? A_TD_LEFT : A_TD_RIGHT;
         } else {                                      // O_LM: is_leftmaximal
           if (P[prefix - 1] != uint8_t(tb)) {
             if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
             ++nem;
           }
           dch = depth; j = 1;
-          addr = reinterpret_cast<uint64_t>(x.U + pos + 1);
+          addr = reinterpret_cast<uint64_t>(c.U + pos + 1);
           st = S_USCAN;
         }
         break;
@@ -417,17 +438,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
           addr += k;
         } else if (op == O_EXT) {
           depth += lc; lc = 0;
-          a_next = A_AFTER;
+          a = A_AFTER;
         } else {
           if (int32_t(lc) > best) { best = int32_t(lc); bl = bh = m; bpos = sp; }
           else if (int32_t(lc) == best) bh = m;
           if (++m <= end) {
-            addr = ia(x.SA, m);
+            addr = ia(c.SA, m);
             st = S_IDX; op = O_SCAN_SA;
           } else {
             depth += uint32_t(best); start = bl; end = bh; pos = bpos;
             have_pos = start == end;
-            a_next = A_AFTER;
+            a = A_AFTER;
           }
         }
         break;
@@ -439,45 +460,44 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
         const uint32_t hm = byte_mask(v, [&](uint32_t b, uint32_t i) { return b + i >= D + ao; }) & inr;
         if (hm) {
           j += uint32_t(__builtin_ctz(hm)) - ao; hit = true;
-          a_next = A_CHAIN_DONE;
+          a = A_CHAIN_DONE;
         } else {
           j += lim;
           if (j < dch) addr += lim;
-          else { hit = false; a_next = A_CHAIN_DONE; }
+          else { hit = false; a = A_CHAIN_DONE; }
         }
         break;
       }
-      case S_EXL: {                                  // expand_link, left side
-        const uint32_t sm = byte_mask(v, [&](uint32_t b, uint32_t) { return b < depth; }) &
-                            ((2u << ao) - 1);
-        const uint32_t k = sm ? ao - (31 - __builtin_clz(sm)) : ao + 1;
-        if (k && expc + k >= thresh) {
-          depth = 0; start = 0; end = N - 1; have_pos = false; a_next = A_TOP;
-        } else {
-          expc += k; es -= k;
-          if (!sm) {
-            addr = reinterpret_cast<uint64_t>(x.L8 + es);
-          } else if (ee < N - 1) {
-            addr = reinterpret_cast<uint64_t>(x.L8 + ee + 1);
-            st = S_EXR;
-          } else {
-            start = es; end = ee; a_next = A_TOP;
-          }
-        }
-        break;
-      }
-      case S_EXR: {                                  // expand_link, right side
+      case S_EXL:                                    // expand_link, both sides
+      case S_EXR: {
+        const bool left = st == S_EXL;
         const uint64_t room = N - 1 - ee;
-        const uint32_t lim = room < uint64_t(16 - ao) ? uint32_t(room) : 16 - ao;
-        const uint32_t sm = byte_mask(v, [&](uint32_t b, uint32_t) { return b < depth; }) &
-                            (((1u << lim) - 1) << ao);
-        const uint32_t k = sm ? uint32_t(__builtin_ctz(sm)) - ao : lim;
+        const uint32_t lim = left ? ao + 1
+                                  : (room < uint64_t(16 - ao) ? uint32_t(room) : 16 - ao);
+        const uint32_t below = byte_mask(v, [&](uint32_t b, uint32_t) { return b < depth; });
+        const uint32_t sm = below & (left ? ((2u << ao) - 1) : (((1u << lim) - 1) << ao));
+        // qualifying bytes before the stop, walking down (left) or up (right)
+        const uint32_t k = sm ? (left ? ao - (31 - __builtin_clz(sm)) : uint32_t(__builtin_ctz(sm)) - ao)
+                              : lim;
         if (k && expc + k >= thresh) {
-          depth = 0; start = 0; end = N - 1; have_pos = false; a_next = A_TOP;
+          depth = 0; start = 0; end = N - 1; have_pos = false; a = A_TOP;
         } else {
-          expc += k; ee += k;
-          if (!sm && ee < N - 1) addr += lim;
-          else { start = es; end = ee; a_next = A_TOP; }
+          expc += k;
+          if (left) {
+            es -= k;
+            if (!sm) {
+              addr = reinterpret_cast<uint64_t>(c.L8 + es);
+            } else if (ee < N - 1) {
+              addr = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
+              st = S_EXR;
+            } else {
+              start = es; end = ee; a = A_TOP;
+            }
+          } else {
+            ee += k;
+            if (!sm && ee < N - 1) addr += lim;
+            else { start = es; end = ee; a = A_TOP; }
+          }
         }
         break;
       }
@@ -485,159 +505,156 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(Ctx<IdxT> c) {
         break;
     }
 
-    // ---- ALU continuations, in the order the common chains run ----
-    while (a_next != A_NONE) {
-      if (a_next == A_TD_LEFT) {
-        if (r > l + 1) {
-          m = (l + r) >> 1;
-          addr = ia(x.SA, m);
-          st = S_IDX; op = O_TD_SA; td_left = true;
-          a_next = A_NONE;
-        } else {
-          l = r;
-          a_next = A_TD_AFTER_LEFT;
-        }
+    // ---------------- decide ----------------
+    if (a == A_TD_LEFT) {
+      if (r > l + 1) {
+        m = (l + r) >> 1;
+        addr = ia(c.SA, m);
+        st = S_IDX; op = O_TD_SA; td_left = true;
+        a = A_NONE;
+      } else {
+        l = r;
+        a = A_TD_AFTER_LEFT;
       }
-      if (a_next == A_TD_AFTER_LEFT) {
-        if (!found) l2 = l - 1;
-        if (cl == 0) { l2 = end; a_next = A_TD_DONE; }
-        else a_next = A_TD_RIGHT;
+    }
+    if (a == A_TD_AFTER_LEFT) {
+      if (!found) l2 = l - 1;
+      if (cl == 0) l2 = end;
+      a = cl == 0 ? A_TD_DONE : A_TD_RIGHT;
+    }
+    if (a == A_TD_RIGHT) {
+      if (r2 > l2 + 1) {
+        m = (l2 + r2) >> 1;
+        addr = ia(c.SA, m);
+        st = S_IDX; op = O_TD_SA; td_left = false;
+        a = A_NONE;
+      } else {
+        a = A_TD_DONE;
       }
-      if (a_next == A_TD_RIGHT) {
-        if (r2 > l2 + 1) {
-          m = (l2 + r2) >> 1;
-          addr = ia(x.SA, m);
-          st = S_IDX; op = O_TD_SA; td_left = false;
-          a_next = A_NONE;
-        } else {
-          a_next = A_TD_DONE;
-        }
+    }
+    if (a == A_TD_DONE) {
+      const bool ok = l <= l2;
+      if (ok) { start = l; end = l2; ++depth; have_pos = false; }
+      a = (ok && depth != L) ? A_TRAV : A_AFTER;
+    }
+    if (a == A_CHAIN_DONE) {
+      prefix += j;
+      if (!hit) {
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        a = A_TOP;
+      } else {
+        depth = dch - j;
+        addr = ia(c.ISA, pos + j);
+        st = S_IDX; op = O_ISAJ;
+        a = A_NONE;
       }
-      if (a_next == A_TD_DONE) {
-        if (l <= l2) {
-          start = l; end = l2; ++depth; have_pos = false;
-          a_next = depth == L ? A_AFTER : A_TRAV;
-        } else {
-          a_next = A_AFTER;
-        }
-      }
-      if (a_next == A_CHAIN_DONE) {
-        prefix += j;
-        if (!hit) {
-          depth = 0; start = 0; end = N - 1; have_pos = false;
-          a_next = A_TOP;
-        } else {
-          depth = dch - j;
-          addr = ia(x.ISA, pos + j);
-          st = S_IDX; op = O_ISAJ;
-          a_next = A_NONE;
-        }
-      }
-      if (a_next == A_EXPAND) {
-        thresh = uint32_t(2ull * depth * x.logN);
-        expc = 0;
-        es = start; ee = end;
-        addr = reinterpret_cast<uint64_t>(x.L8 + es);
-        st = S_EXL;
-        a_next = A_NONE;
-      }
-      if (a_next == A_AFTER) {
-        if (depth <= 1) {
-          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
-          a_next = A_TOP;
-        } else if (start == end) {
-          if (!have_pos) {
-            addr = ia(x.SA, start);
-            st = S_IDX; op = O_SAPOS2;
-          } else if (depth >= c.min_len && prefix != 0 && pos != 0) {
-            addr = reinterpret_cast<uint64_t>(x.T + pos - 1);
-            st = S_BYTE; op = O_LM;
-          } else {
-            if (depth >= c.min_len) {
-              if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
-              ++nem;
-            }
-            dch = depth; j = 1;
-            addr = reinterpret_cast<uint64_t>(x.U + pos + 1);
-            st = S_USCAN;
-          }
-          a_next = A_NONE;
-        } else {                                     // non-singleton suffix link
+    }
+    if (a == A_EXPAND) {
+      thresh = 2u * depth * c.logN;
+      expc = 0;
+      es = start; ee = end;
+      addr = reinterpret_cast<uint64_t>(c.L8 + es);
+      st = S_EXL;
+      a = A_NONE;
+    }
+    if (a == A_AFTER) {
+      if (depth <= 1) {
+        depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
+        a = A_TOP;
+      } else {
+        a = A_NONE;
+        if (start != end) {                          // non-singleton suffix link
           --depth;
-          addr = ia(x.SA, start); addr2 = ia(x.SA, end); need2 = true;
+          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
           st = S_IDX; op = O_NS_SA2;
-          a_next = A_NONE;
+        } else if (!have_pos) {
+          addr = ia(c.SA, start);
+          st = S_IDX; op = O_SAPOS2;
+        } else if (depth >= c.min_len && prefix != 0 && pos != 0) {
+          addr = reinterpret_cast<uint64_t>(c.T + pos - 1);
+          st = S_BYTE; op = O_LM;
+        } else {
+          if (depth >= c.min_len) {
+            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
+            ++nem;
+          }
+          dch = depth; j = 1;
+          addr = reinterpret_cast<uint64_t>(c.U + pos + 1);
+          st = S_USCAN;
         }
       }
-      if (a_next == A_TOP) {
-        if (prefix >= L) goto read_done;
-        if (depth < c.min_len && !skip_f) {                        // (F)
-          if (prefix + c.min_len > L) goto read_done;
-          int32_t kb = bad.last(prefix, c.min_len);
-
-          while (kb >= 0 && in_text(x, P[kb])) kb = bad.last(prefix, uint32_t(kb) - prefix);
-          if (kb >= 0) {
-            depth = 0; start = 0; end = N - 1; have_pos = false;
-            prefix = uint32_t(kb) + 1;
-            continue;                                               // A_TOP again
-          }
-          const uint32_t B = uint32_t(x.B);
-          if (B > 0 && B <= c.min_len) {
-            const uint32_t q1 = prefix + c.min_len - B;
-            if (bad.bits(prefix, B) == 0 && bad.bits(q1, B) == 0) {
-              c0 = codes_at(C, prefix, B);
-              c1 = codes_at(C, q1, B);
-              addr = reinterpret_cast<uint64_t>(x.BM + (c0 >> 6));
-              st = S_BM; bm2 = false;
-              a_next = A_NONE;
-              break;
-            }
-          }
+    }
+    if (a == A_TOP) {
+      // (F) runs while the state is shallow, once per prefix (skip_f: this
+      // prefix's window already passed the bitmap)
+      bool proceed = skip_f || depth >= c.min_len;
+      skip_f = false;
+      if (prefix >= L || (!proceed && prefix + c.min_len > L)) {
+        a = A_DONE;
+      } else if (!proceed) {
+        int32_t kb = bad.last(prefix, c.min_len);
+        while (kb >= 0 && ((s_in_text[P[kb] >> 6] >> (P[kb] & 63)) & 1ull))
+          kb = bad.last(prefix, uint32_t(kb) - prefix);
+        const uint32_t B = c.B;
+        const uint32_t q1 = prefix + c.min_len - B;
+        if (kb >= 0) {                                // absent byte: next window
+          depth = 0; start = 0; end = N - 1; have_pos = false;
+          prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
+        } else if (B > 0 && B <= c.min_len && bad.bits(prefix, B) == 0 && bad.bits(q1, B) == 0) {
+          c0 = codes_at(C, prefix, B);
+          c1 = codes_at(C, q1, B);
+          addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
+          st = S_BM; bm2 = false;
+          a = A_NONE;
+        } else {
+          proceed = true;                             // no bitmap verdict
         }
-        skip_f = false;
-        // (C) from the root
-        if (depth == 0 && prefix + uint32_t(x.K) <= L && bad.bits(prefix, uint32_t(x.K)) == 0) {
-          addr = reinterpret_cast<uint64_t>(x.KT + 2 * codes_at(C, prefix, uint32_t(x.K)));
+      }
+      if (a == A_TOP && proceed) {                     // (C) from the root
+        if (depth == 0 && prefix + c.K <= L && bad.bits(prefix, c.K) == 0) {
+          addr = reinterpret_cast<uint64_t>(c.KT + 2 * codes_at(C, prefix, c.K));
           st = S_KT;
-          a_next = A_NONE;
-          break;
+          a = A_NONE;
+        } else {
+          a = A_TRAV;
         }
-        a_next = A_TRAV;
       }
-      if (a_next == A_TRAV) {
-        if (depth >= L || prefix + depth >= L) {
-          a_next = A_AFTER;
-          continue;
-        }
+    }
+    if (a == A_TRAV) {
+      if (depth >= L || prefix + depth >= L) {
+        a = A_AFTER;                                  // (backwards: parks in S_ALU)
+      } else {
+        a = A_NONE;
         if (start == end) {
           if (!have_pos) {
-            addr = ia(x.SA, start);
+            addr = ia(c.SA, start);
             st = S_IDX; op = O_SAPOS;
           } else {
-            addr = reinterpret_cast<uint64_t>(x.T + pos + depth);
+            addr = reinterpret_cast<uint64_t>(c.T + pos + depth);
             st = S_CMP; op = O_EXT; lc = 0;
           }
         } else if (end - start + 1 <= uint64_t(kScan)) {
           m = start; best = -1; bl = bh = start; bpos = 0;
-          addr = ia(x.SA, m);
+          addr = ia(c.SA, m);
           st = S_IDX; op = O_SCAN_SA;
         } else {
           ch = int32_t(int8_t(P[prefix + depth]));
-          addr = ia(x.SA, start); addr2 = ia(x.SA, end); need2 = true;
+          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
           st = S_IDX; op = O_TD_SA2;
         }
-        a_next = A_NONE;
       }
-      continue;
-    read_done:
+    }
+    if (a == A_DONE) {
       c.n_out[rd] = nem;
-      if (c.iters) c.iters[rd] = it;
+      if (STATS && c.iters) c.iters[rd] = it;
       it = 0;
       st = S_NEW;
-      break;
+    } else if (a != A_NONE) {
+      pend = a;
+      st = S_ALU;
     }
   }
-  if (c.wave_stats && lane == 0) {
+  if (STATS && lane == 0) {
     atomicAdd(c.wave_stats, (unsigned long long)w_iters);
     atomicAdd(c.wave_stats + 1, (unsigned long long)w_active);
   }

@@ -5,6 +5,18 @@
 // oracle (tests/test_sm_emu.py), and it is the debugger for that kernel
 // (rocgdb is not available on the GPU pool).  Not linked into the product.
 #include "hip/hip_runtime.h"
+
+// every probe must fall inside the array it targets (the device build checks
+// only the span of all arrays)
+static const uint64_t *emu_spans;
+static uint64_t emu_rec_lo, emu_rec_hi, emu_bad;
+static uint4 emu_load16(uint64_t a) {
+  bool ok = a >= emu_rec_lo && a < emu_rec_hi;
+  for (int k = 0; k < 7 && !ok; ++k) ok = a >= emu_spans[2 * k] && a < emu_spans[2 * k + 1];
+  if (!ok) { ++emu_bad; return uint4{0, 0, 0, 0}; }
+  return *reinterpret_cast<const uint4 *>(a & ~uint64_t(15));
+}
+#define SM_LOAD16(a) emu_load16(a)
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
 
 thread_local dim3 threadIdx, blockIdx, blockDim;
@@ -30,22 +42,30 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   }
   threadIdx.x = 0;
   sm::Ctx<IdxT> c;
-  c.x.T = T; c.x.SA = static_cast<const IdxT *>(SA); c.x.ISA = static_cast<const IdxT *>(ISA);
-  c.x.L8 = L8; c.x.U = U; c.x.KT = KT; c.x.BM = BM;
-  c.x.N = N; c.x.logN = logN; c.x.K = K; c.x.B = B;
-  for (int k = 0; k < 4; ++k) c.x.in_text[k] = in_text[k];
-  c.rec = rec.data(); c.g = g; c.lens = nullptr; c.len0 = L; c.min_len = min_len; c.cap = cap;
-  c.n_reads = n; c.out = out; c.n_out = n_out;
+  c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);
+  c.L8 = L8; c.U = U; c.KT = KT; c.BM = BM;
+  c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
+  c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
+  c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
+  c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
   c.work = &work;
-  c.iters = iters; c.wave_stats = nullptr;
-  for (int k = 0; k < 7; ++k) { c.rlo[k] = spans[2 * k]; c.rhi[k] = spans[2 * k + 1]; }
-  c.rlo[7] = reinterpret_cast<uint64_t>(rec.data());
-  c.rhi[7] = c.rlo[7] + rec.size() * sizeof(uint4);
+  for (int k = 0; k < 4; ++k) c.in_text[k] = in_text[k];
+  unsigned long long ws[2] = {0, 0};
+  c.iters = iters; c.wave_stats = ws;
+  // the emulator checks every probe against its own array (the device checks
+  // the span of all of them)
+  (void)spans;
+  c.lo = 0; c.hi = ~0ull;
   unsigned long long v[10] = {0};
   c.viol = v;
-  sm::k_mam_sm<IdxT, 1, true>(c);
+  emu_spans = spans;
+  emu_rec_lo = reinterpret_cast<uint64_t>(rec.data());
+  emu_rec_hi = emu_rec_lo + rec.size() * sizeof(uint4);
+  emu_bad = 0;
+  sm::k_mam_sm<IdxT, 1, true, true>(c);
   for (int k = 0; k < 10; ++k) viol[k] = v[k];
+  viol[0] += emu_bad;
   return 0;
 }
 
