@@ -86,8 +86,8 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   std::vector<uint32_t> h_iters;
   if (STATS) {
     SMASH_HIP(hipMalloc(&c.iters, n_reads * sizeof(uint32_t)));
-    SMASH_HIP(hipMalloc(&c.wave_stats, 16));
-    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 16, s));
+    SMASH_HIP(hipMalloc(&c.wave_stats, 64 * 8));
+    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 64 * 8, s));
   }
   c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;   // d_work[1..10]
   SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 11 * 8, s));
@@ -108,9 +108,9 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   }
   if (STATS) {
     std::vector<uint32_t> hv(n_reads);
-    unsigned long long ws[2];
+    unsigned long long ws[64];
     SMASH_HIP(hipMemcpy(hv.data(), c.iters, n_reads * 4, hipMemcpyDeviceToHost));
-    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 16, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 64 * 8, hipMemcpyDeviceToHost));
     SMASH_HIP(hipFree(c.iters));
     SMASH_HIP(hipFree(c.wave_stats));
     std::vector<uint32_t> srt(hv);
@@ -124,6 +124,21 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
                  (unsigned long long)n_reads, (unsigned long long)blocks, per_cu, c.w_row, sum / n_reads,
                  q(0.5), q(0.9), q(0.99), q(0.999), srt.back(), ws[0],
                  double(ws[1]) / double(ws[0] ? ws[0] : 1));
+    static const char *names[] = {"EXIT", "NEW", "ALU", "COPY", "BM", "KT", "IDX", "BYTE", "CMP",
+                                  "USCAN", "EXL", "EXR"};
+    static const char *idx_ops[] = {"SAPOS", "SAPOS2", "SCAN_SA", "ISAJ", "NS_SA2", "NS_ISA2",
+                                    "TD_SA2", "TD_SA"};
+    static const char *byte_ops[] = {"TD_T2", "TD_T", "LM"};
+    std::fprintf(stderr, "[k_mam_sm] lane-iterations per read by state:");
+    for (int k = 0; k < 12; ++k)
+      if (ws[2 + k]) std::fprintf(stderr, " %s %.1f", names[k], double(ws[2 + k]) / n_reads);
+    for (int k = 0; k < 8; ++k)
+      if (ws[18 + k]) std::fprintf(stderr, " IDX.%s %.1f", idx_ops[k], double(ws[18 + k]) / n_reads);
+    for (int k = 0; k < 3; ++k)
+      if (ws[34 + k]) std::fprintf(stderr, " BYTE.%s %.1f", byte_ops[k], double(ws[34 + k]) / n_reads);
+    for (int k = 0; k < 2; ++k)
+      if (ws[42 + k]) std::fprintf(stderr, " CMP.%s %.1f", k ? "SCAN" : "EXT", double(ws[42 + k]) / n_reads);
+    std::fprintf(stderr, "\n");
   }
   return SMASH_OK;
 }
@@ -160,6 +175,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(ix->d_rec);
   c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
+  c.lin_blocks = 2;
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
   c.out = out; c.n_out = n_out;
   c.work = reinterpret_cast<unsigned long long *>(ix->d_work);

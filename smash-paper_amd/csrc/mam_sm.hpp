@@ -107,14 +107,15 @@ __global__ void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
 enum : uint32_t { S_EXIT = 0, S_NEW, S_ALU, S_COPY, S_BM, S_KT, S_IDX, S_BYTE, S_CMP, S_USCAN,
                   S_EXL, S_EXR };
 // S_IDX ops (an SA / ISA element arrived; *2: a second one in v2)
-enum : uint32_t { O_SAPOS, O_SAPOS2, O_SCAN_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2, O_TD_SA2, O_TD_SA };
-// S_BYTE ops (one text byte; *2: a second one in v2)
-enum : uint32_t { O_TD_T2 = 0, O_TD_T, O_LM };
-// S_CMP ops (16 text bytes compared with the read)
-enum : uint32_t { O_EXT = 0, O_SCAN };
+enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
+// S_CMP ops (16-32 text bytes compared with the read)
+enum : uint32_t { O_EXT = 0, O_BS };
 // ALU continuations, in the order the decide chain runs them
-enum : uint32_t { A_NONE = 0, A_TD_LEFT, A_TD_AFTER_LEFT, A_TD_RIGHT, A_TD_DONE, A_CHAIN_DONE,
-                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE };
+enum : uint32_t { A_NONE = 0, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE, A_EXPAND,
+                  A_AFTER, A_TOP, A_TRAV, A_DONE };
+// binary-search modes: 0 where P' sorts (traverse); 1 / 2 the left / right
+// end of a run of suffixes sharing `cap` characters (from `cbase`) with P
+enum : uint32_t { BS_INSERT = 0, BS_LEFT, BS_RIGHT };
 
 __device__ __forceinline__ uint64_t lo64(const uint4 &v) { return uint64_t(v.x) | (uint64_t(v.y) << 32); }
 __device__ __forceinline__ uint64_t hi64(const uint4 &v) { return uint64_t(v.z) | (uint64_t(v.w) << 32); }
@@ -200,6 +201,7 @@ struct Ctx {
   // k_prep records and the LDS row geometry
   const uint4 *rec;
   uint32_t chunks, c_bad, w_row, w_raw;
+  uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -215,7 +217,7 @@ struct Ctx {
   // STATS builds only: per-read loop iterations; per-kernel sums of wave
   // iterations and of active lanes over them
   uint32_t *iters;
-  unsigned long long *wave_stats;
+  unsigned long long *wave_stats;   // [0] wave iterations [1] active lanes [2..] lane iterations per state
 };
 
 template <class IdxT>
@@ -235,6 +237,18 @@ __device__ __forceinline__ uint64_t idx_val(const uint4 &v, uint32_t ao) {
 // transitions that go backwards in it (end of read inside traverse ->
 // after-traverse; a window filter skip -> the next window) park the lane in
 // S_ALU for one iteration.
+//
+// traverse (longSA.cpp:297-316) over an interval [start, end] whose suffixes
+// share `depth` characters with P' = P[prefix..L): its result is the longest
+// match  best = max_i lcp(P'[depth..], T[SA[i]+depth..])  and the suffixes
+// reaching it.  top_down_faster finds it character by character; here a
+// binary search with full comparisons (lcp skipping as in Manber-Myers) finds
+// where P' sorts: the suffix with the longest match is next to that point and
+// both neighbours are probed; the suffixes sharing `best` more characters
+// form the run around it with L8 >= depth + best (found by the expand_link
+// scanner, bounded by [start, end]).  Same final (depth, interval) as the
+// reference's traverse; ~2.5 log2(interval) probes instead of 4 log2 per
+// character.
 template <class IdxT, int BLOCK, bool CHECK, bool STATS>
 __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   extern __shared__ uint32_t ldsw[];
@@ -258,14 +272,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint64_t start = 0, end = 0, pos = 0;
   bool have_pos = false;
   // phase registers, shared by phases that are never live together
-  uint64_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0;
-  uint64_t &l = x0, &r = x1, &l2 = x2, &r2 = x3, &m = x4;      // top_down_faster
-  uint64_t &bl = x0, &bh = x1, &bpos = x2, &sp = x3;            // (S) scan (m = x4)
-  uint64_t &es = x0, &ee = x1;                                  // expand_link
-  uint64_t &c0 = x2, &c1 = x3;                                  // (F) bitmap codes
-  int32_t cf = 0, cl = 0, best = -1, ch = 0;
-  bool found = false, hit = false, bm2 = false, td_left = false, skip_f = false;
-  uint32_t lc = 0, dch = 0, j = 0, expc = 0, thresh = 0;
+  uint64_t lo = 0, hi = 0, bpos = 0, sp = 0, m = 0, bi = 0, es = 0, ee = 0;
+  uint64_t &c0 = bpos, &c1 = sp;                                // (F) bitmap codes
+  uint32_t lL = 0, lR = 0, best = 0, lc = 0, cbase = 0, cap = 0, bsm = 0, nblk = 0;
+  bool hit = false, bm2 = false, skip_f = false, xrun = false;
+  uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
 
@@ -302,13 +313,18 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {
           L = c.lens ? c.lens[rd] : c.len0;
           addr = reinterpret_cast<uint64_t>(c.rec + rd * c.chunks);
+          addr2 = addr + 16;
+          need2 = c.chunks > 1;
           kc = 0;
           st = S_COPY;
         }
       }
     }
     if (st < S_ALU || fresh) continue;
-    if (STATS) ++it;
+    if (STATS) {
+      ++it;
+      atomicAdd(c.wave_stats + 2 + (st == S_IDX ? 16 + op : st == S_CMP ? 40 + op : st), 1ull);
+    }
 #ifdef SM_TRACE
     if (st != S_COPY)
       printf("it %u st %u op %u prefix %u depth %u [%llu,%llu] pos %llu hp %d\n", it, st, op, prefix,
@@ -323,27 +339,35 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       case S_ALU:
         a = pend;
         break;
-      case S_COPY: {
-        if (kc < c.c_bad) {
-          if (kc == 0) { bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w; }
-          else { bad.w4 = v.x; bad.w5 = v.y; bad.w6 = v.z; bad.w7 = v.w; }
-        } else {
-          const uint32_t q = 4 * (kc - c.c_bad);
-          if (q + 0 < c.w_row) row[q + 0] = v.x;
-          if (q + 1 < c.w_row) row[q + 1] = v.y;
-          if (q + 2 < c.w_row) row[q + 2] = v.z;
-          if (q + 3 < c.w_row) row[q + 3] = v.w;
+      case S_COPY: {                                 // record chunks kc (v), kc+1 (v2)
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+          const uint4 &u = h ? v2 : v;
+          const uint32_t k = kc + h;
+          if (k >= c.chunks) break;
+          if (k < c.c_bad) {
+            if (k == 0) { bad.w0 = u.x; bad.w1 = u.y; bad.w2 = u.z; bad.w3 = u.w; }
+            else { bad.w4 = u.x; bad.w5 = u.y; bad.w6 = u.z; bad.w7 = u.w; }
+          } else {
+            const uint32_t q = 4 * (k - c.c_bad);
+            if (q + 0 < c.w_row) row[q + 0] = u.x;
+            if (q + 1 < c.w_row) row[q + 1] = u.y;
+            if (q + 2 < c.w_row) row[q + 2] = u.z;
+            if (q + 3 < c.w_row) row[q + 3] = u.w;
+          }
         }
-        if (++kc < c.chunks) {
-          addr += 16;
+        kc += 2;
+        if (kc < c.chunks) {
+          addr += 32; addr2 = addr + 16; need2 = kc + 1 < c.chunks;
         } else {
+          need2 = false;
           prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
           skip_f = false;
           a = A_TOP;
         }
         break;
       }
-      case S_BM: {                                   // (F) B-mer presence
+      case S_BM: {                                   // (F) first, then last B-mer present?
         const uint64_t cc = bm2 ? c1 : c0;
         if (!((((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull)) {
           depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
@@ -357,8 +381,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_KT: {                                   // (C)
-        const uint64_t lo = lo64(v), hi = hi64(v);
-        if (lo <= hi) { depth = c.K; start = lo; end = hi; have_pos = false; }
+        const uint64_t l0 = lo64(v), h0 = hi64(v);
+        if (l0 <= h0) { depth = c.K; start = l0; end = h0; have_pos = false; }
         a = A_TRAV;
         break;
       }
@@ -368,88 +392,72 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         if (op == O_SAPOS || op == O_SAPOS2) {
           pos = iv; have_pos = true;
           a = op == O_SAPOS ? A_TRAV : A_AFTER;
-        } else if (op == O_SCAN_SA) {
-          sp = iv; lc = 0;
-          addr = reinterpret_cast<uint64_t>(c.T + sp + depth);
-          st = S_CMP; op = O_SCAN;
+        } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
+          sp = iv;
+          addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
+          addr2 = (addr & ~uint64_t(15)) + 16;
+          need2 = cap - lc > 16 - (uint32_t(addr) & 15);
+          st = S_CMP; op = O_BS;
         } else if (op == O_ISAJ) {
           start = end = iv; have_pos = false;
           a = A_EXPAND;
         } else if (op == O_NS_SA2) {                  // suffix link, both ends
           addr = ia(c.ISA, iv + 1); addr2 = ia(c.ISA, iv2 + 1);
           op = O_NS_ISA2;
-        } else if (op == O_NS_ISA2) {
+        } else {                                      // O_NS_ISA2
           start = iv; end = iv2; need2 = false;
           ++prefix; have_pos = false;
           if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
           else a = A_EXPAND;
-        } else {                                      // top_down_faster probes
-          addr = reinterpret_cast<uint64_t>(c.T + iv + depth);
-          if (op == O_TD_SA2) addr2 = reinterpret_cast<uint64_t>(c.T + iv2 + depth);
-          op = op == O_TD_SA2 ? O_TD_T2 : O_TD_T;
-          st = S_BYTE;
         }
         break;
       }
-      case S_BYTE: {
-        const int32_t tb = int32_t(int8_t(byte_at(v, ao)));
-        if (op == O_TD_T2) {                          // both ends of the interval
-          cf = ch - tb;
-          cl = ch - int32_t(int8_t(byte_at(v2, uint32_t(addr2) & 15)));
-          need2 = false;
-          if (cf < 0 || cl > 0) {
-            a = A_AFTER;                              // no occurrence: traverse ends
-          } else {
-            l = start; r = end; found = false; l2 = start; r2 = end;
-            if (cf == 0) found = true;
-            a = cf == 0 ? A_TD_AFTER_LEFT : A_TD_LEFT;
-          }
-        } else if (op == O_TD_T) {                    // a bisection probe
-          const int32_t vg = ch - tb;
-          if (td_left) {
-            if (vg <= 0) {
-              if (!found && vg == 0) { found = true; l2 = m; r2 = r; }
-              r = m;
-            } else {
-              l = m;
-            }
-          } else {
-            if (vg < 0) r2 = m; else l2 = m;
-          }
-          a = td_left ? A_TD_LEFT : A_TD_RIGHT;
-        } else {                                      // O_LM: is_leftmaximal
-          if (P[prefix - 1] != uint8_t(tb)) {
-            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
-            ++nem;
-          }
-          dch = depth; j = 1;
-          addr = reinterpret_cast<uint64_t>(c.U + pos + 1);
-          st = S_USCAN;
+      case S_BYTE: {                                 // is_leftmaximal: T[pos-1]
+        if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
+          if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
+          ++nem;
         }
+        dch = depth; j = 1;
+        addr = reinterpret_cast<uint64_t>(c.U + pos + 1);
+        st = S_USCAN;
         break;
       }
-      case S_CMP: {                                  // (A) extension / (S) candidate
-        const uint32_t off = prefix + depth + lc;
-        const uint32_t rem = L - off;
+      case S_CMP: {                                  // (A) extension / traverse probe
+        // bytes [ao, 16) of v, then (need2) the next block v2
+        const uint32_t off = prefix + (op == O_BS ? cbase : depth) + lc;
+        const uint32_t rem = op == O_BS ? cap - lc : L - off;
         const uint32_t lim = rem < 16 - ao ? rem : 16 - ao;
-        const uint32_t k = agree_block(v, ao, P, off, lim);
+        uint32_t k = agree_block(v, ao, P, off, lim);
+        if (need2 && k == lim && k < rem) {
+          const uint32_t lim2 = rem - k < 16 ? rem - k : 16u;
+          k += agree_block(v2, 0, P, off + k, lim2);
+        }
+        const uint32_t got = need2 ? (rem < 32 - ao ? rem : 32 - ao) : lim;   // bytes available
         lc += k;
-        if (k == lim && k < rem) {
+        if (k == got && k < rem) {                    // agreed on all loaded bytes: go on
           addr += k;
+          addr2 = (addr & ~uint64_t(15)) + 16;
+          need2 = rem - k > 16 - (uint32_t(addr) & 15);
         } else if (op == O_EXT) {
+          need2 = false;
           depth += lc; lc = 0;
           a = A_AFTER;
-        } else {
-          if (int32_t(lc) > best) { best = int32_t(lc); bl = bh = m; bpos = sp; }
-          else if (int32_t(lc) == best) bh = m;
-          if (++m <= end) {
-            addr = ia(c.SA, m);
-            st = S_IDX; op = O_SCAN_SA;
-          } else {
-            depth += uint32_t(best); start = bl; end = bh; pos = bpos;
-            have_pos = start == end;
-            a = A_AFTER;
+        } else {                                      // O_BS: probe m decided
+          need2 = false;
+          bool left;                                  // keep [lo, m) (else (m, hi))
+          if (bsm == BS_INSERT) {
+            // P' < S_m iff P' ran out (prefix of S_m) or the first differing
+            // byte of P' is smaller (signed chars, like the reference)
+            const uint32_t tpos = ao + k;
+            const uint32_t tbyte = tpos < 16 ? byte_at(v, tpos) : byte_at(v2, tpos - 16);
+            left = k == rem || int8_t(P[off + k]) < int8_t(tbyte);
+            if (lc > best) { best = lc; bpos = sp; bi = m; }
+          } else {                                    // in the run iff lcp reaches cap
+            left = (lc >= cap) == (bsm == BS_LEFT);
           }
+          if (left) { hi = m; lR = lc; }
+          else { lo = m + 1; lL = lc; }
+          a = A_BS;
         }
         break;
       }
@@ -468,36 +476,30 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         }
         break;
       }
-      case S_EXL:                                    // expand_link, both sides
-      case S_EXR: {
+      case S_EXL:                                    // L8 runs: expand_link (xrun = 0)
+      case S_EXR: {                                  // or the traverse's final run (1)
         const bool left = st == S_EXL;
-        const uint64_t room = N - 1 - ee;
-        const uint32_t lim = left ? ao + 1
-                                  : (room < uint64_t(16 - ao) ? uint32_t(room) : 16 - ao);
-        const uint32_t below = byte_mask(v, [&](uint32_t b, uint32_t) { return b < depth; });
-        const uint32_t sm = below & (left ? ((2u << ao) - 1) : (((1u << lim) - 1) << ao));
-        // qualifying bytes before the stop, walking down (left) or up (right)
+        const uint64_t lb = xrun ? start : 0, hb = xrun ? end : N - 1;
+        const uint64_t roomL = es - lb, roomR = hb - ee;
+        const uint32_t lim = left ? (roomL < uint64_t(ao + 1) ? uint32_t(roomL) : ao + 1)
+                                  : (roomR < uint64_t(16 - ao) ? uint32_t(roomR) : 16 - ao);
+        const uint32_t below = byte_mask(v, [&](uint32_t b, uint32_t) { return b < xd; });
+        const uint32_t win = left ? (((1u << lim) - 1) << (ao + 1 - lim)) : (((1u << lim) - 1) << ao);
+        const uint32_t sm = below & win;
+        // run members before the stop, walking down (left) or up (right)
         const uint32_t k = sm ? (left ? ao - (31 - __builtin_clz(sm)) : uint32_t(__builtin_ctz(sm)) - ao)
                               : lim;
-        if (k && expc + k >= thresh) {
-          depth = 0; start = 0; end = N - 1; have_pos = false; a = A_TOP;
-        } else {
-          expc += k;
-          if (left) {
-            es -= k;
-            if (!sm) {
-              addr = reinterpret_cast<uint64_t>(c.L8 + es);
-            } else if (ee < N - 1) {
-              addr = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
-              st = S_EXR;
-            } else {
-              start = es; end = ee; a = A_TOP;
-            }
-          } else {
-            ee += k;
-            if (!sm && ee < N - 1) addr += lim;
-            else { start = es; end = ee; a = A_TOP; }
-          }
+        const bool more = !sm && (left ? es - k > lb : ee + k < hb);
+        if (left) es -= k; else ee += k;
+        if (!more) {
+          a = left ? A_XL_DONE : A_RUN_DONE;
+        } else if (++nblk < c.lin_blocks) {
+          addr = reinterpret_cast<uint64_t>(c.L8 + (left ? es : ee + 1));
+        } else {                                      // long run: bisect for its end
+          bsm = left ? BS_LEFT : BS_RIGHT;
+          if (left) { lo = lb; hi = es; lL = 0; lR = cap; }
+          else { lo = ee + 1; hi = hb + 1; lL = cap; lR = 0; }
+          a = A_BS;
         }
         break;
       }
@@ -506,36 +508,65 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
 
     // ---------------- decide ----------------
-    if (a == A_TD_LEFT) {
-      if (r > l + 1) {
-        m = (l + r) >> 1;
+    if (a == A_BS) {                                  // next probe of a binary search
+      if (lo < hi) {
+        m = (lo + hi) >> 1;
+        lc = lL < lR ? lL : lR;
         addr = ia(c.SA, m);
-        st = S_IDX; op = O_TD_SA; td_left = true;
+        st = S_IDX; op = O_BS_SA;
         a = A_NONE;
       } else {
-        l = r;
-        a = A_TD_AFTER_LEFT;
+        a = A_BS_DONE;
       }
     }
-    if (a == A_TD_AFTER_LEFT) {
-      if (!found) l2 = l - 1;
-      if (cl == 0) l2 = end;
-      a = cl == 0 ? A_TD_DONE : A_TD_RIGHT;
+    if (a == A_BS_DONE) {
+      lc = 0;
+      if (bsm == BS_LEFT) {
+        es = lo;                                      // first suffix of the run
+        a = A_XL_DONE;
+      } else if (bsm == BS_RIGHT) {
+        ee = lo - 1;                                  // last suffix of the run
+        a = A_RUN_DONE;
+      } else if (best == 0) {
+        a = A_AFTER;                                  // no longer match: interval unchanged
+      } else {                                        // the run of suffixes sharing best more
+        xd = depth + best; xrun = true;
+        cbase = depth; cap = best;
+        es = bi; ee = bi; nblk = 0;
+        if (es > start) {
+          addr = reinterpret_cast<uint64_t>(c.L8 + es);
+          st = S_EXL;
+          a = A_NONE;
+        } else {
+          a = A_XL_DONE;
+        }
+      }
     }
-    if (a == A_TD_RIGHT) {
-      if (r2 > l2 + 1) {
-        m = (l2 + r2) >> 1;
-        addr = ia(c.SA, m);
-        st = S_IDX; op = O_TD_SA; td_left = false;
+    if (a == A_XL_DONE) {                             // left end known: right side
+      const uint64_t hb = xrun ? end : N - 1;
+      nblk = 0;
+      if (!xrun && start - es >= thresh) {            // expand_link gives up (longSA.h:164)
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        a = A_TOP;
+      } else if (ee < hb) {
+        addr = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
+        st = S_EXR;
         a = A_NONE;
       } else {
-        a = A_TD_DONE;
+        a = A_RUN_DONE;
       }
     }
-    if (a == A_TD_DONE) {
-      const bool ok = l <= l2;
-      if (ok) { start = l; end = l2; ++depth; have_pos = false; }
-      a = (ok && depth != L) ? A_TRAV : A_AFTER;
+    if (a == A_RUN_DONE) {
+      if (xrun) {                                     // traverse result
+        start = es; end = ee; depth = xd; pos = bpos; have_pos = start == end;
+        a = A_AFTER;
+      } else if ((start - es) + (ee - end) >= thresh) {
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        a = A_TOP;
+      } else {                                        // expand_link succeeded
+        start = es; end = ee;
+        a = A_TOP;
+      }
     }
     if (a == A_CHAIN_DONE) {
       prefix += j;
@@ -549,10 +580,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_NONE;
       }
     }
-    if (a == A_EXPAND) {
+    if (a == A_EXPAND) {                              // expand_link (longSA.h:158-174)
+      // the run around [start, end] with L8 >= depth = the suffixes sharing
+      // P[prefix, prefix+depth); it fails iff it holds >= thresh more
       thresh = 2u * depth * c.logN;
-      expc = 0;
-      es = start; ee = end;
+      xd = depth; xrun = false;
+      cbase = 0; cap = depth;
+      es = start; ee = end; nblk = 0;
       addr = reinterpret_cast<uint64_t>(c.L8 + es);
       st = S_EXL;
       a = A_NONE;
@@ -572,7 +606,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           st = S_IDX; op = O_SAPOS2;
         } else if (depth >= c.min_len && prefix != 0 && pos != 0) {
           addr = reinterpret_cast<uint64_t>(c.T + pos - 1);
-          st = S_BYTE; op = O_LM;
+          st = S_BYTE;
         } else {
           if (depth >= c.min_len) {
             if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
@@ -625,22 +659,23 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_AFTER;                                  // (backwards: parks in S_ALU)
       } else {
         a = A_NONE;
-        if (start == end) {
+        if (start == end) {                          // (A) singleton: extend
           if (!have_pos) {
             addr = ia(c.SA, start);
             st = S_IDX; op = O_SAPOS;
           } else {
             addr = reinterpret_cast<uint64_t>(c.T + pos + depth);
+            addr2 = (addr & ~uint64_t(15)) + 16;
+            need2 = L - prefix - depth > 16 - (uint32_t(addr) & 15);
             st = S_CMP; op = O_EXT; lc = 0;
           }
-        } else if (end - start + 1 <= uint64_t(kScan)) {
-          m = start; best = -1; bl = bh = start; bpos = 0;
+        } else {                                     // search [start, end] for P'
+          lo = start; hi = end + 1; lL = 0; lR = 0; best = 0;
+          bsm = BS_INSERT; cbase = depth; cap = L - prefix - depth;
+          m = (lo + hi) >> 1;
+          lc = 0;
           addr = ia(c.SA, m);
-          st = S_IDX; op = O_SCAN_SA;
-        } else {
-          ch = int32_t(int8_t(P[prefix + depth]));
-          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
-          st = S_IDX; op = O_TD_SA2;
+          st = S_IDX; op = O_BS_SA;
         }
       }
     }

@@ -24,10 +24,13 @@ def emu(tiny_ix):
 
 @pytest.mark.parametrize("s", ["s100", "s150"])
 @pytest.mark.parametrize("wide", [False, True])
-def test_state_machine_matches_reference_goldens(emu, s, wide):
+@pytest.mark.parametrize("lin", [2, 1])
+def test_state_machine_matches_reference_goldens(emu, s, wide, lin):
+    """lin: L8 blocks scanned per side of a run before bisecting (1 forces
+    the bisection path on every run longer than one block)."""
     exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
            for l in read_gz_lines("%s_MAM.txt.gz" % s)]
-    got, iters = emu[int(wide)].map(interleaved_reads(s))
+    got, iters = emu[int(wide)].map(interleaved_reads(s), lin_blocks=lin)
     bad = [i for i in range(len(exp)) if got[i] != exp[i]]
     assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)
     assert iters.min() > 0
@@ -53,10 +56,10 @@ def test_state_machine_edge_reads(emu, tiny_ix, L):
     reads = _edge_reads(tiny_ix, L, 120, rng)
     extra = [b"z" * L, b"n" * L, b"a" * L, (b"acgt" * 64)[:L], (b"c" * (L // 2) + b"z" + b"c" * L)[:L]]
     reads = np.concatenate([reads, np.array([np.frombuffer(x, np.uint8) for x in extra])])
-    for ml in (20, 12, 30):
-        got, _ = emu[0].map(reads, min_len=ml)
+    for ml, lin in ((20, 2), (12, 2), (30, 2), (20, 1), (12, 1)):
+        got, _ = emu[0].map(reads, min_len=ml, lin_blocks=lin)
         for i in range(len(reads)):
-            assert got[i] == tiny_ix.search(reads[i].tobytes(), min_len=ml), (ml, i)
+            assert got[i] == tiny_ix.search(reads[i].tobytes(), min_len=ml), (ml, lin, i)
 
 
 def test_state_machine_on_mid_genome():
@@ -72,6 +75,8 @@ def test_state_machine_on_mid_genome():
     lo = np.arange(256, dtype=np.uint8)
     lo[65:91] += 32
     reads = lo[reads]
-    got, _ = sm_emu.Emu(ix).map(reads)
-    for i in range(len(reads)):
-        assert got[i] == ix.search(reads[i].tobytes()), i
+    emu = sm_emu.Emu(ix)
+    for lin in (2, 1):
+        got, _ = emu.map(reads, lin_blocks=lin)
+        for i in range(len(reads)):
+            assert got[i] == ix.search(reads[i].tobytes()), (lin, i)

@@ -30,7 +30,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
                const uint64_t *in_text, uint64_t N, uint64_t logN, const uint8_t *reads,
                uint64_t stride, uint32_t L, uint64_t n, uint32_t min_len, uint64_t *out,
                uint32_t cap, uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
-               uint64_t *viol) {
+               uint64_t *viol, uint32_t lin_blocks) {
   const sm::Geom g = sm::make_geom(L);
   if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
   std::vector<uint4> rec(n * g.chunks);
@@ -46,12 +46,13 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   c.L8 = L8; c.U = U; c.KT = KT; c.BM = BM;
   c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
   c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
+  c.lin_blocks = lin_blocks;
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
   c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
   c.work = &work;
   for (int k = 0; k < 4; ++k) c.in_text[k] = in_text[k];
-  unsigned long long ws[2] = {0, 0};
+  unsigned long long ws[64] = {0};
   c.iters = iters; c.wave_stats = ws;
   // the emulator checks every probe against its own array (the device checks
   // the span of all of them)
@@ -75,10 +76,10 @@ extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int
                           uint64_t logN, const uint8_t *reads, uint64_t stride, uint32_t L,
                           uint64_t n, uint32_t min_len, uint64_t *out, uint32_t cap,
                           uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
-                          uint64_t *viol) {
+                          uint64_t *viol, uint32_t lin_blocks) {
   if (idx_bytes == 4)
     return run<uint32_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
-                         min_len, out, cap, n_out, iters, spans, viol);
+                         min_len, out, cap, n_out, iters, spans, viol, lin_blocks);
   return run<uint64_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
-                       min_len, out, cap, n_out, iters, spans, viol);
+                       min_len, out, cap, n_out, iters, spans, viol, lin_blocks);
 }

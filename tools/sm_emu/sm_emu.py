@@ -78,7 +78,7 @@ class Emu:
         self.it = in_text_words(list(ix.acc.in_text))
         self.isz = np.dtype(it).itemsize
 
-    def map(self, reads, min_len=20, cap=512):
+    def map(self, reads, min_len=20, cap=512, lin_blocks=2):
         """reads: uint8 [n, L].  Returns (list of [(ref, q, len)], iterations)."""
         reads = np.ascontiguousarray(reads, np.uint8)
         n, L = reads.shape
@@ -97,7 +97,8 @@ class Emu:
             C.c_uint64(L), C.c_uint32(L), C.c_uint64(n), C.c_uint32(min_len),
             out.ctypes.data_as(C.c_void_p), C.c_uint32(cap),
             nout.ctypes.data_as(C.c_void_p), iters.ctypes.data_as(C.c_void_p),
-            spans.ctypes.data_as(C.c_void_p), viol.ctypes.data_as(C.c_void_p))
+            spans.ctypes.data_as(C.c_void_p), viol.ctypes.data_as(C.c_void_p),
+            C.c_uint32(lin_blocks))
         assert rc == 0
         assert viol[0] == 0, ("out-of-range probe", viol.tolist())
         res = []
