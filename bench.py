@@ -13,9 +13,10 @@ de-dup -> varbin adjacent de-dup -> bin counts (+ the multi-GPU exchanges and
 the RCCL all-reduce of the count vector when N > 1).  value = reads (mates)
 processed by all ranks / max-over-ranks wall time of the K timed steps.
 
-Also reported: `roofline` of the dominant kernel (k_mam: algorithmic bytes =
-64 B x distinct line transitions per read, counted by the oracle on a sample
-of the same reads, over the HIP-event-timed kernel duration) and
+Also reported: `roofline` of the dominant kernel (k_mam_sm: algorithmic bytes
+= 64 B x the line transitions of the kernel's own probe sequence, counted by
+running the kernel source on the host (tools/sm_emu) over the downloaded index
+for a sample of the same reads, over the HIP-event-timed kernel duration) and
 `cpu_baseline` (the C oracle of the whole chain on the host cores, rank 0,
 N = 1, bounded sample).  The bench also checks that the device's bin counts on
 that sample are identical to the oracle's.
@@ -28,7 +29,7 @@ import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-for _p in ("smash-paper_amd", "tools", "oracle"):
+for _p in ("smash-paper_amd", "tools", "tools/sm_emu", "oracle"):
     sys.path.insert(0, os.path.join(ROOT, _p))
 
 import numpy as np  # noqa: E402
@@ -238,22 +239,26 @@ def main():
         t2 = time.time()
         oix, mp = host_index(S, O, dix, T, sp, sz, names)
         log("host copy of the index for the oracle: %.1fs" % (time.time() - t2))
-        # algorithmic bytes per read: 64 B x line transitions of the algorithm
-        # the kernel runs (orc_mam_fast = the device's accelerated search)
+        # algorithmic bytes per read: 64 B x the 64-byte line transitions of
+        # k_mam_sm's own probe sequence, counted by running the kernel's code
+        # on the host (tools/sm_emu: the same source, one lane) over this
+        # index and a sample of the same reads
+        import sm_emu
         ns = min(4000, 2 * P)
-        _, ctr = O.map_only_v3(oix, reads_h[:ns], threads=min(16, os.cpu_count() or 1),
-                               count=True)
-        lines = ctr.lines()
+        emu = sm_emu.Emu(oix, copy=False)
+        _, emu_it = emu.map(reads_h[:ns])
+        lines = sum(v[1] for v in emu.counters.values())
         b_read = 64.0 * lines / ns
         achieved = reads_per_launch * b_read / (avg_ms / 1e3) / 1e9
-        roof = {"bound": "hbm", "kernel": "k_mam", "achieved": round(achieved, 2),
+        roof = {"bound": "hbm", "kernel": "k_mam_sm", "achieved": round(achieved, 2),
                 "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
                 "traffic": None, "bytes_per_read": round(b_read, 1),
                 "avg_kernel_ms": round(avg_ms, 3), "reads_per_launch": int(reads_per_launch),
-                "lines_per_read": {"sa": ctr.sa_lines / ns, "isa": ctr.isa_lines / ns,
-                                   "ref": ctr.ref_lines / ns, "lcp": ctr.lcp_lines / ns,
-                                   "kmer": ctr.kt_lines / ns, "uniq": ctr.u_lines / ns,
-                                   "bitmap": ctr.bm_lines / ns}}
+                "lines_per_read": {k: round(v[1] / ns, 3) for k, v in emu.counters.items()},
+                "probes_per_read": {k: round(v[0] / ns, 3) for k, v in emu.counters.items()},
+                "loop_iterations_per_read": round(float(emu_it.mean()), 1),
+                "bytes_method": "64 B x line transitions of the kernel's probe sequence "
+                                "(tools/sm_emu on the downloaded index, %d reads)" % ns}
         pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
         if os.path.exists(pmc):
             try:

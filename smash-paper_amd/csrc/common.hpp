@@ -98,6 +98,9 @@ struct smash_index {
   // smash_map_batch; like d_work, one batch in flight per index
   mutable uint32_t *d_rec = nullptr;
   mutable uint64_t rec_bytes = 0;
+  // optional event pair recorded right around the k_mam_sm launch (set by
+  // smash_pipeline profiling for the duration of one smash_map_batch call)
+  mutable hipEvent_t kev[2] = {nullptr, nullptr};
   uint64_t *d_startpos = nullptr;
   uint64_t *d_sizes = nullptr;
   double build_seconds = 0;

@@ -91,8 +91,10 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   }
   c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;   // d_work[1..10]
   SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 11 * 8, s));
+  if (ix->kev[0]) SMASH_HIP(hipEventRecord(ix->kev[0], s));
   kern<<<unsigned(blocks), B, lds, s>>>(c);
   SMASH_HIP(hipGetLastError());
+  if (ix->kev[1]) SMASH_HIP(hipEventRecord(ix->kev[1], s));
   unsigned long long h[10];
   SMASH_HIP(hipMemcpyAsync(h, c.viol, sizeof(h), hipMemcpyDeviceToHost, s));
   SMASH_HIP(hipStreamSynchronize(s));
@@ -230,10 +232,12 @@ int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   if (blocks > need) blocks = need;
   DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
   SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
+  if (ix->kev[0]) SMASH_HIP(hipEventRecord(ix->kev[0], s));
   k_mam<IdxT, B, PLAIN><<<unsigned(blocks), B, lds, s>>>(
       x, seqs, stride, lens, len, n_reads, min_len, out, cap, n_out, row,
       reinterpret_cast<unsigned long long *>(ix->d_work));
   SMASH_HIP(hipGetLastError());
+  if (ix->kev[1]) SMASH_HIP(hipEventRecord(ix->kev[1], s));
   return SMASH_OK;
 }
 

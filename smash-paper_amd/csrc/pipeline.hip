@@ -583,14 +583,15 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
         p->ev.push_back(e);
       }
     }
-    SMASH_HIP(hipEventRecord(p->ev[2 * p->n_ev], s));
+    p->ix->kev[0] = p->ev[2 * p->n_ev];          // recorded around k_mam_sm itself
+    p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
   rc = smash_map_batch(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len,
                        nullptr, p->read_len, 2 * n_pairs, p->d_match, p->slots,
                        p->d_nmatch, stream);
+  p->ix->kev[0] = p->ix->kev[1] = nullptr;
   if (rc) return rc;
   if (p->prof) {
-    SMASH_HIP(hipEventRecord(p->ev[2 * p->n_ev + 1], s));
     ++p->n_ev;
     p->prof_reads += 2 * n_pairs;
   }

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
@@ -43,6 +44,23 @@ __global__ __launch_bounds__(256) void k_chase(const uint4 *buf, uint64_t n16, i
 int main(int argc, char **argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  if (argc > 1 && std::string(argv[1]) == "calib") {
+    // FETCH_SIZE calibration for random 16-byte probes: one launch of a known
+    // number of dependent random loads over 64 GiB (no line is reused)
+    const uint64_t bytes = 64ull << 30, n16 = bytes / 16;
+    void *buf = nullptr;
+    uint64_t *sink;
+    CK(hipMalloc(&buf, bytes));
+    CK(hipMemset(buf, 0, bytes));
+    CK(hipMalloc(&sink, 8));
+    const uint64_t threads = 4ull * 4 * cus * 64;
+    const int steps = 64;
+    k_chase<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, 7);
+    CK(hipDeviceSynchronize());
+    std::printf("calib: %llu random 16-byte loads (%llu threads x %d) over 64 GiB\n",
+                (unsigned long long)(threads * steps), (unsigned long long)threads, steps);
+    return 0;
+  }
   std::vector<double> gib;
   for (int i = 1; i < argc; ++i) gib.push_back(std::atof(argv[i]));
   if (gib.empty()) gib = {0.25, 4, 32, 128};

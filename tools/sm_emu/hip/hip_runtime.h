@@ -17,6 +17,7 @@
 
 typedef int hipError_t;
 typedef void *hipStream_t;
+typedef void *hipEvent_t;
 static const hipError_t hipSuccess = 0;
 inline const char *hipGetErrorString(hipError_t) { return "sm_emu: no HIP runtime"; }
 inline hipError_t hipMalloc(void **, size_t) { return 1; }

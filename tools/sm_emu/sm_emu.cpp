@@ -8,13 +8,32 @@
 
 // every probe must fall inside the array it targets (the device build checks
 // only the span of all arrays)
+// Access accounting for the roofline (bench.py): per array (T SA ISA L8 U KT
+// BM records) the 16-byte probes and the distinct 64-byte line transitions
+// (a probe whose line differs from that array's previous probe line), i.e.
+// the algorithmic bytes of the kernel's own access sequence.
 static const uint64_t *emu_spans;
 static uint64_t emu_rec_lo, emu_rec_hi, emu_bad;
+static uint64_t emu_probes[8], emu_lines[8], emu_last[8];
 static uint4 emu_load16(uint64_t a) {
-  bool ok = a >= emu_rec_lo && a < emu_rec_hi;
-  for (int k = 0; k < 7 && !ok; ++k) ok = a >= emu_spans[2 * k] && a < emu_spans[2 * k + 1];
-  if (!ok) { ++emu_bad; return uint4{0, 0, 0, 0}; }
-  return *reinterpret_cast<const uint4 *>(a & ~uint64_t(15));
+  int arr = -1;
+  if (a >= emu_rec_lo && a < emu_rec_hi) arr = 7;
+  for (int k = 0; k < 7 && arr < 0; ++k)
+    if (a >= emu_spans[2 * k] && a < emu_spans[2 * k + 1]) arr = k;
+  if (arr < 0) { ++emu_bad; return uint4{0, 0, 0, 0}; }
+  ++emu_probes[arr];
+  if ((a >> 6) != emu_last[arr]) { ++emu_lines[arr]; emu_last[arr] = a >> 6; }
+  // the block may run past (or start before) the array: copy the valid bytes
+  const uint64_t lo = arr == 7 ? emu_rec_lo : emu_spans[2 * arr];
+  const uint64_t hi = arr == 7 ? emu_rec_hi : emu_spans[2 * arr + 1];
+  const uint64_t b = a & ~uint64_t(15);
+  if (b >= lo && b + 16 <= hi) return *reinterpret_cast<const uint4 *>(b);
+  uint8_t buf[16] = {0};
+  for (uint64_t k = 0; k < 16; ++k)
+    if (b + k >= lo && b + k < hi) buf[k] = *reinterpret_cast<const uint8_t *>(b + k);
+  uint4 r;
+  std::memcpy(&r, buf, 16);
+  return r;
 }
 #define SM_LOAD16(a) emu_load16(a)
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
@@ -30,7 +49,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
                const uint64_t *in_text, uint64_t N, uint64_t logN, const uint8_t *reads,
                uint64_t stride, uint32_t L, uint64_t n, uint32_t min_len, uint64_t *out,
                uint32_t cap, uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
-               uint64_t *viol, uint32_t lin_blocks) {
+               uint64_t *viol, uint32_t lin_blocks, uint64_t *counters) {
   const sm::Geom g = sm::make_geom(L);
   if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
   std::vector<uint4> rec(n * g.chunks);
@@ -64,9 +83,11 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   emu_rec_lo = reinterpret_cast<uint64_t>(rec.data());
   emu_rec_hi = emu_rec_lo + rec.size() * sizeof(uint4);
   emu_bad = 0;
+  for (int k = 0; k < 8; ++k) { emu_probes[k] = emu_lines[k] = 0; emu_last[k] = ~0ull; }
   sm::k_mam_sm<IdxT, 1, true, true>(c);
   for (int k = 0; k < 10; ++k) viol[k] = v[k];
   viol[0] += emu_bad;
+  for (int k = 0; k < 8; ++k) { counters[k] = emu_probes[k]; counters[8 + k] = emu_lines[k]; }
   return 0;
 }
 
@@ -76,10 +97,10 @@ extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int
                           uint64_t logN, const uint8_t *reads, uint64_t stride, uint32_t L,
                           uint64_t n, uint32_t min_len, uint64_t *out, uint32_t cap,
                           uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
-                          uint64_t *viol, uint32_t lin_blocks) {
+                          uint64_t *viol, uint32_t lin_blocks, uint64_t *counters) {
   if (idx_bytes == 4)
     return run<uint32_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
-                         min_len, out, cap, n_out, iters, spans, viol, lin_blocks);
+                         min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters);
   return run<uint64_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
-                       min_len, out, cap, n_out, iters, spans, viol, lin_blocks);
+                       min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters);
 }

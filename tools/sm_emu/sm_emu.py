@@ -50,19 +50,26 @@ def in_text_words(in_text):
     return w
 
 
+ARRAYS = ("text", "sa", "isa", "lcp", "uniq", "kmer", "bitmap", "records")
+
+
 class Emu:
-    def __init__(self, ix, wide=False):
+    def __init__(self, ix, wide=False, copy=True):
         """ix: oracle.Index with accel() built; wide: run the 8-byte SA/ISA
-        instantiation (the device uses it when N >= 2^32)."""
+        instantiation (the device uses it when N >= 2^32); copy=False uses the
+        index arrays in place (hg19-sized indexes: no second copy)."""
         self.ix = ix
         self.keep = []
-
         self.spans = []
 
         def P(a, dt):
-            buf, raw = _padded(a, dt)
-            self.keep.append(raw)
-            nb = np.ascontiguousarray(a, dt).nbytes
+            if copy or a.dtype != np.dtype(dt) or not a.flags.c_contiguous:
+                buf, raw = _padded(a, dt)
+                self.keep.append(raw)
+                nb = np.ascontiguousarray(a, dt).nbytes
+            else:
+                buf, nb = a, a.nbytes
+                self.keep.append(a)
             self.spans += [buf.ctypes.data, buf.ctypes.data + nb]
             return buf.ctypes.data
         self.T = P(ix.T, np.uint8)
@@ -79,7 +86,8 @@ class Emu:
         self.isz = np.dtype(it).itemsize
 
     def map(self, reads, min_len=20, cap=512, lin_blocks=2):
-        """reads: uint8 [n, L].  Returns (list of [(ref, q, len)], iterations)."""
+        """reads: uint8 [n, L].  Returns (list of [(ref, q, len)], iterations);
+        self.counters: {array: (16-byte probes, 64-byte line transitions)}."""
         reads = np.ascontiguousarray(reads, np.uint8)
         n, L = reads.shape
         out = np.zeros(n * cap, np.uint64)
@@ -87,6 +95,7 @@ class Emu:
         iters = np.zeros(n, np.uint32)
         spans = np.array(self.spans, np.uint64)   # T SA ISA L8 U KT BM
         viol = np.zeros(10, np.uint64)
+        ctr = np.zeros(16, np.uint64)
         from oracle import lib as olib
         logN = olib().orc_logN(C.c_uint64(self.ix.N))
         rc = lib().sm_emu_map(
@@ -98,7 +107,7 @@ class Emu:
             out.ctypes.data_as(C.c_void_p), C.c_uint32(cap),
             nout.ctypes.data_as(C.c_void_p), iters.ctypes.data_as(C.c_void_p),
             spans.ctypes.data_as(C.c_void_p), viol.ctypes.data_as(C.c_void_p),
-            C.c_uint32(lin_blocks))
+            C.c_uint32(lin_blocks), ctr.ctypes.data_as(C.c_void_p))
         assert rc == 0
         assert viol[0] == 0, ("out-of-range probe", viol.tolist())
         res = []
@@ -106,4 +115,5 @@ class Emu:
             k = min(int(nout[i]), cap)
             w = out[i * cap:i * cap + k]
             res.append([(int(x & 0xFFFFFFFFFFFF), int((x >> 48) & 0xFF), int(x >> 56)) for x in w])
+        self.counters = {name: (int(ctr[k]), int(ctr[8 + k])) for k, name in enumerate(ARRAYS)}
         return res, iters
