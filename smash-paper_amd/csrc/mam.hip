@@ -164,10 +164,11 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
     ix->rec_bytes = bytes;
   }
   {
-    const uint64_t threads = n_reads * g.chunks * 4;
-    sm::k_prep<<<unsigned((threads + 255) / 256), 256, 0, s>>>(
+    const uint32_t per = sm::prep_per_block(g, stride);
+    const size_t plds = sm::prep_lds_bytes(g, stride, per);
+    sm::k_prep<<<unsigned((n_reads + per - 1) / per), 64, plds, s>>>(
         seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
-        ix->in_text[3], g, ix->d_rec);
+        ix->in_text[3], g, per, ix->d_rec);
     SMASH_HIP(hipGetLastError());
   }
   sm::Ctx<IdxT> c;

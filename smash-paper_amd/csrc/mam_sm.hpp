@@ -57,50 +57,78 @@ __device__ __forceinline__ bool is_acgt(uint32_t b) {
   return b == 'a' || b == 'c' || b == 'g' || b == 't';
 }
 
-// One thread per record word.  Record of read r (g.chunks * 4 words):
+// Record of read r (g.chunks * 4 words), built by k_prep:
 //   [0, 4*c_bad)          bad mask, bit i of word i/32: base i is not ACGT
 //                         or does not occur in the text
 //   [4*c_bad, +w_raw)     the read bytes, zero padded
 //   [.., +w_cod)          2-bit codes (a0 c1 g2 t3, others 0), big-endian:
 //                         base 16j+t at bits 31-2t..30-2t of word j
 //   rest                  zero
-__global__ void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
-                       const uint16_t *__restrict__ lens, uint32_t len0, uint64_t n,
-                       uint64_t it0, uint64_t it1, uint64_t it2, uint64_t it3, Geom g,
-                       uint32_t *__restrict__ rec) {
-  const uint32_t rw = g.chunks * 4;
-  const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
-  if (t >= n * rw) return;
-  const uint64_t r = t / rw;
-  const uint32_t w = uint32_t(t - r * rw);
-  const uint32_t L = lens ? lens[r] : len0;
-  const uint8_t *P = seqs + r * stride;
-  uint32_t out = 0;
-  if (w < 4 * g.c_bad) {
-    for (uint32_t k = 0; k < 32; ++k) {
-      const uint32_t i = 32 * w + k;
-      if (i >= L) break;
+// One block of 64 threads per `per_block` reads: (1) the block copies the
+// reads' bytes into LDS with word loads, (2) each thread builds one read's
+// record in a padded LDS row in one pass over its bytes, (3) the block writes
+// the records out with contiguous word stores.  All loops stride by
+// blockDim.x (the host emulation runs one thread).
+inline uint32_t prep_per_block(const Geom &g, uint64_t stride) {
+  const uint64_t per = 48 * 1024 / (stride + 4 * (g.chunks * 4 + 1) + 8);
+  return uint32_t(per < 1 ? 1 : per > 64 ? 64 : per);
+}
+inline size_t prep_lds_bytes(const Geom &g, uint64_t stride, uint32_t per) {
+  return size_t(((per * stride + 8 + 3) / 4 + 1) * 4) + size_t(per) * (g.chunks * 4 + 1) * 4;
+}
+
+__global__ __launch_bounds__(64) void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
+                                             const uint16_t *__restrict__ lens, uint32_t len0,
+                                             uint64_t n, uint64_t it0, uint64_t it1, uint64_t it2,
+                                             uint64_t it3, Geom g, uint32_t per,
+                                             uint32_t *__restrict__ rec) {
+  extern __shared__ uint32_t prep_lds[];
+  const uint32_t rw = g.chunks * 4, rwp = rw + 1;      // record words, padded LDS row
+  const uint64_t r0 = uint64_t(blockIdx.x) * per;
+  if (r0 >= n) return;
+  const uint32_t nr = uint32_t(n - r0 < per ? n - r0 : per);
+  // (1) input bytes [r0*stride, (r0+nr)*stride), word-aligned
+  const uint64_t a0 = reinterpret_cast<uint64_t>(seqs + r0 * stride);
+  const uint64_t a1 = reinterpret_cast<uint64_t>(seqs + (r0 + nr) * stride);
+  const uint64_t w0 = a0 & ~uint64_t(3);
+  const uint32_t nw = uint32_t(((a1 + 3) & ~uint64_t(3)) - w0) / 4;
+  uint32_t *in = prep_lds;
+  uint32_t *out = prep_lds + ((per * stride + 8 + 3) / 4 + 1);
+  for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x)
+    in[k] = reinterpret_cast<const uint32_t *>(w0)[k];
+  __syncthreads();
+  const uint8_t *inb = reinterpret_cast<const uint8_t *>(in) + (a0 - w0);
+  // (2) one record per thread
+  for (uint32_t t = threadIdx.x; t < nr; t += blockDim.x) {
+    const uint8_t *P = inb + uint64_t(t) * stride;
+    const uint32_t L = lens ? lens[r0 + t] : len0;
+    uint32_t *o = out + t * rwp;
+    for (uint32_t w = 0; w < rw; ++w) o[w] = 0;
+    uint32_t *ob = o, *orw = o + 4 * g.c_bad, *oc = orw + g.w_raw;
+    uint32_t raw = 0, cod = 0, bw = 0;
+    for (uint32_t i = 0; i < L; ++i) {
       const uint32_t b = P[i];
       const uint64_t word = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
       const bool present = (word >> (b & 63)) & 1ull;
-      if (!(is_acgt(b) && present)) out |= 1u << k;
+      const int cd = acgt_code(uint8_t(b));
+      raw |= b << (8 * (i & 3));
+      cod |= uint32_t(cd < 0 ? 0 : cd) << (30 - 2 * (i & 15));
+      bw |= uint32_t(!(cd >= 0 && present)) << (i & 31);
+      if ((i & 3) == 3) { orw[i >> 2] = raw; raw = 0; }
+      if ((i & 15) == 15) { oc[i >> 4] = cod; cod = 0; }
+      if ((i & 31) == 31) { ob[i >> 5] = bw; bw = 0; }
     }
-  } else {
-    const uint32_t q = w - 4 * g.c_bad;
-    if (q < g.w_raw) {
-      for (uint32_t k = 0; k < 4; ++k)
-        if (4 * q + k < L) out |= uint32_t(P[4 * q + k]) << (8 * k);
-    } else if (q < g.w_raw + g.w_cod) {
-      const uint32_t j = q - g.w_raw;
-      for (uint32_t k = 0; k < 16; ++k) {
-        const uint32_t i = 16 * j + k;
-        if (i >= L) break;
-        const int cd = acgt_code(P[i]);
-        out |= uint32_t(cd < 0 ? 0 : cd) << (30 - 2 * k);
-      }
-    }
+    if (L & 3) orw[L >> 2] = raw;
+    if (L & 15) oc[L >> 4] = cod;
+    if (L & 31) ob[L >> 5] = bw;
   }
-  rec[t] = out;
+  __syncthreads();
+  // (3) contiguous stores of the block's records
+  uint32_t *dst = rec + r0 * rw;
+  for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) {
+    const uint32_t t = k / rw, w = k - t * rw;
+    dst[k] = out[t * rwp + w];
+  }
 }
 
 // lane states: S_COPY and above own a pending 16-byte probe at `addr`

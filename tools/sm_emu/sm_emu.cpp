@@ -39,7 +39,7 @@ static uint4 emu_load16(uint64_t a) {
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
 
 thread_local dim3 threadIdx, blockIdx, blockDim;
-namespace smash { namespace sm { uint32_t ldsw[1 << 12]; } }
+namespace smash { namespace sm { uint32_t ldsw[1 << 12]; uint32_t prep_lds[1 << 16]; } }
 
 using namespace smash;
 
@@ -53,12 +53,16 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   const sm::Geom g = sm::make_geom(L);
   if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
   std::vector<uint4> rec(n * g.chunks);
-  blockIdx.x = 0; blockDim.x = 1;
-  for (uint64_t t = 0; t < n * g.chunks * 4; ++t) {
-    threadIdx.x = unsigned(t);
-    sm::k_prep(reads, stride, nullptr, L, n, in_text[0], in_text[1], in_text[2], in_text[3], g,
-               reinterpret_cast<uint32_t *>(rec.data()) + 0 * t);
+  const uint32_t per = sm::prep_per_block(g, stride);
+  if (sm::prep_lds_bytes(g, stride, per) > sizeof(sm::prep_lds)) return -1;
+  blockDim.x = 1;
+  threadIdx.x = 0;
+  for (uint64_t b = 0; b * per < n; ++b) {
+    blockIdx.x = unsigned(b);
+    sm::k_prep(reads, stride, nullptr, L, n, in_text[0], in_text[1], in_text[2], in_text[3], g, per,
+               reinterpret_cast<uint32_t *>(rec.data()));
   }
+  blockIdx.x = 0;
   threadIdx.x = 0;
   sm::Ctx<IdxT> c;
   c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);
