@@ -79,6 +79,10 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
       &per_cu, reinterpret_cast<const void *>(kern), B, lds));
   SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
   if (per_cu < 1) per_cu = 1;
+  if (const char *e = std::getenv("SMASH_SM_BLOCKS_PER_CU")) {   // occupancy experiments
+    const int cap = std::atoi(e);
+    if (cap >= 1 && cap < per_cu) per_cu = cap;
+  }
   uint64_t blocks = uint64_t(per_cu) * uint64_t(cus);
   const uint64_t want = (n_reads + B - 1) / B;
   if (blocks > want) blocks = want;
