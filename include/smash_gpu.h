@@ -49,6 +49,11 @@ void smash_text_free(uint8_t *text, uint32_t n_seq, uint64_t *startpos,
 #define SMASH_MODE_MAM 1         /* -mumreference / default (longSA.cpp:503) */
 #define SMASH_MODE_MAM_PLAIN 2   /* same matches, the reference's probe
                                     sequence without the accelerators (A/B) */
+#define SMASH_MODE_MUM 3         /* -mum: MAM, then cleanMUMcand per read
+                                    (longSA::MUM, longSA.cpp:549-585) */
+#define SMASH_MODE_MEM 4         /* -maxmatch: longSA::MEM / findMEM
+                                    (longSA.cpp:395-490, 587-590); only via
+                                    smash_match_batch (lengths may exceed 255) */
 
 /* ========================================================================== */
 /* Index: replaces longSA::longSA (longSA.cpp:94-210) + Sequence (fasta.cpp)  */
@@ -109,7 +114,8 @@ typedef struct {
 int smash_index_query(const smash_index *ix, smash_index_info *out);
 
 /* ========================================================================== */
-/* Search: replaces longSA::MAM(Aligner&) (longSA.cpp:503-536) for a batch.   */
+/* Search: replaces longSA::MAM(Aligner&) (longSA.cpp:503-536) for a batch   */
+/* (mode MAM / MAM_PLAIN; MUM as longSA::MUM, longSA.cpp:549-585).            */
 /* Each read's matches go to slots [i*cap_per_read, ...) as packed u64:       */
 /*   bits 0-47 ref (text position), 48-55 query offset, 56-63 length          */
 /* (match_t, longSA.h:78-92; reads <= 255 bp), in emission order (ascending   */
@@ -123,6 +129,23 @@ int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len,
                     const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
                     uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out,
                     void *stream);
+
+/* The three search modes with unpacked records (match_t, longSA.h:78-92):  */
+/* mode = SMASH_MODE_MAM, _MUM or _MEM (memsam's default / -mum / -maxmatch,  */
+/* mummer.cpp:77-96).  Read i's matches go to d_out[i*cap_per_read ...] in    */
+/* the order longSA::MAM / MUM / MEM pass them to process_match; d_n_out[i] = */
+/* how many there are (records beyond cap_per_read are counted, not written). */
+/* ========================================================================== */
+typedef struct {
+  uint64_t ref;            /* text position (longSA.h:80) */
+  uint32_t query;          /* query offset */
+  uint32_t len;            /* match length */
+} smash_match;
+int smash_match_batch(const smash_index *ix, int mode, uint32_t min_len,
+                      const uint8_t *d_seqs, uint64_t stride,
+                      const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                      smash_match *d_out, uint32_t cap_per_read,
+                      uint32_t *d_n_out, void *stream);
 
 /* ========================================================================== */
 /* Pipeline: prepare_matches (query.cpp:231-306) + mappability_tag           */

@@ -114,4 +114,8 @@ uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, satu
 void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
 void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
 void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
+// mem.hip: smash_map_batch's MUM mode (MAM, then cleanMUMcand per read)
+int map_batch_mum(const smash_index *ix, uint32_t min_len, const uint8_t *seqs, uint64_t stride,
+                  const uint16_t *lens, uint32_t len, uint64_t n_reads, uint64_t *out, uint32_t cap,
+                  uint32_t *n_out, hipStream_t s);
 }  // namespace smash

@@ -261,11 +261,15 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
     set_error("smash_map_batch: bad arguments");
     return SMASH_ERR_ARG;
   }
-  if (mode != SMASH_MODE_MAM && mode != SMASH_MODE_MAM_PLAIN) {
-    set_error("smash_map_batch: only the MAM modes (the SMASH default) run on the device");
+  if (mode == SMASH_MODE_MEM) {
+    set_error("smash_map_batch: MEM lengths can exceed the packed 8-bit field; use smash_match_batch");
     return SMASH_ERR_UNSUPPORTED;
   }
-  if (mode == SMASH_MODE_MAM && (!ix->d_uniq || !ix->d_kmer || !ix->d_bitmap)) {
+  if (mode != SMASH_MODE_MAM && mode != SMASH_MODE_MAM_PLAIN && mode != SMASH_MODE_MUM) {
+    set_error("smash_map_batch: unknown mode");
+    return SMASH_ERR_ARG;
+  }
+  if (mode != SMASH_MODE_MAM_PLAIN && (!ix->d_uniq || !ix->d_kmer || !ix->d_bitmap)) {
     set_error("smash_map_batch: index lacks the search accelerators");
     return SMASH_ERR_ARG;
   }
@@ -284,6 +288,9 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
   if (n_reads == 0) return SMASH_OK;
   SMASH_HIP(hipSetDevice(ix->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (mode == SMASH_MODE_MUM)
+    return map_batch_mum(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out, cap_per_read,
+                         d_n_out, s);
   const bool plain = mode == SMASH_MODE_MAM_PLAIN;
   if (!plain && !use_direct()) {
     if (ix->idx_bytes == 4)

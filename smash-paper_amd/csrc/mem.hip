@@ -1,0 +1,430 @@
+// smash-paper_amd/csrc/mem.hip -- the other two search modes of memsam on
+// gfx950: -maxmatch (MEM) and -mum (MUM).
+//
+// MEM replaces longSA::MEM / findMEM / collectMEMs / find_Lmaximal
+// (longSA.cpp:395-490, 587-590) with suffixlink (:383-392) and expand_link
+// (longSA.h:158-174).  One lane runs one read, statement by statement, so the
+// match sequence (order included) is the reference's.  Two accelerations
+// change no probe outcome:
+//  (A) a singleton interval extends by comparing 8 read bytes with 8 text
+//      bytes per load (top_down_faster on [s, s] is that byte compare);
+//  (C) a descent from the ROOT interval with k ACGT characters available and
+//      k <= the traverse limit starts at depth k from the k-mer table.
+// LCP is read exactly (u8 + the sorted overflow table, vec_uchar longSA.h:
+// 34-39): unlike MAM, findMEM keeps the max-match interval even when its
+// suffix link fails (longSA.cpp:423 ignores the result), and collectMEMs
+// then compares depths with LCP values that can exceed 255.
+//
+// MUM replaces longSA::MUM (longSA.cpp:549-585): the MAM matches of a read
+// (at most one per prefix, so at most L) sorted by (ref asc, len desc) and
+// filtered as cleanMUMcand does.  Matches tying on (ref, len) are dropped
+// together, so the unspecified order of std::sort among them never shows.
+#include "common.hpp"
+#include "mam_device.hpp"
+
+#include <cstring>
+
+namespace smash {
+namespace {
+
+template <class IdxT>
+struct MemIx {
+  DevIndex<IdxT> x;
+  const uint64_t *ovf;   // {idx, val} for LCP >= 255, sorted by idx
+  uint64_t n_ovf;
+};
+
+template <class IdxT>
+__device__ __forceinline__ uint64_t lcp_at(const MemIx<IdxT> &m, uint64_t i) {
+  const uint32_t v = m.x.L8[i];
+  if (v < 255) return v;
+  uint64_t lo = 0, hi = m.n_ovf;   // lower_bound (longSA.h:36)
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (m.ovf[2 * mid] < i) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < m.n_ovf ? m.ovf[2 * lo + 1] : 255;
+}
+
+struct Ival {
+  uint64_t depth, start, end;
+};
+
+// expand_link (longSA.h:158-174) over the exact LCP
+template <class IdxT>
+__device__ bool expand_link_x(const MemIx<IdxT> &m, Ival &l) {
+  const uint64_t thresh = 2 * l.depth * m.x.logN;
+  uint64_t exp = 0, s = l.start, e = l.end;
+  while (lcp_at(m, s) >= l.depth) {
+    if (++exp >= thresh) return false;
+    --s;
+  }
+  while (e < m.x.N - 1 && lcp_at(m, e + 1) >= l.depth) {
+    if (++exp >= thresh) return false;
+    ++e;
+  }
+  l.start = s;
+  l.end = e;
+  return true;
+}
+
+// suffixlink (longSA.cpp:383-392)
+template <class IdxT>
+__device__ bool suffixlink_x(const MemIx<IdxT> &m, Ival &v) {
+  if (v.depth <= 1) {
+    v.depth = 0;
+    return false;
+  }
+  --v.depth;
+  v.start = m.x.ISA[uint64_t(m.x.SA[v.start]) + 1];
+  v.end = m.x.ISA[uint64_t(m.x.SA[v.end]) + 1];
+  return expand_link_x(m, v);
+}
+
+// traverse (longSA.cpp:297-316) with (A) and (C)
+template <class IdxT>
+__device__ void traverse_x(const MemIx<IdxT> &m, const uint8_t *P, uint64_t L, uint64_t prefix,
+                           Ival &cur, uint64_t limit) {
+  const DevIndex<IdxT> &x = m.x;
+  if (cur.depth >= limit) return;
+  if (cur.depth == 0 && cur.start == 0 && cur.end == x.N - 1 && x.K > 0 &&
+      uint64_t(x.K) <= limit && prefix + uint64_t(x.K) <= L) {   // (C)
+    uint32_t w = 0;
+    bool ok = true;
+    for (int k = 0; k < x.K; ++k) {
+      const int v = acgt_code(P[prefix + k]);
+      ok = ok && v >= 0;
+      w = (w << 2) | uint32_t(v & 3);
+    }
+    if (ok) {
+      const uint64_t lo = x.KT[2 * uint64_t(w)], hi = x.KT[2 * uint64_t(w) + 1];
+      if (lo <= hi) {
+        cur.depth = uint64_t(x.K);
+        cur.start = lo;
+        cur.end = hi;
+        if (cur.depth == limit) return;
+      }
+    }
+  }
+  while (prefix + cur.depth < L) {
+    if (cur.start == cur.end) {                                   // (A)
+      const uint64_t pos = x.SA[cur.start];
+      while (prefix + cur.depth < L && cur.depth < limit) {
+        const uint64_t rem_r = L - prefix - cur.depth, rem_l = limit - cur.depth;
+        const uint64_t rem = rem_r < rem_l ? rem_r : rem_l;
+        const uint32_t lim = rem < 8 ? uint32_t(rem) : 8u;
+        const uint32_t k = agree8(load8(x.T, pos + cur.depth), lds_load8(P, prefix + cur.depth), lim);
+        cur.depth += k;
+        if (k < lim) break;
+      }
+      return;
+    }
+    uint64_t s = cur.start, e = cur.end;
+    if (!td_faster(x, sch(P[prefix + cur.depth]), cur.depth, s, e)) return;
+    cur.depth += 1;
+    cur.start = s;
+    cur.end = e;
+    if (cur.depth == limit) return;
+  }
+}
+
+struct MemSink {
+  uint4 *out;
+  uint32_t cap, n;
+  __device__ void emit(uint64_t ref, uint64_t q, uint64_t len) {
+    if (n < cap)
+      out[n] = make_uint4(uint32_t(ref), uint32_t(ref >> 32), uint32_t(q), uint32_t(len));
+    ++n;
+  }
+};
+
+// find_Lmaximal (longSA.cpp:438-457)
+template <class IdxT>
+__device__ __forceinline__ void find_lmax(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
+                                          uint64_t prefix, uint64_t i, uint64_t len, MemSink &s) {
+  if (prefix == 0 || i == 0 || P[prefix - 1] != m.x.T[i - 1]) {
+    if (len >= min_len) s.emit(i, prefix, len);
+  }
+}
+
+// collectMEMs (longSA.cpp:461-490); xmi by value as in the reference
+template <class IdxT>
+__device__ void collect_mems(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
+                             uint64_t prefix, const Ival &mli, Ival xmi, MemSink &s) {
+  const uint64_t N = m.x.N;
+  for (uint64_t i = xmi.start; i <= xmi.end; ++i)
+    find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[i]), xmi.depth, s);
+  if (mli.start == xmi.start && mli.end == xmi.end) return;
+  while (xmi.depth >= mli.depth) {
+    if (xmi.end + 1 < N) {
+      const uint64_t a = lcp_at(m, xmi.start), b = lcp_at(m, xmi.end + 1);
+      xmi.depth = a > b ? a : b;
+    } else {
+      xmi.depth = lcp_at(m, xmi.start);
+    }
+    if (xmi.depth >= mli.depth) {
+      while (lcp_at(m, xmi.start) >= xmi.depth) {
+        --xmi.start;
+        find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[xmi.start]), xmi.depth, s);
+      }
+      while (xmi.end + 1 < N && lcp_at(m, xmi.end + 1) >= xmi.depth) {
+        ++xmi.end;
+        find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[xmi.end]), xmi.depth, s);
+      }
+    }
+  }
+}
+
+// findMEM (longSA.cpp:395-431)
+template <class IdxT>
+__device__ void mem_read(const MemIx<IdxT> &m, const uint8_t *P, uint32_t L, uint32_t min_len,
+                         MemSink &s) {
+  const uint64_t N = m.x.N;
+  const Ival root{0, 0, N - 1};
+  uint64_t prefix = 1;                     // longSA.cpp:398 (sic)
+  Ival mli = root, xmi = root;
+  while (prefix <= L) {
+    traverse_x(m, P, L, prefix, mli, min_len);
+    if (mli.depth > xmi.depth) xmi = mli;
+    if (mli.depth <= 1) {
+      mli = root;
+      xmi = root;
+      ++prefix;
+      continue;
+    }
+    if (mli.depth >= min_len) {
+      traverse_x(m, P, L, prefix, xmi, L);
+      collect_mems(m, P, min_len, prefix, mli, xmi, s);
+      ++prefix;
+      if (!suffixlink_x(m, mli)) {
+        mli = root;
+        xmi = root;
+        continue;
+      }
+      suffixlink_x(m, xmi);                // result ignored (longSA.cpp:423)
+    } else {
+      ++prefix;
+      if (!suffixlink_x(m, mli)) {
+        mli = root;
+        xmi = root;
+        continue;
+      }
+      xmi = mli;
+    }
+  }
+}
+
+// Persistent lanes pulling reads from a device work counter (a repetitive
+// read only delays its own lane); the read is copied into the lane's LDS row.
+template <class IdxT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_mem(MemIx<IdxT> m, const uint8_t *__restrict__ seqs,
+                                               uint64_t stride, const uint16_t *__restrict__ lens,
+                                               uint32_t len0, uint64_t n_reads, uint32_t min_len,
+                                               uint4 *__restrict__ out, uint32_t cap,
+                                               uint32_t *__restrict__ n_out, uint32_t row,
+                                               unsigned long long *work) {
+  extern __shared__ uint8_t lds[];
+  uint8_t *P = lds + threadIdx.x * row;
+  for (;;) {
+    const uint64_t r = atomicAdd(work, 1ull);
+    if (r >= n_reads) break;
+    const uint32_t L = lens ? lens[r] : len0;
+    const uint8_t *src = seqs + r * stride;
+    for (uint32_t k = 0; k < row; ++k) P[k] = k < L ? src[k] : 0;
+    MemSink s{out + r * cap, cap, 0};
+    mem_read(m, P, L, min_len, s);
+    n_out[r] = s.n;
+  }
+}
+
+// by_ref (longSA.cpp:492-499): ref ascending, then len descending
+__device__ __forceinline__ bool by_ref_less(uint64_t a, uint64_t b) {
+  const uint64_t ra = a & 0xFFFFFFFFFFFFull, rb = b & 0xFFFFFFFFFFFFull;
+  if (ra != rb) return ra < rb;
+  return (a >> 56) > (b >> 56);
+}
+
+// cleanMUMcand over each read's MAM matches (packed, `cap_m` slots per read;
+// sorted in place), out: packed (wide == 0) or smash_match (wide == 1)
+__global__ void k_mum(uint64_t *__restrict__ mam, const uint32_t *__restrict__ n_mam,
+                      uint64_t n_reads, uint32_t cap_m, void *__restrict__ out, int wide,
+                      uint32_t cap, uint32_t *__restrict__ n_out) {
+  const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_reads) return;
+  uint64_t *a = mam + r * cap_m;
+  const uint32_t n = n_mam[r] < cap_m ? n_mam[r] : cap_m;
+  for (uint32_t i = 1; i < n; ++i) {                 // insertion sort (n <= read length)
+    const uint64_t v = a[i];
+    uint32_t j = i;
+    while (j > 0 && by_ref_less(v, a[j - 1])) {
+      a[j] = a[j - 1];
+      --j;
+    }
+    a[j] = v;
+  }
+  uint32_t no = 0;
+  auto emit = [&](uint64_t w) {
+    if (no < cap) {
+      if (wide) {
+        const uint64_t ref = w & 0xFFFFFFFFFFFFull;
+        reinterpret_cast<uint4 *>(out)[r * cap + no] =
+            make_uint4(uint32_t(ref), uint32_t(ref >> 32), uint32_t((w >> 48) & 0xFF), uint32_t(w >> 56));
+      } else {
+        reinterpret_cast<uint64_t *>(out)[r * cap + no] = w;
+      }
+    }
+    ++no;
+  };
+  uint64_t dbright = 0;
+  bool ignoreprevious = false;
+  for (uint32_t i = 0; i < n; ++i) {                 // longSA.cpp:561-579
+    bool ignorecurrent = false;
+    const uint64_t ref = a[i] & 0xFFFFFFFFFFFFull;
+    const uint64_t currentright = ref + (a[i] >> 56) - 1;
+    if (dbright > currentright) {
+      ignorecurrent = true;
+    } else if (dbright == currentright) {
+      ignorecurrent = true;
+      if (!ignoreprevious && (a[i - 1] & 0xFFFFFFFFFFFFull) == ref) ignoreprevious = true;
+    } else {
+      dbright = currentright;
+    }
+    if (i > 0 && !ignoreprevious) emit(a[i - 1]);
+    ignoreprevious = ignorecurrent;
+  }
+  if (!ignoreprevious && n > 0) emit(a[n - 1]);
+  n_out[r] = no;
+}
+
+// packed MAM words -> smash_match records
+__global__ void k_widen(const uint64_t *__restrict__ mam, const uint32_t *__restrict__ n_mam,
+                        uint64_t n_reads, uint32_t cap_m, uint4 *__restrict__ out, uint32_t cap,
+                        uint32_t *__restrict__ n_out) {
+  const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_reads) return;
+  const uint32_t n = n_mam[r] < cap_m ? n_mam[r] : cap_m;
+  for (uint32_t i = 0; i < n && i < cap; ++i) {
+    const uint64_t w = mam[r * cap_m + i];
+    const uint64_t ref = w & 0xFFFFFFFFFFFFull;
+    out[r * cap + i] = make_uint4(uint32_t(ref), uint32_t(ref >> 32), uint32_t((w >> 48) & 0xFF),
+                                  uint32_t(w >> 56));
+  }
+  n_out[r] = n_mam[r];
+}
+
+template <class IdxT>
+int launch_mem(const smash_index *ix, uint32_t min_len, const uint8_t *seqs, uint64_t stride,
+               const uint16_t *lens, uint32_t len, uint64_t n_reads, uint4 *out, uint32_t cap,
+               uint32_t *n_out, hipStream_t s) {
+  constexpr int B = 64;
+  const uint32_t maxL = lens ? 255 : len;
+  uint32_t row = ((maxL + 12 + 3) / 4) | 1;   // words (odd: conflict-free), lds_load8 over-read
+  row *= 4;
+  const size_t lds = size_t(B) * row;
+  auto kern = k_mem<IdxT, B>;
+  int per_cu = 0, cus = 0;
+  SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(kern),
+                                                         B, lds));
+  SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
+  if (per_cu < 1) per_cu = 1;
+  uint64_t blocks = uint64_t(per_cu) * uint64_t(cus);
+  const uint64_t want = (n_reads + B - 1) / B;
+  if (blocks > want) blocks = want;
+  MemIx<IdxT> m;
+  m.x = make_dev_index<IdxT>(ix);
+  m.ovf = ix->d_ovf;
+  m.n_ovf = ix->n_ovf;
+  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
+  if (ix->kev[0]) SMASH_HIP(hipEventRecord(ix->kev[0], s));
+  kern<<<unsigned(blocks), B, lds, s>>>(m, seqs, stride, lens, len, n_reads, min_len, out, cap,
+                                        n_out, row, reinterpret_cast<unsigned long long *>(ix->d_work));
+  SMASH_HIP(hipGetLastError());
+  if (ix->kev[1]) SMASH_HIP(hipEventRecord(ix->kev[1], s));
+  return SMASH_OK;
+}
+
+// MAM into a scratch buffer of L slots per read (exact: one MAM per prefix
+// at most), then k_mum or k_widen
+int mam_then(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *seqs,
+             uint64_t stride, const uint16_t *lens, uint32_t len, uint64_t n_reads, void *out,
+             int wide, uint32_t cap, uint32_t *n_out, hipStream_t s) {
+  const uint32_t cap_m = lens ? 255 : len;
+  uint64_t *tmp = nullptr;
+  uint32_t *ntmp = nullptr;
+  SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&tmp), n_reads * cap_m * 8 + 8, s));
+  SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&ntmp), n_reads * 4 + 4, s));
+  int rc = smash_map_batch(ix, SMASH_MODE_MAM, min_len, seqs, stride, lens, len, n_reads, tmp, cap_m,
+                           ntmp, s);
+  if (rc == SMASH_OK) {
+    const unsigned g = unsigned((n_reads + 255) / 256);
+    if (mode == SMASH_MODE_MUM)
+      k_mum<<<g, 256, 0, s>>>(tmp, ntmp, n_reads, cap_m, out, wide, cap, n_out);
+    else
+      k_widen<<<g, 256, 0, s>>>(tmp, ntmp, n_reads, cap_m, static_cast<uint4 *>(out), cap, n_out);
+    if (hipGetLastError() != hipSuccess) rc = SMASH_ERR_HIP;
+  }
+  (void)hipFreeAsync(tmp, s);
+  (void)hipFreeAsync(ntmp, s);
+  if (rc == SMASH_ERR_HIP) set_error(std::string("mam_then: ") + smash_last_error());
+  return rc;
+}
+
+int check_args(const smash_index *ix, const uint8_t *seqs, const void *out, const uint32_t *n_out,
+               uint32_t cap, const uint16_t *lens, uint32_t len, uint32_t min_len) {
+  if (!ix || !seqs || !out || !n_out || cap == 0) {
+    set_error("smash_match_batch: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  if (!lens && (len == 0 || len > 255)) {
+    set_error("smash_match_batch: read length must be 1..255");
+    return SMASH_ERR_ARG;
+  }
+  if (min_len < 2) {   // "NOTE: min_len must be > 1" (longSA.h:194)
+    set_error("smash_match_batch: min_len must be > 1");
+    return SMASH_ERR_ARG;
+  }
+  return SMASH_OK;
+}
+
+}  // namespace
+
+// smash_map_batch's MUM mode (packed records)
+int map_batch_mum(const smash_index *ix, uint32_t min_len, const uint8_t *seqs, uint64_t stride,
+                  const uint16_t *lens, uint32_t len, uint64_t n_reads, uint64_t *out, uint32_t cap,
+                  uint32_t *n_out, hipStream_t s) {
+  return mam_then(ix, SMASH_MODE_MUM, min_len, seqs, stride, lens, len, n_reads, out, 0, cap, n_out, s);
+}
+
+}  // namespace smash
+
+using namespace smash;
+
+extern "C" int smash_match_batch(const smash_index *ix, int mode, uint32_t min_len,
+                                 const uint8_t *d_seqs, uint64_t stride, const uint16_t *d_lens,
+                                 uint32_t len, uint64_t n_reads, smash_match *d_out,
+                                 uint32_t cap_per_read, uint32_t *d_n_out, void *stream) {
+  int rc = check_args(ix, d_seqs, d_out, d_n_out, cap_per_read, d_lens, len, min_len);
+  if (rc != SMASH_OK) return rc;
+  if (mode != SMASH_MODE_MAM && mode != SMASH_MODE_MUM && mode != SMASH_MODE_MEM) {
+    set_error("smash_match_batch: mode must be SMASH_MODE_MAM, _MUM or _MEM");
+    return SMASH_ERR_ARG;
+  }
+  if (mode == SMASH_MODE_MEM && !ix->d_kmer) {
+    set_error("smash_match_batch: index lacks the k-mer table");
+    return SMASH_ERR_ARG;
+  }
+  if (n_reads == 0) return SMASH_OK;
+  SMASH_HIP(hipSetDevice(ix->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint4 *out = reinterpret_cast<uint4 *>(d_out);
+  if (mode == SMASH_MODE_MEM) {
+    if (ix->idx_bytes == 4)
+      return launch_mem<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, out,
+                                  cap_per_read, d_n_out, s);
+    return launch_mem<uint64_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, out,
+                                cap_per_read, d_n_out, s);
+  }
+  return mam_then(ix, mode, min_len, d_seqs, stride, d_lens, len, n_reads, out, 1, cap_per_read,
+                  d_n_out, s);
+}

@@ -27,6 +27,9 @@ vp = C.c_void_p
 
 SMASH_MODE_MAM = 1
 SMASH_MODE_MAM_PLAIN = 2
+SMASH_MODE_MUM = 3
+SMASH_MODE_MEM = 4
+MODES = {"MAM": SMASH_MODE_MAM, "MUM": SMASH_MODE_MUM, "MEM": SMASH_MODE_MEM}
 ERRORS = {1: "left mappability too big (mappability_tag.cpp:110)",
           2: "right mappability too big (mappability_tag.cpp:113)",
           -4: "out of device memory / key set full",
@@ -35,7 +38,7 @@ ERRORS = {1: "left mappability too big (mappability_tag.cpp:110)",
 EXPORTS = [
     "smash_last_error", "smash_text_from_fasta", "smash_text_free",
     "smash_index_create", "smash_index_load", "smash_index_save",
-    "smash_index_free", "smash_index_query", "smash_map_batch",
+    "smash_index_free", "smash_index_query", "smash_map_batch", "smash_match_batch",
     "smash_pipeline_create", "smash_pipeline_free", "smash_count_batch",
     "smash_phase_map", "smash_phase_export", "smash_dedup_owner",
     "smash_phase_import", "smash_phase_positions", "smash_phase_bin",
@@ -104,6 +107,8 @@ def lib():
     L.smash_index_query.argtypes = [vp, C.POINTER(IndexInfo)]
     L.smash_map_batch.argtypes = [vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp,
                                   C.c_uint32, C.c_uint64, vp, C.c_uint32, vp, vp]
+    L.smash_match_batch.argtypes = [vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp,
+                                    C.c_uint32, C.c_uint64, vp, C.c_uint32, vp, vp]
     L.smash_pipeline_create.argtypes = [vp, C.POINTER(PipelineCfg), C.POINTER(vp)]
     L.smash_pipeline_free.argtypes = [vp]
     L.smash_pipeline_free.restype = None
@@ -413,6 +418,22 @@ def map_batch(index: Index, d_reads, n_reads, read_len, d_out, cap, d_n, min_len
     check(lib().smash_map_batch(index.h, mode, min_len, _ptr(d_reads),
                                 read_len, None, read_len, n_reads, _ptr(d_out), cap,
                                 _ptr(d_n), vp(_stream(stream))), "smash_map_batch")
+
+
+def match_batch(index: Index, d_reads, n_reads, read_len, d_out, cap, d_n, mode="MAM",
+                min_len=20, stream=None):
+    """longSA::MAM / MUM / MEM over a batch (smash_match_batch, memsam's default /
+    -mum / -maxmatch).  d_out: int64 tensor of 2*cap*n_reads words (smash_match
+    {u64 ref; u32 query; u32 len})."""
+    check(lib().smash_match_batch(index.h, MODES.get(mode, mode), min_len, _ptr(d_reads),
+                                  read_len, None, read_len, n_reads, _ptr(d_out), cap,
+                                  _ptr(d_n), vp(_stream(stream))), "smash_match_batch")
+
+
+def unpack_records(words, n, cap):
+    """smash_match records (2 u64 words each) -> [(ref, query, len)] (first min(n, cap))"""
+    w = np.asarray(words, np.uint64).reshape(-1, 2)[:min(int(n), cap)]
+    return [(int(a), int(b & 0xFFFFFFFF), int(b >> 32)) for a, b in w]
 
 
 def unpack_matches(words, n):
