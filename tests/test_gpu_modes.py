@@ -44,8 +44,8 @@ def test_modes_match_reference_triples(gix, s, mode):
     reads = interleaved_reads(s)
     exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
            for l in read_gz_lines("%s_%s.txt.gz" % (s, mode))]
-    got, n = run_match(gix, reads[:len(exp)], mode)
-    assert max(n) <= 512
+    got, n = run_match(gix, reads[:len(exp)], mode, cap=16384)
+    assert max(n) <= 16384
     bad = [i for i in range(len(exp)) if got[i] != exp[i]]
     assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)
 
