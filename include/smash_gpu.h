@@ -237,6 +237,24 @@ int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
  * and the stats (a fresh smashMEM.py + varbin.py invocation). */
 int smash_pipeline_reset(smash_pipeline *p, void *stream);
 
+/* The positions the last batch emitted, in order: pos0 (0-based, smashMEM.py
+ * column 5) and absolute position (pos0 + chrom_sizes.txt col 3) -- the
+ * `chr pos` lines smash_mapping.sh:29 writes for varbin.py, with the chrom
+ * recoverable from abspos - pos0.  *n_out = count; up to cap copied to host.
+ * Synchronises. */
+int smash_pipeline_positions(smash_pipeline *p, int64_t *h_pos0,
+                             int64_t *h_abspos, uint64_t cap, uint64_t *n_out);
+
+/* varbin.py's counting loop (varbin.py:52-92) on the device for a positions
+ * list already restricted to binned chromosomes (varbin.py:38-49): adjacent
+ * de-dup on pos0 against the previous line (prev_pos0 < 0 = none),
+ * bisect_right over d_bin_starts[nbins], add into d_counts[nbins];
+ * h_stats[0..2] += TotalReads, DupsRemoved, ReadsKept.  Synchronises. */
+int smash_bin_positions(const int64_t *d_pos0, const int64_t *d_abspos,
+                        uint64_t n, int64_t prev_pos0,
+                        const int64_t *d_bin_starts, uint32_t nbins,
+                        uint64_t *d_counts, uint64_t *h_stats, void *stream);
+
 /* Debug/test view of the last batch's per-pair filter output: for pair q,
  * h_nk[q] = kept hits (-1 = no key), h_keep[q] = survives de-dup, hits as
  * (tid << 48 | pos0) in h_hits[q*2*slots ...]. slots = read_len - min_len + 1. */

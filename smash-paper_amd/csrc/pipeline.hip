@@ -875,3 +875,72 @@ extern "C" int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
   if (reads) *reads = p->prof_reads;
   return SMASH_OK;
 }
+
+// The positions the last batch emitted (the awk/perl output of
+// smash_mapping.sh:29 that varbin.py reads): pos0 and absolute position, in
+// emission order.  Synchronises.
+extern "C" int smash_pipeline_positions(smash_pipeline *p, int64_t *h_pos0, int64_t *h_abspos,
+                                        uint64_t cap, uint64_t *n_out) {
+  if (!p || !n_out) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  if (p->last) SMASH_HIP(hipStreamSynchronize(p->last));
+  uint32_t n = 0;
+  if (p->n_pairs)
+    SMASH_HIP(hipMemcpy(&n, p->d_posoff + p->n_pairs, 4, hipMemcpyDeviceToHost));
+  *n_out = n;
+  const uint64_t k = n < cap ? n : cap;
+  if (k && h_pos0) SMASH_HIP(hipMemcpy(h_pos0, p->d_pos0, 8 * k, hipMemcpyDeviceToHost));
+  if (k && h_abspos) SMASH_HIP(hipMemcpy(h_abspos, p->d_abs, 8 * k, hipMemcpyDeviceToHost));
+  return SMASH_OK;
+}
+
+// varbin.py's loop (varbin.py:52-92) over positions already filtered to
+// binned chromosomes (varbin.py:38-49): adjacent de-dup on pos0 against the
+// previous line (prev_pos0 < 0: none), bisect_right over the bin starts,
+// count.  h_stats[0..2] += TotalReads, DupsRemoved, ReadsKept.  Synchronises.
+extern "C" int smash_bin_positions(const int64_t *d_pos0, const int64_t *d_abspos, uint64_t n,
+                                   int64_t prev_pos0, const int64_t *d_bin_starts,
+                                   uint32_t nbins, uint64_t *d_counts, uint64_t *h_stats,
+                                   void *stream) {
+  if ((n && (!d_pos0 || !d_abspos)) || !d_bin_starts || nbins == 0 || !d_counts || !h_stats) {
+    set_error("smash_bin_positions: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint64_t *scratch = nullptr;   // [0] npos (u32) [1] prev [2..] stats
+  SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&scratch), 8 * (2 + S_N), s));
+  SMASH_HIP(hipMemsetAsync(scratch, 0, 8 * (2 + S_N), s));
+  int rc = SMASH_OK;
+  for (uint64_t b = 0; b < n && rc == SMASH_OK; b += (1ull << 30)) {
+    const uint64_t m = n - b < (1ull << 30) ? n - b : (1ull << 30);
+    const uint32_t m32 = uint32_t(m);
+    // the line before the chunk: the caller's prev_pos0, then the previous chunk's last
+    const bool first = b == 0;
+    if (hipMemcpyAsync(scratch, &m32, 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(scratch + 1, first ? static_cast<const void *>(&prev_pos0) : &d_pos0[b - 1],
+                       8, first ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice,
+                       s) != hipSuccess) {
+      rc = SMASH_ERR_HIP;
+      break;
+    }
+    k_bin<<<2048, kB, 0, s>>>(d_pos0 + b, d_abspos + b, reinterpret_cast<const uint32_t *>(scratch),
+                              reinterpret_cast<const int64_t *>(scratch + 1), d_bin_starts, nbins,
+                              reinterpret_cast<unsigned long long *>(d_counts),
+                              reinterpret_cast<unsigned long long *>(scratch + 2));
+    if (hipGetLastError() != hipSuccess) rc = SMASH_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) rc = SMASH_ERR_HIP;   // m32/prev are host locals
+  }
+  uint64_t st[S_N] = {0};
+  if (rc == SMASH_OK && hipMemcpyAsync(st, scratch + 2, sizeof(st), hipMemcpyDeviceToHost, s) != hipSuccess)
+    rc = SMASH_ERR_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) rc = SMASH_ERR_HIP;
+  (void)hipFree(scratch);
+  if (rc != SMASH_OK) {
+    set_error("smash_bin_positions: HIP error");
+    return rc;
+  }
+  h_stats[0] += st[S_POS];
+  h_stats[1] += st[S_DUPS];
+  h_stats[2] += st[S_KEPT];
+  return SMASH_OK;
+}

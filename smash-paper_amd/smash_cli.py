@@ -1,0 +1,349 @@
+"""smash_cli -- the reference's command-line surface over the MI355X path.
+
+The reference is driven by three shell scripts around its binaries; each
+subcommand below takes the same inputs and writes the same files:
+
+  index REF.fa                  index_setup.sh: REF.fa.bin/ cache (rc1.*,
+                                `mummer -rcref`), map.bin (`mummer -rcref
+                                -mappability`), chrom_sizes.txt, sam_header.txt
+  map ID "R1.gz.." "R2.gz.."    smash_mapping.sh: fastqs_to_sam | mummer -samin |
+                                mappability_tag | samtools sort -n | smashMEM.py
+                                0 0 10000 4 | awk/perl -> ID.positions.txt
+  varbin POS BINS OUT STATS CS  varbin.py's five arguments (binning.sh:36)
+  count ID "R1.gz.." "R2.gz.." BINDIR
+                                map + varbin fused on the device, no positions
+                                file: ID.varbin.txt and ID.stats.txt
+  search [-mum|-maxmatch] [-l N] REF.fa QUERY
+                                mummer's match triples for FASTA/FASTQ/SAM queries
+                                (one line per read: name, then ref,query,len)
+
+REF.fa comes from --ref or $SMASH_REF as in the scripts.  Every computation
+runs in libsmashgpu.so (include/smash_gpu.h); without it the commands fail.
+Pairs are processed in `samtools sort -n` order (strnum_cmp,
+smash_mapping.sh:23), read 1 before read 2.
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+import smashgpu as S  # noqa: E402
+
+
+# ---------------------------------------------------------------------------
+# inputs
+# ---------------------------------------------------------------------------
+def _open(path):
+    if path == "-":
+        return sys.stdin.buffer
+    with open(path, "rb") as f:
+        magic = f.read(2)
+    return gzip.open(path, "rb") if magic == b"\x1f\x8b" else open(path, "rb")
+
+
+def fastq_records(path):
+    """(name, optional, bases) per record, parsed as fastqs_to_sam does
+    (fastqs_to_sam.cpp:48-76): '@' or '>' records, name = first token after
+    the marker, `optional` = the second token, FASTQ: '+' line and qualities."""
+    f = _open(path)
+    lines = iter(f)
+    for line in lines:
+        line = line.strip()
+        if not line:
+            continue
+        mark, rest = line[:1], line[1:]
+        if mark not in (b"@", b">"):
+            raise SystemExit("Fastq @ parse error: %r" % line[:40])
+        tok = rest.split()
+        if not tok:
+            raise SystemExit("Problem reading read name")
+        bases = next(lines, b"").rstrip(b"\r\n")
+        if mark == b"@":
+            plus = next(lines, b"").strip()
+            if plus[:1] != b"+":
+                raise SystemExit("Fastq + parse error")
+            next(lines, None)
+        yield tok[0], (tok[1] if len(tok) > 1 else b""), bases
+
+
+def fastq_pairs(r1s, r2s):
+    """Interleaved mates of the FASTQ lists (zcat r1s / zcat r2s, as
+    smash_mapping.sh:19 feeds fastqs_to_sam); records with empty bases are
+    dropped as fastqs_to_sam drops them (fastqs_to_sam.cpp:80)."""
+    def chain(paths):
+        for p in paths:
+            yield from fastq_records(p)
+    out = []
+    for a, b in zip(chain(r1s), chain(r2s)):
+        if a[2] and b[2]:
+            out.append((a[0], a[2], b[2]))
+    return out
+
+
+def sam_pairs(path):
+    """Mate pairs of an unmapped SAM (fastqs_to_sam output, mummer -samin):
+    consecutive lines, flag 64 = read 1 (query.cpp:614-687)."""
+    out, pend = [], None
+    for line in _open(path):
+        if line.startswith(b"@"):
+            continue
+        f = line.rstrip(b"\r\n").split(b"\t")
+        if len(f) < 10:
+            continue
+        flag = int(f[1])
+        if flag & 64:
+            pend = (f[0], f[9])
+        elif flag & 128 and pend is not None:
+            out.append((pend[0], pend[1], f[9]))
+            pend = None
+    return out
+
+
+_DIG = re.compile(rb"(\d+)")
+
+
+def strnum_key(name: bytes):
+    """samtools sort -n order (strnum_cmp): digit runs compare numerically."""
+    parts = _DIG.split(name)
+    return tuple((0, p) if i % 2 == 0 else (1, int(p)) for i, p in enumerate(parts))
+
+
+def reads_matrix(pairs):
+    """[2n, L] uint8 mates (read 1, read 2, ...) after replaceN + lowercasing
+    (fastqs_to_sam.cpp:74 with argc == 4, query.cpp:125-144)."""
+    if not pairs:
+        return np.zeros((0, 0), np.uint8)
+    L = len(pairs[0][1])
+    if any(len(a) != L or len(b) != L for _, a, b in pairs):
+        raise SystemExit("all mates must have the same length (the device batches are "
+                         "fixed-length); split the input by read length")
+    raw = np.frombuffer(b"".join(a + b for _, a, b in pairs), np.uint8).reshape(-1, L)
+    return S.prepare_reads(raw)
+
+
+def contig_offsets(ix, chrom_sizes):
+    return {off: name for name, off in chrom_sizes.items()}
+
+
+# ---------------------------------------------------------------------------
+# outputs (varbin.py:95-114)
+# ---------------------------------------------------------------------------
+def write_varbin(bins_rows, counts, total, dups, kept, out_path, stats_path):
+    nb = len(bins_rows)
+    print(nb)
+    print(nb)
+    if kept == 0:
+        raise SystemExit("ZeroDivisionError: no read kept (varbin.py:96)")
+    with open(out_path, "w") as o:
+        for row, c in zip(bins_rows, counts):
+            ratio = float(int(c)) / (float(kept) / float(nb))
+            o.write("\t".join(row[0:3]) + "\t" + str(int(c)) + "\t" + repr(ratio) + "\n")
+    with open(stats_path, "w") as o:
+        med = sorted(int(c) for c in counts)[nb // 2]
+        o.write("TotalReads\tDupsRemoved\tReadsKept\tMedianBinCount\n")
+        o.write("%d\t%d\t%d\t%d\n" % (total, dups, kept, med))
+
+
+# ---------------------------------------------------------------------------
+# commands
+# ---------------------------------------------------------------------------
+def _ref(args):
+    ref = args.ref or os.environ.get("SMASH_REF", "")
+    if not ref or not os.path.isfile(ref):
+        raise SystemExit("export SMASH_REF variable as fasta file path")
+    return ref
+
+
+def load_index(ref, device=0):
+    if os.path.isdir(ref + ".bin") and any(
+            os.path.exists(ref + ".bin/rc1.i%d.index.bin" % w) for w in (4, 8)):
+        return S.Index.load(ref, device=device)
+    return S.Index.from_fasta(ref, device=device)
+
+
+def cmd_index(args):
+    ref = _ref(args)
+    if os.path.exists(ref + ".bin") and not args.force:
+        raise SystemExit("binary index directory %s.bin already exists - quitting" % ref)
+    ix = S.Index.from_fasta(ref, device=args.device)
+    ix.save(ref)
+    d = ref + ".bin"
+    n = 0
+    with open(os.path.join(d, "chrom_sizes.txt"), "w") as cs, \
+            open(os.path.join(d, "sam_header.txt"), "w") as sh:
+        for name, size in zip(ix.contigs, ix.contig_sizes):
+            if "_" not in name:
+                cs.write("%s\t%d\t%d\n" % (name, size, n))
+                n += size
+            sh.write("@SQ\tSN:%s\tLN:%d\n" % (name, size))
+    print("index: N=%d, %.1f GB in HBM, %.1f s" % (ix.N, ix.info.device_bytes / 1e9,
+                                                  ix.info.build_seconds), file=sys.stderr)
+
+
+class _Run:
+    """Index + pipeline + batches over pairs in name order."""
+
+    def __init__(self, args, bins_path=None):
+        import torch
+        self.torch = torch
+        self.ref = _ref(args)
+        self.ix = load_index(self.ref, args.device)
+        cs_path = args.chrom_sizes or self.ref + ".bin/chrom_sizes.txt"
+        self.cs = S.read_chrom_sizes(cs_path)
+        if bins_path:
+            self.bins_rows, self.starts = S.read_bins(bins_path)
+        else:
+            self.bins_rows, self.starts = [], np.zeros(1, np.int64)
+        pairs = sam_pairs(args.sam) if args.sam else \
+            fastq_pairs(args.reads1.split(), args.reads2.split())
+        pairs.sort(key=lambda p: strnum_key(p[0]))
+        self.reads = reads_matrix(pairs)
+        self.n = len(pairs)
+        self.batch = min(args.batch, max(self.n, 1))
+        self.dev = torch.device("cuda", args.device)
+
+    def run(self, on_batch):
+        torch = self.torch
+        L = self.reads.shape[1] if self.n else 150
+        pipe = S.Pipeline(self.ix, self.cs, self.starts, L, self.batch,
+                          dedup_capacity=max(self.n, 1))
+        counts = torch.zeros(len(self.starts), dtype=torch.int64, device=self.dev)
+        pipe.reset()
+        for b0 in range(0, self.n, self.batch):
+            b1 = min(self.n, b0 + self.batch)
+            d = torch.from_numpy(np.ascontiguousarray(self.reads[2 * b0:2 * b1])).to(self.dev)
+            pipe.count_batch(d, b1 - b0, counts)
+            on_batch(pipe)
+        st = pipe.stats()
+        if st.error:
+            raise SystemExit("mappability_tag: %s" % S.ERRORS.get(st.error, st.error))
+        return counts.cpu().numpy(), st
+
+
+def cmd_map(args):
+    run = _Run(args)
+    names = contig_offsets(run.ix, run.cs)
+    with open(args.id + ".positions.txt", "w") as out:
+        def emit(pipe):
+            pos0, absp = pipe.positions()
+            for p, a in zip(pos0.tolist(), absp.tolist()):
+                out.write("%s %d\n" % (names[a - p], p))
+        _, st = run.run(emit)
+    with open(args.id + ".smash.summary.txt", "w") as o:   # smashMEM.py:230
+        o.write("%d dupes\t%d non-dupes\n" % (st.dupe_pairs, st.key_pairs - st.dupe_pairs))
+
+
+def cmd_count(args):
+    bins = os.path.join(args.bindir, "bins.txt")
+    run = _Run(args, bins)
+    counts, st = run.run(lambda pipe: None)
+    write_varbin(run.bins_rows, counts, st.positions, st.dups, st.kept,
+                 args.out or args.id + ".varbin.txt", args.id + ".stats.txt")
+
+
+def cmd_varbin(args):
+    import torch
+    chrominfo = S.read_chrom_sizes(args.chrom_sizes)
+    rows, starts = S.read_bins(args.bins)
+    pos0, absp = [], []
+    with open(args.positions) as f:
+        for x in f:
+            arow = x.rstrip().split(" ")                   # varbin.py:38-49
+            chrom = arow[0]
+            if chrom.find("_") > -1 or chrom == "chrM" or chrom == "" or chrom not in chrominfo:
+                continue
+            s = arow[1]
+            p = int(s)
+            if str(p) != s:
+                raise SystemExit("position %r is not a canonical integer: varbin.py compares "
+                                 "the strings" % s)
+            pos0.append(p)
+            absp.append(p + chrominfo[chrom])
+    dev = torch.device("cuda", args.device)
+    d_pos = torch.tensor(pos0, dtype=torch.int64, device=dev)
+    d_abs = torch.tensor(absp, dtype=torch.int64, device=dev)
+    d_bins = torch.from_numpy(starts).to(dev)
+    counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+    total, dups, kept = S.bin_positions(d_pos, d_abs, len(pos0), -1, d_bins, len(starts), counts)
+    write_varbin(rows, counts.cpu().numpy(), total, dups, kept, args.out, args.stats)
+
+
+def cmd_search(args):
+    import torch
+    ref = _ref(args)
+    ix = load_index(ref, args.device)
+    mode = "MUM" if args.mum else "MEM" if args.maxmatch else "MAM"
+    q = args.query
+    if q.endswith((".sam", ".sam.gz")):
+        recs = []
+        for a, s1, s2 in sam_pairs(q):
+            recs += [(a + b":0", s1), (a + b":1", s2)]
+    else:
+        recs = [(r[0], r[2]) for r in fastq_records(q)]
+    dev = torch.device("cuda", args.device)
+    out = sys.stdout
+    for L in sorted({len(s) for _, s in recs}):
+        sel = [(n, s) for n, s in recs if len(s) == L and L > 0]
+        if not sel:
+            continue
+        reads = S.prepare_reads(np.frombuffer(b"".join(s for _, s in sel), np.uint8).reshape(-1, L))
+        cap = args.cap
+        d = torch.from_numpy(np.ascontiguousarray(reads)).to(dev)
+        o = torch.zeros(len(sel) * cap * 2, dtype=torch.int64, device=dev)
+        nn = torch.zeros(len(sel), dtype=torch.int32, device=dev)
+        S.match_batch(ix, d, len(sel), L, o, cap, nn, mode=mode, min_len=args.l)
+        w = o.cpu().numpy().view(np.uint64).reshape(len(sel), 2 * cap)
+        k = nn.cpu().numpy()
+        for i, (name, _) in enumerate(sel):
+            if k[i] > cap:
+                raise SystemExit("%s: %d matches exceed --cap %d" % (name.decode(), k[i], cap))
+            ms = S.unpack_records(w[i], k[i], cap)
+            out.write(name.decode() + "\t" + str(int(k[i])) + "".join(
+                "\t%d,%d,%d" % m for m in ms) + "\n")
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="smash_cli", description=__doc__.split("\n\n")[0])
+    ap.add_argument("--ref", default=None, help="reference FASTA (default $SMASH_REF)")
+    ap.add_argument("--device", type=int, default=0)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("index")
+    p.add_argument("--force", action="store_true")
+    p.set_defaults(fn=cmd_index)
+    for name, fn in (("map", cmd_map), ("count", cmd_count)):
+        p = sub.add_parser(name)
+        p.add_argument("id")
+        p.add_argument("reads1", nargs="?", default="", help="space-separated r1 fastq(.gz) list")
+        p.add_argument("reads2", nargs="?", default="", help="space-separated r2 fastq(.gz) list")
+        if name == "count":
+            p.add_argument("bindir")
+            p.add_argument("--out", default=None)
+        p.add_argument("--sam", default=None, help="unmapped SAM input instead (mummer -samin)")
+        p.add_argument("--chrom-sizes", default=None)
+        p.add_argument("--batch", type=int, default=2_000_000, help="pairs per device batch")
+        p.set_defaults(fn=fn)
+    p = sub.add_parser("varbin")
+    for a in ("positions", "bins", "out", "stats", "chrom_sizes"):
+        p.add_argument(a)
+    p.set_defaults(fn=cmd_varbin)
+    p = sub.add_parser("search")
+    p.add_argument("-mum", action="store_true")
+    p.add_argument("-maxmatch", action="store_true")
+    p.add_argument("-l", type=int, default=20, help="minimum match length (query.h:129)")
+    p.add_argument("--cap", type=int, default=65536, help="records per read")
+    p.add_argument("query")
+    p.set_defaults(fn=cmd_search)
+    args = ap.parse_args(argv)
+    args.fn(args)
+
+
+if __name__ == "__main__":
+    main()

@@ -44,6 +44,7 @@ EXPORTS = [
     "smash_phase_import", "smash_phase_positions", "smash_phase_bin",
     "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_peek",
     "smash_pipeline_profile", "smash_pipeline_profile_read",
+    "smash_pipeline_positions", "smash_bin_positions",
 ]
 
 
@@ -124,6 +125,9 @@ def lib():
     L.smash_pipeline_peek.argtypes = [vp, i32p, u8p, u64p, u64p]
     L.smash_pipeline_profile.argtypes = [vp, C.c_int]
     L.smash_pipeline_profile_read.argtypes = [vp, C.POINTER(C.c_double), u64p, u64p]
+    L.smash_pipeline_positions.argtypes = [vp, i64p, i64p, C.c_uint64, u64p]
+    L.smash_bin_positions.argtypes = [vp, vp, C.c_uint64, C.c_int64, vp, C.c_uint32, vp, u64p,
+                                      vp]
     _LIB = L
     return L
 
@@ -387,6 +391,18 @@ class Pipeline:
               "smash_pipeline_profile_read")
         return ms.value, n.value, r.value
 
+    def positions(self):
+        """(pos0, abspos) int64 arrays of the positions the last batch emitted
+        (smash_pipeline_positions), in emission order."""
+        n = C.c_uint64()
+        check(lib().smash_pipeline_positions(self.h, None, None, 0, C.byref(n)),
+              "smash_pipeline_positions")
+        pos0 = np.zeros(n.value, np.int64)
+        absp = np.zeros(n.value, np.int64)
+        check(lib().smash_pipeline_positions(self.h, _p(pos0, i64p), _p(absp, i64p), n.value,
+                                             C.byref(n)), "smash_pipeline_positions")
+        return pos0, absp
+
     def peek(self, n_pairs):
         nk = np.zeros(n_pairs, np.int32)
         keep = np.zeros(n_pairs, np.uint8)
@@ -428,6 +444,16 @@ def match_batch(index: Index, d_reads, n_reads, read_len, d_out, cap, d_n, mode=
     check(lib().smash_match_batch(index.h, MODES.get(mode, mode), min_len, _ptr(d_reads),
                                   read_len, None, read_len, n_reads, _ptr(d_out), cap,
                                   _ptr(d_n), vp(_stream(stream))), "smash_match_batch")
+
+
+def bin_positions(d_pos0, d_abspos, n, prev_pos0, d_bin_starts, nbins, d_counts, stream=None):
+    """varbin.py's counting loop on the device (smash_bin_positions); returns
+    [TotalReads, DupsRemoved, ReadsKept] of this call."""
+    st = np.zeros(3, np.uint64)
+    check(lib().smash_bin_positions(_ptr(d_pos0), _ptr(d_abspos), n, prev_pos0,
+                                    _ptr(d_bin_starts), nbins, _ptr(d_counts), _p(st, u64p),
+                                    vp(_stream(stream))), "smash_bin_positions")
+    return [int(x) for x in st]
 
 
 def unpack_records(words, n, cap):

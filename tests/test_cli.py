@@ -1,0 +1,139 @@
+"""The command-line surface (smash-paper_amd/bin/fastqs_to_sam and
+smash-paper_amd/smash_cli.py) against the reference's outputs.
+
+CPU: fastqs_to_sam byte-identical to the reference binary's output on the
+golden FASTQ pairs and on a parser edge-case pair; the CLI's FASTQ/SAM readers
+and its `samtools sort -n` key.  GPU (`gpu` marker): `varbin`, `map` and
+`count` on the tiny genome reproduce varbin.py's rows (the real varbin.py
+output, tests/golden/*_varbin.txt) and the positions files.
+"""
+import gzip
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, gold
+
+BIN = os.path.join(ROOT, "smash-paper_amd", "bin", "fastqs_to_sam")
+sys.path.insert(0, os.path.join(ROOT, "smash-paper_amd"))
+import smash_cli  # noqa: E402
+
+
+def _fq(tmp_path, s, k):
+    p = tmp_path / ("%s_r%d.fq" % (s, k))
+    p.write_bytes(gzip.open(gold("%s_r%d.fq.gz" % (s, k))).read())
+    return str(p)
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_fastqs_to_sam_matches_reference(tmp_path, s):
+    out = subprocess.run([BIN, _fq(tmp_path, s, 1), _fq(tmp_path, s, 2), "1"],
+                         capture_output=True, check=True).stdout
+    assert out == gzip.open(gold("%s_fastqs_to_sam.sam.gz" % s)).read()
+
+
+@pytest.mark.parametrize("replace", [False, True])
+def test_fastqs_to_sam_edge_cases(replace):
+    args = [BIN, gold("edge_r1.fq"), gold("edge_r2.fq")] + (["1"] if replace else [])
+    out = subprocess.run(args, capture_output=True, check=True).stdout
+    exp = open(gold("edge_fastqs_to_sam%s.sam" % ("_replaceN" if replace else "")), "rb").read()
+    assert out == exp
+
+
+def test_fastqs_to_sam_usage_error():
+    r = subprocess.run([BIN, "only_one"], capture_output=True)
+    assert r.returncode == 1 and b"usage" in r.stderr
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_cli_readers_agree_with_fastqs_to_sam(tmp_path, s):
+    pairs = smash_cli.fastq_pairs([_fq(tmp_path, s, 1)], [_fq(tmp_path, s, 2)])
+    sam = tmp_path / "x.sam"
+    sam.write_bytes(gzip.open(gold("%s_fastqs_to_sam.sam.gz" % s)).read())
+    spairs = smash_cli.sam_pairs(str(sam))
+    assert [p[0] for p in pairs] == [p[0] for p in spairs]
+    m = smash_cli.reads_matrix(pairs)
+    assert np.array_equal(m, smash_cli.reads_matrix(spairs))   # replaceN before / after
+    from conftest import interleaved_reads
+    assert np.array_equal(m, interleaved_reads(s))
+
+
+def test_strnum_key_orders_like_samtools_sort_n():
+    names = [b"r10", b"r9", b"r009", b"a2b10", b"a2b9", b"r1", b"b"]
+    got = sorted(names, key=smash_cli.strnum_key)
+    assert got.index(b"r9") < got.index(b"r10")
+    assert got.index(b"a2b9") < got.index(b"a2b10")
+    assert got.index(b"r1") < got.index(b"r9")
+
+
+# ---------------------------------------------------------------------------
+# GPU: the device-backed subcommands
+# ---------------------------------------------------------------------------
+def _ref_dir(tmp_path, tiny_fa):
+    import shutil
+    fa = tmp_path / "tiny.fa"
+    shutil.copy(tiny_fa, fa)
+    return str(fa)
+
+
+@pytest.mark.gpu
+def test_cli_index_varbin_map_count(tmp_path, tiny_fa, monkeypatch):
+    pytest.importorskip("torch")
+    fa = _ref_dir(tmp_path, tiny_fa)
+    monkeypatch.chdir(tmp_path)
+    smash_cli.main(["--ref", fa, "index"])
+    cs = open(fa + ".bin/chrom_sizes.txt").read()
+    assert cs == open(gold("tiny_chrom_sizes.txt")).read()
+    assert open(fa + ".bin/sam_header.txt").read() == open(gold("tiny_sam_header.txt")).read()
+    bindir = tmp_path / "bins"
+    bindir.mkdir()
+    (bindir / "bins.txt").write_text(open(gold("tiny_bins.txt")).read())
+    for s in ("s100", "s150"):
+        exp_rows = open(gold("%s_varbin.txt" % s)).read()
+        part = open(gold("%s_varbin_stats_partial.txt" % s)).read()
+        # varbin.py on the golden positions
+        smash_cli.main(["varbin", gold("%s_positions.txt" % s), str(bindir / "bins.txt"),
+                        "v.txt", "st.txt", fa + ".bin/chrom_sizes.txt"])
+        assert open("v.txt").read() == exp_rows
+        assert open("st.txt").read().startswith(part)
+        # the whole chain from FASTQ
+        r1, r2 = _fq(tmp_path, s, 1), _fq(tmp_path, s, 2)
+        smash_cli.main(["--ref", fa, "map", s, r1, r2, "--batch", "97"])
+        assert open(s + ".positions.txt").read() == open(gold("%s_positions.txt" % s)).read()
+        smash_cli.main(["--ref", fa, "count", s, r1, r2, str(bindir), "--out", "c.txt"])
+        assert open("c.txt").read() == exp_rows
+        assert open(s + ".stats.txt").read().startswith(part)
+        # from the unmapped SAM (mummer -samin)
+        sam = tmp_path / "x.sam"
+        sam.write_bytes(gzip.open(gold("%s_fastqs_to_sam.sam.gz" % s)).read())
+        smash_cli.main(["--ref", fa, "count", s, "--sam", str(sam), str(bindir), "--out", "c2.txt"])
+        assert open("c2.txt").read() == exp_rows
+
+
+@pytest.mark.gpu
+def test_cli_varbin_edge_positions_hg19_bins(tmp_path, monkeypatch):
+    pytest.importorskip("torch")
+    monkeypatch.chdir(tmp_path)
+    bins = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    smash_cli.main(["varbin", gold("edge_positions.txt"), bins, "v.txt", "st.txt",
+                    gold("chrom_sizes_hg19.txt")])
+    assert open("v.txt").read() == gzip.open(gold("edge_varbin.txt.gz"), "rt").read()
+    assert open("st.txt").read().startswith(open(gold("edge_varbin_stats_partial.txt")).read())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flag,mode", [([], "MAM"), (["-mum"], "MUM"), (["-maxmatch"], "MEM")])
+def test_cli_search_triples(tmp_path, tiny_fa, capsys, flag, mode):
+    pytest.importorskip("torch")
+    fa = _ref_dir(tmp_path, tiny_fa)
+    sam = tmp_path / "x.sam"
+    sam.write_bytes(gzip.open(gold("s100_fastqs_to_sam.sam.gz")).read())
+    smash_cli.main(["--ref", fa, "search"] + flag + [str(sam)])
+    got = capsys.readouterr().out.splitlines()
+    exp = gzip.open(gold("s100_%s.txt.gz" % mode), "rt").read().splitlines()
+    for g, e in zip(got, exp):
+        gt, et = g.split("\t"), e.split()
+        assert gt[2:] == et[2:], (g[:80], e[:80])

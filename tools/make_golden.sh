@@ -123,3 +123,10 @@ cp edge_positions.txt chrom_sizes_hg19.txt "$OUT/"
 gzip -9 -n -c edge_varbin.txt > "$OUT/edge_varbin.txt.gz"
 cp edge_stats.txt "$OUT/edge_varbin_stats_partial.txt"
 echo "golden written to $OUT"
+
+# fastqs_to_sam parser quirks (blank lines, '+name' lines, an empty record,
+# FASTA records whose qualities keep the N): tests/golden/edge_r{1,2}.fq are
+# hand-written; the outputs are the reference binary's, with and without
+# the replaceN argument.
+"$R/fastqs_to_sam" "$OUT/edge_r1.fq" "$OUT/edge_r2.fq" > "$OUT/edge_fastqs_to_sam.sam"
+"$R/fastqs_to_sam" "$OUT/edge_r1.fq" "$OUT/edge_r2.fq" 1 > "$OUT/edge_fastqs_to_sam_replaceN.sam"
