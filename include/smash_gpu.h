@@ -148,6 +148,25 @@ int smash_match_batch(const smash_index *ix, int mode, uint32_t min_len,
                       uint32_t *d_n_out, void *stream);
 
 /* ========================================================================== */
+/* Mappability self-scan (BASELINE config C5): replaces longSA::show ->       */
+/* map.bin (longSA.cpp:612-690, `mummer -rcref -mappability`, index_setup.sh: */
+/* 22) for the forward bases [begin, end) of the concatenated forward contigs */
+/* (map.bin byte 2 + 2*g is base g), from the resident ISA + LCP.             */
+/*  d_map_out: 2*(end-begin) bytes [left, right] per base, or NULL;           */
+/*  derived counts of unique k-mers (the k-mer at a base is unique iff        */
+/*  1 <= right <= k): d_contig_counts[n_seq/2] += per contig (or NULL), and,  */
+/*  when d_bin_starts is given, d_bin_counts[nbins] += per bin of              */
+/*  abspos = h_chrom_off[contig] + base (contigs with offset < 0 unbinned;    */
+/*  bisect_right as varbin.py:89-92).  Asynchronous on `stream`.              */
+/* ========================================================================== */
+int smash_mappability_scan(const smash_index *ix, uint64_t begin, uint64_t end,
+                           uint32_t k, uint8_t *d_map_out,
+                           const int64_t *h_chrom_off,
+                           const int64_t *d_bin_starts, uint32_t nbins,
+                           uint64_t *d_bin_counts, uint64_t *d_contig_counts,
+                           void *stream);
+
+/* ========================================================================== */
 /* Pipeline: prepare_matches (query.cpp:231-306) + mappability_tag           */
 /* (mappability_tag.cpp:93-124) + smashMEM.py filters & global pair de-dup   */
 /* (smashMEM.py:154-228) + varbin.py (varbin.py:52-92), fused per batch.      */

@@ -44,7 +44,7 @@ EXPORTS = [
     "smash_phase_import", "smash_phase_positions", "smash_phase_bin",
     "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_peek",
     "smash_pipeline_profile", "smash_pipeline_profile_read",
-    "smash_pipeline_positions", "smash_bin_positions",
+    "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
 ]
 
 
@@ -128,6 +128,8 @@ def lib():
     L.smash_pipeline_positions.argtypes = [vp, i64p, i64p, C.c_uint64, u64p]
     L.smash_bin_positions.argtypes = [vp, vp, C.c_uint64, C.c_int64, vp, C.c_uint32, vp, u64p,
                                       vp]
+    L.smash_mappability_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, i64p, vp,
+                                         C.c_uint32, vp, vp, vp]
     _LIB = L
     return L
 
@@ -454,6 +456,19 @@ def bin_positions(d_pos0, d_abspos, n, prev_pos0, d_bin_starts, nbins, d_counts,
                                     _ptr(d_bin_starts), nbins, _ptr(d_counts), _p(st, u64p),
                                     vp(_stream(stream))), "smash_bin_positions")
     return [int(x) for x in st]
+
+
+def mappability_scan(index: Index, begin, end, k=36, d_map_out=None, chrom_off=None,
+                     d_bin_starts=None, nbins=0, d_bin_counts=None, d_contig_counts=None,
+                     stream=None):
+    """map.bin bytes of forward bases [begin, end) and unique-k-mer counts
+    (smash_mappability_scan).  chrom_off: host int64 per contig or None."""
+    off = None if chrom_off is None else np.ascontiguousarray(chrom_off, np.int64)
+    check(lib().smash_mappability_scan(index.h, begin, end, k, _ptr(d_map_out),
+                                       None if off is None else _p(off, i64p),
+                                       _ptr(d_bin_starts), nbins, _ptr(d_bin_counts),
+                                       _ptr(d_contig_counts), vp(_stream(stream))),
+          "smash_mappability_scan")
 
 
 def unpack_records(words, n, cap):

@@ -1,0 +1,118 @@
+"""The mappability self-scan (BASELINE config C5) on the device:
+smash_mappability_scan's map.bin bytes against the reference's map.bin
+(`mummer -rcref -mappability`, hashed in tests/golden/tiny_index.sha256) and
+the oracle's restatement of longSA::show, for any split of the genome into
+ranges (the multi-GPU partition), with 4- and 8-byte ISA; the unique-k-mer
+counts per contig and per bin against numpy over the oracle's map.  Marked
+`gpu`."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import gold
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import smashgpu as S  # noqa: E402
+import oracle as O  # noqa: E402
+
+
+def scan(ix, begin, end, k, off=None, starts=None):
+    dev = "cuda"
+    out = torch.zeros(max(2 * (end - begin), 1), dtype=torch.uint8, device=dev)
+    nc = len(ix.contigs)
+    cc = torch.zeros(nc, dtype=torch.int64, device=dev)
+    if starts is not None:
+        db = torch.from_numpy(np.ascontiguousarray(starts, np.int64)).to(dev)
+        bc = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+        S.mappability_scan(ix, begin, end, k, out, off, db, len(starts), bc, cc)
+    else:
+        bc = None
+        S.mappability_scan(ix, begin, end, k, out, None, None, 0, None, cc)
+    torch.cuda.synchronize()
+    return (out.cpu().numpy()[:2 * (end - begin)], cc.cpu().numpy(),
+            None if bc is None else bc.cpu().numpy())
+
+
+def expected_counts(mp, sizes, k, off, starts):
+    right = mp[1::2]
+    uniq = (right >= 1) & (right <= k)
+    cc, bc = [], np.zeros(len(starts), np.int64)
+    g = 0
+    for q, S_ in enumerate(sizes):
+        u = uniq[g:g + S_]
+        cc.append(int(u.sum()))
+        if off is not None and off[q] >= 0:
+            a = off[q] + np.nonzero(u)[0]
+            b = np.searchsorted(starts, a, side="right") - 1
+            b[b < 0] = len(starts) - 1
+            np.add.at(bc, b, 1)
+        g += S_
+    return np.array(cc), bc
+
+
+def test_tiny_map_equals_reference(tiny_fa):
+    ix = S.Index.from_fasta(tiny_fa)
+    total = sum(ix.contig_sizes)
+    mp, _, _ = scan(ix, 0, total, 36)
+    sums = {l.split()[0]: l.split()[1] for l in open(gold("tiny_index.sha256"))}
+    assert hashlib.sha256(mp.tobytes()).hexdigest() == sums["map.bin[2:]"]
+
+
+@pytest.fixture(scope="module", params=[4, 8])
+def mid(request, tmp_path_factory):
+    import synth
+    g = synth.make_genome("mid")
+    T, sp, sz, names = O.text_from_contigs(g)
+    oix = O.Index(T, sp, sz, names)
+    old = os.environ.get("SMASH_IDX_BYTES")
+    os.environ["SMASH_IDX_BYTES"] = str(request.param)
+    try:
+        dix = S.Index.create(T, sp, sz, names)
+    finally:
+        if old is None:
+            os.environ.pop("SMASH_IDX_BYTES")
+        else:
+            os.environ["SMASH_IDX_BYTES"] = old
+    d = tmp_path_factory.mktemp("mid%d" % request.param)
+    synth.write_index_side_files(str(d), g)
+    synth.make_bins(g, 16, str(d / "bins.txt"))
+    cs = S.read_chrom_sizes(str(d / "chrom_sizes.txt"))
+    off = np.array([cs.get(c, -1) if "_" not in c and c != "chrM" else -1
+                    for c in dix.contigs], np.int64)
+    _, starts = S.read_bins(str(d / "bins.txt"))
+    return oix, dix, off, starts
+
+
+@pytest.mark.parametrize("k", [20, 36])
+def test_mid_scan_equals_oracle(mid, k):
+    oix, dix, off, starts = mid
+    total = sum(dix.contig_sizes)
+    omap = oix.mappability()
+    mp, cc, bc = scan(dix, 0, total, k, off, starts)
+    assert np.array_equal(mp, omap[2:])
+    ecc, ebc = expected_counts(omap[2:], dix.contig_sizes, k, off, starts)
+    assert cc.tolist() == ecc.tolist()
+    assert bc.tolist() == ebc.tolist()
+    # the index's own map.bin agrees
+    assert np.array_equal(S.download(dix.info.d_map, dix.info.map_bytes)[2:], omap[2:])
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+def test_mid_scan_any_partition(mid, parts):
+    oix, dix, off, starts = mid
+    total = sum(dix.contig_sizes)
+    rng = np.random.default_rng(parts)
+    cuts = [0] + sorted(int(x) for x in rng.integers(1, total, parts - 1)) + [total]
+    full, fcc, fbc = scan(dix, 0, total, 36, off, starts)
+    maps, cc, bc = [], 0, 0
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        m, c1, b1 = scan(dix, a, b, 36, off, starts)
+        maps.append(m)
+        cc = cc + c1
+        bc = bc + b1
+    assert np.array_equal(np.concatenate(maps), full)
+    assert np.array_equal(cc, fcc) and np.array_equal(bc, fbc)
