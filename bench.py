@@ -47,6 +47,10 @@ CONFIGS = {
     # configs[0]-like plumbing on the chr21-sized genome (bins split 10-way)
     "c1": dict(genome="chr21", read_len=100, pairs=500_000, bins="500000", seed=1,
                workload="C1-shaped chr21-sized genome, 100 bp, sample_bins/500000"),
+    # configs[4]: whole-genome mappability self-scan (every 36-mer), C5
+    "c5": dict(genome="hg19", bins="50000", k=36,
+               workload="C5 hg19-shaped mappability self-scan (map.bin + unique 36-mer "
+                        "counts per chromosome and per 50 k bin)"),
     # quick functional run
     "mid": dict(genome="mid", read_len=150, pairs=200_000, bins="synthetic", seed=2,
                 workload="3.2 Mbp synthetic genome, 150 bp (functional check)"),
@@ -117,6 +121,115 @@ def host_index(S, O, dix, T, sp, sz, names):
     return oix, mp
 
 
+def bench_c5(args, cfg, world, rank, local, dist):
+    """C5: map.bin of every forward base (longSA::show) + unique 36-mer counts,
+    bases split into `world` contiguous ranges, counts all-reduced."""
+    import torch
+    import smashgpu as S
+    import synth
+    dev = torch.device("cuda", local)
+    t0 = time.time()
+    contigs = synth.make_genome(cfg["genome"])
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    dix = S.Index.create(T, sp, sz, names, device=local)
+    log("device index: %.1f s, %.1f GB in HBM" % (dix.info.build_seconds,
+                                                  dix.info.device_bytes / 1e9))
+    starts = bin_starts_for(cfg, contigs, tempfile.mkdtemp())
+    cs = chrom_sizes_for(cfg, contigs)
+    off = np.array([cs.get(c, -1) if ("_" not in c and c != "chrM") else -1
+                    for c in dix.contigs], np.int64)
+    total = int(sum(dix.contig_sizes))
+    g0, g1 = total * rank // world, total * (rank + 1) // world
+    k = cfg["k"]
+    d_bins = torch.from_numpy(starts).to(dev)
+    bc = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+    cc = torch.zeros(len(dix.contigs), dtype=torch.int64, device=dev)
+    out = torch.empty(2 * (g1 - g0), dtype=torch.uint8, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+
+    def step(i, timed):
+        bc.zero_()
+        cc.zero_()
+        if timed:
+            ev[2 * i].record()
+        S.mappability_scan(dix, g0, g1, k, out, off, d_bins, len(starts), bc, cc)
+        if timed:
+            ev[2 * i + 1].record()
+        if world > 1:
+            dist.all_reduce(bc)
+            dist.all_reduce(cc)
+
+    for i in range(args.warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.steps)) / args.steps
+    # full-size properties: the scan reproduces the build's map.bin bytes
+    dmap = S.download(dix.info.d_map, dix.info.map_bytes)
+    same_map = bool(np.array_equal(out.cpu().numpy(), dmap[2 + 2 * g0:2 + 2 * g1]))
+    n_uniq = int(cc.sum().item())
+    value = total * args.steps / el
+    log("timed %d steps: %.3f s -> %.3e bases/s; scan %.1f ms; unique %d-mers %d; "
+        "map == build map: %s" % (args.steps, el, value, kms, k, n_uniq, same_map))
+    bpb = 2 * dix.info.idx_bytes + 2 * 64 + 2
+    achieved = (g1 - g0) * bpb / (kms / 1e3) / 1e9
+    out_j = {
+        "metric": "bases/sec mappability self-scan (hg19, every 36-mer; map.bin + unique "
+                  "counts, C5)",
+        "value": value, "unit": "bases/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u8/u64 (integer)", "data": "synthetic (tools/synth.py hg19-shaped genome)",
+        "config": {"workload": cfg["workload"], "genome": cfg["genome"], "bases": total,
+                   "k": k, "bins": int(len(starts)),
+                   "parallelism": "%d contiguous base ranges, all_reduce counts" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_mapscan", "achieved": round(achieved, 2),
+                     "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
+                     "traffic": None, "bytes_per_base": bpb,
+                     "bytes_method": "2 sequential ISA reads + 2 random 64-B LCP lines "
+                                     "+ 2 output bytes per base",
+                     "avg_kernel_ms": round(kms, 3)},
+        "map_identical_to_index_build": same_map, "unique_kmers": n_uniq,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle as O
+        oix, _ = host_index(S, O, dix, T, sp, sz, names)
+        n0 = 1 << 20
+        t3 = time.perf_counter()
+        oix.mappability_range(g0, g0 + n0, k)
+        dt0 = time.perf_counter() - t3
+        n1 = int(min(g1 - g0, max(n0, n0 * args.cpu_seconds / max(dt0, 1e-3))))
+        a = (g1 - g0 - n1) // 2 + g0
+        t3 = time.perf_counter()
+        m, _ = oix.mappability_range(a, a + n1, k)
+        dt = time.perf_counter() - t3
+        exact = bool(np.array_equal(m, dmap[2 + 2 * a:2 + 2 * (a + n1)]))
+        out_j["cpu_baseline"] = {
+            "value": n1 / dt, "unit": "bases/s", "cores": 1, "kind": "port",
+            "sample": "%d consecutive forward bases from %d (oracle/smash_oracle.c "
+                      "orc_mappability_range), %.1f s" % (n1, a, dt),
+            "map_identical_to_device": exact}
+        log("cpu baseline: %.3e bases/s on 1 core; identical: %s" % (n1 / dt, exact))
+    if rank == 0:
+        print(json.dumps(out_j), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,6 +258,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.config == "c5":
+        return bench_c5(args, cfg, world, rank, local, dist)
 
     t0 = time.time()
     contigs = synth.make_genome(cfg["genome"])

@@ -105,6 +105,9 @@ def lib():
                                   C.POINTER(OrcMatch), C.c_uint32,
                                   C.POINTER(OrcHit), C.c_uint32, u32p, i64p]
         L.orc_mappability.argtypes = [C.POINTER(OrcIndex), u8p]
+        L.orc_mappability_range.argtypes = [C.POINTER(OrcIndex), C.c_uint64, C.c_uint64,
+                                            C.c_uint32, u8p]
+        L.orc_mappability_range.restype = C.c_uint64
         L.orc_tag.argtypes = [C.POINTER(OrcHit), u32p, u8p, C.c_uint64, C.c_int]
         L.orc_smash_pair.argtypes = [C.POINTER(OrcHit), C.c_uint32,
                                      C.POINTER(OrcHit), C.c_uint32, C.c_int,
@@ -319,6 +322,12 @@ class Index:
         if lib().orc_mappability(C.byref(self.c), _p(out, u8p)):
             raise MemoryError
         return out
+
+    def mappability_range(self, g0, g1, k=36):
+        """(map.bin bytes of forward bases [g0, g1), unique k-mer count)"""
+        out = np.zeros(2 * (g1 - g0), np.uint8)
+        n = lib().orc_mappability_range(C.byref(self.c), g0, g1, k, _p(out, u8p))
+        return out, int(n)
 
 
 def lower_read(seq: bytes) -> bytes:

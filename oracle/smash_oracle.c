@@ -716,6 +716,34 @@ int orc_mappability(const orc_index *ix, uint8_t *out) {
   return 0;
 }
 
+static uint64_t min_len_at(const orc_index *ix, uint64_t r) {   /* :628-641 */
+  const uint64_t a = lcp_exact(ix, r, NULL);
+  const uint64_t b = r + 1 < ix->N ? lcp_exact(ix, r + 1, NULL) : 0;
+  return (a > b ? a : b) + 1;
+}
+
+uint64_t orc_mappability_range(const orc_index *ix, uint64_t g0, uint64_t g1,
+                               uint32_t k, uint8_t *out) {
+  uint64_t g = 0, w = 0, uniq = 0;
+  for (uint32_t chrom = 0; chrom < ix->n_seq && g < g1; chrom += 2) {
+    const uint64_t sp = ix->startpos[chrom], sz = ix->sizes[chrom];
+    const uint64_t a = g0 > g ? g0 - g : 0, b = g1 < g + sz ? g1 - g : sz;
+    for (uint64_t i = a; i < b; ++i) {
+      const uint64_t sapos = idx_at(ix->ISA, ix->idx_bytes, i + sp);
+      const uint64_t rcsapos = idx_at(ix->ISA, ix->idx_bytes, sp + 2 * sz - i);
+      uint64_t right = min_len_at(ix, sapos), left = min_len_at(ix, rcsapos);
+      if (right + i >= sz) right = 0;                  /* :666 */
+      if (left >= i) left = 0;                         /* :667 */
+      if (right > 255) right = 255;
+      out[w++] = (uint8_t)(left < 255 ? left : 255);
+      out[w++] = (uint8_t)right;
+      uniq += right >= 1 && right <= k;
+    }
+    g += sz;
+  }
+  return uniq;
+}
+
 /* ======================================================================== */
 /* mappability_tag (mappability_tag.cpp:81-124)                              */
 /* ======================================================================== */

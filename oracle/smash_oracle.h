@@ -160,6 +160,12 @@ int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
  * separately), then [left,right] per forward base of every contig. out must
  * hold 2 + 2*sum(forward sizes).  min_lengths is recomputed per rank. */
 int orc_mappability(const orc_index *ix, uint8_t *out);
+/* The same bytes for forward bases [g0, g1) of the concatenated forward
+ * contigs only (out: 2*(g1-g0) bytes), m[r] computed per base from the exact
+ * LCP instead of an N-sized array; returns the number of those bases whose
+ * k-mer is unique (1 <= right <= k) -- the C5 self-scan's restatement. */
+uint64_t orc_mappability_range(const orc_index *ix, uint64_t g0, uint64_t g1,
+                               uint32_t k, uint8_t *out);
 
 /* ---- mappability_tag (mappability_tag.cpp:93-124) ----------------------- */
 /* offsets: u32 sam_header offsets per tid; map: map.bin content;
