@@ -230,6 +230,8 @@ struct Ctx {
   const uint4 *rec;
   uint32_t chunks, c_bad, w_row, w_raw;
   uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
+  uint32_t pad;           // experiment: dependent ALU ops added per iteration (0 = none)
+  uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -289,6 +291,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   const uint32_t *C = row + c.w_raw;
   const uint32_t lane = threadIdx.x & 63;
 
+  uint64_t q_next = 0, q_end = 0;   // this wave's claimed, unassigned reads
   uint32_t st = S_NEW, op = 0, pend = A_NONE;
   uint64_t addr = 0, addr2 = 0;
   bool need2 = false;
@@ -309,11 +312,20 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint64_t w_iters = 0, w_active = 0;
 
   for (;;) {
+    // Work claiming: lanes that need a read take it from the wave's private
+    // range [q_next, q_end); a wave refills it with ONE atomic on the global
+    // counter for `grab` reads (or as many as its lanes need), so the
+    // counter's single-address atomics stay far below what its L2 channel
+    // serialises.  Reads past n_reads retire the lane as before.
     const uint64_t newm = __ballot(st == S_NEW);
+    const uint32_t need = uint32_t(__popcll(newm));
+    const uint64_t avail = q_end - q_next;
     unsigned long long base = 0;
-    if (newm) {
+    uint32_t take = 0;
+    if (newm && avail < need) {
+      take = need > c.grab ? need : c.grab;
       if (lane == uint32_t(__builtin_ctzll(newm)))
-        base = atomicAdd(c.work, (unsigned long long)__popcll(newm));
+        base = atomicAdd(c.work, (unsigned long long)take);
     }
     const uint64_t live = __ballot(st != S_EXIT);
     if (live == 0) break;
@@ -332,10 +344,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     if (need2) v2 = SM_LOAD16(addr2);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
     if (newm) {
-      base = __shfl(base, int(__builtin_ctzll(newm)), 64);
+      if (take) base = __shfl(base, int(__builtin_ctzll(newm)), 64);
       if (st == S_NEW) {
         fresh = true;
-        rd = base + __popcll(newm & ((1ull << lane) - 1));
+        const uint32_t r = uint32_t(__popcll(newm & ((1ull << lane) - 1)));
+        rd = r < avail ? q_next + r : base + (r - avail);
         if (rd >= c.n_reads) {
           st = S_EXIT;
         } else {
@@ -347,6 +360,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           st = S_COPY;
         }
       }
+      if (take) { q_next = base + (need - avail); q_end = base + take; }
+      else q_next += need;
     }
     if (st < S_ALU || fresh) continue;
     if (STATS) {
@@ -533,6 +548,12 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       default:
         break;
+    }
+
+    if (c.pad) {                                    // issue-bound experiment (SMASH_SM_PAD)
+      uint32_t x = uint32_t(addr);
+      for (uint32_t k = 0; k < c.pad; ++k) x = x * 2654435761u + k;
+      if (x == 0x9E3779B9u && st == S_EXIT) c.viol[0] = x;
     }
 
     // ---------------- decide ----------------

@@ -70,6 +70,8 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
   c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
   c.lin_blocks = lin_blocks;
+  c.pad = 0;
+  c.grab = 1;
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
   c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
