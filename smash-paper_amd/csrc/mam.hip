@@ -65,10 +65,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam(
 // SMASH_MODE_MAM default: the state-machine kernel (mam_sm.hpp).  Setting
 // SMASH_MAM_KERNEL=direct selects the direct per-lane v3 kernel instead (same
 // results; kept for A/B measurement).
+// 64-lane blocks: the LDS row of a lane is its read (40 words at 150 bp), so
+// 16 blocks (4 waves per SIMD, the VGPR limit) fit the CU's 160 KB.
+constexpr int kSmBlock = 64;
+
 template <class IdxT, bool STATS>
 int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, size_t lds,
            hipStream_t s) {
-  constexpr int B = 128;
+  constexpr int B = kSmBlock;
   // Every probe is checked against the span of the index arrays and the
   // records: a wild address retires its lane and fails the call instead of
   // faulting the GPU.
@@ -154,7 +158,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
               uint64_t stride, const uint16_t *lens, uint32_t len,
               uint64_t n_reads, uint64_t *out, uint32_t cap, uint32_t *n_out,
               hipStream_t s) {
-  constexpr int B = 128;
+  constexpr int B = kSmBlock;
   const sm::Geom g = sm::make_geom(lens ? 255 : len);
   // read records (k_prep)
   const uint64_t need = n_reads * g.chunks * 16;
@@ -185,6 +189,8 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.lin_blocks = 2;
   c.pad = 0;
   c.grab = 16;
+  c.bm_dual = 0;
+  if (const char *e = std::getenv("SMASH_SM_BM_DUAL")) c.bm_dual = uint32_t(std::atoi(e));
   if (const char *e = std::getenv("SMASH_SM_GRAB")) c.grab = uint32_t(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("SMASH_SM_PAD")) c.pad = uint32_t(std::atoi(e));
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
@@ -210,7 +216,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
       c.hi = std::max<uint64_t>(c.hi, spans[k][0] + spans[k][1]);
     }
   }
-  const size_t lds = size_t(B) * g.w_row * 4 + 16;
+  const size_t lds = size_t(B) * g.w_row * 4;
   if (std::getenv("SMASH_SM_STATS")) return run_sm<IdxT, true>(ix, c, n_reads, lds, s);
   return run_sm<IdxT, false>(ix, c, n_reads, lds, s);
 }

@@ -36,18 +36,16 @@ namespace sm {
 // record / LDS row geometry for a launch (reads up to max_len bases)
 struct Geom {
   uint32_t w_raw;    // read bytes + lds_load8 over-read, in words
-  uint32_t w_cod;    // 2-bit code stream words (+2: 3-word extraction)
-  uint32_t w_row;    // LDS row words (odd: conflict-free lane rows)
+  uint32_t w_row;    // LDS row words (= w_raw: lanes read their rows at
+                     // unrelated offsets, so no padding against bank conflicts)
   uint32_t c_bad;    // record chunks holding the bad mask (1 or 2)
   uint32_t chunks;   // 16-byte record chunks per read
 };
 
 inline Geom make_geom(uint32_t max_len) {
   Geom g;
-  g.w_raw = (max_len + 12 + 3) / 4;
-  g.w_cod = (2 * max_len + 31) / 32 + 2;
-  g.w_row = g.w_raw + g.w_cod;
-  if ((g.w_row & 1) == 0) ++g.w_row;
+  g.w_raw = (max_len + 11) / 4;      // lds_load8 at offset <= L-1 reads 3 words
+  g.w_row = g.w_raw;
   g.c_bad = max_len > 128 ? 2 : 1;
   g.chunks = g.c_bad + (g.w_row + 3) / 4;
   return g;
@@ -61,9 +59,10 @@ __device__ __forceinline__ bool is_acgt(uint32_t b) {
 //   [0, 4*c_bad)          bad mask, bit i of word i/32: base i is not ACGT
 //                         or does not occur in the text
 //   [4*c_bad, +w_raw)     the read bytes, zero padded
-//   [.., +w_cod)          2-bit codes (a0 c1 g2 t3, others 0), big-endian:
-//                         base 16j+t at bits 31-2t..30-2t of word j
 //   rest                  zero
+// The 2-bit base codes the B-mer / k-mer lookups need are derived from the
+// bytes where they are used (codes_raw), which keeps the LDS row at the
+// read's bytes (occupancy: 4 waves per SIMD at 150 bp).
 // One block of 64 threads per `per_block` reads: (1) the block copies the
 // reads' bytes into LDS with word loads, (2) each thread builds one read's
 // record in a padded LDS row in one pass over its bytes, (3) the block writes
@@ -104,22 +103,19 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t *__restrict__ seqs, u
     const uint32_t L = lens ? lens[r0 + t] : len0;
     uint32_t *o = out + t * rwp;
     for (uint32_t w = 0; w < rw; ++w) o[w] = 0;
-    uint32_t *ob = o, *orw = o + 4 * g.c_bad, *oc = orw + g.w_raw;
-    uint32_t raw = 0, cod = 0, bw = 0;
+    uint32_t *ob = o, *orw = o + 4 * g.c_bad;
+    uint32_t raw = 0, bw = 0;
     for (uint32_t i = 0; i < L; ++i) {
       const uint32_t b = P[i];
       const uint64_t word = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
       const bool present = (word >> (b & 63)) & 1ull;
       const int cd = acgt_code(uint8_t(b));
       raw |= b << (8 * (i & 3));
-      cod |= uint32_t(cd < 0 ? 0 : cd) << (30 - 2 * (i & 15));
       bw |= uint32_t(!(cd >= 0 && present)) << (i & 31);
       if ((i & 3) == 3) { orw[i >> 2] = raw; raw = 0; }
-      if ((i & 15) == 15) { oc[i >> 4] = cod; cod = 0; }
       if ((i & 31) == 31) { ob[i >> 5] = bw; bw = 0; }
     }
     if (L & 3) orw[L >> 2] = raw;
-    if (L & 15) oc[L >> 4] = cod;
     if (L & 31) ob[L >> 5] = bw;
   }
   __syncthreads();
@@ -209,12 +205,23 @@ struct Bad {   // the read's bad mask (registers; named, never an array)
   }
 };
 
-// 2n code bits of bases [p, p+n) (first base most significant), n <= 32
-__device__ __forceinline__ uint64_t codes_at(const uint32_t *C, uint32_t p, uint32_t n) {
-  const uint32_t b = 2 * p, q = b >> 5, s = b & 31;
-  const uint64_t hi = (uint64_t(C[q]) << 32) | C[q + 1];
-  const uint64_t x = s ? (hi << s) | (uint64_t(C[q + 2]) >> (32 - s)) : hi;
-  return x >> (64 - 2 * n);
+// 2-bit codes (a0 c1 g2 t3) of the 4 lowercase bytes of w, first byte most
+// significant: code = ((b >> 1) ^ (b >> 2)) & 3 for a c g t, and one
+// multiply gathers the four 2-bit fields (no carries: the partial products
+// land on disjoint bits).  Other bytes give garbage (callers check `bad`).
+__device__ __forceinline__ uint32_t byte4_codes(uint32_t w) {
+  return ((((w >> 1) ^ (w >> 2)) & 0x03030303u) * 0x40100401u) >> 24;
+}
+
+// 2n code bits of bases [p, p+n) of the LDS row R (first base most
+// significant), n <= 20; reads only the words holding those bases
+__device__ __forceinline__ uint64_t codes_raw(const uint32_t *R, uint32_t p, uint32_t n) {
+  const uint32_t q = p >> 2, sh = p & 3, nw = (sh + n + 3) >> 2;
+  uint64_t x = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 6; ++k)
+    if (k < nw) x = (x << 8) | byte4_codes(R[q + k]);
+  return (x >> (8 * nw - 2 * (sh + n))) & ((1ull << (2 * n)) - 1);
 }
 
 template <class IdxT>
@@ -232,6 +239,7 @@ struct Ctx {
   uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
   uint32_t pad;           // experiment: dependent ALU ops added per iteration (0 = none)
   uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
+  uint32_t bm_dual;       // (F): load both B-mer words in one iteration
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -282,13 +290,16 @@ __device__ __forceinline__ uint64_t idx_val(const uint4 &v, uint32_t ao) {
 template <class IdxT, int BLOCK, bool CHECK, bool STATS>
 __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   extern __shared__ uint32_t ldsw[];
-  __shared__ uint64_t s_in_text[4];
-  for (uint32_t k = threadIdx.x; k < 4; k += blockDim.x) s_in_text[k] = c.in_text[k];
-  __syncthreads();
+  // (the 256-bit in-text set stays in scalar registers: dynamic LDS is
+  // exactly 16 blocks x 64 rows x 160 B = the CU's 160 KB at 150 bp)
+  const uint64_t it0 = c.in_text[0], it1 = c.in_text[1], it2 = c.in_text[2], it3 = c.in_text[3];
+  auto in_text = [&](uint32_t b) {
+    const uint64_t w = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
+    return ((w >> (b & 63)) & 1ull) != 0;
+  };
   const uint64_t N = c.N;
   uint32_t *row = ldsw + threadIdx.x * c.w_row;
   const uint8_t *P = reinterpret_cast<const uint8_t *>(row);
-  const uint32_t *C = row + c.w_raw;
   const uint32_t lane = threadIdx.x & 63;
 
   uint64_t q_next = 0, q_end = 0;   // this wave's claimed, unassigned reads
@@ -411,10 +422,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_BM: {                                   // (F) first, then last B-mer present?
+        // (bm_dual: both words arrived together, v2 holds the last B-mer's)
         const uint64_t cc = bm2 ? c1 : c0;
-        if (!((((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull)) {
+        const bool p0 = (((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull;
+        const bool p1 = !c.bm_dual || ((((addr2 & 8) ? hi64(v2) : lo64(v2)) >> (c1 & 63)) & 1ull);
+        need2 = false;
+        if (!(p0 && p1)) {
           depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
-        } else if (!bm2) {
+        } else if (!bm2 && !c.bm_dual) {
           bm2 = true;
           addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
         } else {
@@ -676,7 +691,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_DONE;
       } else if (!proceed) {
         int32_t kb = bad.last(prefix, c.min_len);
-        while (kb >= 0 && ((s_in_text[P[kb] >> 6] >> (P[kb] & 63)) & 1ull))
+        while (kb >= 0 && in_text(P[kb]))
           kb = bad.last(prefix, uint32_t(kb) - prefix);
         const uint32_t B = c.B;
         const uint32_t q1 = prefix + c.min_len - B;
@@ -684,10 +699,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
         } else if (B > 0 && B <= c.min_len && bad.bits(prefix, B) == 0 && bad.bits(q1, B) == 0) {
-          c0 = codes_at(C, prefix, B);
-          c1 = codes_at(C, q1, B);
+          c0 = codes_raw(row, prefix, B);
+          c1 = codes_raw(row, q1, B);
           addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
           st = S_BM; bm2 = false;
+          if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6)); need2 = true; }
           a = A_NONE;
         } else {
           proceed = true;                             // no bitmap verdict
@@ -695,7 +711,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       if (a == A_TOP && proceed) {                     // (C) from the root
         if (depth == 0 && prefix + c.K <= L && bad.bits(prefix, c.K) == 0) {
-          addr = reinterpret_cast<uint64_t>(c.KT + 2 * codes_at(C, prefix, c.K));
+          addr = reinterpret_cast<uint64_t>(c.KT + 2 * codes_raw(row, prefix, c.K));
           st = S_KT;
           a = A_NONE;
         } else {

@@ -25,9 +25,12 @@ def emu(tiny_ix):
 @pytest.mark.parametrize("s", ["s100", "s150"])
 @pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("lin", [2, 1])
-def test_state_machine_matches_reference_goldens(emu, s, wide, lin):
+@pytest.mark.parametrize("bm_dual", ["0", "1"])
+def test_state_machine_matches_reference_goldens(emu, s, wide, lin, bm_dual, monkeypatch):
     """lin: L8 blocks scanned per side of a run before bisecting (1 forces
-    the bisection path on every run longer than one block)."""
+    the bisection path on every run longer than one block); bm_dual: the (F)
+    filter loads both B-mer words in one iteration."""
+    monkeypatch.setenv("SMASH_SM_BM_DUAL", bm_dual)
     exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
            for l in read_gz_lines("%s_MAM.txt.gz" % s)]
     got, iters = emu[int(wide)].map(interleaved_reads(s), lin_blocks=lin)

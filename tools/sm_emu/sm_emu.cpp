@@ -72,6 +72,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   c.lin_blocks = lin_blocks;
   c.pad = 0;
   c.grab = 1;
+  c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 0;
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
   c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
