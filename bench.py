@@ -102,8 +102,27 @@ def make_reads(contigs, cfg, n_pairs, seed):
     return S.prepare_reads(reads)
 
 
-def host_index(S, O, dix, T, sp, sz, names):
-    """Download the device index into the oracle's host layout (cpu leg)."""
+def kmer_codes(reads, K):
+    """Distinct 2-bit codes of the all-ACGT K-mers of the reads (host)."""
+    lut = np.full(256, -1, np.int64)
+    for i, ch in enumerate(b"acgt"):
+        lut[ch] = i
+    a = lut[np.asarray(reads, np.uint8)]
+    if a.shape[1] < K:
+        return np.zeros(0, np.uint64)
+    w = np.lib.stride_tricks.sliding_window_view(a, K, axis=1)
+    ok = (w >= 0).all(axis=2)
+    code = np.zeros(w.shape[:2], np.uint64)
+    for k in range(K):
+        code = (code << np.uint64(2)) | np.where(w[:, :, k] >= 0, w[:, :, k], 0).astype(np.uint64)
+    return np.unique(code[ok])
+
+
+def host_index(S, O, dix, T, sp, sz, names, sample_reads=None):
+    """Download the device index into the oracle's host layout (cpu leg).
+    The k-mer table (4^K x 16 B, 69 GB at K = 16) is not copied: a lazily
+    committed zero array gets only the entries of sample_reads' k-mers
+    (what the host emulation of the kernel looks up)."""
     i = dix.info
     N = i.N
     dt = np.uint32 if i.idx_bytes == 4 else np.uint64
@@ -114,7 +133,15 @@ def host_index(S, O, dix, T, sp, sz, names):
     mp = S.download(i.d_map, i.map_bytes)
     oix = O.Index(T, sp, sz, names, SA=SA, ISA=ISA, L8=L8, ovf=ovf)
     U = S.download(i.d_uniq, N + 64)
-    KT = S.download(i.d_kmer, 16 << (2 * i.kmer_k), np.uint64)
+    KT = np.zeros(2 << (2 * i.kmer_k), np.uint64)          # calloc: pages on first touch
+    if sample_reads is not None:
+        import torch
+        codes = kmer_codes(sample_reads, i.kmer_k)
+        if len(codes):
+            kt_dev = S.device_view(i.d_kmer, 16 << (2 * i.kmer_k), torch.int64).view(-1, 2)
+            idx = torch.from_numpy(codes.astype(np.int64)).to(kt_dev.device)
+            got = kt_dev.index_select(0, idx).cpu().numpy().view(np.uint64)
+            KT.reshape(-1, 2)[codes.astype(np.int64)] = got
     BM = S.download(i.d_bitmap, 8 * ((1 << (2 * i.bitmap_b)) // 64 + 1), np.uint64)
     it = np.array([(i.in_text[c >> 6] >> (c & 63)) & 1 for c in range(256)], np.uint8)
     oix.accel(U, KT, i.kmer_k, BM, i.bitmap_b, it)
@@ -352,14 +379,14 @@ def main():
     if rank == 0:
         import oracle as O
         t2 = time.time()
-        oix, mp = host_index(S, O, dix, T, sp, sz, names)
+        ns = min(4000, 2 * P)
+        oix, mp = host_index(S, O, dix, T, sp, sz, names, sample_reads=reads_h[:ns])
         log("host copy of the index for the oracle: %.1fs" % (time.time() - t2))
         # algorithmic bytes per read: 64 B x the 64-byte line transitions of
         # k_mam_sm's own probe sequence, counted by running the kernel's code
         # on the host (tools/sm_emu: the same source, one lane) over this
         # index and a sample of the same reads
         import sm_emu
-        ns = min(4000, 2 * P)
         emu = sm_emu.Emu(oix, copy=False)
         _, emu_it = emu.map(reads_h[:ns])
         lines = sum(v[1] for v in emu.counters.values())

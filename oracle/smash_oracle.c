@@ -1054,8 +1054,8 @@ uint64_t orc_map_only(const orc_index *ix, const uint8_t *reads, uint32_t L,
 /* ======================================================================== */
 
 uint32_t orc_accel_k(uint64_t N) {
-  uint32_t K = 4;
-  while (K < 14 && (1ull << (2 * (K + 2))) <= N) ++K;
+  uint32_t K = 4;                       /* aux_build.hip: floor(log4 N), <= 16 */
+  while (K < 16 && (1ull << (2 * (K + 1))) <= N) ++K;
   return K;
 }
 

@@ -110,9 +110,10 @@ void build_aux_t(smash_index *ix, hipStream_t s) {
   SMASH_HIPX(hipMemsetAsync(ix->d_uniq + N, 0, 64, s));
   k_uniq<IdxT><<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
       static_cast<const IdxT *>(ix->d_isa), ix->d_lcp8, N, ix->d_uniq);
-  // k: about log4(N) - 2 characters (a few tens of suffixes per k-mer), <= 14
+  // k: floor(log4 N) characters, <= 16 (about one suffix per k-mer: a root
+  // descent lands on a singleton or a short run; hg19: 4^16 x 16 B = 69 GB)
   int K = 4;
-  while (K < 14 && (1ull << (2 * (K + 2))) <= N) ++K;
+  while (K < 16 && (1ull << (2 * (K + 1))) <= N) ++K;
   ix->kmer_k = uint32_t(K);
   const uint64_t nk = 1ull << (2 * K);
   if (!ix->d_kmer) ix->d_kmer = dalloc<uint64_t>(2 * nk);

@@ -421,17 +421,24 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         }
         break;
       }
-      case S_BM: {                                   // (F) first, then last B-mer present?
-        // (bm_dual: both words arrived together, v2 holds the last B-mer's)
-        const uint64_t cc = bm2 ? c1 : c0;
-        const bool p0 = (((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull;
-        const bool p1 = !c.bm_dual || ((((addr2 & 8) ? hi64(v2) : lo64(v2)) >> (c1 & 63)) & 1ull);
+      case S_BM: {                                   // (F) last, then first B-mer present?
+        // The last B-mer [q1, q1+B) (q1 = prefix+min_len-B) is probed first:
+        // absent, it lies inside every window starting in [prefix, q1], so
+        // all of them are skipped at once; an absent first B-mer rules out
+        // this window only.  (bm_dual: v2 holds the first B-mer's word.)
+        const uint64_t cc = bm2 ? c0 : c1;
+        const bool pa = (((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull;
+        const bool pb = !c.bm_dual || ((((addr2 & 8) ? hi64(v2) : lo64(v2)) >> (c0 & 63)) & 1ull);
         need2 = false;
-        if (!(p0 && p1)) {
+        if (!pa && !bm2) {
+          depth = 0; start = 0; end = N - 1; have_pos = false;
+          prefix += c.min_len - c.B + 1;
+          a = A_TOP;
+        } else if (!pa || !pb) {
           depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
         } else if (!bm2 && !c.bm_dual) {
           bm2 = true;
-          addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
+          addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
         } else {
           skip_f = true;                              // window passed: go on at (C)
           a = A_TOP;
@@ -701,9 +708,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (B > 0 && B <= c.min_len && bad.bits(prefix, B) == 0 && bad.bits(q1, B) == 0) {
           c0 = codes_raw(row, prefix, B);
           c1 = codes_raw(row, q1, B);
-          addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
+          addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
           st = S_BM; bm2 = false;
-          if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6)); need2 = true; }
+          if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6)); need2 = true; }
           a = A_NONE;
         } else {
           proceed = true;                             // no bitmap verdict

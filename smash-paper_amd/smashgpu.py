@@ -486,6 +486,23 @@ def unpack_matches(words, n):
 _HIP = None
 
 
+class _DeviceArray:
+    """__cuda_array_interface__ view of raw device memory (torch.as_tensor)."""
+
+    def __init__(self, ptr, n, typestr):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr,
+                                         "data": (int(ptr), False), "version": 3,
+                                         "strides": None}
+
+
+def device_view(dptr, nbytes, torch_dtype):
+    """A torch tensor aliasing nbytes of device memory at dptr (no copy)."""
+    import torch
+    size = torch.tensor([], dtype=torch_dtype).element_size()
+    ts = {1: "|u1", 4: "<i4", 8: "<i8"}[size]
+    return torch.as_tensor(_DeviceArray(dptr, nbytes // size, ts), device="cuda")
+
+
 def download(dptr, nbytes, dtype=np.uint8):
     """Device -> host copy of raw device memory (tests / index export)."""
     global _HIP
