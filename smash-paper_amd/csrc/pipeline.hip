@@ -12,6 +12,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.hpp"
@@ -53,6 +54,9 @@ struct smash_pipeline {
   int64_t *d_pos0 = nullptr, *d_abs = nullptr;
   int64_t *d_prev = nullptr;      // [2] carried {last pos0 or -1, -}
   unsigned long long *d_stats = nullptr;
+  uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast -> k_post pair list
+  bool post_fast = false;
+  uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
   unsigned long long *d_owner = nullptr;  // per-owner counters (<= 64 ranks)
   uint64_t n_pairs = 0, n_export = 0;
@@ -76,6 +80,7 @@ struct PostCfg {
   uint64_t map_bytes;
   int32_t min_excess;
   int64_t window;
+  uint32_t fast_cap;   // k_post_fast: mates with more matches go to k_post
 };
 
 struct Aln {
@@ -201,16 +206,14 @@ __device__ inline uint64_t mix64(uint64_t z) {
   return z;
 }
 
-__global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restrict__ match,
-                                             const uint32_t *__restrict__ nmatch,
-                                             uint64_t n_pairs, int32_t *nk_out,
-                                             uint32_t *nmajor_out, uint64_t *hits_out,
-                                             uint64_t *hash_out,
-                                             unsigned long long *stats) {
-  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  int32_t err = 0;
-  unsigned long long nm = 0;
-  if (q < n_pairs) {
+// the general per-pair body (any number of matches, per-thread arrays);
+// k_post_fast hands it the pairs whose mates exceed its register capacity
+__device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restrict__ match,
+                                       const uint32_t *__restrict__ nmatch, uint64_t q,
+                                       int32_t *nk_out, uint32_t *nmajor_out,
+                                       uint64_t *hits_out, uint64_t *hash_out, int32_t &err,
+                                       unsigned long long &nm) {
+  {
     Hit h1[MAXA], h2[MAXA];
     const uint32_t n1 = nmatch[2 * q], n2 = nmatch[2 * q + 1];
     nm = n1 + n2;
@@ -258,16 +261,20 @@ __global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restri
     hash_out[2 * q] = hh;
     hash_out[2 * q + 1] = hl;
   }
-  // block-aggregated stats
+}
+
+// block-aggregated stats of the pairs this thread handled
+__device__ __forceinline__ void post_stats(unsigned long long nm, unsigned long long np,
+                                           int32_t err, unsigned long long *stats) {
   __shared__ unsigned long long s_nm, s_pairs;
   __shared__ int s_err;
   if (threadIdx.x == 0) { s_nm = 0; s_pairs = 0; s_err = 0; }
   __syncthreads();
-  if (q < n_pairs) {
+  if (np) {
     atomicAdd(&s_nm, nm);
-    atomicAdd(&s_pairs, 1ull);
-    if (err) atomicCAS(&s_err, 0, err);
+    atomicAdd(&s_pairs, np);
   }
+  if (err) atomicCAS(&s_err, 0, err);
   __syncthreads();
   if (threadIdx.x == 0) {
     if (s_pairs) {
@@ -276,6 +283,205 @@ __global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restri
     }
     if (s_err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)s_err);
   }
+}
+
+// general path: every pair (list == nullptr), or the pairs listed by
+// k_post_fast (grid-stride over *n_list)
+__global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restrict__ match,
+                                             const uint32_t *__restrict__ nmatch,
+                                             uint64_t n_pairs, const uint32_t *list,
+                                             const uint32_t *n_list, int32_t *nk_out,
+                                             uint32_t *nmajor_out, uint64_t *hits_out,
+                                             uint64_t *hash_out, unsigned long long *stats) {
+  int32_t err = 0;
+  unsigned long long nm = 0, np = 0;
+  if (!list) {
+    const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (q < n_pairs) {
+      post_pair(c, match, nmatch, q, nk_out, nmajor_out, hits_out, hash_out, err, nm);
+      np = 1;
+    }
+  } else {
+    const uint32_t n = *n_list;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += gridDim.x * blockDim.x) {
+      unsigned long long m = 0;
+      post_pair(c, match, nmatch, list[i], nk_out, nmajor_out, hits_out, hash_out, err, m);
+      nm += m;
+      ++np;
+    }
+  }
+  post_stats(nm, np, err, stats);
+}
+
+// ---------------------------------------------------------------------------
+// k_post_fast: the same per-pair chain with every per-mate list in
+// registers.  A mate's alignments and hits are single u64 words whose
+// unsigned order is the order the reference sorts them in, so the two sorts
+// of Aligner::prepare_matches (to_merge, query.cpp:286; to_print, :301) are
+// fixed compare-exchange networks over FCAP words (invalid words are ~0 and
+// sort last).  Mates with more than FCAP matches go to k_post.
+//   alignment: rc:1 | tid:15 | pos:32 | prefix:8 | len:8   (to_merge order)
+//   hit:       qmin:8 | rc:1 | pass:1 | - | tid:16 | pos:32 (to_print order)
+// Valid when the contig table fits in LDS (n_seq <= kSeqLds), every contig
+// is shorter than 2^31 and there are fewer than 2^15 contigs (host check).
+// ---------------------------------------------------------------------------
+constexpr int FCAP = 16;
+constexpr uint32_t kSeqLds = 1024;
+
+__device__ __forceinline__ void cx(uint64_t &a, uint64_t &b) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = lo;
+  b = hi;
+}
+
+// Batcher odd-even merge sort, N a power of two (fully unrolled)
+template <int N>
+__device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+      for (int j = k % p; j <= N - 1 - k; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i < k; ++i)
+          if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p))
+            cx(v[i + j], v[i + j + k]);
+}
+
+__device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *sp, const uint64_t *m,
+                                          uint32_t n, uint64_t (&H)[FCAP], int32_t &err) {
+  const uint32_t L = c.L;
+  uint64_t A[FCAP];
+  uint64_t w[FCAP];
+#pragma unroll
+  for (int k = 0; k < FCAP; ++k) w[k] = uint32_t(k) < n ? m[k] : 0;
+#pragma unroll
+  for (int k = 0; k < FCAP; ++k) {
+    const uint64_t ref = w[k] & 0xFFFFFFFFFFFFull;
+    const uint32_t q = uint32_t((w[k] >> 48) & 0xFF), len = uint32_t(w[k] >> 56);
+    uint32_t lo = 0, hi = c.n_seq;          // upper_bound(startpos, ref), LDS copy
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sp[mid] <= ref) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t si = lo ? lo - 1 : 0;
+    int64_t pos = int64_t(ref - q - sp[si]);
+    const uint32_t extra = L - len - q;
+    const uint32_t rc = si & 1;
+    if (rc) pos = int64_t(c.sizes[si - 1] - uint64_t(pos)) - int64_t(L);
+    const uint64_t prefix = rc ? extra : q;
+    const bool ok = uint32_t(k) < n && lo != 0 && pos >= 0;   // erase pos < 0
+    A[k] = ok ? (uint64_t(rc) << 63) | (uint64_t(si >> 1) << 48) | (uint64_t(pos) << 16) |
+                    (prefix << 8) | len
+              : ~0ull;
+  }
+  sort_net(A);
+  // merge runs on one diagonal (rc, tid, pos) into hits; tag every block
+  uint32_t g_prefix = 0, g_qmin = 0;
+  int32_t g_l0 = 0, g_r0 = 0;
+#pragma unroll
+  for (int i = 0; i < FCAP; ++i) {
+    const uint64_t a = A[i];
+    const bool valid = a != ~0ull;
+    const uint32_t rc = uint32_t(a >> 63), tid = valid ? uint32_t(a >> 48) & 0x7FFF : 0u;
+    const uint32_t pos = uint32_t(a >> 16), prefix = uint32_t(a >> 8) & 0xFF, len = uint32_t(a) & 0xFF;
+    const uint32_t qpos = rc ? L - len - prefix : prefix;
+    const bool start = i == 0 || (A[i - 1] >> 16) != (a >> 16);
+    const bool endg = i + 1 == FCAP || (A[i + 1 < FCAP ? i + 1 : i] >> 16) != (a >> 16);
+    const uint32_t abspos = c.tag_off[tid] + pos + 1;
+    const uint32_t li = abspos + prefix + len - 1, ri = abspos + prefix - 1;
+    const unsigned lm = valid ? mapb(c, 2 + uint64_t(li) * 2) : 0u;
+    const unsigned rm = valid ? mapb(c, 2 + uint64_t(ri) * 2 + 1) : 0u;
+    const int32_t left = lm ? int32_t(lm) - 1 : 255, right = rm ? int32_t(rm) : 255;
+    if (start) {
+      g_prefix = prefix; g_qmin = qpos; g_l0 = left; g_r0 = right;
+    } else {
+      g_qmin = qpos < g_qmin ? qpos : g_qmin;
+    }
+    if (valid && err == 0 && !c.small[tid]) {
+      if (uint32_t(left) > len) err = SMASH_ERR_TAG_LEFT;
+      else if (uint32_t(right) > len) err = SMASH_ERR_TAG_RIGHT;
+    }
+    const int32_t mx = g_l0 > g_r0 ? g_l0 : g_r0;
+    const uint32_t pass = int32_t(prefix + len) - int32_t(g_prefix) - mx >= c.min_excess;
+    H[i] = valid && endg ? (uint64_t(g_qmin) << 56) | (uint64_t(rc) << 55) |
+                               (uint64_t(pass) << 54) | (uint64_t(tid) << 32) | pos
+                         : ~0ull;
+  }
+  sort_net(H);
+}
+
+__device__ __forceinline__ bool hit_kept(uint64_t h) { return h != ~0ull && ((h >> 54) & 1); }
+
+__global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__restrict__ match,
+                                                  const uint32_t *__restrict__ nmatch,
+                                                  uint64_t n_pairs, uint32_t *fb_list,
+                                                  uint32_t *fb_n, int32_t *nk_out,
+                                                  uint32_t *nmajor_out, uint64_t *hits_out,
+                                                  uint64_t *hash_out,
+                                                  unsigned long long *stats) {
+  __shared__ uint64_t sp[kSeqLds];
+  for (uint32_t i = threadIdx.x; i < c.n_seq; i += blockDim.x) sp[i] = c.startpos[i];
+  __syncthreads();
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  int32_t err = 0;
+  unsigned long long nm = 0, np = 0;
+  if (q < n_pairs) {
+    const uint32_t n1 = nmatch[2 * q], n2 = nmatch[2 * q + 1];
+    if (n1 > c.fast_cap || n2 > c.fast_cap) {
+      fb_list[atomicAdd(fb_n, 1u)] = uint32_t(q);   // general path
+    } else {
+      nm = n1 + n2;
+      np = 1;
+      uint64_t H1[FCAP], H2[FCAP];
+      mate_fast(c, sp, match + (2 * q) * c.slots, n1, H1, err);
+      mate_fast(c, sp, match + (2 * q + 1) * c.slots, n2, H2, err);
+      uint64_t *ho = hits_out + q * (2 * uint64_t(c.slots));
+      int32_t nk = -1;
+      uint32_t nmaj = 0;
+      uint64_t hh = 0x9E3779B97F4A7C15ull, hl = 0xD1B54A32D192ED03ull;
+      bool any = false;
+#pragma unroll
+      for (int i = 0; i < FCAP; ++i) any = any || hit_kept(H1[i]) || hit_kept(H2[i]);
+      if (any) {                              // smashMEM.py:162
+        nk = 0;
+        auto put = [&](uint64_t h) {
+          const uint32_t tid = uint32_t(h >> 32) & 0xFFFF;
+          const int64_t pos = int64_t(uint32_t(h));
+          ho[nk++] = (uint64_t(tid) << 48) | uint64_t(pos);
+          const uint64_t x = (uint64_t(tid) << 48) ^ uint64_t(pos);
+          hh = mix64(hh ^ x) + 0x632BE59BD9B4E019ull;
+          hl = mix64(hl + x * 0x9E3779B97F4A7C15ull) ^ (hl >> 29);
+          if (c.chrom_off[tid] >= 0) ++nmaj;
+        };
+#pragma unroll
+        for (int i = 0; i < FCAP; ++i)
+          if (hit_kept(H1[i])) put(H1[i]);
+#pragma unroll
+        for (int b = 0; b < FCAP; ++b) {      // hit window (smashMEM.py:193-200)
+          if (!hit_kept(H2[b])) continue;
+          bool close = false;
+#pragma unroll
+          for (int i = 0; i < FCAP; ++i) {
+            int64_t d = int64_t(uint32_t(H1[i])) - int64_t(uint32_t(H2[b]));
+            d = d < 0 ? -d : d;
+            close |= hit_kept(H1[i]) && ((H1[i] >> 32) & 0xFFFF) == ((H2[b] >> 32) & 0xFFFF) &&
+                     d < c.window;
+          }
+          if (!close) put(H2[b]);
+        }
+        hh = mix64(hh ^ uint64_t(nk)) | 1;
+        hl = mix64(hl + uint64_t(nk)) | 1;
+      }
+      nk_out[q] = nk;
+      nmajor_out[q] = nmaj;
+      hash_out[2 * q] = hh;
+      hash_out[2 * q + 1] = hl;
+    }
+  }
+  post_stats(nm, np, err, stats);
 }
 
 __global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n,
@@ -454,6 +660,7 @@ PostCfg post_cfg(const smash_pipeline *p) {
   c.map_bytes = p->ix->map_bytes;
   c.min_excess = p->min_excess;
   c.window = p->hit_window;
+  c.fast_cap = p->post_cap;
   return c;
 }
 
@@ -538,6 +745,17 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_stats = dalloc<unsigned long long>(S_N);
     SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * S_N));
     p->d_send_q = dalloc<uint32_t>(P);
+    p->d_fb = dalloc<uint32_t>(P + 1);
+    {
+      bool ok = ix->n_seq <= kSeqLds && p->n_contig < 0x7FFF;
+      for (uint64_t z : ix->sizes) ok = ok && z < (1ull << 31);
+      const char *e = getenv("SMASH_POST_LEGACY");
+      p->post_fast = ok && !(e && *e && *e != '0');
+      // SMASH_POST_CAP < 16 routes more pairs to the general kernel (tests)
+      const char *pc = getenv("SMASH_POST_CAP");
+      const uint32_t cap = pc && *pc ? uint32_t(atoi(pc)) : uint32_t(FCAP);
+      p->post_cap = std::min<uint32_t>({cap, uint32_t(FCAP), p->slots});
+    }
     p->d_owner = dalloc<unsigned long long>(2 * 64);
     SMASH_HIPX(hipMemset(p->d_posoff, 0, 4));
   } catch (hip_failure &f) {
@@ -561,7 +779,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
-                  (void *)p->d_send_q, (void *)p->d_owner})
+                  (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb})
     dfree(q);
   delete p;
 }
@@ -595,9 +813,20 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
     ++p->n_ev;
     p->prof_reads += 2 * n_pairs;
   }
-  k_post<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
-      post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_nk, p->d_nmajor,
-      p->d_hits, p->d_hash, p->d_stats);
+  if (p->post_fast) {
+    SMASH_HIP(hipMemsetAsync(p->d_fb, 0, 4, s));
+    k_post_fast<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
+        post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_fb + 1, p->d_fb, p->d_nk,
+        p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+    SMASH_HIP(hipGetLastError());
+    k_post<<<256, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_fb + 1,
+                              p->d_fb, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash,
+                              p->d_stats);
+  } else {
+    k_post<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
+        post_cfg(p), p->d_match, p->d_nmatch, n_pairs, nullptr, nullptr, p->d_nk,
+        p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+  }
   SMASH_HIP(hipGetLastError());
   // in-batch ordering for de-dup: stable radix sort of key hi, value = pair
   k_dedup_keys<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_nk, p->d_hash, n_pairs,

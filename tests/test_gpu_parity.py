@@ -264,3 +264,28 @@ def test_mid_genome_pipeline_equals_oracle(mid, tmp_path):
     assert counts.tolist() == op.counts.tolist()
     assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
     assert st.dupe_pairs == op.n_dupe.value
+
+
+@pytest.mark.parametrize("env", [{"SMASH_POST_LEGACY": "1"}, {"SMASH_POST_CAP": "1"},
+                                 {"SMASH_POST_CAP": "3"}])
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_post_paths_agree(gix, s, env, monkeypatch):
+    """k_post_fast (register lists), its k_post hand-off for mates above the
+    capacity, and the general k_post alone give the same per-pair output."""
+    reads = interleaved_reads(s)
+    n = reads.shape[0] // 2
+
+    def run():
+        pipe, starts = make_pipe(gix, reads.shape[1], n)
+        counts, st = run_pipeline(pipe, reads, len(starts))
+        nk, keep, hits = pipe.peek(n)
+        return counts.tolist(), st.as_dict(), nk.copy(), keep.copy(), \
+            [hits[q, :max(nk[q], 0)].tolist() for q in range(n)]
+
+    a = run()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    b = run()
+    assert a[0] == b[0] and a[1] == b[1]
+    assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+    assert a[4] == b[4]
