@@ -174,7 +174,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   {
     const uint32_t per = sm::prep_per_block(g, stride);
     const size_t plds = sm::prep_lds_bytes(g, stride, per);
-    sm::k_prep<<<unsigned((n_reads + per - 1) / per), 64, plds, s>>>(
+    sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
         seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
         ix->in_text[3], g, per, ix->d_rec);
     SMASH_HIP(hipGetLastError());

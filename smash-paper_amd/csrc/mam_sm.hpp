@@ -51,9 +51,6 @@ inline Geom make_geom(uint32_t max_len) {
   return g;
 }
 
-__device__ __forceinline__ bool is_acgt(uint32_t b) {
-  return b == 'a' || b == 'c' || b == 'g' || b == 't';
-}
 
 // Record of read r (g.chunks * 4 words), built by k_prep:
 //   [0, 4*c_bad)          bad mask, bit i of word i/32: base i is not ACGT
@@ -63,26 +60,32 @@ __device__ __forceinline__ bool is_acgt(uint32_t b) {
 // The 2-bit base codes the B-mer / k-mer lookups need are derived from the
 // bytes where they are used (codes_raw), which keeps the LDS row at the
 // read's bytes (occupancy: 4 waves per SIMD at 150 bp).
-// One block of 64 threads per `per_block` reads: (1) the block copies the
-// reads' bytes into LDS with word loads, (2) each thread builds one read's
-// record in a padded LDS row in one pass over its bytes, (3) the block writes
-// the records out with contiguous word stores.  All loops stride by
-// blockDim.x (the host emulation runs one thread).
+// One block of 256 threads per `per_block` reads: (1) the block copies the
+// reads' bytes into LDS with word loads and zeroes the records' LDS image,
+// (2) one thread per (read, 32-base group) builds that group's bad-mask word
+// and its 8 raw words from 9 LDS words (no per-thread byte loop over the
+// whole read), (3) the block writes the records out with contiguous word
+// stores.  All loops stride by blockDim.x (the host emulation runs one
+// thread).
 inline uint32_t prep_per_block(const Geom &g, uint64_t stride) {
-  const uint64_t per = 48 * 1024 / (stride + 4 * (g.chunks * 4 + 1) + 8);
+  const uint64_t per = 24 * 1024 / (stride + 4 * (g.chunks * 4) + 8);
   return uint32_t(per < 1 ? 1 : per > 64 ? 64 : per);
 }
+__host__ __device__ inline uint32_t prep_in_words(uint64_t stride, uint32_t per) {
+  return uint32_t((per * stride + 8 + 3) / 4 + 10);   // + the 9-word over-read of (2)
+}
 inline size_t prep_lds_bytes(const Geom &g, uint64_t stride, uint32_t per) {
-  return size_t(((per * stride + 8 + 3) / 4 + 1) * 4) + size_t(per) * (g.chunks * 4 + 1) * 4;
+  return size_t(prep_in_words(stride, per)) * 4 + size_t(per) * (g.chunks * 4) * 4;
 }
 
-__global__ __launch_bounds__(64) void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
-                                             const uint16_t *__restrict__ lens, uint32_t len0,
-                                             uint64_t n, uint64_t it0, uint64_t it1, uint64_t it2,
-                                             uint64_t it3, Geom g, uint32_t per,
-                                             uint32_t *__restrict__ rec) {
+__global__ __launch_bounds__(256) void k_prep(const uint8_t *__restrict__ seqs, uint64_t stride,
+                                              const uint16_t *__restrict__ lens, uint32_t len0,
+                                              uint64_t n, uint64_t it0, uint64_t it1, uint64_t it2,
+                                              uint64_t it3, Geom g, uint32_t per,
+                                              uint32_t *__restrict__ rec) {
   extern __shared__ uint32_t prep_lds[];
-  const uint32_t rw = g.chunks * 4, rwp = rw + 1;      // record words, padded LDS row
+  const uint32_t rw = g.chunks * 4;                    // record words
+  const uint32_t G = 4 * g.c_bad;                      // 32-base groups (bad-mask words)
   const uint64_t r0 = uint64_t(blockIdx.x) * per;
   if (r0 >= n) return;
   const uint32_t nr = uint32_t(n - r0 < per ? n - r0 : per);
@@ -92,39 +95,48 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t *__restrict__ seqs, u
   const uint64_t w0 = a0 & ~uint64_t(3);
   const uint32_t nw = uint32_t(((a1 + 3) & ~uint64_t(3)) - w0) / 4;
   uint32_t *in = prep_lds;
-  uint32_t *out = prep_lds + ((per * stride + 8 + 3) / 4 + 1);
+  uint32_t *out = prep_lds + prep_in_words(stride, per);
   for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x)
     in[k] = reinterpret_cast<const uint32_t *>(w0)[k];
+  for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) out[k] = 0;
   __syncthreads();
-  const uint8_t *inb = reinterpret_cast<const uint8_t *>(in) + (a0 - w0);
-  // (2) one record per thread
-  for (uint32_t t = threadIdx.x; t < nr; t += blockDim.x) {
-    const uint8_t *P = inb + uint64_t(t) * stride;
+  // a/c/g/t occur in the text (anything else is always bad)
+  auto itx = [&](uint32_t b) {
+    const uint64_t w = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
+    return uint32_t((w >> (b & 63)) & 1ull);
+  };
+  const uint32_t ia = itx('a'), ic = itx('c'), ig = itx('g'), iu = itx('t');
+  // (2) one (read, group) per thread
+  for (uint32_t item = threadIdx.x; item < nr * G; item += blockDim.x) {
+    const uint32_t t = item / G, gi = item - t * G;
     const uint32_t L = lens ? lens[r0 + t] : len0;
-    uint32_t *o = out + t * rwp;
-    for (uint32_t w = 0; w < rw; ++w) o[w] = 0;
-    uint32_t *ob = o, *orw = o + 4 * g.c_bad;
-    uint32_t raw = 0, bw = 0;
-    for (uint32_t i = 0; i < L; ++i) {
-      const uint32_t b = P[i];
-      const uint64_t word = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
-      const bool present = (word >> (b & 63)) & 1ull;
-      const int cd = acgt_code(uint8_t(b));
-      raw |= b << (8 * (i & 3));
-      bw |= uint32_t(!(cd >= 0 && present)) << (i & 31);
-      if ((i & 3) == 3) { orw[i >> 2] = raw; raw = 0; }
-      if ((i & 31) == 31) { ob[i >> 5] = bw; bw = 0; }
+    if (32 * gi >= L) continue;
+    const uint32_t boff = uint32_t(a0 - w0) + uint32_t(t * stride) + 32 * gi;
+    const uint32_t wq = boff >> 2, sh = (boff & 3) * 8;
+    uint32_t *o = out + t * rw;
+    uint32_t bw = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      uint32_t w = in[wq + k];
+      if (sh) w = (w >> sh) | (in[wq + k + 1] << (32 - sh));
+      const uint32_t i0 = 32 * gi + 4 * k;             // base index of byte 0
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t b = (w >> (8 * j)) & 0xFF;
+        const bool live = i0 + j < L;
+        if (!live) w &= ~(0xFFu << (8 * j));
+        const uint32_t good = (b == 'a' ? ia : 0u) | (b == 'c' ? ic : 0u) |
+                              (b == 'g' ? ig : 0u) | (b == 't' ? iu : 0u);
+        bw |= uint32_t(live && !good) << (4 * k + j);
+      }
+      if (8 * gi + k < g.w_raw) o[4 * g.c_bad + 8 * gi + k] = w;
     }
-    if (L & 3) orw[L >> 2] = raw;
-    if (L & 31) ob[L >> 5] = bw;
+    o[gi] = bw;
   }
   __syncthreads();
   // (3) contiguous stores of the block's records
   uint32_t *dst = rec + r0 * rw;
-  for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) {
-    const uint32_t t = k / rw, w = k - t * rw;
-    dst[k] = out[t * rwp + w];
-  }
+  for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) dst[k] = out[k];
 }
 
 // lane states: S_COPY and above own a pending 16-byte probe at `addr`
