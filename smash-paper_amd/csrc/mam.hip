@@ -135,12 +135,12 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
                  q(0.5), q(0.9), q(0.99), q(0.999), srt.back(), ws[0],
                  double(ws[1]) / double(ws[0] ? ws[0] : 1));
     static const char *names[] = {"EXIT", "NEW", "ALU", "COPY", "BM", "KT", "IDX", "BYTE", "CMP",
-                                  "USCAN", "EXL", "EXR"};
+                                  "USCAN", "EXL", "EXR", "EXB"};
     static const char *idx_ops[] = {"SAPOS", "SAPOS2", "SCAN_SA", "ISAJ", "NS_SA2", "NS_ISA2",
                                     "TD_SA2", "TD_SA"};
     static const char *byte_ops[] = {"TD_T2", "TD_T", "LM"};
     std::fprintf(stderr, "[k_mam_sm] lane-iterations per read by state:");
-    for (int k = 0; k < 12; ++k)
+    for (int k = 0; k < 13; ++k)
       if (ws[2 + k]) std::fprintf(stderr, " %s %.1f", names[k], double(ws[2 + k]) / n_reads);
     for (int k = 0; k < 8; ++k)
       if (ws[18 + k]) std::fprintf(stderr, " IDX.%s %.1f", idx_ops[k], double(ws[18 + k]) / n_reads);

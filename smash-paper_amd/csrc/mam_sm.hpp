@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void k_prep(const uint8_t *__restrict__ seqs, 
 
 // lane states: S_COPY and above own a pending 16-byte probe at `addr`
 enum : uint32_t { S_EXIT = 0, S_NEW, S_ALU, S_COPY, S_BM, S_KT, S_IDX, S_BYTE, S_CMP, S_USCAN,
-                  S_EXL, S_EXR };
+                  S_EXL, S_EXR, S_EXB };
 // S_IDX ops (an SA / ISA element arrived; *2: a second one in v2)
 enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
 // S_CMP ops (16-32 text bytes compared with the read)
@@ -330,9 +330,31 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint64_t &c0 = bpos, &c1 = sp;                                // (F) bitmap codes
   uint32_t lL = 0, lR = 0, best = 0, lc = 0, cbase = 0, cap = 0, bsm = 0, nblk = 0;
   bool hit = false, bm2 = false, skip_f = false, xrun = false;
+  bool rdone = false;     // a run's right side was finished by S_EXB
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
+  // (B) from a singleton at (pos, d): scan U[pos+1 ...] for the chain's exit,
+  // 32 bytes per iteration
+  auto uscan_start = [&](uint64_t p, uint32_t d) {
+    dch = d; j = 1;
+    addr = reinterpret_cast<uint64_t>(c.U + p + 1);
+    addr2 = (addr & ~uint64_t(15)) + 16;
+    need2 = d - 1 > 16 - (uint32_t(addr) & 15);
+    st = S_USCAN;
+  };
+  // a run [es, ee] grows within [lb, hb] while L8 >= xd: both sides' first
+  // blocks in one iteration (S_EXB), or the one side with room; false: none
+  auto ex_start = [&](uint64_t lb, uint64_t hb) {
+    const bool l = es > lb, r = ee < hb;
+    nblk = 0;
+    rdone = !r;
+    addr = reinterpret_cast<uint64_t>(c.L8 + (l ? es : ee + 1));
+    addr2 = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
+    need2 = l && r;
+    st = l && r ? S_EXB : l ? S_EXL : S_EXR;
+    return l || r;
+  };
 
   for (;;) {
     // Work claiming: lanes that need a read take it from the wave's private
@@ -494,9 +516,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
           ++nem;
         }
-        dch = depth; j = 1;
-        addr = reinterpret_cast<uint64_t>(c.U + pos + 1);
-        st = S_USCAN;
+        uscan_start(pos, depth);
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
@@ -539,39 +559,68 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_USCAN: {                                // (B) first j with U[pos+j] >= d-j
-        const uint32_t D = dch - j;
-        const uint32_t lim = D < 16 - ao ? D : 16 - ao;
-        const uint32_t inr = ((1u << lim) - 1) << ao;
-        const uint32_t hm = byte_mask(v, [&](uint32_t b, uint32_t i) { return b + i >= D + ao; }) & inr;
-        if (hm) {
-          j += uint32_t(__builtin_ctz(hm)) - ao; hit = true;
+        // bytes [ao, 16) of v, then (need2) the whole next block v2
+        bool fin = false;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+          if (fin || (h == 1 && !need2)) break;
+          const uint4 &u = h ? v2 : v;
+          const uint32_t o = h ? 0u : ao;
+          const uint32_t D = dch - j;
+          const uint32_t lim = D < 16 - o ? D : 16 - o;
+          const uint32_t inr = ((1u << lim) - 1) << o;
+          const uint32_t hm = byte_mask(u, [&](uint32_t b, uint32_t i) { return b + i >= D + o; }) & inr;
+          if (hm) {
+            j += uint32_t(__builtin_ctz(hm)) - o; hit = true; fin = true;
+          } else {
+            j += lim;
+            if (j >= dch) { hit = false; fin = true; }
+          }
+        }
+        if (fin) {
+          need2 = false;
           a = A_CHAIN_DONE;
         } else {
-          j += lim;
-          if (j < dch) addr += lim;
-          else { hit = false; a = A_CHAIN_DONE; }
+          addr = (addr & ~uint64_t(15)) + (need2 ? 32 : 16);
+          addr2 = addr + 16;
+          need2 = dch - j > 16;
         }
         break;
       }
       case S_EXL:                                    // L8 runs: expand_link (xrun = 0)
-      case S_EXR: {                                  // or the traverse's final run (1)
-        const bool left = st == S_EXL;
+      case S_EXR:                                    // or the traverse's final run (1);
+      case S_EXB: {                                  // S_EXB: both sides in one iteration
         const uint64_t lb = xrun ? start : 0, hb = xrun ? end : N - 1;
-        const uint64_t roomL = es - lb, roomR = hb - ee;
-        const uint32_t lim = left ? (roomL < uint64_t(ao + 1) ? uint32_t(roomL) : ao + 1)
-                                  : (roomR < uint64_t(16 - ao) ? uint32_t(roomR) : 16 - ao);
-        const uint32_t below = byte_mask(v, [&](uint32_t b, uint32_t) { return b < xd; });
-        const uint32_t win = left ? (((1u << lim) - 1) << (ao + 1 - lim)) : (((1u << lim) - 1) << ao);
-        const uint32_t sm = below & win;
-        // run members before the stop, walking down (left) or up (right)
-        const uint32_t k = sm ? (left ? ao - (31 - __builtin_clz(sm)) : uint32_t(__builtin_ctz(sm)) - ao)
-                              : lim;
-        const bool more = !sm && (left ? es - k > lb : ee + k < hb);
-        if (left) es -= k; else ee += k;
+        // run members before the stop in one block, walking down (left:
+        // bytes (o-lim, o]) or up (right: bytes [o, o+lim)); *more: no stop
+        // in the window and room beyond it
+        auto side = [&](const uint4 &u, uint32_t o, bool left, bool &more) {
+          const uint64_t room = left ? es - lb : hb - ee;
+          const uint32_t w = left ? o + 1 : 16 - o;
+          const uint32_t lim = room < uint64_t(w) ? uint32_t(room) : w;
+          const uint32_t below = byte_mask(u, [&](uint32_t b, uint32_t) { return b < xd; });
+          const uint32_t win = left ? (((1u << lim) - 1) << (o + 1 - lim)) : (((1u << lim) - 1) << o);
+          const uint32_t sm = below & win;
+          const uint32_t k = sm ? (left ? o - (31 - __builtin_clz(sm)) : uint32_t(__builtin_ctz(sm)) - o)
+                                : lim;
+          more = !sm && uint64_t(k) < room;
+          return k;
+        };
+        bool moreL = false, moreR = false;
+        if (st != S_EXR) es -= side(v, ao, true, moreL);
+        if (st != S_EXL) {
+          const bool b2 = st == S_EXB;
+          ee += side(b2 ? v2 : v, b2 ? (uint32_t(addr2) & 15) : ao, false, moreR);
+          if (b2) rdone = !moreR;
+        }
+        need2 = false;
+        const bool left = st != S_EXR;                // the side that continues here
+        const bool more = left ? moreL : moreR;
         if (!more) {
           a = left ? A_XL_DONE : A_RUN_DONE;
         } else if (++nblk < c.lin_blocks) {
           addr = reinterpret_cast<uint64_t>(c.L8 + (left ? es : ee + 1));
+          st = left ? S_EXL : S_EXR;
         } else {                                      // long run: bisect for its end
           bsm = left ? BS_LEFT : BS_RIGHT;
           if (left) { lo = lb; hi = es; lL = 0; lR = cap; }
@@ -615,14 +664,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       } else {                                        // the run of suffixes sharing best more
         xd = depth + best; xrun = true;
         cbase = depth; cap = best;
-        es = bi; ee = bi; nblk = 0;
-        if (es > start) {
-          addr = reinterpret_cast<uint64_t>(c.L8 + es);
-          st = S_EXL;
-          a = A_NONE;
-        } else {
-          a = A_XL_DONE;
-        }
+        es = bi; ee = bi;
+        a = ex_start(start, end) ? A_NONE : A_RUN_DONE;
       }
     }
     if (a == A_XL_DONE) {                             // left end known: right side
@@ -631,7 +674,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       if (!xrun && start - es >= thresh) {            // expand_link gives up (longSA.h:164)
         depth = 0; start = 0; end = N - 1; have_pos = false;
         a = A_TOP;
-      } else if (ee < hb) {
+      } else if (ee < hb && !rdone) {
         addr = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
         st = S_EXR;
         a = A_NONE;
@@ -669,10 +712,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       thresh = 2u * depth * c.logN;
       xd = depth; xrun = false;
       cbase = 0; cap = depth;
-      es = start; ee = end; nblk = 0;
-      addr = reinterpret_cast<uint64_t>(c.L8 + es);
-      st = S_EXL;
-      a = A_NONE;
+      es = start; ee = end;
+      a = ex_start(0, N - 1) ? A_NONE : A_RUN_DONE;
     }
     if (a == A_AFTER) {
       if (depth <= 1) {
@@ -695,9 +736,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
             ++nem;
           }
-          dch = depth; j = 1;
-          addr = reinterpret_cast<uint64_t>(c.U + pos + 1);
-          st = S_USCAN;
+          uscan_start(pos, depth);
         }
       }
     }

@@ -30,6 +30,7 @@ struct uint4 { uint32_t x, y, z, w; };
 inline uint4 make_uint4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return uint4{a, b, c, d}; }
 
 inline void __syncthreads() {}
+inline void __builtin_amdgcn_wave_barrier() {}
 inline uint64_t __ballot(int p) { return p ? 1ull : 0ull; }
 template <class T> inline T __shfl(T v, int, int = 64) { return v; }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }

@@ -15,6 +15,7 @@
 static const uint64_t *emu_spans;
 static uint64_t emu_rec_lo, emu_rec_hi, emu_bad;
 static uint64_t emu_probes[8], emu_lines[8], emu_last[8];
+static unsigned long long emu_ws[64];   // the kernel's STATS counters of the last run
 static uint4 emu_load16(uint64_t a) {
   int arr = -1;
   if (a >= emu_rec_lo && a < emu_rec_hi) arr = 7;
@@ -95,7 +96,14 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   for (int k = 0; k < 10; ++k) viol[k] = v[k];
   viol[0] += emu_bad;
   for (int k = 0; k < 8; ++k) { counters[k] = emu_probes[k]; counters[8 + k] = emu_lines[k]; }
+  for (int k = 0; k < 64; ++k) emu_ws[k] = ws[k];
   return 0;
+}
+
+// lane iterations of the last sm_emu_map by state (k_mam_sm STATS layout:
+// [2 + state], IDX ops at [18 + op], CMP ops at [42 + op])
+extern "C" void sm_emu_ws(uint64_t *out) {
+  for (int k = 0; k < 64; ++k) out[k] = emu_ws[k];
 }
 
 extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int idx_bytes,

@@ -51,6 +51,10 @@ def in_text_words(in_text):
 
 
 ARRAYS = ("text", "sa", "isa", "lcp", "uniq", "kmer", "bitmap", "records")
+# k_mam_sm lane states and ops (mam_sm.hpp enums), for the STATS counters
+STATES = ("EXIT", "NEW", "ALU", "COPY", "BM", "KT", "IDX", "BYTE", "CMP", "USCAN", "EXL", "EXR", "EXB")
+IDX_OPS = ("SAPOS", "SAPOS2", "BS_SA", "ISAJ", "NS_SA2", "NS_ISA2")
+CMP_OPS = ("EXT", "BS")
 
 
 class Emu:
@@ -116,4 +120,16 @@ class Emu:
             w = out[i * cap:i * cap + k]
             res.append([(int(x & 0xFFFFFFFFFFFF), int((x >> 48) & 0xFF), int(x >> 56)) for x in w])
         self.counters = {name: (int(ctr[k]), int(ctr[8 + k])) for k, name in enumerate(ARRAYS)}
+        ws = np.zeros(64, np.uint64)
+        lib().sm_emu_ws(ws.ctypes.data_as(C.c_void_p))
+        self.states = {}
+        for k, nm in enumerate(STATES):
+            if ws[2 + k]:
+                self.states[nm] = int(ws[2 + k])
+        for k, nm in enumerate(IDX_OPS):
+            if ws[18 + k]:
+                self.states["IDX." + nm] = int(ws[18 + k])
+        for k, nm in enumerate(CMP_OPS):
+            if ws[42 + k]:
+                self.states["CMP." + nm] = int(ws[42 + k])
         return res, iters
