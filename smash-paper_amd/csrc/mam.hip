@@ -186,13 +186,14 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(ix->d_rec);
   c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
-  c.lin_blocks = 2;
+  c.lin_blocks = 8;
   c.pad = 0;
   c.grab = 16;
-  c.bm_dual = 1;
+  c.bm_dual = 2;
   if (const char *e = std::getenv("SMASH_SM_BM_DUAL")) c.bm_dual = uint32_t(std::atoi(e));
   if (const char *e = std::getenv("SMASH_SM_GRAB")) c.grab = uint32_t(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("SMASH_SM_PAD")) c.pad = uint32_t(std::atoi(e));
+  if (const char *e = std::getenv("SMASH_SM_LIN")) c.lin_blocks = uint32_t(std::max(1, std::atoi(e)));
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
   c.out = out; c.n_out = n_out;
   c.work = reinterpret_cast<unsigned long long *>(ix->d_work);

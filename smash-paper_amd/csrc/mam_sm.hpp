@@ -26,6 +26,12 @@
 
 // the 16-byte probe (the host emulation, tools/sm_emu, substitutes a checked
 // load here)
+#ifndef SM_HOOK_BM
+#define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes
+#endif
+#ifndef SM_HOOK_BS
+#define SM_HOOK_BS(size, depth)   // host emulation: interval statistics
+#endif
 #ifndef SM_LOAD16
 #define SM_LOAD16(a) (*reinterpret_cast<const uint4 *>((a) & ~uint64_t(15)))
 #endif
@@ -251,7 +257,8 @@ struct Ctx {
   uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
   uint32_t pad;           // experiment: dependent ALU ops added per iteration (0 = none)
   uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
-  uint32_t bm_dual;       // (F): load both B-mer words in one iteration
+  uint32_t bm_dual;       // (F): 0 one B-mer word per iteration, 1 last + first in one,
+                          // 2 the cover policy (two words per iteration chosen by mode)
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -331,6 +338,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint32_t lL = 0, lR = 0, best = 0, lc = 0, cbase = 0, cap = 0, bsm = 0, nblk = 0;
   bool hit = false, bm2 = false, skip_f = false, xrun = false;
   bool rdone = false;     // a run's right side was finished by S_EXB
+  uint32_t fm = 0;        // (F) probe mode (bm_dual 2)
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
@@ -450,7 +458,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {
           need2 = false;
           prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
-          skip_f = false;
+          skip_f = false; fm = 0;
           a = A_TOP;
         }
         break;
@@ -464,7 +472,37 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         const bool pa = (((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull;
         const bool pb = !c.bm_dual || ((((addr2 & 8) ? hi64(v2) : lo64(v2)) >> (c0 & 63)) & 1ull);
         need2 = false;
-        if (!pa && !bm2) {
+        if (c.bm_dual == 2) {
+          // cover policy (bm_dual 2): the pair probed depends on the mode fm
+          // (A_TOP); an absent B-mer at s rules out the windows [s-D, s]
+          // (D = min_len - B), so the window advances past every window an
+          // absent probe covers.  Modes: 0 {L(p), F(p)}, 1 {L(p), L(p+D+1)},
+          // 2 {F(p), F(p+1)} with L(p) known present.
+          const uint32_t D = c.min_len - c.B;
+          SM_HOOK_BM(fm, pa, pb);
+          uint32_t adv = 0, nfm = 0;
+          bool pass = false;
+          if (fm == 0) {
+            if (!pa) { adv = D + 1; nfm = 1; }
+            else if (!pb) adv = 1;
+            else pass = true;
+          } else if (fm == 1) {
+            if (!pa && !pb) { adv = 2 * D + 2; nfm = 1; }
+            else if (!pa) { adv = D + 1; nfm = 2; }   // L of the new window = the 2nd probe
+            else nfm = 2;                               // L(p) present: same window
+          } else {
+            if (!pb) adv = 2;
+            else if (!pa) adv = 1;
+            else pass = true;
+          }
+          if (pass) {
+            skip_f = true; fm = 1;                      // window passed: go on at (C)
+          } else {
+            fm = nfm;
+            if (adv) { depth = 0; start = 0; end = N - 1; have_pos = false; prefix += adv; }
+          }
+          a = A_TOP;
+        } else if (!pa && !bm2) {
           depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix += c.min_len - c.B + 1;
           a = A_TOP;
@@ -752,19 +790,32 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         while (kb >= 0 && in_text(P[kb]))
           kb = bad.last(prefix, uint32_t(kb) - prefix);
         const uint32_t B = c.B;
-        const uint32_t q1 = prefix + c.min_len - B;
+        const uint32_t D = c.min_len - B;
+        // probes: c1 <- B-mer at s1 (v), c0 <- B-mer at s2 (v2); mode 0 is
+        // {last, first} of this window, 1 and 2 (bm_dual 2) see S_BM
+        uint32_t s1 = prefix + D, s2 = prefix;
+        auto okb = [&](uint32_t x) { return x + B <= L && bad.bits(x, B) == 0; };
+        if (c.bm_dual == 2 && fm == 1 && okb(prefix + 2 * D + 1)) {
+          s2 = prefix + 2 * D + 1;
+        } else if (c.bm_dual == 2 && fm == 2 && okb(prefix) && okb(prefix + 1)) {
+          s1 = prefix; s2 = prefix + 1;
+        } else {
+          fm = 0;
+        }
         if (kb >= 0) {                                // absent byte: next window
           depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
-        } else if (B > 0 && B <= c.min_len && bad.bits(prefix, B) == 0 && bad.bits(q1, B) == 0) {
-          c0 = codes_raw(row, prefix, B);
-          c1 = codes_raw(row, q1, B);
+          fm = 0;
+        } else if (B > 0 && B <= c.min_len && okb(s1) && okb(s2)) {
+          c0 = codes_raw(row, s2, B);
+          c1 = codes_raw(row, s1, B);
           addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
           st = S_BM; bm2 = false;
           if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6)); need2 = true; }
           a = A_NONE;
         } else {
           proceed = true;                             // no bitmap verdict
+          fm = 1;
         }
       }
       if (a == A_TOP && proceed) {                     // (C) from the root
@@ -793,6 +844,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             st = S_CMP; op = O_EXT; lc = 0;
           }
         } else {                                     // search [start, end] for P'
+          SM_HOOK_BS(end - start + 1, depth);
           lo = start; hi = end + 1; lL = 0; lR = 0; best = 0;
           bsm = BS_INSERT; cbase = depth; cap = L - prefix - depth;
           m = (lo + hi) >> 1;

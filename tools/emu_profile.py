@@ -68,6 +68,19 @@ def main():
     print("  probes/read %.1f: " % sum(pr.values()) + " ".join("%s %.2f" % kv for kv in pr.items()))
     print("  lines/read  %.1f: " % sum(ln.values()) + " ".join("%s %.2f" % kv for kv in ln.items()))
     print("  matches/read %.2f" % (sum(len(g) for g in got) / n))
+    import ctypes as C
+    hs, hd = np.zeros(65, np.uint64), np.zeros(256, np.uint64)
+    sm_emu.lib().sm_emu_bs_hist(hs.ctypes.data_as(C.c_void_p), hd.ctypes.data_as(C.c_void_p), 1)
+    tot = max(1, int(hs.sum()))
+    print("  binary searches/read %.2f; by interval size: " % (tot / n)
+          + " ".join("%d:%.1f%%" % (k, 100.0 * hs[k] / tot) for k in range(1, 65) if hs[k] * 200 >= tot))
+    bm = hd[244:256].copy()
+    hd[244:256] = 0
+    print("  by start depth: " + " ".join("%d:%.1f%%" % (k, 100.0 * hd[k] / tot)
+                                          for k in range(244) if hd[k] * 50 >= tot))
+    if bm.sum():
+        print("  (F) cover policy per read, mode:probe1 probe2 present: " + " ".join(
+            "%d:%d%d %.2f" % (k // 4, (k >> 1) & 1, k & 1, bm[k] / n) for k in range(12) if bm[k]))
     if not a.no_check:
         bad = 0
         for i in range(n):

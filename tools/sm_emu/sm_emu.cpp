@@ -37,6 +37,11 @@ static uint4 emu_load16(uint64_t a) {
   return r;
 }
 #define SM_LOAD16(a) emu_load16(a)
+// traverse binary searches by interval size (1..63, 64 = larger) and start depth
+static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
+#define SM_HOOK_BM(mode, a1, a2) (++emu_bm[4 * (mode) + 2 * (a1) + (a2)])
+#define SM_HOOK_BS(size, depth) \
+  do { ++emu_bs_size[(size) < 64 ? (size) : 64]; ++emu_bs_depth[(depth) < 255 ? (depth) : 255]; } while (0)
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
 
 thread_local dim3 threadIdx, blockIdx, blockDim;
@@ -73,7 +78,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   c.lin_blocks = lin_blocks;
   c.pad = 0;
   c.grab = 1;
-  c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 0;
+  c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 2;   // = the device default (mam.hip)
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
   c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
@@ -104,6 +109,13 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
 // [2 + state], IDX ops at [18 + op], CMP ops at [42 + op])
 extern "C" void sm_emu_ws(uint64_t *out) {
   for (int k = 0; k < 64; ++k) out[k] = emu_ws[k];
+}
+
+// binary-search start histograms since the last reset (size[65], depth[256])
+extern "C" void sm_emu_bs_hist(uint64_t *size, uint64_t *depth, int reset) {
+  for (int k = 0; k < 65; ++k) { size[k] = emu_bs_size[k]; if (reset) emu_bs_size[k] = 0; }
+  for (int k = 0; k < 256; ++k) { depth[k] = emu_bs_depth[k]; if (reset) emu_bs_depth[k] = 0; }
+  for (int k = 0; k < 12; ++k) { depth[244 + k] = emu_bm[k]; if (reset) emu_bm[k] = 0; }
 }
 
 extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int idx_bytes,

@@ -89,7 +89,7 @@ class Emu:
         self.it = in_text_words(list(ix.acc.in_text))
         self.isz = np.dtype(it).itemsize
 
-    def map(self, reads, min_len=20, cap=512, lin_blocks=2):
+    def map(self, reads, min_len=20, cap=512, lin_blocks=8):   # = the device default (mam.hip)
         """reads: uint8 [n, L].  Returns (list of [(ref, q, len)], iterations);
         self.counters: {array: (16-byte probes, 64-byte line transitions)}."""
         reads = np.ascontiguousarray(reads, np.uint8)
