@@ -17,6 +17,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsmashgpu.so")
+# A/B measurement of library builds (tools/ab.sh): SMASH_LIB names another build
+LIB_PATH = os.environ.get("SMASH_LIB", LIB_PATH)
 
 u64p = C.POINTER(C.c_uint64)
 u32p = C.POINTER(C.c_uint32)
