@@ -26,6 +26,9 @@
 
 // the 16-byte probe (the host emulation, tools/sm_emu, substitutes a checked
 // load here)
+#ifndef PAD_KEEP
+#define PAD_KEEP(x) asm volatile("" : "+v"(x))
+#endif
 #ifndef SM_HOOK_BM
 #define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes
 #endif
@@ -194,6 +197,18 @@ __device__ __forceinline__ uint32_t byte_mask(const uint4 &v, F f) {
   return m;
 }
 
+// one bit of a lane's flag word, used like a bool
+struct FlagRef {
+  uint32_t &f;
+  uint32_t b;
+  __device__ __forceinline__ operator bool() const { return (f >> b) & 1u; }
+  __device__ __forceinline__ FlagRef &operator=(bool x) {
+    f = (f & ~(1u << b)) | (uint32_t(x) << b);
+    return *this;
+  }
+  __device__ __forceinline__ FlagRef &operator=(const FlagRef &o) { return *this = bool(o); }
+};
+
 struct Bad {   // the read's bad mask (registers; named, never an array)
   uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
   __device__ __forceinline__ uint32_t word(uint32_t i) const {
@@ -324,21 +339,26 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint64_t q_next = 0, q_end = 0;   // this wave's claimed, unassigned reads
   uint32_t st = S_NEW, op = 0, pend = A_NONE;
   uint64_t addr = 0, addr2 = 0;
-  bool need2 = false;
+  // per-lane flags live as bits of ONE vector register: as `bool`s the
+  // compiler keeps them as lane masks in SGPR pairs, which spill
+  uint32_t fl = 0;
+  FlagRef need2{fl, 0};
   uint64_t rd = 0;
   uint32_t L = 0, nem = 0, kc = 0;
   Bad bad{0, 0, 0, 0, 0, 0, 0, 0};
   // search state (longSA.h interval_t + prefix)
   uint32_t prefix = 0, depth = 0;
   uint64_t start = 0, end = 0, pos = 0;
-  bool have_pos = false;
+  FlagRef have_pos{fl, 1};
   // phase registers, shared by phases that are never live together
   uint64_t lo = 0, hi = 0, bpos = 0, sp = 0, m = 0, bi = 0, es = 0, ee = 0;
   uint64_t &c0 = bpos, &c1 = sp;                                // (F) bitmap codes
   uint32_t lL = 0, lR = 0, best = 0, lc = 0, cbase = 0, cap = 0, bsm = 0, nblk = 0;
-  bool hit = false, bm2 = false, skip_f = false, xrun = false;
-  bool rdone = false;     // a run's right side was finished by S_EXB
+  FlagRef hit{fl, 2}, bm2{fl, 3}, skip_f{fl, 4}, xrun{fl, 5};
+  FlagRef rdone{fl, 6};   // a run's right side was finished by S_EXB
   uint32_t fm = 0;        // (F) probe mode (bm_dual 2)
+  FlagRef ktr_set{fl, 7};   // a passed window's k-mer code is in m
+  FlagRef clean{fl, 8};     // the read has no bad base (bad mask all zero)
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
@@ -458,7 +478,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {
           need2 = false;
           prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
-          skip_f = false; fm = 0;
+          skip_f = false; fm = 0; ktr_set = false;
+          clean = (bad.w0 | bad.w1 | bad.w2 | bad.w3 | bad.w4 | bad.w5 | bad.w6 | bad.w7) == 0;
           a = A_TOP;
         }
         break;
@@ -479,6 +500,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           // absent probe covers.  Modes: 0 {L(p), F(p)}, 1 {L(p), L(p+D+1)},
           // 2 {F(p), F(p+1)} with L(p) known present.
           const uint32_t D = c.min_len - c.B;
+          const uint32_t fm0 = fm;
           SM_HOOK_BM(fm, pa, pb);
           uint32_t adv = 0, nfm = 0;
           bool pass = false;
@@ -497,6 +519,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           }
           if (pass) {
             skip_f = true; fm = 1;                      // window passed: go on at (C)
+            m = (fm0 == 0 ? c0 : c1) >> (2 * (c.B - c.K));   // F(p) -> the k-mer code
+            ktr_set = true;
           } else {
             fm = nfm;
             if (adv) { depth = 0; start = 0; end = N - 1; have_pos = false; prefix += adv; }
@@ -672,9 +696,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
 
     if (c.pad) {                                    // issue-bound experiment (SMASH_SM_PAD)
+      // c.pad dependent v_add per lane; the empty asm keeps every one of them
+      // (an earlier form let the compiler sink the chain under a rare branch)
       uint32_t x = uint32_t(addr);
-      for (uint32_t k = 0; k < c.pad; ++k) x = x * 2654435761u + k;
-      if (x == 0x9E3779B9u && st == S_EXIT) c.viol[0] = x;
+      for (uint32_t k = 0; k < c.pad; ++k) {
+        x += k;
+        PAD_KEEP(x);
+      }
     }
 
     // ---------------- decide ----------------
@@ -782,23 +810,35 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       // (F) runs while the state is shallow, once per prefix (skip_f: this
       // prefix's window already passed the bitmap)
       bool proceed = skip_f || depth >= c.min_len;
-      skip_f = false;
+      const bool ktr = skip_f && ktr_set;             // k-mer code of this window in m
+      skip_f = false; ktr_set = false;
       if (prefix >= L || (!proceed && prefix + c.min_len > L)) {
         a = A_DONE;
       } else if (!proceed) {
-        int32_t kb = bad.last(prefix, c.min_len);
-        while (kb >= 0 && in_text(P[kb]))
-          kb = bad.last(prefix, uint32_t(kb) - prefix);
+        // bad-mask work only for reads holding a bad base (clean: none)
+        int32_t kb = -1;
         const uint32_t B = c.B;
         const uint32_t D = c.min_len - B;
+        const uint32_t sM = prefix + 2 * D + 1;     // mode 1's second B-mer
+        bool okP = true, okQ = true;                // [p, p+B), [p+D, p+D+B): inside the read
+        bool okP1 = prefix + 1 + B <= L, okM = sM + B <= L;
+        if (!clean) {
+          kb = bad.last(prefix, c.min_len);
+          while (kb >= 0 && in_text(P[kb]))
+            kb = bad.last(prefix, uint32_t(kb) - prefix);
+          okP = bad.bits(prefix, B) == 0;
+          okQ = bad.bits(prefix + D, B) == 0;
+          okP1 = okP1 && bad.bits(prefix + 1, B) == 0;
+          okM = okM && bad.bits(sM, B) == 0;
+        }
         // probes: c1 <- B-mer at s1 (v), c0 <- B-mer at s2 (v2); mode 0 is
         // {last, first} of this window, 1 and 2 (bm_dual 2) see S_BM
         uint32_t s1 = prefix + D, s2 = prefix;
-        auto okb = [&](uint32_t x) { return x + B <= L && bad.bits(x, B) == 0; };
-        if (c.bm_dual == 2 && fm == 1 && okb(prefix + 2 * D + 1)) {
-          s2 = prefix + 2 * D + 1;
-        } else if (c.bm_dual == 2 && fm == 2 && okb(prefix) && okb(prefix + 1)) {
-          s1 = prefix; s2 = prefix + 1;
+        bool ok = okQ && okP;
+        if (c.bm_dual == 2 && fm == 1 && okQ && okM) {
+          s2 = sM; ok = true;
+        } else if (c.bm_dual == 2 && fm == 2 && okP && okP1) {
+          s1 = prefix; s2 = prefix + 1; ok = true;
         } else {
           fm = 0;
         }
@@ -806,9 +846,19 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
           fm = 0;
-        } else if (B > 0 && B <= c.min_len && okb(s1) && okb(s2)) {
-          c0 = codes_raw(row, s2, B);
-          c1 = codes_raw(row, s1, B);
+        } else if (B > 0 && B <= c.min_len && ok) {
+          // both codes from one pass over the row when the span allows
+          const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;
+          const uint32_t span = hi_s + B - lo_s;
+          if (span <= 21) {
+            const uint64_t X = codes_raw(row, lo_s, span);
+            const uint64_t mk = (1ull << (2 * B)) - 1;
+            c1 = (X >> (2 * (lo_s + span - s1 - B))) & mk;
+            c0 = (X >> (2 * (lo_s + span - s2 - B))) & mk;
+          } else {
+            c0 = codes_raw(row, s2, B);
+            c1 = codes_raw(row, s1, B);
+          }
           addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
           st = S_BM; bm2 = false;
           if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6)); need2 = true; }
@@ -819,8 +869,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         }
       }
       if (a == A_TOP && proceed) {                     // (C) from the root
-        if (depth == 0 && prefix + c.K <= L && bad.bits(prefix, c.K) == 0) {
-          addr = reinterpret_cast<uint64_t>(c.KT + 2 * codes_raw(row, prefix, c.K));
+        if (depth == 0 && prefix + c.K <= L && (clean || bad.bits(prefix, c.K) == 0)) {
+          // the window's first B-mer code (c.B >= c.K) from the filter pass
+          const uint64_t kc = ktr ? m : codes_raw(row, prefix, c.K);
+          addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
           st = S_KT;
           a = A_NONE;
         } else {

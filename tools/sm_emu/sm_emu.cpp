@@ -37,6 +37,7 @@ static uint4 emu_load16(uint64_t a) {
   return r;
 }
 #define SM_LOAD16(a) emu_load16(a)
+#define PAD_KEEP(x) ((void)(x))
 // traverse binary searches by interval size (1..63, 64 = larger) and start depth
 static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
 #define SM_HOOK_BM(mode, a1, a2) (++emu_bm[4 * (mode) + 2 * (a1) + (a2)])
