@@ -436,6 +436,30 @@ def main():
                 % (cpu["value"], threads, exact))
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
+    # host-buffer boundary: the same batch copied H2D from pinned memory
+    # (not part of `value`, whose inputs are resident in HBM)
+    try:
+        hb = torch.from_numpy(reads_h).pin_memory()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        d_reads.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(3):
+            d_reads.copy_(hb, non_blocking=True)
+        e1.record()
+        torch.cuda.synchronize()
+        h2d_ms = e0.elapsed_time(e1) / 3
+        step_ms = 1000.0 * el / args.steps
+        out["host_boundary"] = {
+            "h2d_ms_per_step": round(h2d_ms, 3),
+            "h2d_GBps": round(reads_h.nbytes / h2d_ms / 1e6, 1),
+            "reads_per_s_h2d_serial": round(2 * P * world / ((step_ms + h2d_ms) / 1e3), 1),
+            "reads_per_s_h2d_overlapped": round(2 * P * world / (max(step_ms, h2d_ms) / 1e3), 1),
+            "note": "pinned host batch -> HBM per step; serial = copy then step, "
+                    "overlapped = copy of the next batch on another stream (estimate)"}
+        del hb
+    except Exception as ex:   # measurement extra only
+        out["host_boundary"] = {"error": str(ex)}
     out["deterministic_counts"] = same
     out["stats_last_step"] = st.as_dict()
     if rank == 0:
