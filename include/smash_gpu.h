@@ -280,6 +280,47 @@ int smash_bin_positions(const int64_t *d_pos0, const int64_t *d_abspos,
 int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_keep,
                         uint64_t *h_hits, uint64_t *h_hash);
 
+/* ========================================================================== */
+/* mapout SAM writer: replaces Aligner::prepare_matches + print_matches       */
+/* (query.cpp:231-415, `mummer -rcref -samin -samout [-nomap]`) and, with     */
+/* tag = 1, appends mappability_tag's L<i>/R<i> columns (mappability_tag.cpp: */
+/* 93-124) to the same lines.                                                 */
+/* smash_sam_records: one record per match slot of smash_map_batch's output   */
+/* (Alignment::resolve, query.cpp:68-97; XE of the match's diagonal,          */
+/* :270-274; map.bin L/R of its '=' block when d_tag_offsets, the u32         */
+/* sam_header offsets per forward contig, is given).  Asynchronous.           */
+/* smash_sam_format: host formatting of 2 mates per pair (read 1, read 2 as   */
+/* Pair::run alternates them, query.cpp:486-505) from the records copied to   */
+/* the host (pure host code: contigs[] = forward contig names).  names carry the ":0"/":1" mate suffix QueryReader adds          */
+/* (query.cpp:641-642); seqs are the original bases, quals the QUAL column    */
+/* (NULL: '!' per base), optionals the extra columns, each prefixed by a tab  */
+/* (query.cpp:153-156).  *out_text is malloc'ed (smash_sam_free) and holds    */
+/* the SAM lines without the header; *tag_error gets the first                */
+/* SMASH_ERR_TAG_* that mappability_tag would throw (0 = none).               */
+/* ========================================================================== */
+typedef struct {
+  int64_t pos;             /* 0-based on the forward contig (< 0: erased)   */
+  uint32_t tid;            /* forward contig index                          */
+  uint32_t xe;             /* XE (n_matched_bases) of the diagonal          */
+  uint16_t prefix, len, suffix, qpos;
+  uint8_t rc, pad;
+  uint16_t spare;
+  int32_t left, right;     /* mappability_tag L/R of this '=' block         */
+  uint32_t reserved;       /* 40-byte record                                */
+} smash_sam_rec;
+int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
+                      uint32_t len, uint64_t n_reads, const uint64_t *d_match,
+                      uint32_t cap_per_read, const uint32_t *d_n_match,
+                      const uint32_t *d_tag_offsets, smash_sam_rec *d_out, void *stream);
+int smash_sam_format(const char *const *contigs, uint32_t n_contig,
+                     const smash_sam_rec *h_rec,
+                     const uint32_t *h_n, uint32_t cap_per_read, uint64_t n_reads,
+                     const char *const *names, const char *const *seqs,
+                     const char *const *quals, const char *const *optionals,
+                     int nomap, int tag, const uint8_t *h_small_chr,
+                     char **out_text, uint64_t *out_len, int32_t *tag_error);
+void smash_sam_free(char *text);
+
 #ifdef __cplusplus
 }
 #endif

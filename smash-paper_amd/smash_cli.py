@@ -13,6 +13,10 @@ subcommand below takes the same inputs and writes the same files:
   count ID "R1.gz.." "R2.gz.." BINDIR
                                 map + varbin fused on the device, no positions
                                 file: ID.varbin.txt and ID.stats.txt
+  memsam [-nomap] [--tag] QUERY.sam
+                                `mummer -rcref -samin -samout [-nomap]`: the
+                                mapout SAM file; --tag adds mappability_tag's
+                                L/R columns (the next smash_mapping.sh stage)
   search [-mum|-maxmatch] [-l N] REF.fa QUERY
                                 mummer's match triples for FASTA/FASTQ/SAM queries
                                 (one line per read: name, then ref,query,len)
@@ -310,6 +314,61 @@ def cmd_search(args):
                 "\t%d,%d,%d" % m for m in ms) + "\n")
 
 
+def sam_records_in(path):
+    """QueryReader::run with -samin (query.cpp:638-646): per record the name with
+    the ':0'/':1' mate suffix by flag, SEQ, QUAL and the optional columns, each
+    prefixed by a tab."""
+    for line in _open(path):
+        if line.startswith(b"@"):
+            continue
+        f = line.rstrip(b"\r\n").split(b"\t")
+        if len(f) < 11:
+            continue
+        flag = int(f[1])
+        name = f[0] + (b":0" if flag & 64 else b":1" if flag & 128 else b"")
+        yield name, f[9], f[10], b"".join(b"\t" + x for x in f[11:])
+
+
+def cmd_memsam(args):
+    """`mummer -rcref -samin -samout [-nomap] ref.fa query.sam` (mummer.cpp:77-96):
+    mapout SAM text (header fasta.cpp:243-252, lines query.cpp:331-415); with
+    --tag the mappability_tag L/R columns are appended (mappability_tag.cpp:
+    93-124) and a tag error exits 1 as the reference throws."""
+    import torch
+    ref = _ref(args)
+    ix = load_index(ref, args.device)
+    dev = torch.device("cuda", args.device)
+    sizes = ix.contig_sizes
+    offsets = np.cumsum([0] + sizes[:-1]).astype(np.uint32) if args.tag else None
+    small = np.array([1 if ("_gl000" in c or "chrM" in c) else 0 for c in ix.contigs], np.uint8)
+    out_path = args.out or os.path.join("mapout", "mapout.1.txt")
+    os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
+    with open(out_path, "wb") as out:
+        out.write(b"@HD\tVN:1.0\tSO:unsorted\n")
+        for name, size in zip(ix.contigs, sizes):
+            out.write(b"@SQ\tSN:%s\tLN:%d\n" % (name.encode(), size))
+        out.write(b"@PG\tID:longMEM\tPN:longMEM\tVN:0.5\n")
+        recs = sam_records_in(args.query)
+        while True:
+            batch = [r for _, r in zip(range(2 * args.batch), recs)]
+            if not batch:
+                break
+            L = len(batch[0][1])
+            if any(len(r[1]) != L for r in batch) or L == 0 or L > 255:
+                raise SystemExit("all reads must have one length in 1..255 (device batches)")
+            # NewQuery::extend lowercases only (replaceN is fastqs_to_sam's, upstream)
+            reads = S._LOWER[np.frombuffer(b"".join(r[1] for r in batch),
+                                           np.uint8).reshape(-1, L)]
+            d = torch.from_numpy(np.ascontiguousarray(reads)).to(dev)
+            text, terr = S.sam_lines(ix, d, L, [r[0] for r in batch], [r[1] for r in batch],
+                                     [r[2] for r in batch], [r[3] for r in batch],
+                                     nomap=args.nomap, tag_offsets=offsets, small_chr=small,
+                                     min_len=args.l)
+            out.write(text)
+            if terr:
+                raise SystemExit(S.ERRORS.get(terr, terr))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="smash_cli", description=__doc__.split("\n\n")[0])
     ap.add_argument("--ref", default=None, help="reference FASTA (default $SMASH_REF)")
@@ -334,6 +393,14 @@ def main(argv=None):
     for a in ("positions", "bins", "out", "stats", "chrom_sizes"):
         p.add_argument(a)
     p.set_defaults(fn=cmd_varbin)
+    p = sub.add_parser("memsam")
+    p.add_argument("-nomap", action="store_true", help="print unmapped reads (query.cpp:308)")
+    p.add_argument("-l", type=int, default=20, help="minimum match length (query.h:129)")
+    p.add_argument("--tag", action="store_true", help="append mappability_tag L/R columns")
+    p.add_argument("--out", default=None, help="default mapout/mapout.1.txt")
+    p.add_argument("--batch", type=int, default=1_000_000, help="pairs per device batch")
+    p.add_argument("query", help="unmapped SAM (fastqs_to_sam output)")
+    p.set_defaults(fn=cmd_memsam)
     p = sub.add_parser("search")
     p.add_argument("-mum", action="store_true")
     p.add_argument("-maxmatch", action="store_true")

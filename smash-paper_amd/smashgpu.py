@@ -47,6 +47,7 @@ EXPORTS = [
     "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_peek",
     "smash_pipeline_profile", "smash_pipeline_profile_read",
     "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
+    "smash_sam_records", "smash_sam_format", "smash_sam_free",
 ]
 
 
@@ -132,6 +133,14 @@ def lib():
                                       vp]
     L.smash_mappability_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, i64p, vp,
                                          C.c_uint32, vp, vp, vp]
+    L.smash_sam_records.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, vp, C.c_uint32,
+                                    vp, vp, vp, vp]
+    L.smash_sam_format.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, vp, u32p, C.c_uint32, C.c_uint64,
+                                   C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                   C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                   u8p, C.POINTER(C.c_void_p), u64p, i32p]
+    L.smash_sam_free.argtypes = [C.c_void_p]
+    L.smash_sam_free.restype = None
     _LIB = L
     return L
 
@@ -518,3 +527,74 @@ def download(dptr, nbytes, dtype=np.uint8):
     if rc != 0:
         raise SmashError("hipMemcpy D2H failed (%d)" % rc)
     return out.view(dtype)
+
+
+SAM_REC = np.dtype([("pos", "<i8"), ("tid", "<u4"), ("xe", "<u4"), ("prefix", "<u2"),
+                    ("len", "<u2"), ("suffix", "<u2"), ("qpos", "<u2"), ("rc", "u1"),
+                    ("pad", "u1"), ("spare", "<u2"), ("left", "<i4"), ("right", "<i4"),
+                    ("reserved", "<u4")])
+
+
+def _cstrs(xs):
+    if xs is None:
+        return None
+    return (C.c_char_p * len(xs))(*[None if x is None else bytes(x) for x in xs])
+
+
+def sam_format(contigs, h_rec, h_n, cap, names, seqs, quals=None, optionals=None, nomap=True,
+               tag=False, small_chr=None):
+    """Host half of the mapout writer (smash_sam_format, query.cpp:231-415):
+    SAM lines from the per-match records; returns (bytes, tag_error)."""
+    h_rec = np.ascontiguousarray(h_rec)
+    h_n = np.ascontiguousarray(h_n, np.uint32)
+    assert h_rec.nbytes >= len(names) * cap * SAM_REC.itemsize and len(h_n) == len(names)
+    sm = None if small_chr is None else np.ascontiguousarray(small_chr, np.uint8)
+    out = C.c_void_p()
+    olen = C.c_uint64()
+    terr = C.c_int32()
+    check(lib().smash_sam_format(_cstrs([c.encode() for c in contigs]), len(contigs),
+                                 _p(h_rec, vp), _p(h_n, u32p), cap, len(names), _cstrs(names),
+                                 _cstrs(seqs), _cstrs(quals), _cstrs(optionals), int(nomap),
+                                 int(tag), None if sm is None else _p(sm, u8p), C.byref(out),
+                                 C.byref(olen), C.byref(terr)), "smash_sam_format")
+    try:
+        text = C.string_at(out.value, olen.value)
+    finally:
+        lib().smash_sam_free(out)
+    return text, terr.value
+
+
+def sam_records(index: Index, d_reads, n, read_len, cap, tag_offsets=None, min_len=20,
+                stream=None):
+    """MAM search + per-match records on the device (smash_map_batch ->
+    smash_sam_records); returns host copies (SAM_REC[n*cap], counts[n])."""
+    import torch
+    dev = d_reads.device
+    d_m = torch.empty(n * cap, dtype=torch.int64, device=dev)
+    d_n = torch.empty(n, dtype=torch.int32, device=dev)
+    map_batch(index, d_reads, n, read_len, d_m, cap, d_n, min_len=min_len, stream=stream)
+    d_rec = torch.zeros(n * cap * SAM_REC.itemsize, dtype=torch.uint8, device=dev)
+    d_off = None
+    if tag_offsets is not None:
+        d_off = torch.from_numpy(np.ascontiguousarray(tag_offsets, np.uint32).view(np.int32)).to(dev)
+    check(lib().smash_sam_records(index.h, _ptr(d_reads), read_len, read_len, n, _ptr(d_m), cap,
+                                  _ptr(d_n), _ptr(d_off), _ptr(d_rec), vp(_stream(stream))),
+          "smash_sam_records")
+    torch.cuda.synchronize(dev)
+    return d_rec.cpu().numpy().view(SAM_REC), d_n.cpu().numpy().view(np.uint32).copy()
+
+
+def sam_lines(index: Index, d_reads, read_len, names, seqs, quals=None, optionals=None,
+              nomap=True, tag_offsets=None, small_chr=None, cap=None, min_len=20, stream=None):
+    """memsam `-rcref -samin -samout [-nomap]` lines for 2n mates (read 1, read 2 of
+    each pair, names with the ':0'/':1' suffix of query.cpp:641-642): the MAM search
+    (smash_map_batch), the per-match records on the device (smash_sam_records) and
+    the host formatting of print_matches (query.cpp:331-415).  With tag_offsets
+    (u32 sam_header offsets per forward contig) the mappability_tag L/R columns
+    are appended (mappability_tag.cpp:93-124).  Returns (bytes, tag_error)."""
+    n = len(names)
+    if cap is None:
+        cap = read_len - min_len + 1
+    h_rec, h_n = sam_records(index, d_reads, n, read_len, cap, tag_offsets, min_len, stream)
+    return sam_format(index.contigs, h_rec, h_n, cap, names, seqs, quals, optionals, nomap,
+                      tag_offsets is not None, small_chr)

@@ -137,3 +137,24 @@ def test_cli_search_triples(tmp_path, tiny_fa, capsys, flag, mode):
     for g, e in zip(got, exp):
         gt, et = g.split("\t"), e.split()
         assert gt[2:] == et[2:], (g[:80], e[:80])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_cli_memsam_mapout_tagged(tmp_path, tiny_fa, s):
+    """`smash_cli memsam -nomap --tag` == `mummer -rcref -nomap -samin -samout`
+    piped through mappability_tag (reduced as tools/make_golden.sh does)."""
+    pytest.importorskip("torch")
+    from test_samout import reduce_line
+    fa = _ref_dir(tmp_path, tiny_fa)
+    sam = tmp_path / "x.sam"
+    sam.write_bytes(gzip.open(gold("%s_fastqs_to_sam.sam.gz" % s)).read())
+    out = tmp_path / "mapout" / "mapout.1.txt"
+    smash_cli.main(["--ref", fa, "memsam", "-nomap", "--tag", "--out", str(out),
+                    "--batch", "97", str(sam)])
+    lines = out.read_text().splitlines()
+    head = [l for l in lines if l.startswith("@")]
+    assert head[0] == "@HD\tVN:1.0\tSO:unsorted" and head[-1].startswith("@PG\tID:longMEM")
+    got = sorted(reduce_line(l) for l in lines if not l.startswith("@"))
+    exp = sorted(gzip.open(gold("%s_mapout_tagged.txt.gz" % s), "rt").read().splitlines())
+    assert got == exp
