@@ -321,6 +321,26 @@ int smash_sam_format(const char *const *contigs, uint32_t n_contig,
                      char **out_text, uint64_t *out_len, int32_t *tag_error);
 void smash_sam_free(char *text);
 
+/* ========================================================================== */
+/* Read ingest: replaces `zcat r1s | fastqs_to_sam r1 r2 1 | ... samtools     */
+/* sort -n` (smash_mapping.sh:19-23, fastqs_to_sam.cpp:48-96) for the device  */
+/* batches.  smash_fastq_read parses up to max_pairs pairs (gzip or plain;    */
+/* pairs with empty bases dropped) into h_reads[2*n*len] (mate 2q = read 1;   */
+/* N -> Z and lowercase applied) and, if h_names, the read-1 names into       */
+/* name_stride-byte NUL-padded slots.  *len = 0 takes the length of the first */
+/* pair; every mate must have it.  *n_pairs < max_pairs means the end.        */
+/* smash_strnum_order: perm[] = stable `samtools sort -n` order (strnum_cmp)  */
+/* of n NUL-padded names.  Host code only.                                    */
+/* ========================================================================== */
+typedef struct smash_fastq smash_fastq;
+int smash_fastq_open(const char *const *r1_paths, uint32_t n1,
+                     const char *const *r2_paths, uint32_t n2, smash_fastq **out);
+int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *len,
+                     uint8_t *h_reads, char *h_names, uint32_t name_stride,
+                     uint64_t *n_pairs);
+void smash_fastq_close(smash_fastq *f);
+int smash_strnum_order(const char *names, uint32_t stride, uint64_t n, uint64_t *perm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,279 @@
+// smash-paper_amd/csrc/ingest.cpp -- native read ingest for the device batches.
+//
+// Replaces the `zcat r1s | fastqs_to_sam ... | samtools sort -n` front of
+// smash_mapping.sh:19-23 for the counting path:
+//  * smash_fastq_*: the FASTQ/FASTA lists of both mates (gzip or plain, zlib
+//    reads both), parsed as fastqs_to_sam.cpp:48-96 does (blank lines
+//    skipped, '@'/'>' records, name = first token after the marker, '+' line
+//    and qualities for '@' records, pairs with empty bases dropped), with
+//    replaceN (N -> Z, fastqs_to_sam.cpp:74 with argc == 4) and the
+//    NewQuery::extend lowercasing (query.cpp:125-144) applied on the way into
+//    the caller's (pinned) mate matrix: mate 2q = read 1, 2q + 1 = read 2.
+//  * smash_strnum_order: the pair order of `samtools sort -n` (strnum_cmp:
+//    digit runs compare as numbers), stable, so read 1 stays before read 2.
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/smash_gpu.h"
+
+namespace smash {
+void set_error(const std::string &msg);
+}
+using smash::set_error;
+
+namespace {
+
+struct Reader {
+  std::vector<std::string> paths;
+  size_t next_path = 0;
+  gzFile f = nullptr;
+  std::vector<char> buf = std::vector<char>(1 << 16);
+  std::string msg;   // error text (set_error is per thread; the caller reports it)
+
+  ~Reader() {
+    if (f) gzclose(f);
+  }
+  // one line without the trailing \r\n; false at the end of the last file
+  bool line(std::string &out, int &err) {
+    out.clear();
+    for (;;) {
+      if (!f) {
+        if (next_path >= paths.size()) return false;
+        f = gzopen(paths[next_path].c_str(), "rb");
+        if (!f) {
+          msg = ("cannot open " + paths[next_path]);
+          err = SMASH_ERR_IO;
+          return false;
+        }
+        gzbuffer(f, 1 << 20);
+        ++next_path;
+      }
+      bool got = false;
+      while (gzgets(f, buf.data(), int(buf.size()))) {
+        got = true;
+        const size_t n = strlen(buf.data());
+        out.append(buf.data(), n);
+        if (n && buf[n - 1] == '\n') break;
+      }
+      if (got) {
+        while (!out.empty() && (out.back() == '\n' || out.back() == '\r')) out.pop_back();
+        return true;
+      }
+      gzclose(f);
+      f = nullptr;
+    }
+  }
+  // fastqs_to_sam record: name, bases; false at the end
+  bool record(std::string &name, std::string &bases, int &err) {
+    std::string l;
+    for (;;) {
+      if (!line(l, err)) return false;
+      size_t b = 0, e = l.size();
+      while (b < e && isspace(uint8_t(l[b]))) ++b;
+      while (e > b && isspace(uint8_t(l[e - 1]))) --e;
+      if (b == e) continue;
+      const char mark = l[b];
+      if (mark != '@' && mark != '>') {
+        msg = ("Fastq @ parse error: " + l.substr(0, 40));
+        err = SMASH_ERR_IO;
+        return false;
+      }
+      size_t t = b + 1;
+      while (t < e && isspace(uint8_t(l[t]))) ++t;
+      size_t te = t;
+      while (te < e && !isspace(uint8_t(l[te]))) ++te;
+      if (t == te) {
+        msg = ("Problem reading read name");
+        err = SMASH_ERR_IO;
+        return false;
+      }
+      name.assign(l, t, te - t);
+      if (!line(bases, err)) bases.clear();
+      if (err) return false;
+      if (mark == '@') {
+        std::string plus, qual;
+        if (!line(plus, err) || plus.find_first_not_of(" \t") == std::string::npos ||
+            plus[plus.find_first_not_of(" \t")] != '+') {
+          if (!err) {
+            msg = ("Fastq + parse error");
+            err = SMASH_ERR_IO;
+          }
+          return false;
+        }
+        line(qual, err);
+        if (err) return false;
+      }
+      return true;
+    }
+  }
+};
+
+// samtools sort -n (strnum_cmp): text runs bytewise, digit runs as numbers
+int strnum_cmp(const char *a, size_t na, const char *b, size_t nb) {
+  size_t i = 0, j = 0;
+  bool digits = false;   // runs alternate text, digits, text, ... from the start
+  while (i < na || j < nb) {
+    if (i >= na) return -1;
+    if (j >= nb) return 1;
+    size_t ie = i, je = j;
+    auto isd = [](char c) { return c >= '0' && c <= '9'; };
+    while (ie < na && isd(a[ie]) == digits) ++ie;
+    while (je < nb && isd(b[je]) == digits) ++je;
+    if (!digits) {
+      const size_t m = std::min(ie - i, je - j);
+      const int c = memcmp(a + i, b + j, m);
+      if (c) return c < 0 ? -1 : 1;
+      if (ie - i != je - j) return ie - i < je - j ? -1 : 1;
+    } else {
+      size_t zi = i, zj = j;
+      while (zi < ie && a[zi] == '0') ++zi;
+      while (zj < je && b[zj] == '0') ++zj;
+      if (ie - zi != je - zj) return ie - zi < je - zj ? -1 : 1;
+      const int c = memcmp(a + zi, b + zj, ie - zi);
+      if (c) return c < 0 ? -1 : 1;
+    }
+    i = ie;
+    j = je;
+    digits = !digits;
+  }
+  return 0;
+}
+
+uint8_t g_lut[256];
+struct LutInit {
+  LutInit() {
+    for (int c = 0; c < 256; ++c) g_lut[c] = uint8_t(c >= 'A' && c <= 'Z' ? c + 32 : c);
+    g_lut[uint8_t('N')] = uint8_t('z');   // replaceN, then lowercase
+  }
+} g_lut_init;
+
+}  // namespace
+
+struct smash_fastq {
+  Reader r1, r2;
+  uint32_t L = 0;
+  bool done = false;
+};
+
+extern "C" int smash_fastq_open(const char *const *r1, uint32_t n1, const char *const *r2,
+                                uint32_t n2, smash_fastq **out) {
+  if (!r1 || !r2 || !out || n1 == 0 || n2 == 0) {
+    set_error("smash_fastq_open: need read-1 and read-2 paths");
+    return SMASH_ERR_ARG;
+  }
+  auto *f = new smash_fastq;
+  for (uint32_t i = 0; i < n1; ++i) f->r1.paths.emplace_back(r1[i]);
+  for (uint32_t i = 0; i < n2; ++i) f->r2.paths.emplace_back(r2[i]);
+  *out = f;
+  return SMASH_OK;
+}
+
+namespace {
+// up to `want` records of one mate list: names (read 1 only) and bases, flat
+struct Chunk {
+  std::vector<char> bases, names;
+  std::vector<uint64_t> boff, noff;   // n + 1 offsets each
+  bool end = false;
+  int err = 0;
+  void parse(Reader &r, uint64_t want, bool keep_names) {
+    bases.clear();
+    names.clear();
+    boff.assign(1, 0);
+    noff.assign(1, 0);
+    end = false;
+    std::string nm, b;
+    for (uint64_t i = 0; i < want; ++i) {
+      if (!r.record(nm, b, err)) {
+        end = true;
+        return;
+      }
+      bases.insert(bases.end(), b.begin(), b.end());
+      boff.push_back(bases.size());
+      if (keep_names) names.insert(names.end(), nm.begin(), nm.end());
+      noff.push_back(names.size());
+    }
+  }
+  uint64_t size() const { return boff.size() - 1; }
+};
+}  // namespace
+
+extern "C" int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *len,
+                                uint8_t *h_reads, char *h_names, uint32_t name_stride,
+                                uint64_t *n_pairs) {
+  if (!f || !len || !h_reads || !n_pairs || (h_names && name_stride < 2)) {
+    set_error("smash_fastq_read: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  *n_pairs = 0;
+  uint64_t q = 0;
+  Chunk c1, c2;
+  // the two mate lists are parsed (and inflated) on two threads, then zipped
+  while (q < max_pairs && !f->done) {
+    const uint64_t want = max_pairs - q;
+    std::thread t([&] { c2.parse(f->r2, want, false); });
+    c1.parse(f->r1, want, true);
+    t.join();
+    if (c1.err || c2.err) {
+      set_error(c1.err ? f->r1.msg : f->r2.msg);
+      return c1.err ? c1.err : c2.err;
+    }
+    const uint64_t n = std::min(c1.size(), c2.size());
+    if (c1.end || c2.end) f->done = true;   // zip(): the shorter list ends the pairs
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t la = c1.boff[i + 1] - c1.boff[i], lb = c2.boff[i + 1] - c2.boff[i];
+      if (la == 0 || lb == 0) continue;   // fastqs_to_sam.cpp:80
+      const std::string na(c1.names.data() + c1.noff[i], c1.noff[i + 1] - c1.noff[i]);
+      if (*len == 0) {
+        if (la > 255) {
+          set_error("smash_fastq_read: reads longer than 255 bases");
+          return SMASH_ERR_UNSUPPORTED;
+        }
+        f->L = *len = uint32_t(la);
+      }
+      if (la != *len || lb != *len) {
+        set_error("smash_fastq_read: all mates must have the same length (" + na + ")");
+        return SMASH_ERR_ARG;
+      }
+      const char *a = c1.bases.data() + c1.boff[i], *b = c2.bases.data() + c2.boff[i];
+      uint8_t *d = h_reads + q * 2 * *len;
+      for (uint32_t j = 0; j < *len; ++j) d[j] = g_lut[uint8_t(a[j])];
+      for (uint32_t j = 0; j < *len; ++j) d[*len + j] = g_lut[uint8_t(b[j])];
+      if (h_names) {
+        if (na.size() >= name_stride) {
+          set_error("smash_fastq_read: read name longer than name_stride - 1: " + na);
+          return SMASH_ERR_ARG;
+        }
+        char *o = h_names + q * name_stride;
+        memcpy(o, na.data(), na.size());
+        memset(o + na.size(), 0, name_stride - na.size());
+      }
+      ++q;
+    }
+  }
+  *n_pairs = q;
+  return SMASH_OK;
+}
+
+extern "C" void smash_fastq_close(smash_fastq *f) { delete f; }
+
+extern "C" int smash_strnum_order(const char *names, uint32_t stride, uint64_t n,
+                                  uint64_t *perm) {
+  if ((!names && n) || (!perm && n) || stride == 0) {
+    set_error("smash_strnum_order: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  std::vector<uint32_t> len(n);
+  for (uint64_t i = 0; i < n; ++i) len[i] = uint32_t(strnlen(names + i * stride, stride));
+  std::iota(perm, perm + n, uint64_t(0));
+  std::stable_sort(perm, perm + n, [&](uint64_t x, uint64_t y) {
+    return strnum_cmp(names + x * stride, len[x], names + y * stride, len[y]) < 0;
+  });
+  return SMASH_OK;
+}

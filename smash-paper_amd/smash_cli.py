@@ -206,11 +206,17 @@ class _Run:
             self.bins_rows, self.starts = S.read_bins(bins_path)
         else:
             self.bins_rows, self.starts = [], np.zeros(1, np.int64)
-        pairs = sam_pairs(args.sam) if args.sam else \
-            fastq_pairs(args.reads1.split(), args.reads2.split())
-        pairs.sort(key=lambda p: strnum_key(p[0]))
-        self.reads = reads_matrix(pairs)
-        self.n = len(pairs)
+        if args.sam:
+            pairs = sam_pairs(args.sam)
+            pairs.sort(key=lambda p: strnum_key(p[0]))
+            self.reads = reads_matrix(pairs)
+            self.n = len(pairs)
+        else:   # native ingest (smash_fastq_read) + samtools sort -n order
+            names, reads = S.read_fastq_pairs(args.reads1.split(), args.reads2.split())
+            order = S.strnum_order(names)
+            n = len(names)
+            self.reads = reads.reshape(n, -1)[order].reshape(2 * n, -1) if n else reads
+            self.n = n
         self.batch = min(args.batch, max(self.n, 1))
         self.dev = torch.device("cuda", args.device)
 

@@ -48,6 +48,7 @@ EXPORTS = [
     "smash_pipeline_profile", "smash_pipeline_profile_read",
     "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
+    "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
 ]
 
 
@@ -141,6 +142,12 @@ def lib():
                                    u8p, C.POINTER(C.c_void_p), u64p, i32p]
     L.smash_sam_free.argtypes = [C.c_void_p]
     L.smash_sam_free.restype = None
+    L.smash_fastq_open.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, C.POINTER(C.c_char_p),
+                                   C.c_uint32, C.POINTER(vp)]
+    L.smash_fastq_read.argtypes = [vp, C.c_uint64, u32p, vp, vp, C.c_uint32, u64p]
+    L.smash_fastq_close.argtypes = [vp]
+    L.smash_fastq_close.restype = None
+    L.smash_strnum_order.argtypes = [vp, C.c_uint32, C.c_uint64, u64p]
     _LIB = L
     return L
 
@@ -598,3 +605,45 @@ def sam_lines(index: Index, d_reads, read_len, names, seqs, quals=None, optional
     h_rec, h_n = sam_records(index, d_reads, n, read_len, cap, tag_offsets, min_len, stream)
     return sam_format(index.contigs, h_rec, h_n, cap, names, seqs, quals, optionals, nomap,
                       tag_offsets is not None, small_chr)
+
+
+def read_fastq_pairs(r1_paths, r2_paths, batch_pairs=1 << 20, name_stride=64):
+    """All pairs of the two FASTQ lists through the native reader
+    (smash_fastq_*): (names[n] as a fixed-width bytes array, reads[2n, L] u8
+    after replaceN + lowercasing), in file order."""
+    arr1 = _cstrs([p.encode() for p in r1_paths])
+    arr2 = _cstrs([p.encode() for p in r2_paths])
+    h = vp()
+    check(lib().smash_fastq_open(arr1, len(r1_paths), arr2, len(r2_paths), C.byref(h)),
+          "smash_fastq_open")
+    try:
+        L = C.c_uint32(0)
+        reads, names = [], []
+        while True:
+            cap_len = L.value or 255
+            rb = np.empty(2 * batch_pairs * cap_len, np.uint8)
+            nb = np.zeros(batch_pairs, "S%d" % name_stride)
+            n = C.c_uint64()
+            check(lib().smash_fastq_read(h, batch_pairs, C.byref(L), _p(rb, vp), _p(nb, vp),
+                                         name_stride, C.byref(n)), "smash_fastq_read")
+            k = n.value
+            if k:
+                reads.append(rb[:2 * k * L.value].reshape(2 * k, L.value).copy())
+                names.append(nb[:k].copy())
+            if k < batch_pairs:
+                break
+    finally:
+        lib().smash_fastq_close(h)
+    if not reads:
+        return np.zeros(0, "S%d" % name_stride), np.zeros((0, 0), np.uint8)
+    return np.concatenate(names), np.concatenate(reads)
+
+
+def strnum_order(names):
+    """Stable `samtools sort -n` order of a fixed-width bytes array
+    (smash_strnum_order)."""
+    names = np.ascontiguousarray(names)
+    perm = np.empty(len(names), np.uint64)
+    check(lib().smash_strnum_order(_p(names, vp), names.dtype.itemsize, len(names),
+                                   _p(perm, u64p)), "smash_strnum_order")
+    return perm.astype(np.int64)

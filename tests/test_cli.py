@@ -158,3 +158,56 @@ def test_cli_memsam_mapout_tagged(tmp_path, tiny_fa, s):
     got = sorted(reduce_line(l) for l in lines if not l.startswith("@"))
     exp = sorted(gzip.open(gold("%s_mapout_tagged.txt.gz" % s), "rt").read().splitlines())
     assert got == exp
+
+
+# ---------------------------------------------------------------------------
+# native ingest (smash_fastq_read / smash_strnum_order): host code, CPU tests
+# ---------------------------------------------------------------------------
+import smashgpu as S  # noqa: E402
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_native_fastq_reader_equals_fastqs_to_sam(tmp_path, s):
+    """gzip and plain inputs, the read-1 list split over two files, small
+    batches: same pairs, names and bytes as the fastqs_to_sam restatement."""
+    pairs = smash_cli.fastq_pairs([_fq(tmp_path, s, 1)], [_fq(tmp_path, s, 2)])
+    lines = open(_fq(tmp_path, s, 1), "rb").read().split(b"\n")
+    cut = 4 * 37
+    a, b = tmp_path / "a.fq.gz", tmp_path / "b.fq"
+    with gzip.open(a, "wb") as f:
+        f.write(b"\n".join(lines[:cut]) + b"\n")
+    b.write_bytes(b"\n".join(lines[cut:]))
+    names, reads = S.read_fastq_pairs([str(a), str(b)], [gold("%s_r2.fq.gz" % s)],
+                                      batch_pairs=50)
+    assert [n for n in names.tolist()] == [p[0] for p in pairs]
+    assert np.array_equal(reads, smash_cli.reads_matrix(pairs))
+
+
+def test_native_fastq_reader_edge_cases(tmp_path):
+    """Blank lines, '+name' lines, '>' records, a pair with empty bases
+    dropped (fastqs_to_sam.cpp:80); N -> z; a mate of another length is an
+    error (the device batches have one read length)."""
+    a, b = tmp_path / "a.fq", tmp_path / "b.fq"
+    a.write_bytes(b"@a1 1:N:0\nACGTNNAC\n+\nIIIIIIII\n\n@a3 x y\n\n+\n\n>f1 opt\nACGNTACG\n")
+    b.write_bytes(b"@b1 2:N:0\r\nTTTTNNTT\r\n+b1\r\nIIIIIIII\r\n@b3 z\nCCCC\n+\nJJJJ\n"
+                  b">f2\nNNNNACGT")
+    exp = smash_cli.fastq_pairs([str(a)], [str(b)])
+    assert [p[0] for p in exp] == [b"a1", b"f1"]
+    names, reads = S.read_fastq_pairs([str(a)], [str(b)], batch_pairs=1)
+    assert names.tolist() == [b"a1", b"f1"]
+    assert reads.tobytes() == b"acgtzzac" + b"ttttzztt" + b"acgztacg" + b"zzzzacgt"
+    with pytest.raises(S.SmashError, match="same length"):
+        S.read_fastq_pairs([gold("edge_r1.fq")], [gold("edge_r2.fq")], batch_pairs=8)
+    with pytest.raises(S.SmashError, match="cannot open"):
+        S.read_fastq_pairs(["/nonexistent.fq"], [gold("edge_r2.fq")])
+
+
+def test_native_strnum_order_equals_samtools_key():
+    rng = np.random.default_rng(5)
+    alpha = list("ab:_") + [str(d) for d in range(10)]
+    names = [bytes("".join(rng.choice(alpha, rng.integers(1, 12))), "ascii") for _ in range(3000)]
+    names += [b"r10", b"r9", b"r009", b"r1", b"", b"0", b"00", b"a2b10", b"a2b9"]
+    arr = np.array(names, "S16")
+    got = S.strnum_order(arr).tolist()
+    exp = sorted(range(len(names)), key=lambda i: smash_cli.strnum_key(names[i]))
+    assert got == exp
