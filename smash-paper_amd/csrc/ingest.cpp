@@ -34,15 +34,15 @@ struct Reader {
   std::vector<std::string> paths;
   size_t next_path = 0;
   gzFile f = nullptr;
-  std::vector<char> buf = std::vector<char>(1 << 16);
+  std::vector<char> buf = std::vector<char>(1 << 22);
+  size_t beg = 0, fill = 0;   // unread bytes buf[beg, fill)
   std::string msg;   // error text (set_error is per thread; the caller reports it)
 
   ~Reader() {
     if (f) gzclose(f);
   }
-  // one line without the trailing \r\n; false at the end of the last file
-  bool line(std::string &out, int &err) {
-    out.clear();
+  // refill from the current file (opening the next at EOF); false at the end
+  bool more(int &err) {
     for (;;) {
       if (!f) {
         if (next_path >= paths.size()) return false;
@@ -55,19 +55,54 @@ struct Reader {
         gzbuffer(f, 1 << 20);
         ++next_path;
       }
-      bool got = false;
-      while (gzgets(f, buf.data(), int(buf.size()))) {
-        got = true;
-        const size_t n = strlen(buf.data());
-        out.append(buf.data(), n);
-        if (n && buf[n - 1] == '\n') break;
+      if (beg) {
+        memmove(buf.data(), buf.data() + beg, fill - beg);
+        fill -= beg;
+        beg = 0;
       }
-      if (got) {
-        while (!out.empty() && (out.back() == '\n' || out.back() == '\r')) out.pop_back();
+      if (fill == buf.size()) buf.resize(buf.size() * 2);
+      const int n = gzread(f, buf.data() + fill, unsigned(buf.size() - fill));
+      if (n < 0) {
+        msg = ("read error in " + paths[next_path - 1]);
+        err = SMASH_ERR_IO;
+        return false;
+      }
+      if (n > 0) {
+        fill += size_t(n);
         return true;
       }
       gzclose(f);
       f = nullptr;
+      // a file that does not end in '\n' ends its last line (as getline does)
+      if (fill > beg && buf[fill - 1] != '\n') {
+        if (fill == buf.size()) buf.resize(buf.size() * 2);
+        buf[fill++] = '\n';
+        return true;
+      }
+    }
+  }
+  // one line without the trailing \r\n; false at the end of the last file
+  bool line(std::string &out, int &err) {
+    out.clear();
+    size_t scan = beg;
+    for (;;) {
+      const char *nl = static_cast<const char *>(memchr(buf.data() + scan, '\n', fill - scan));
+      if (nl) {
+        size_t e = size_t(nl - buf.data());
+        out.assign(buf.data() + beg, e - beg);
+        beg = e + 1;
+        while (!out.empty() && out.back() == '\r') out.pop_back();
+        return true;
+      }
+      scan = fill - beg;   // offset after the memmove in more()
+      if (!more(err)) {
+        if (fill > beg) {   // unreachable: more() terminates a last line
+          out.assign(buf.data() + beg, fill - beg);
+          beg = fill;
+          return true;
+        }
+        return false;
+      }
     }
   }
   // fastqs_to_sam record: name, bases; false at the end
