@@ -21,7 +21,6 @@ import pytest
 
 from conftest import gold, read_gz_lines
 
-import oracle as O
 import smashgpu as S
 
 TAGS = re.compile(r"^(XM|XU|XE|XS|NH|HI|L0|R0|cc|cp|xo|xc|CC|CP|XO|XC):")
