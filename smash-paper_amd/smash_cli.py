@@ -335,12 +335,47 @@ def sam_records_in(path):
         yield name, f[9], f[10], b"".join(b"\t" + x for x in f[11:])
 
 
+def query_records_in(path, fastq):
+    """QueryReader::run without -samin (query.cpp:648-676): '>' (or '@' with
+    -fastq) records; the name runs to the first space after trimming spaces, and
+    a '1' / '2' right after that space adds ':0' / ':1'; one sequence line
+    (spaces dropped, NewQuery::extend); with -fastq a '+' line and one QUAL
+    line, else QUAL is '!' per base (Aligner::run, query.cpp:323)."""
+    mark = b"@" if fastq else b">"
+    it = iter(_open(path))
+    for raw in it:
+        line = raw.rstrip(b"\n")
+        if not line:
+            continue
+        if line[:1] != mark:
+            raise SystemExit("missing query start character %sin input line%s"
+                             % (mark.decode(), line.decode(errors="replace")))
+        body = line[1:].strip(b" ")
+        sp = body.find(b" ")
+        name = body if sp < 0 else body[:sp]
+        if 0 <= sp < len(body) - 1:
+            name += {b"1": b":0", b"2": b":1"}.get(body[sp + 1:sp + 2], b"")
+        seq = next(it, b"").rstrip(b"\n")
+        if not seq:
+            raise SystemExit("empty sequence")
+        seq = seq.rstrip(b" ").replace(b" ", b"")
+        qual = None
+        if fastq:
+            next(it, None)
+            qual = next(it, b"").rstrip(b"\n")
+            if not qual:
+                raise SystemExit("empty errors")
+        yield name, seq, qual, b""
+
+
 def cmd_memsam(args):
     """`mummer -rcref -samin -samout [-nomap] ref.fa query.sam` (mummer.cpp:77-96):
     mapout SAM text (header fasta.cpp:243-252, lines query.cpp:331-415); with
     --tag the mappability_tag L/R columns are appended (mappability_tag.cpp:
     93-124) and a tag error exits 1 as the reference throws."""
     import torch
+    if args.fastq and args.samin:
+        raise SystemExit("-fastq cannot be used with -samin")   # mummer.cpp:143
     ref = _ref(args)
     ix = load_index(ref, args.device)
     dev = torch.device("cuda", args.device)
@@ -354,7 +389,8 @@ def cmd_memsam(args):
         for name, size in zip(ix.contigs, sizes):
             out.write(b"@SQ\tSN:%s\tLN:%d\n" % (name.encode(), size))
         out.write(b"@PG\tID:longMEM\tPN:longMEM\tVN:0.5\n")
-        recs = sam_records_in(args.query)
+        recs = sam_records_in(args.query) if args.samin or args.query.endswith(
+            (".sam", ".sam.gz")) else query_records_in(args.query, args.fastq)
         while True:
             batch = [r for _, r in zip(range(2 * args.batch), recs)]
             if not batch:
@@ -401,11 +437,13 @@ def main(argv=None):
     p.set_defaults(fn=cmd_varbin)
     p = sub.add_parser("memsam")
     p.add_argument("-nomap", action="store_true", help="print unmapped reads (query.cpp:308)")
+    p.add_argument("-samin", action="store_true", help="SAM input (default for *.sam[.gz])")
+    p.add_argument("-fastq", action="store_true", help="FASTQ input (else FASTA)")
     p.add_argument("-l", type=int, default=20, help="minimum match length (query.h:129)")
     p.add_argument("--tag", action="store_true", help="append mappability_tag L/R columns")
     p.add_argument("--out", default=None, help="default mapout/mapout.1.txt")
     p.add_argument("--batch", type=int, default=1_000_000, help="pairs per device batch")
-    p.add_argument("query", help="unmapped SAM (fastqs_to_sam output)")
+    p.add_argument("query", help="unmapped SAM (fastqs_to_sam output), FASTA or FASTQ")
     p.set_defaults(fn=cmd_memsam)
     p = sub.add_parser("search")
     p.add_argument("-mum", action="store_true")

@@ -211,3 +211,49 @@ def test_native_strnum_order_equals_samtools_key():
     got = S.strnum_order(arr).tolist()
     exp = sorted(range(len(names)), key=lambda i: smash_cli.strnum_key(names[i]))
     assert got == exp
+
+
+def _interleaved_fastq_from_sam(s, path):
+    """The golden fastqs_to_sam SAM (replaceN applied) as one interleaved FASTQ
+    with Illumina '1:N:0' / '2:N:0' comments."""
+    out = []
+    for line in gzip.open(gold("%s_fastqs_to_sam.sam.gz" % s)):
+        f = line.rstrip(b"\n").split(b"\t")
+        mate = b"1" if int(f[1]) & 64 else b"2"
+        out.append(b"@%s %s:N:0\n%s\n+\n%s\n" % (f[0], mate, f[9], f[10]))
+    path.write_bytes(b"".join(out))
+    return out
+
+
+def test_memsam_query_reader_fastq_and_fasta(tmp_path):
+    """QueryReader::run's FASTA/FASTQ branch (query.cpp:648-676)."""
+    fq = tmp_path / "q.fq"
+    _interleaved_fastq_from_sam("s100", fq)
+    recs = list(smash_cli.query_records_in(str(fq), True))
+    sam = list(smash_cli.sam_records_in(gold("s100_fastqs_to_sam.sam.gz")))
+    assert [(r[0], r[1], r[2]) for r in recs] == [(r[0], r[1], r[2]) for r in sam]
+    fa = tmp_path / "q.fa"
+    fa.write_bytes(b">  x1 2extra  \nAC GT \n\n>y\nAAAA\n>z 1\nC\n")
+    recs = list(smash_cli.query_records_in(str(fa), False))
+    assert recs == [(b"x1:1", b"ACGT", None, b""), (b"y", b"AAAA", None, b""),
+                    (b"z:0", b"C", None, b"")]
+    with pytest.raises(SystemExit):
+        list(smash_cli.query_records_in(str(fa), True))
+
+
+@pytest.mark.gpu
+def test_cli_memsam_fastq_input(tmp_path, tiny_fa):
+    """`mummer -rcref -fastq -nomap -samout` on the same reads as FASTQ: the
+    lines equal the -samin golden without the SAM input's optional column."""
+    pytest.importorskip("torch")
+    from test_samout import reduce_line
+    fa = _ref_dir(tmp_path, tiny_fa)
+    fq = tmp_path / "q.fq"
+    _interleaved_fastq_from_sam("s150", fq)
+    out = tmp_path / "m.txt"
+    smash_cli.main(["--ref", fa, "memsam", "-nomap", "-fastq", "--tag", "--out", str(out),
+                    str(fq)])
+    got = sorted(reduce_line(l) for l in out.read_text().splitlines() if not l.startswith("@"))
+    exp = sorted("\t".join(x for x in l.split("\t") if not x.startswith("XO:Z:"))
+                 for l in gzip.open(gold("s150_mapout_tagged.txt.gz"), "rt").read().splitlines())
+    assert got == exp
