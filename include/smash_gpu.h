@@ -325,7 +325,8 @@ void smash_sam_free(char *text);
 /* Read ingest: replaces `zcat r1s | fastqs_to_sam r1 r2 1 | ... samtools     */
 /* sort -n` (smash_mapping.sh:19-23, fastqs_to_sam.cpp:48-96) for the device  */
 /* batches.  smash_fastq_read parses up to max_pairs pairs (gzip or plain;    */
-/* pairs with empty bases dropped) into h_reads[2*n*len] (mate 2q = read 1;   */
+/* pairs whose mates both have no bases dropped, a pair with one empty mate  */
+/* is SMASH_ERR_ARG) into h_reads[2*n*len] (mate 2q = read 1;                 */
 /* N -> Z and lowercase applied) and, if h_names, the read-1 names into       */
 /* name_stride-byte NUL-padded slots.  *len = 0 takes the length of the first */
 /* pair; every mate must have it.  *n_pairs < max_pairs means the end.        */

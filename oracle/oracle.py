@@ -54,7 +54,7 @@ class OrcMatch(C.Structure):
     _fields_ = [("ref", C.c_uint64), ("query", C.c_uint64), ("len", C.c_uint64)]
 
 
-CIGAR_MAX = 160
+CIGAR_MAX = 1024   # smash_oracle.h ORC_CIGAR_MAX
 
 
 class OrcHit(C.Structure):
@@ -308,11 +308,14 @@ class Index:
         m = (OrcMatch * max(1, len(matches)))()
         for i, (r, q, l) in enumerate(matches):
             m[i].ref, m[i].query, m[i].len = r, q, l
-        hits = (OrcHit * 64)()
+        cap = max(1, len(matches))              # hits <= matches: never truncated
+        hits = (OrcHit * cap)()
         bt = C.c_uint32()
         bp = C.c_int64()
         n = lib().orc_resolve(C.byref(self.c), _p(P, u8p), len(P), m, len(matches),
-                              hits, 64, C.byref(bt), C.byref(bp))
+                              hits, cap, C.byref(bt), C.byref(bp))
+        if n < 0:
+            raise RuntimeError("orc_resolve: capacity exceeded (%d matches)" % len(matches))
         best = None if bt.value == 0xFFFFFFFF else (bt.value, bp.value)
         return [hits[i] for i in range(n)], best
 
@@ -346,10 +349,12 @@ def tag(hit, offsets, mapbin, small):
 def smash_pair(h1, h2, min_excess=4, window=10000):
     a = (OrcHit * max(1, len(h1)))(*h1)
     b = (OrcHit * max(1, len(h2)))(*h2)
-    tid = np.zeros(128, np.uint32)
-    pos = np.zeros(128, np.int64)
+    tid = np.zeros(len(h1) + len(h2) + 1, np.uint32)   # kept <= hits: never truncated
+    pos = np.zeros(len(h1) + len(h2) + 1, np.int64)
     n = lib().orc_smash_pair(a, len(h1), b, len(h2), min_excess, window,
                              _p(tid, u32p), _p(pos, i64p))
+    if n < -1:
+        raise RuntimeError("orc_smash_pair: capacity exceeded")
     if n < 0:
         return None
     return list(zip(tid[:n].tolist(), pos[:n].tolist()))

@@ -563,12 +563,12 @@ static void isort(uint32_t *idx, uint32_t n, const aln_t *base,
 int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
                 const orc_match *m, uint32_t n, orc_hit *out, uint32_t cap,
                 uint32_t *best_tid, int64_t *best_pos) {
-  aln_t al[256];
-  uint32_t idx[256];
+  aln_t al[ORC_MAX_MATCH];
+  uint32_t idx[ORC_MAX_MATCH];
   uint32_t na = 0;
   *best_tid = UINT32_MAX;
   *best_pos = 0;
-  if (n > 256) n = 256;
+  if (n > ORC_MAX_MATCH) return -ORC_ERR_CAP;   /* never truncate */
   for (uint32_t k = 0; k < n; ++k) {
     aln_t *a = &al[na];
     memset(a, 0, sizeof(*a));
@@ -609,6 +609,7 @@ int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
   uint64_t last_end = 0;
   uint8_t nb = 0; uint16_t boff[16], blen[16];
   uint64_t off_walk = 0;
+  int cig_over = 0;   /* a CIGAR longer than ORC_CIGAR_MAX - 1 (never truncated) */
   for (uint32_t i = 0; i < na; ++i) {
     aln_t *a = &al[idx[i]];
     aln_t *nx = (i + 1 == na) ? NULL : &al[idx[i + 1]];
@@ -626,6 +627,7 @@ int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
       if (a->suffix)
         cend += snprintf(cig + cend, sizeof(cig) - (size_t)cend, "%luS",
                          (unsigned long)a->suffix);
+      if (cend >= (int)sizeof(cig) - 1) { cig_over = 1; cend = (int)sizeof(cig) - 1; }
       uint32_t nm = 0;
       for (uint32_t j = 0; j < L; ++j) {
         int64_t rp = a->rcpos + (int64_t)j;
@@ -659,9 +661,11 @@ int orc_resolve(const orc_index *ix, const uint8_t *P, uint32_t L,
   uint32_t nh = 0;
   for (uint32_t i = 0; i < na; ++i) if (al[i].n_matches) ++nh;
   uint32_t hi = 0;
+  if (cig_over) return -ORC_ERR_CAP;
   for (uint32_t i = 0; i < na; ++i) {
     aln_t *a = &al[idx[i]];
     if (!a->n_matches) continue;
+    if (hi >= cap) return -ORC_ERR_CAP;          /* never truncate */
     if (hi < cap) {
       orc_hit *h = &out[hi];
       memset(h, 0, sizeof(*h));
@@ -786,13 +790,14 @@ int orc_tag(orc_hit *h, const uint32_t *offsets, const uint8_t *map,
 int orc_smash_pair(const orc_hit *h1, uint32_t n1, const orc_hit *h2,
                    uint32_t n2, int min_excess, int64_t hit_window,
                    uint32_t *out_tid, int64_t *out_pos) {
-  uint32_t k1[64], k2[64], m1 = 0, m2 = 0;
-  for (uint32_t i = 0; i < n1 && m1 < 64; ++i) {
+  uint32_t k1[ORC_MAX_MATCH], k2[ORC_MAX_MATCH], m1 = 0, m2 = 0;
+  if (n1 > ORC_MAX_MATCH || n2 > ORC_MAX_MATCH) return -2;   /* never truncate */
+  for (uint32_t i = 0; i < n1; ++i) {
     int qlen = (int)h1[i].qend - (int)h1[i].qstart;
     int mx = h1[i].L0 > h1[i].R0 ? h1[i].L0 : h1[i].R0;
     if (qlen - mx >= min_excess) k1[m1++] = i;
   }
-  for (uint32_t i = 0; i < n2 && m2 < 64; ++i) {
+  for (uint32_t i = 0; i < n2; ++i) {
     int qlen = (int)h2[i].qend - (int)h2[i].qstart;
     int mx = h2[i].L0 > h2[i].R0 ? h2[i].L0 : h2[i].R0;
     if (qlen - mx >= min_excess) k2[m2++] = i;
@@ -904,7 +909,8 @@ static int dedup_insert(orc_dedup *d, const uint8_t *k, uint32_t n) {
 /* whole chain                                                               */
 /* ======================================================================== */
 
-#define PAIR_CAP 64
+#define PAIR_CAP (2 * ORC_MAX_MATCH)   /* kept hits of a pair: <= hits(r1) + hits(r2) */
+#define PAIR_CHUNK 16384               /* pairs per worker round (bounds the out arrays) */
 typedef struct {
   int32_t nkept;          /* -1: no key */
   int32_t err;
@@ -920,14 +926,17 @@ typedef struct {
   pair_out_t *out;
 } job_t;
 
+/* every capacity below holds the largest possible input (reads <= 255 bp:
+ * <= 254 matches, hits <= matches); exceeding one is an error, never a cut */
 static void process_mate(const orc_pipeline *p, const uint8_t *P, uint32_t L,
                          orc_hit *hits, uint32_t *nh, int *err) {
-  orc_match m[256];
-  int n = orc_mam(p->ix, P, L, p->min_len, m, 256, NULL);
-  if (n > 256) n = 256;
+  orc_match m[ORC_MAX_MATCH];
+  *nh = 0;
+  int n = orc_mam(p->ix, P, L, p->min_len, m, ORC_MAX_MATCH, NULL);
+  if (n > ORC_MAX_MATCH) { if (!*err) *err = ORC_ERR_CAP; return; }
   uint32_t bt; int64_t bp;
-  int k = orc_resolve(p->ix, P, L, m, (uint32_t)n, hits, 32, &bt, &bp);
-  if (k > 32) k = 32;
+  int k = orc_resolve(p->ix, P, L, m, (uint32_t)n, hits, ORC_MAX_MATCH, &bt, &bp);
+  if (k < 0) { if (!*err) *err = ORC_ERR_CAP; return; }
   for (int i = 0; i < k; ++i) {
     int e = orc_tag(&hits[i], p->tag_offsets, p->map, p->map_size,
                     p->small_chr[hits[i].tid]);
@@ -939,7 +948,8 @@ static void process_mate(const orc_pipeline *p, const uint8_t *P, uint32_t L,
 static void *pair_worker(void *arg) {
   job_t *j = (job_t *)arg;
   const orc_pipeline *p = j->p;
-  orc_hit h1[32], h2[32];
+  orc_hit *h1 = (orc_hit *)malloc(2 * ORC_MAX_MATCH * sizeof(orc_hit));
+  orc_hit *h2 = h1 + ORC_MAX_MATCH;
   for (uint64_t q = j->begin; q < j->end; ++q) {
     uint32_t n1 = 0, n2 = 0;
     int err = 0;
@@ -948,7 +958,9 @@ static void *pair_worker(void *arg) {
     pair_out_t *o = &j->out[q - j->begin];
     o->err = err;
     o->nkept = orc_smash_pair(h1, n1, h2, n2, 4, 10000, o->tid, o->pos);
+    if (o->nkept < -1) { o->err = ORC_ERR_CAP; o->nkept = -1; }
   }
+  free(h1);
   return NULL;
 }
 
@@ -957,40 +969,45 @@ int orc_run_pairs(const orc_pipeline *p, const uint8_t *reads, uint32_t L,
                   orc_dedup *dedup, uint64_t *counts, orc_varbin_state *st,
                   uint64_t *n_dupe_pairs, uint64_t *n_pos_out) {
   if (threads < 1) threads = 1;
-  pair_out_t *out = (pair_out_t *)malloc((n_pairs ? n_pairs : 1) * sizeof(pair_out_t));
+  const uint64_t chunk = n_pairs < PAIR_CHUNK * (uint64_t)threads ? (n_pairs ? n_pairs : 1)
+                                                                    : PAIR_CHUNK * (uint64_t)threads;
+  pair_out_t *out = (pair_out_t *)malloc(chunk * sizeof(pair_out_t));
   pthread_t th[256];
   job_t jobs[256];
   if (threads > 256) threads = 256;
-  for (int t = 0; t < threads; ++t) {
-    jobs[t].p = p; jobs[t].reads = reads; jobs[t].L = L; jobs[t].stride = stride;
-    jobs[t].begin = n_pairs * (uint64_t)t / (uint64_t)threads;
-    jobs[t].end = n_pairs * (uint64_t)(t + 1) / (uint64_t)threads;
-    jobs[t].out = out + jobs[t].begin;
-    pthread_create(&th[t], NULL, pair_worker, &jobs[t]);
-  }
-  for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
   int err = 0;
   uint8_t key[PAIR_CAP * 12 + 4];
   int64_t pos0[PAIR_CAP], absp[PAIR_CAP];
-  for (uint64_t q = 0; q < n_pairs; ++q) {
-    pair_out_t *o = &out[q];
-    if (o->err && !err) err = o->err;
-    if (o->nkept < 0) continue;
-    uint32_t kl = 0;
-    for (int32_t i = 0; i < o->nkept; ++i) {
-      memcpy(key + kl, &o->tid[i], 4); kl += 4;
-      memcpy(key + kl, &o->pos[i], 8); kl += 8;
+  for (uint64_t c0 = 0; c0 < n_pairs; c0 += chunk) {
+    const uint64_t cn = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
+    for (int t = 0; t < threads; ++t) {
+      jobs[t].p = p; jobs[t].reads = reads; jobs[t].L = L; jobs[t].stride = stride;
+      jobs[t].begin = c0 + cn * (uint64_t)t / (uint64_t)threads;
+      jobs[t].end = c0 + cn * (uint64_t)(t + 1) / (uint64_t)threads;
+      jobs[t].out = out + (jobs[t].begin - c0);
+      pthread_create(&th[t], NULL, pair_worker, &jobs[t]);
     }
-    if (!dedup_insert(dedup, key, kl)) { if (n_dupe_pairs) (*n_dupe_pairs)++; continue; }
-    uint64_t np = 0;
-    for (int32_t i = 0; i < o->nkept; ++i) {
-      if (!p->major[o->tid[i]]) continue;
-      pos0[np] = o->pos[i];
-      absp[np] = o->pos[i] + p->chrom_off[o->tid[i]];
-      ++np;
+    for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+    for (uint64_t q = 0; q < cn; ++q) {
+      pair_out_t *o = &out[q];
+      if (o->err && !err) err = o->err;
+      if (o->nkept < 0) continue;
+      uint32_t kl = 0;
+      for (int32_t i = 0; i < o->nkept; ++i) {
+        memcpy(key + kl, &o->tid[i], 4); kl += 4;
+        memcpy(key + kl, &o->pos[i], 8); kl += 8;
+      }
+      if (!dedup_insert(dedup, key, kl)) { if (n_dupe_pairs) (*n_dupe_pairs)++; continue; }
+      uint64_t np = 0;
+      for (int32_t i = 0; i < o->nkept; ++i) {
+        if (!p->major[o->tid[i]]) continue;
+        pos0[np] = o->pos[i];
+        absp[np] = o->pos[i] + p->chrom_off[o->tid[i]];
+        ++np;
+      }
+      if (n_pos_out) *n_pos_out += np;
+      orc_varbin(pos0, absp, np, p->bin_starts, p->nbins, counts, st);
     }
-    if (n_pos_out) *n_pos_out += np;
-    orc_varbin(pos0, absp, np, p->bin_starts, p->nbins, counts, st);
   }
   free(out);
   return err;

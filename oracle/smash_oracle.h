@@ -134,7 +134,9 @@ int orc_mum(const orc_index *ix, const uint8_t *P, uint32_t L,
             uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr);
 
 /* ---- hit resolution (query.cpp:68-97, 231-306) -------------------------- */
-#define ORC_CIGAR_MAX 160
+#define ORC_CIGAR_MAX 1024   /* <= 254 matches x "255=255M" */
+#define ORC_MAX_MATCH 256     /* MAM/MUM matches per read: <= L - min_len + 1 <= 254 */
+#define ORC_ERR_CAP 9         /* a fixed oracle capacity would be exceeded: never truncate */
 typedef struct {
   uint32_t tid;          /* forward contig index = seq_index/2 */
   uint32_t rc;

@@ -114,6 +114,13 @@ uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, satu
 void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
 void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
 void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
+// mam.hip: smash_map_batch without the per-launch synchronisation of the
+// probe check (sync_check = false: the caller runs probe_check later)
+int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
+                   uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                   uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out, void *stream,
+                   bool sync_check);
+int probe_check(const smash_index *ix);   // synchronous; SMASH_OK or the probe error
 // mem.hip: smash_map_batch's MUM mode (MAM, then cleanMUMcand per read)
 int map_batch_mum(const smash_index *ix, uint32_t min_len, const uint8_t *seqs, uint64_t stride,
                   const uint16_t *lens, uint32_t len, uint64_t n_reads, uint64_t *out, uint32_t cap,

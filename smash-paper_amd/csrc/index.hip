@@ -49,7 +49,10 @@ void free_index(smash_index *ix) {
 }
 
 void upload_tables(smash_index *ix, hipStream_t s) {
-  if (!ix->d_work) ix->d_work = dalloc<uint64_t>(16);   // [0] work counter, [1..10] k_mam_sm probe check
+  if (!ix->d_work) {   // [0] work counter, [1..10] k_mam_sm's sticky probe check
+    ix->d_work = dalloc<uint64_t>(16);
+    SMASH_HIPX(hipMemsetAsync(ix->d_work, 0, 16 * 8, s));
+  }
   ix->d_startpos = dalloc<uint64_t>(ix->n_seq);
   ix->d_sizes = dalloc<uint64_t>(ix->n_seq);
   SMASH_HIPX(hipMemcpyAsync(ix->d_startpos, ix->startpos.data(), 8 * ix->n_seq,

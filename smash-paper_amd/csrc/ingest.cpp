@@ -5,7 +5,8 @@
 //  * smash_fastq_*: the FASTQ/FASTA lists of both mates (gzip or plain, zlib
 //    reads both), parsed as fastqs_to_sam.cpp:48-96 does (blank lines
 //    skipped, '@'/'>' records, name = first token after the marker, '+' line
-//    and qualities for '@' records, pairs with empty bases dropped), with
+//    and qualities for '@' records, a pair whose two mates have no bases
+//    dropped, a pair with ONE empty mate rejected), with
 //    replaceN (N -> Z, fastqs_to_sam.cpp:74 with argc == 4) and the
 //    NewQuery::extend lowercasing (query.cpp:125-144) applied on the way into
 //    the caller's (pinned) mate matrix: mate 2q = read 1, 2q + 1 = read 2.
@@ -150,35 +151,36 @@ struct Reader {
   }
 };
 
-// samtools sort -n (strnum_cmp): text runs bytewise, digit runs as numbers
+// samtools sort -n (bam_sort.c strnum_cmp; samtools is absent from the
+// reference and unpinned: this follows samtools 1.x): bytes compare one by
+// one; where both sides are at a digit, leading zeros are skipped, matching
+// digits walked, and the longer digit run wins, else the first differing
+// digit; a non-digit on either side compares the two bytes.  Names are
+// NUL-terminated within their n bytes.
 int strnum_cmp(const char *a, size_t na, const char *b, size_t nb) {
+  auto at = [](const char *s, size_t n, size_t i) -> int {
+    return i < n ? static_cast<unsigned char>(s[i]) : 0;
+  };
+  auto isd = [](int c) { return c >= '0' && c <= '9'; };
   size_t i = 0, j = 0;
-  bool digits = false;   // runs alternate text, digits, text, ... from the start
-  while (i < na || j < nb) {
-    if (i >= na) return -1;
-    if (j >= nb) return 1;
-    size_t ie = i, je = j;
-    auto isd = [](char c) { return c >= '0' && c <= '9'; };
-    while (ie < na && isd(a[ie]) == digits) ++ie;
-    while (je < nb && isd(b[je]) == digits) ++je;
-    if (!digits) {
-      const size_t m = std::min(ie - i, je - j);
-      const int c = memcmp(a + i, b + j, m);
-      if (c) return c < 0 ? -1 : 1;
-      if (ie - i != je - j) return ie - i < je - j ? -1 : 1;
+  while (at(a, na, i) && at(b, nb, j)) {
+    const int ca = at(a, na, i), cb = at(b, nb, j);
+    if (!isd(ca) || !isd(cb)) {
+      if (ca != cb) return ca - cb;
+      ++i;
+      ++j;
     } else {
-      size_t zi = i, zj = j;
-      while (zi < ie && a[zi] == '0') ++zi;
-      while (zj < je && b[zj] == '0') ++zj;
-      if (ie - zi != je - zj) return ie - zi < je - zj ? -1 : 1;
-      const int c = memcmp(a + zi, b + zj, ie - zi);
-      if (c) return c < 0 ? -1 : 1;
+      while (at(a, na, i) == '0') ++i;
+      while (at(b, nb, j) == '0') ++j;
+      while (isd(at(a, na, i)) && at(a, na, i) == at(b, nb, j)) ++i, ++j;
+      const int diff = at(a, na, i) - at(b, nb, j);
+      while (isd(at(a, na, i)) && isd(at(b, nb, j))) ++i, ++j;
+      if (isd(at(a, na, i))) return 1;
+      if (isd(at(b, nb, j))) return -1;
+      if (diff) return diff;
     }
-    i = ie;
-    j = je;
-    digits = !digits;
   }
-  return 0;
+  return at(a, na, i) ? 1 : at(b, nb, j) ? -1 : 0;
 }
 
 uint8_t g_lut[256];
@@ -263,7 +265,15 @@ extern "C" int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *le
     if (c1.end || c2.end) f->done = true;   // zip(): the shorter list ends the pairs
     for (uint64_t i = 0; i < n; ++i) {
       const uint64_t la = c1.boff[i + 1] - c1.boff[i], lb = c2.boff[i + 1] - c2.boff[i];
-      if (la == 0 || lb == 0) continue;   // fastqs_to_sam.cpp:80
+      if (la == 0 && lb == 0) continue;   // fastqs_to_sam.cpp:80 prints neither
+      if (la == 0 || lb == 0) {
+        // fastqs_to_sam.cpp:80 would print the other mate alone, which
+        // misaligns memsam's read-1 / read-2 alternation (query.cpp:486-505)
+        // for every later pair: such input is rejected, not silently changed
+        set_error("smash_fastq_read: one mate of a pair has no bases (" +
+                  std::string(c1.names.data() + c1.noff[i], c1.noff[i + 1] - c1.noff[i]) + ")");
+        return SMASH_ERR_ARG;
+      }
       const std::string na(c1.names.data() + c1.noff[i], c1.noff[i + 1] - c1.noff[i]);
       if (*len == 0) {
         if (la > 255) {

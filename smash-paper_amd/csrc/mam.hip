@@ -69,14 +69,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam(
 // 16 blocks (4 waves per SIMD, the VGPR limit) fit the CU's 160 KB.
 constexpr int kSmBlock = 64;
 
-template <class IdxT, bool STATS>
+template <class IdxT, bool STATS, bool CHECK>
 int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, size_t lds,
-           hipStream_t s) {
+           hipStream_t s, bool sync_check) {
   constexpr int B = kSmBlock;
-  // Every probe is checked against the span of the index arrays and the
-  // records: a wild address retires its lane and fails the call instead of
-  // faulting the GPU.
-  constexpr bool CHECK = true;
+  // CHECK: every probe is checked against the span of the index arrays and
+  // the records: a wild address retires its lane and fails the call instead
+  // of faulting the GPU.
   auto kern = sm::k_mam_sm<IdxT, B, CHECK, STATS>;
   int per_cu = 0, cus = 0;
   SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -97,24 +96,18 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
     SMASH_HIP(hipMalloc(&c.wave_stats, 64 * 8));
     SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 64 * 8, s));
   }
-  c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;   // d_work[1..10]
-  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 11 * 8, s));
+  // d_work[1..10]: sticky probe-check record (zeroed at index creation,
+  // never reset): the pipeline reads it at stats time, so a batch does not
+  // synchronise the stream (smash::probe_check)
+  c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;
+  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
   if (ix->kev[0]) SMASH_HIP(hipEventRecord(ix->kev[0], s));
   kern<<<unsigned(blocks), B, lds, s>>>(c);
   SMASH_HIP(hipGetLastError());
   if (ix->kev[1]) SMASH_HIP(hipEventRecord(ix->kev[1], s));
-  unsigned long long h[10];
-  SMASH_HIP(hipMemcpyAsync(h, c.viol, sizeof(h), hipMemcpyDeviceToHost, s));
-  SMASH_HIP(hipStreamSynchronize(s));
-  if (h[0]) {
-    char msg[512];
-    std::snprintf(msg, sizeof(msg),
-                  "k_mam_sm: %llu probes outside the index; first: state %llu op %llu addr %#llx "
-                  "addr2 %#llx prefix %llu depth %llu interval [%llu,%llu] read %llu",
-                  h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
-    std::fprintf(stderr, "%s\n", msg);
-    set_error(msg);
-    return SMASH_ERR_HIP;
+  if (CHECK && sync_check) {
+    SMASH_HIP(hipStreamSynchronize(s));
+    if (int rc = probe_check(ix)) return rc;
   }
   if (STATS) {
     std::vector<uint32_t> hv(n_reads);
@@ -157,7 +150,7 @@ template <class IdxT>
 int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
               uint64_t stride, const uint16_t *lens, uint32_t len,
               uint64_t n_reads, uint64_t *out, uint32_t cap, uint32_t *n_out,
-              hipStream_t s) {
+              hipStream_t s, bool sync_check) {
   constexpr int B = kSmBlock;
   const sm::Geom g = sm::make_geom(lens ? 255 : len);
   // read records (k_prep)
@@ -218,8 +211,10 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
     }
   }
   const size_t lds = size_t(B) * g.w_row * 4;
-  if (std::getenv("SMASH_SM_STATS")) return run_sm<IdxT, true>(ix, c, n_reads, lds, s);
-  return run_sm<IdxT, false>(ix, c, n_reads, lds, s);
+  if (std::getenv("SMASH_SM_STATS")) return run_sm<IdxT, true, true>(ix, c, n_reads, lds, s, true);
+  const char *ck = std::getenv("SMASH_SM_CHECK");
+  if (ck && ck[0] == '0') return run_sm<IdxT, false, false>(ix, c, n_reads, lds, s, sync_check);
+  return run_sm<IdxT, false, true>(ix, c, n_reads, lds, s, sync_check);
 }
 
 bool use_direct() {
@@ -260,14 +255,27 @@ int launch(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
 }  // namespace
 }  // namespace smash
 
-using namespace smash;
+namespace smash {
 
-extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len,
-                               const uint8_t *d_seqs, uint64_t stride,
-                               const uint16_t *d_lens, uint32_t len,
-                               uint64_t n_reads, uint64_t *d_out,
-                               uint32_t cap_per_read, uint32_t *d_n_out,
-                               void *stream) {
+// The sticky probe-check record of k_mam_sm (d_work[1..10]); synchronous.
+int probe_check(const smash_index *ix) {
+  unsigned long long h[10];
+  SMASH_HIP(hipMemcpy(h, ix->d_work + 1, sizeof(h), hipMemcpyDeviceToHost));
+  if (!h[0]) return SMASH_OK;
+  char msg[512];
+  std::snprintf(msg, sizeof(msg),
+                "k_mam_sm: %llu probes outside the index; first: state %llu op %llu addr %#llx "
+                "addr2 %#llx prefix %llu depth %llu interval [%llu,%llu] read %llu",
+                h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[9]);
+  std::fprintf(stderr, "%s\n", msg);
+  set_error(msg);
+  return SMASH_ERR_HIP;
+}
+
+int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
+                   uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                   uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out, void *stream,
+                   bool sync_check) {
   if (!ix || !d_seqs || !d_out || !d_n_out || cap_per_read == 0) {
     set_error("smash_map_batch: bad arguments");
     return SMASH_ERR_ARG;
@@ -306,9 +314,9 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
   if (!plain && !use_direct()) {
     if (ix->idx_bytes == 4)
       return launch_sm<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
-                                 cap_per_read, d_n_out, s);
+                                 cap_per_read, d_n_out, s, sync_check);
     return launch_sm<uint64_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
-                               cap_per_read, d_n_out, s);
+                               cap_per_read, d_n_out, s, sync_check);
   }
   if (ix->idx_bytes == 4)
     return plain ? launch<uint32_t, true>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
@@ -319,4 +327,20 @@ extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len
                                         d_out, cap_per_read, d_n_out, s)
                : launch<uint64_t, false>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,
                                          d_out, cap_per_read, d_n_out, s);
+}
+
+}  // namespace smash
+
+using namespace smash;
+
+// Synchronous w.r.t. the probe check: a probe outside the index fails this
+// call (the pipeline uses the asynchronous form and checks at stats time).
+extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len,
+                               const uint8_t *d_seqs, uint64_t stride,
+                               const uint16_t *d_lens, uint32_t len,
+                               uint64_t n_reads, uint64_t *d_out,
+                               uint32_t cap_per_read, uint32_t *d_n_out,
+                               void *stream) {
+  return map_batch_impl(ix, mode, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
+                        cap_per_read, d_n_out, stream, true);
 }

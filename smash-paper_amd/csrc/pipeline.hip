@@ -19,8 +19,13 @@
 #include "mam_device.hpp"
 
 namespace {
-constexpr int MAXA = 48;        // alignments per mate kept on chip
 constexpr int kB = 256;
+// k_post (the general per-pair body) keeps a mate's alignments and both
+// mates' hit lists in a per-thread slice of a global workspace sized for the
+// largest possible mate (slots = L - min_len + 1 matches), so no input is
+// ever cut; it runs as a bounded grid-stride launch of kPostThreads threads.
+constexpr unsigned kPostBlocks = 64;
+constexpr unsigned kPostThreads = kPostBlocks * kB;
 enum Stat { S_PAIRS, S_KEYPAIRS, S_DUPEPAIRS, S_POS, S_DUPS, S_KEPT, S_MATCHES, S_ERR, S_N };
 }  // namespace
 
@@ -55,6 +60,7 @@ struct smash_pipeline {
   int64_t *d_prev = nullptr;      // [2] carried {last pos0 or -1, -}
   unsigned long long *d_stats = nullptr;
   uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast -> k_post pair list
+  uint8_t *d_post_ws = nullptr;   // k_post workspace: kPostThreads slices
   bool post_fast = false;
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
@@ -111,11 +117,10 @@ __device__ inline unsigned mapb(const PostCfg &c, uint64_t at) {
 
 // resolve + merge + to_print order + tags for one mate; returns #hits
 __device__ int mate_hits(const PostCfg &c, const uint64_t *m, uint32_t n,
-                         Hit *hits, int32_t &err) {
-  Aln a[MAXA];
+                         Hit *hits, Aln *a, int32_t &err) {
   int na = 0;
   const uint32_t L = c.L;
-  for (uint32_t k = 0; k < n && k < MAXA; ++k) {
+  for (uint32_t k = 0; k < n; ++k) {
     const uint64_t w = m[k];
     const uint64_t ref = w & 0xFFFFFFFFFFFFull;
     const uint32_t q = uint32_t((w >> 48) & 0xFF), len = uint32_t(w >> 56);
@@ -146,7 +151,6 @@ __device__ int mate_hits(const PostCfg &c, const uint64_t *m, uint32_t n,
     x.pos = pos;
     if (pos >= 0) a[na++] = x;            // erase pos < 0 (query.cpp:239-246)
   }
-  if (n > MAXA) err = SMASH_ERR_UNSUPPORTED;
   // insertion sort by to_merge (distinct keys: no ties)
   for (int i = 1; i < na; ++i) {
     Aln t = a[i];
@@ -208,17 +212,24 @@ __device__ inline uint64_t mix64(uint64_t z) {
 
 // the general per-pair body (any number of matches, per-thread arrays);
 // k_post_fast hands it the pairs whose mates exceed its register capacity
+// workspace slice of one k_post thread: slots Aln, then 2 * slots Hit
+__host__ __device__ inline uint64_t post_ws_bytes(uint32_t slots) {
+  return (uint64_t(slots) * sizeof(Aln) + 2ull * slots * sizeof(Hit) + 15) & ~uint64_t(15);
+}
+
 __device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restrict__ match,
                                        const uint32_t *__restrict__ nmatch, uint64_t q,
                                        int32_t *nk_out, uint32_t *nmajor_out,
                                        uint64_t *hits_out, uint64_t *hash_out, int32_t &err,
-                                       unsigned long long &nm) {
+                                       unsigned long long &nm, uint8_t *ws) {
   {
-    Hit h1[MAXA], h2[MAXA];
+    Aln *a = reinterpret_cast<Aln *>(ws);
+    Hit *h1 = reinterpret_cast<Hit *>(ws + uint64_t(c.slots) * sizeof(Aln));
+    Hit *h2 = h1 + c.slots;
     const uint32_t n1 = nmatch[2 * q], n2 = nmatch[2 * q + 1];
     nm = n1 + n2;
-    const int k1 = mate_hits(c, match + (2 * q) * c.slots, n1 < c.slots ? n1 : c.slots, h1, err);
-    const int k2 = mate_hits(c, match + (2 * q + 1) * c.slots, n2 < c.slots ? n2 : c.slots, h2, err);
+    const int k1 = mate_hits(c, match + (2 * q) * c.slots, n1 < c.slots ? n1 : c.slots, h1, a, err);
+    const int k2 = mate_hits(c, match + (2 * q + 1) * c.slots, n2 < c.slots ? n2 : c.slots, h2, a, err);
     if (n1 > c.slots || n2 > c.slots) err = SMASH_ERR_UNSUPPORTED;
     // smashMEM excess-mappability filter (smashMEM.py:84-92)
     int m1 = 0, m2 = 0;
@@ -286,30 +297,25 @@ __device__ __forceinline__ void post_stats(unsigned long long nm, unsigned long 
 }
 
 // general path: every pair (list == nullptr), or the pairs listed by
-// k_post_fast (grid-stride over *n_list)
+// k_post_fast; grid-stride, kPostThreads threads, one workspace slice each
 __global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restrict__ match,
                                              const uint32_t *__restrict__ nmatch,
                                              uint64_t n_pairs, const uint32_t *list,
                                              const uint32_t *n_list, int32_t *nk_out,
                                              uint32_t *nmajor_out, uint64_t *hits_out,
-                                             uint64_t *hash_out, unsigned long long *stats) {
+                                             uint64_t *hash_out, unsigned long long *stats,
+                                             uint8_t *ws) {
   int32_t err = 0;
   unsigned long long nm = 0, np = 0;
-  if (!list) {
-    const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (q < n_pairs) {
-      post_pair(c, match, nmatch, q, nk_out, nmajor_out, hits_out, hash_out, err, nm);
-      np = 1;
-    }
-  } else {
-    const uint32_t n = *n_list;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += gridDim.x * blockDim.x) {
-      unsigned long long m = 0;
-      post_pair(c, match, nmatch, list[i], nk_out, nmajor_out, hits_out, hash_out, err, m);
-      nm += m;
-      ++np;
-    }
+  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint8_t *my = ws + t * post_ws_bytes(c.slots);
+  const uint64_t n = list ? *n_list : n_pairs;
+  for (uint64_t i = t; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+    unsigned long long m = 0;
+    post_pair(c, match, nmatch, list ? list[i] : i, nk_out, nmajor_out, hits_out, hash_out, err,
+              m, my);
+    nm += m;
+    ++np;
   }
   post_stats(nm, np, err, stats);
 }
@@ -637,6 +643,11 @@ __global__ void k_tail(const uint32_t *npos_p, const int64_t *pos0, int64_t *pre
   if (prev && n) prev[0] = last;
 }
 
+__global__ void k_reset_prev(int64_t *prev) {
+  prev[0] = -1;
+  prev[1] = -1;
+}
+
 int check_pipe(smash_pipeline *p, uint64_t n_pairs) {
   if (!p) { set_error("null pipeline"); return SMASH_ERR_ARG; }
   if (n_pairs > p->max_pairs) {
@@ -746,6 +757,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * S_N));
     p->d_send_q = dalloc<uint32_t>(P);
     p->d_fb = dalloc<uint32_t>(P + 1);
+    p->d_post_ws = dalloc<uint8_t>(uint64_t(kPostThreads) * post_ws_bytes(p->slots));
     {
       bool ok = ix->n_seq <= kSeqLds && p->n_contig < 0x7FFF;
       for (uint64_t z : ix->sizes) ok = ok && z < (1ull << 31);
@@ -779,7 +791,8 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
-                  (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb})
+                  (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb,
+                  (void *)p->d_post_ws})
     dfree(q);
   delete p;
 }
@@ -804,9 +817,9 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
     p->ix->kev[0] = p->ev[2 * p->n_ev];          // recorded around k_mam_sm itself
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
-  rc = smash_map_batch(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len,
-                       nullptr, p->read_len, 2 * n_pairs, p->d_match, p->slots,
-                       p->d_nmatch, stream);
+  rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
+                      p->read_len, 2 * n_pairs, p->d_match, p->slots, p->d_nmatch, stream,
+                      false);   // no per-batch sync: the probe check runs at stats time
   p->ix->kev[0] = p->ix->kev[1] = nullptr;
   if (rc) return rc;
   if (p->prof) {
@@ -819,13 +832,13 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
         post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_fb + 1, p->d_fb, p->d_nk,
         p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
     SMASH_HIP(hipGetLastError());
-    k_post<<<256, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_fb + 1,
-                              p->d_fb, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash,
-                              p->d_stats);
+    k_post<<<kPostBlocks, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs,
+                                      p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, p->d_hits,
+                                      p->d_hash, p->d_stats, p->d_post_ws);
   } else {
-    k_post<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
-        post_cfg(p), p->d_match, p->d_nmatch, n_pairs, nullptr, nullptr, p->d_nk,
-        p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+    k_post<<<kPostBlocks, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs, nullptr,
+                                      nullptr, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash,
+                                      p->d_stats, p->d_post_ws);
   }
   SMASH_HIP(hipGetLastError());
   // in-batch ordering for de-dup: stable radix sort of key hi, value = pair
@@ -1041,6 +1054,7 @@ extern "C" int smash_pipeline_stats(smash_pipeline *p, smash_stats *o) {
   SMASH_HIP(hipSetDevice(p->device));
   if (p->last) SMASH_HIP(hipStreamSynchronize(p->last));
   SMASH_HIP(hipDeviceSynchronize());
+  if (int rc = probe_check(p->ix)) return rc;   // k_mam_sm's sticky probe check
   unsigned long long st[S_N];
   SMASH_HIP(hipMemcpy(st, p->d_stats, sizeof(st), hipMemcpyDeviceToHost));
   o->pairs = st[S_PAIRS];
@@ -1074,9 +1088,8 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   SMASH_HIP(hipSetDevice(p->device));
   SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * (p->table_mask + 1), s));
   SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * S_N, s));
-  static const int64_t init[2] = {-1, -1};
-  SMASH_HIP(hipMemcpyAsync(p->d_prev, init, 16, hipMemcpyHostToDevice, s));
-  SMASH_HIP(hipStreamSynchronize(s));
+  k_reset_prev<<<1, 1, 0, s>>>(p->d_prev);   // no host source: stays asynchronous
+  SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }
 

@@ -29,6 +29,7 @@ smash_mapping.sh:23), read 1 before read 2.
 from __future__ import annotations
 
 import argparse
+import functools
 import gzip
 import os
 import re
@@ -80,8 +81,10 @@ def fastq_records(path):
 
 def fastq_pairs(r1s, r2s):
     """Interleaved mates of the FASTQ lists (zcat r1s / zcat r2s, as
-    smash_mapping.sh:19 feeds fastqs_to_sam); records with empty bases are
-    dropped as fastqs_to_sam drops them (fastqs_to_sam.cpp:80)."""
+    smash_mapping.sh:19 feeds fastqs_to_sam); a pair whose mates both have no
+    bases is dropped (fastqs_to_sam.cpp:80 prints neither); a pair with ONE
+    empty mate is an error (fastqs_to_sam would print the other mate alone,
+    misaligning memsam's mate alternation, query.cpp:486-505)."""
     def chain(paths):
         for p in paths:
             yield from fastq_records(p)
@@ -89,6 +92,8 @@ def fastq_pairs(r1s, r2s):
     for a, b in zip(chain(r1s), chain(r2s)):
         if a[2] and b[2]:
             out.append((a[0], a[2], b[2]))
+        elif a[2] or b[2]:
+            raise SystemExit("one mate of pair %s has no bases" % a[0].decode(errors="replace"))
     return out
 
 
@@ -111,13 +116,48 @@ def sam_pairs(path):
     return out
 
 
-_DIG = re.compile(rb"(\d+)")
+def strnum_cmp(a: bytes, b: bytes) -> int:
+    """samtools sort -n's strnum_cmp (bam_sort.c, samtools 1.x; samtools is
+    absent here, so the version is unpinned): bytes compare one by one; where
+    both sides are at a digit, leading zeros are skipped, matching digits
+    walked, the longer digit run wins, else the first differing digit."""
+    i = j = 0
+    na, nb = len(a), len(b)
+
+    def at(s, n, k):
+        return s[k] if k < n else 0
+
+    def isd(c):
+        return 48 <= c <= 57
+    while at(a, na, i) and at(b, nb, j):
+        ca, cb = at(a, na, i), at(b, nb, j)
+        if not isd(ca) or not isd(cb):
+            if ca != cb:
+                return ca - cb
+            i += 1
+            j += 1
+        else:
+            while at(a, na, i) == 48:
+                i += 1
+            while at(b, nb, j) == 48:
+                j += 1
+            while isd(at(a, na, i)) and at(a, na, i) == at(b, nb, j):
+                i += 1
+                j += 1
+            diff = at(a, na, i) - at(b, nb, j)
+            while isd(at(a, na, i)) and isd(at(b, nb, j)):
+                i += 1
+                j += 1
+            if isd(at(a, na, i)):
+                return 1
+            if isd(at(b, nb, j)):
+                return -1
+            if diff:
+                return diff
+    return 1 if at(a, na, i) else -1 if at(b, nb, j) else 0
 
 
-def strnum_key(name: bytes):
-    """samtools sort -n order (strnum_cmp): digit runs compare numerically."""
-    parts = _DIG.split(name)
-    return tuple((0, p) if i % 2 == 0 else (1, int(p)) for i, p in enumerate(parts))
+strnum_key = functools.cmp_to_key(strnum_cmp)
 
 
 def reads_matrix(pairs):

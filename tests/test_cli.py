@@ -69,6 +69,35 @@ def test_strnum_key_orders_like_samtools_sort_n():
     assert got.index(b"r1") < got.index(b"r9")
 
 
+# samtools 1.x strnum_cmp (bam_sort.c) worked by hand: a non-digit on either
+# side compares the two bytes, so a byte below '0' sorts before a digit run
+STRNUM_CASES = [
+    (b"x-5", b"x5", -1),      # '-' (45) < '5'
+    (b"a-", b"a1", -1),       # '-' < '1'
+    (b"r.1", b"r1", -1),      # '.' (46) < '1'
+    (b"r/2", b"r10", -1),     # '/' (47) < '1'
+    (b"r 9", b"r1", -1),      # ' ' (32) < '1'
+    (b"r9", b"r10", -1),      # longer digit run wins
+    (b"r009", b"r10", -1),    # leading zeros skipped
+    (b"r01", b"r1", 0),       # equal as numbers: samtools keeps input order
+    (b"r1a", b"r01b", -1),    # then the bytes after the run
+    (b"r1", b"r1a", -1),      # a prefix sorts first
+    (b"a10b2", b"a10b10", -1),
+    (b"ra", b"r5", 1),        # 'a' (97) > '5'
+]
+
+
+@pytest.mark.parametrize("a,b,sign", STRNUM_CASES)
+def test_strnum_cmp_hand_cases(a, b, sign):
+    c = smash_cli.strnum_cmp(a, b)
+    assert (c > 0) - (c < 0) == sign
+    c = smash_cli.strnum_cmp(b, a)
+    assert (c > 0) - (c < 0) == -sign
+    # the native port orders the pair the same way (stable on ties)
+    got = S.strnum_order(np.array([a, b], "S16")).tolist()
+    assert got == ([1, 0] if sign > 0 else [0, 1])
+
+
 # ---------------------------------------------------------------------------
 # GPU: the device-backed subcommands
 # ---------------------------------------------------------------------------
@@ -184,12 +213,12 @@ def test_native_fastq_reader_equals_fastqs_to_sam(tmp_path, s):
 
 
 def test_native_fastq_reader_edge_cases(tmp_path):
-    """Blank lines, '+name' lines, '>' records, a pair with empty bases
-    dropped (fastqs_to_sam.cpp:80); N -> z; a mate of another length is an
-    error (the device batches have one read length)."""
+    """Blank lines, '+name' lines, '>' records, a pair whose mates both have
+    no bases dropped (fastqs_to_sam.cpp:80 prints neither); N -> z; a mate of
+    another length is an error (the device batches have one read length)."""
     a, b = tmp_path / "a.fq", tmp_path / "b.fq"
     a.write_bytes(b"@a1 1:N:0\nACGTNNAC\n+\nIIIIIIII\n\n@a3 x y\n\n+\n\n>f1 opt\nACGNTACG\n")
-    b.write_bytes(b"@b1 2:N:0\r\nTTTTNNTT\r\n+b1\r\nIIIIIIII\r\n@b3 z\nCCCC\n+\nJJJJ\n"
+    b.write_bytes(b"@b1 2:N:0\r\nTTTTNNTT\r\n+b1\r\nIIIIIIII\r\n@b3 z\n\n+\n\n"
                   b">f2\nNNNNACGT")
     exp = smash_cli.fastq_pairs([str(a)], [str(b)])
     assert [p[0] for p in exp] == [b"a1", b"f1"]
@@ -202,9 +231,22 @@ def test_native_fastq_reader_edge_cases(tmp_path):
         S.read_fastq_pairs(["/nonexistent.fq"], [gold("edge_r2.fq")])
 
 
+def test_one_empty_mate_is_an_error(tmp_path):
+    """fastqs_to_sam.cpp:80 drops only the empty record and prints its mate
+    alone, which shifts memsam's read-1 / read-2 alternation (query.cpp:486-
+    505) for every later pair; both readers reject such input instead."""
+    a, b = tmp_path / "a.fq", tmp_path / "b.fq"
+    a.write_bytes(b"@p1\nACGT\n+\nIIII\n@p2\n\n+\n\n")
+    b.write_bytes(b"@p1\nTTTT\n+\nIIII\n@p2\nCCCC\n+\nJJJJ\n")
+    with pytest.raises(SystemExit, match="no bases"):
+        smash_cli.fastq_pairs([str(a)], [str(b)])
+    with pytest.raises(S.SmashError, match="no bases"):
+        S.read_fastq_pairs([str(a)], [str(b)])
+
+
 def test_native_strnum_order_equals_samtools_key():
     rng = np.random.default_rng(5)
-    alpha = list("ab:_") + [str(d) for d in range(10)]
+    alpha = list("ab:_-./ ") + [str(d) for d in range(10)]
     names = [bytes("".join(rng.choice(alpha, rng.integers(1, 12))), "ascii") for _ in range(3000)]
     names += [b"r10", b"r9", b"r009", b"r1", b"", b"0", b"00", b"a2b10", b"a2b9"]
     arr = np.array(names, "S16")

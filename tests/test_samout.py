@@ -210,3 +210,26 @@ def test_device_records_equal_restatement(tiny_fa, tiny_ix, tables, s):
     for r in range(reads.shape[0]):
         a, b = got[r * cap:r * cap + cnt[r]], exp[r * cap:r * cap + cnt[r]]
         assert a.tobytes() == b.tobytes(), (r, a, b)
+
+
+def _golden_full(s, tagged):
+    return sorted(read_gz_lines("%s_mapout%s_full.txt.gz" % (s, "_tagged" if tagged else "")))
+
+
+@pytest.mark.parametrize("tagged", [False, True])
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_formatter_full_lines_equal_reference(tiny_ix, tables, s, tagged):
+    """Every column (SEQ reverse-complemented on '-' hits, QUAL reversed, the
+    XO:Z comment from fastqs_to_sam) against the reference's own mapout of
+    smash_mapping.sh:19 as written (-verbose -rcref -qthreads 12 -nomap
+    -samin -samout) and, tagged, after mappability_tag (:23)."""
+    mapbin, offsets, small = tables
+    names, seqs, quals, opts, reads = load_sam_input(s)
+    triples = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+               for l in read_gz_lines("%s_MAM.txt.gz" % s)]
+    cap = reads.shape[1] - 20 + 1
+    rec, cnt = py_records(tiny_ix, mapbin, offsets, reads, triples, cap)
+    text, terr = S.sam_format(tiny_ix.contigs, rec, cnt, cap, names, seqs, quals, opts,
+                              nomap=True, tag=tagged, small_chr=small)
+    assert terr == 0
+    assert sorted(text.decode().splitlines()) == _golden_full(s, tagged)

@@ -41,6 +41,29 @@ __global__ __launch_bounds__(256) void k_chase(const uint4 *buf, uint64_t n16, i
   if (acc == 0x123456789ull) sink[0] = acc;
 }
 
+// W 16-byte loads per step into ONE 64-byte line (W = 2: the kernel's
+// addr/addr2 pairs; W = 4: the whole line): does a second request to a line
+// cost at the random-request ceiling?
+template <int W>
+__global__ __launch_bounds__(256) void k_chase_line(const uint4 *buf, uint64_t n16, int steps,
+                                                    uint64_t *sink, uint64_t seed) {
+  const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  uint64_t h = mix(t + seed);
+  uint64_t acc = 0;
+  for (int s = 0; s < steps; ++s) {
+    const uint64_t i = (h % n16) & ~uint64_t(3);
+    uint4 v[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) v[k] = buf[i + k];
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) x += v[k].x ^ v[k].w;
+    acc += x;
+    h = mix(h + x + 1);
+  }
+  if (acc == 0x123456789ull) sink[0] = acc;
+}
+
 int main(int argc, char **argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -62,7 +85,11 @@ int main(int argc, char **argv) {
     return 0;
   }
   std::vector<double> gib;
-  for (int i = 1; i < argc; ++i) gib.push_back(std::atof(argv[i]));
+  bool lines = false;   // "lines": W = 1, 2, 4 loads per 64-byte line
+  for (int i = 1; i < argc; ++i) {
+    if (std::string(argv[i]) == "lines") lines = true;
+    else gib.push_back(std::atof(argv[i]));
+  }
   if (gib.empty()) gib = {0.25, 4, 32, 128};
   uint64_t *sink;
   CK(hipMalloc(&sink, 8));
@@ -72,6 +99,34 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&buf, bytes));
     CK(hipMemset(buf, 0, bytes));
     const uint64_t n16 = bytes / 16;
+    if (lines) {
+      const int wps = 4, steps = 64;
+      const uint64_t threads = uint64_t(wps) * 4 * cus * 64;
+      for (int w : {1, 2, 4}) {
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+        auto launch = [&](uint64_t seed) {
+          if (w == 1) k_chase_line<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
+          else if (w == 2) k_chase_line<2><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
+          else k_chase_line<4><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
+        };
+        launch(1);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        for (int r = 0; r < 3; ++r) launch(100 + r);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        const double ln = 3.0 * threads * steps;
+        std::printf("footprint %8.3f GiB  waves/SIMD %d  %d x 16 B per line : %.3f G lines/s  %.3f G loads/s\n",
+                    g, wps, w, ln / (ms * 1e-3) * 1e-9, w * ln / (ms * 1e-3) * 1e-9);
+        std::fflush(stdout);
+        CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
+      }
+      CK(hipFree(buf));
+      continue;
+    }
     for (int wps : {4, 8}) {
       for (int ilp : {1, 4}) {
         const uint64_t threads = uint64_t(wps) * 4 * cus * 64;
