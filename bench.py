@@ -1,25 +1,33 @@
 #!/usr/bin/env python
 """bench.py -- reads/s mapped + binned on MI355X (BASELINE.json metric).
 
-Workload (default --config c3, the 1-GPU configuration BASELINE.json's metric
-is quoted on: "hg19, 150 bp", sample_bins/50000): the hg19-shaped synthetic
-genome (tools/synth.py: hg19 contig lengths, N runs over the assembly gaps,
+Workload (default --config c3, BASELINE.json configs[2], the 1-GPU
+configuration its metric is quoted on: "hg19, 50M synthetic 150 bp reads,
+1xMI355X, sample_bins/50000"): the hg19-shaped synthetic genome
+(tools/synth.py: hg19 contig lengths, N runs over the assembly gaps,
 repeats; 3.1 Gbp, doubled text N = 6.19e9, 64-bit SA/ISA) is indexed ON THE
-DEVICE and kept resident in HBM; every rank holds its own batch of synthetic
-150 bp SMASH read pairs in HBM.  One step = one complete independent run of
-the hot path over that batch (fresh pair-key set and adjacent-dup state):
-MAM search -> resolve -> mappability tag -> smashMEM filters -> global pair
-de-dup -> varbin adjacent de-dup -> bin counts (+ the multi-GPU exchanges and
-the RCCL all-reduce of the count vector when N > 1).  value = reads (mates)
-processed by all ranks / max-over-ranks wall time of the K timed steps.
+DEVICE and kept resident in HBM; each rank's 25 M synthetic 150 bp SMASH
+read pairs (50 M reads, 7.5 GB; generated on the device by tools/readgen.hip)
+are resident in HBM before the timed region.  One step = one complete run of
+the hot path over those 50 M reads, as the reference scripts run one sample:
+13 batches of <= 2 M pairs through MAM search -> resolve -> mappability tag
+-> smashMEM filters -> global first-wins pair de-dup (one 25 M-key set for
+the whole run) -> varbin adjacent de-dup (carried across batches) -> bin
+counts; with N ranks each rank runs its own 25 M pairs (400 M reads at N = 8
+is BASELINE config C4) plus the de-dup all_to_all, the tail all_gather and
+the RCCL all_reduce of the count vector.  value = reads processed by all
+ranks / max-over-ranks wall time of the K timed steps.
 
 Also reported: `roofline` of the dominant kernel (k_mam_sm: algorithmic bytes
 = 64 B x the line transitions of the kernel's own probe sequence, counted by
 running the kernel source on the host (tools/sm_emu) over the downloaded index
-for a sample of the same reads, over the HIP-event-timed kernel duration) and
-`cpu_baseline` (the C oracle of the whole chain on the host cores, rank 0,
-N = 1, bounded sample).  The bench also checks that the device's bin counts on
-that sample are identical to the oracle's.
+for a sample of the same reads, over the HIP-event-timed kernel duration),
+`cpu_baseline` (the C oracle of the whole chain and of the search alone, on
+all os.cpu_count() host threads, rank 0, N = 1, bounded sample of the same
+reads; the device's counts on that sample must be identical) and `c5`
+(BASELINE config C5 on the same resident index: the map.bin self-scan of
+every forward base with unique-36-mer counts, bases/s, its roofline and a CPU
+baseline).
 """
 import argparse
 import json
@@ -38,22 +46,24 @@ METRIC = ("reads/sec mapped+binned (hg19, 150 bp) at 1/2/4/8 MI355X; "
           "bit-exact bin counts")
 
 CONFIGS = {
-    # BASELINE.json configs[2]: hg19, 150 bp, sample_bins/50000 (metric's config)
-    "c3": dict(genome="hg19", read_len=150, pairs=2_000_000, bins="50000", seed=3,
-               workload="C3 hg19-shaped 150 bp SMASH reads, sample_bins/50000"),
+    # BASELINE.json configs[2]: hg19, 50 M x 150 bp, sample_bins/50000 (the
+    # metric's config); configs[3] (C4) is this at N = 8: 400 M reads
+    "c3": dict(genome="hg19", read_len=150, pairs=25_000_000, batch=2_000_000, bins="50000",
+               seed=3, workload="C3 hg19-shaped, 50 M x 150 bp SMASH reads per rank "
+                                "(25 M pairs, 13 batches, one run), sample_bins/50000"),
     # configs[1]: hg19 1M x 100 bp, sample_bins/100000 (synthesized 2-way split)
-    "c2": dict(genome="hg19", read_len=100, pairs=500_000, bins="100000", seed=2,
+    "c2": dict(genome="hg19", read_len=100, pairs=500_000, batch=500_000, bins="100000", seed=2,
                workload="C2 hg19-shaped 1M x 100 bp SMASH reads, sample_bins/100000"),
     # configs[0]-like plumbing on the chr21-sized genome (bins split 10-way)
-    "c1": dict(genome="chr21", read_len=100, pairs=500_000, bins="500000", seed=1,
-               workload="C1-shaped chr21-sized genome, 100 bp, sample_bins/500000"),
+    "c1": dict(genome="chr21", read_len=100, pairs=5_000, batch=5_000, bins="500000", seed=1,
+               workload="C1 chr21-sized genome, 10 k x 100 bp, sample_bins/500000"),
     # configs[4]: whole-genome mappability self-scan (every 36-mer), C5
     "c5": dict(genome="hg19", bins="50000", k=36,
                workload="C5 hg19-shaped mappability self-scan (map.bin + unique 36-mer "
                         "counts per chromosome and per 50 k bin)"),
     # quick functional run
-    "mid": dict(genome="mid", read_len=150, pairs=200_000, bins="synthetic", seed=2,
-                workload="3.2 Mbp synthetic genome, 150 bp (functional check)"),
+    "mid": dict(genome="mid", read_len=150, pairs=200_000, batch=200_000, bins="synthetic",
+                seed=2, workload="3.2 Mbp synthetic genome, 150 bp (functional check)"),
 }
 
 
@@ -148,31 +158,24 @@ def host_index(S, O, dix, T, sp, sz, names, sample_reads=None):
     return oix, mp
 
 
-def bench_c5(args, cfg, world, rank, local, dist):
-    """C5: map.bin of every forward base (longSA::show) + unique 36-mer counts,
-    bases split into `world` contiguous ranges, counts all-reduced."""
+def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps=3):
+    """C5 on the resident index: map.bin bytes of every forward base (longSA::
+    show) + unique 36-mer counts per contig and per bin, bases split into
+    `world` contiguous ranges, counts all-reduced.  Returns (json, per-rep s)."""
     import torch
     import smashgpu as S
-    import synth
-    dev = torch.device("cuda", local)
-    t0 = time.time()
-    contigs = synth.make_genome(cfg["genome"])
-    T, sp, sz, names = S.text_from_contigs(contigs)
-    dix = S.Index.create(T, sp, sz, names, device=local)
-    log("device index: %.1f s, %.1f GB in HBM" % (dix.info.build_seconds,
-                                                  dix.info.device_bytes / 1e9))
-    starts = bin_starts_for(cfg, contigs, tempfile.mkdtemp())
-    cs = chrom_sizes_for(cfg, contigs)
+    starts = bin_starts_for(dict(bins=cfg_bins), contigs, tempfile.mkdtemp())
+    cs = chrom_sizes_of(contigs)
     off = np.array([cs.get(c, -1) if ("_" not in c and c != "chrM") else -1
                     for c in dix.contigs], np.int64)
     total = int(sum(dix.contig_sizes))
     g0, g1 = total * rank // world, total * (rank + 1) // world
-    k = cfg["k"]
+    k = 36
     d_bins = torch.from_numpy(starts).to(dev)
     bc = torch.zeros(len(starts), dtype=torch.int64, device=dev)
     cc = torch.zeros(len(dix.contigs), dtype=torch.int64, device=dev)
     out = torch.empty(2 * (g1 - g0), dtype=torch.uint8, device=dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
 
     def step(i, timed):
         bc.zero_()
@@ -186,14 +189,12 @@ def bench_c5(args, cfg, world, rank, local, dist):
             dist.all_reduce(bc)
             dist.all_reduce(cc)
 
-    for i in range(args.warmup):
-        step(i, False)
+    step(0, False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(reps):
         step(i, True)
     torch.cuda.synchronize()
     if world > 1:
@@ -203,54 +204,83 @@ def bench_c5(args, cfg, world, rank, local, dist):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.steps)) / args.steps
-    # full-size properties: the scan reproduces the build's map.bin bytes
-    dmap = S.download(dix.info.d_map, dix.info.map_bytes)
-    same_map = bool(np.array_equal(out.cpu().numpy(), dmap[2 + 2 * g0:2 + 2 * g1]))
+    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)) / reps
+    # the scan reproduces the index build's map.bin (compared on the device)
+    dmap = S.device_view(dix.info.d_map, dix.info.map_bytes, torch.uint8)
+    same_map = bool(torch.equal(out, dmap[2 + 2 * g0:2 + 2 * g1]))
     n_uniq = int(cc.sum().item())
-    value = total * args.steps / el
-    log("timed %d steps: %.3f s -> %.3e bases/s; scan %.1f ms; unique %d-mers %d; "
-        "map == build map: %s" % (args.steps, el, value, kms, k, n_uniq, same_map))
+    value = total * reps / el
     bpb = 2 * dix.info.idx_bytes + 2 * 64 + 2
     achieved = (g1 - g0) * bpb / (kms / 1e3) / 1e9
-    out_j = {
-        "metric": "bases/sec mappability self-scan (hg19, every 36-mer; map.bin + unique "
-                  "counts, C5)",
-        "value": value, "unit": "bases/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1000.0 * el / args.steps,
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-        "dtype": "u8/u64 (integer)", "data": "synthetic (tools/synth.py hg19-shaped genome)",
-        "config": {"workload": cfg["workload"], "genome": cfg["genome"], "bases": total,
-                   "k": k, "bins": int(len(starts)),
-                   "parallelism": "%d contiguous base ranges, all_reduce counts" % world},
-        "roofline": {"bound": "hbm", "kernel": "k_mapscan", "achieved": round(achieved, 2),
-                     "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
-                     "traffic": None, "bytes_per_base": bpb,
-                     "bytes_method": "2 sequential ISA reads + 2 random 64-B LCP lines "
-                                     "+ 2 output bytes per base",
-                     "avg_kernel_ms": round(kms, 3)},
-        "map_identical_to_index_build": same_map, "unique_kmers": n_uniq,
-        "cpu_baseline": None,
-    }
+    res = {"metric": "bases/sec mappability self-scan (hg19, every 36-mer; map.bin + unique "
+                     "counts, C5)",
+           "value": value, "unit": "bases/s", "ms_per_scan": 1000.0 * el / reps,
+           "scaling": "strong", "bases": total, "k": k, "bins": int(len(starts)),
+           "roofline": {"bound": "hbm", "kernel": "k_mapscan", "achieved": round(achieved, 2),
+                        "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
+                        "traffic": None, "bytes_per_base": bpb,
+                        "bytes_method": "2 sequential ISA reads + 2 random 64-B LCP lines "
+                                        "+ 2 output bytes per base",
+                        "avg_kernel_ms": round(kms, 3)},
+           "map_identical_to_index_build": same_map, "unique_kmers": n_uniq,
+           "cpu_baseline": None}
+    log("C5: %d reps %.3f s -> %.3e bases/s; scan %.1f ms; unique %d-mers %d; map == build: %s"
+        % (reps, el, value, kms, k, n_uniq, same_map))
+    if oix is not None and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # oracle/smash_oracle.c orc_mappability_range on every host thread,
+        # contiguous sub-windows of one window in the middle of the genome
+        from concurrent.futures import ThreadPoolExecutor
+        threads = os.cpu_count() or 1
+        n0 = 1 << 18
+        t3 = time.perf_counter()
+        oix.mappability_range(g0, g0 + n0, k)
+        rate1 = n0 / (time.perf_counter() - t3)
+        n1 = int(min(g1 - g0, max(n0, rate1 * threads * args.cpu_seconds / 3)))
+        a = (g1 - g0 - n1) // 2 + g0
+        cuts = [a + n1 * j // threads for j in range(threads + 1)]
+        t3 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            parts = list(ex.map(lambda j: oix.mappability_range(cuts[j], cuts[j + 1], k)[0],
+                                range(threads)))
+        dt = time.perf_counter() - t3
+        got = np.concatenate(parts)
+        dev_part = out[2 * (a - g0):2 * (a - g0 + n1)].cpu().numpy()
+        exact = bool(np.array_equal(got, dev_part))
+        res["cpu_baseline"] = {
+            "value": n1 / dt, "unit": "bases/s", "cores": threads, "kind": "port",
+            "sample": "%d consecutive forward bases from %d (oracle/smash_oracle.c "
+                      "orc_mappability_range, %d threads), %.1f s" % (n1, a, threads, dt),
+            "map_identical_to_device": exact}
+        log("C5 cpu baseline: %.3e bases/s on %d threads; identical: %s"
+            % (n1 / dt, threads, exact))
+    return res
+
+
+def bench_c5(args, cfg, world, rank, local, dist):
+    """--config c5: the C5 scan as the headline line."""
+    import torch
+    import smashgpu as S
+    import synth
+    dev = torch.device("cuda", local)
+    contigs = synth.make_genome(cfg["genome"])
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    dix = S.Index.create(T, sp, sz, names, device=local)
+    log("device index: %.1f s, %.1f GB in HBM" % (dix.info.build_seconds,
+                                                  dix.info.device_bytes / 1e9))
+    oix = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle as O
         oix, _ = host_index(S, O, dix, T, sp, sz, names)
-        n0 = 1 << 20
-        t3 = time.perf_counter()
-        oix.mappability_range(g0, g0 + n0, k)
-        dt0 = time.perf_counter() - t3
-        n1 = int(min(g1 - g0, max(n0, n0 * args.cpu_seconds / max(dt0, 1e-3))))
-        a = (g1 - g0 - n1) // 2 + g0
-        t3 = time.perf_counter()
-        m, _ = oix.mappability_range(a, a + n1, k)
-        dt = time.perf_counter() - t3
-        exact = bool(np.array_equal(m, dmap[2 + 2 * a:2 + 2 * (a + n1)]))
-        out_j["cpu_baseline"] = {
-            "value": n1 / dt, "unit": "bases/s", "cores": 1, "kind": "port",
-            "sample": "%d consecutive forward bases from %d (oracle/smash_oracle.c "
-                      "orc_mappability_range), %.1f s" % (n1, a, dt),
-            "map_identical_to_device": exact}
-        log("cpu baseline: %.3e bases/s on 1 core; identical: %s" % (n1 / dt, exact))
+    r = c5_scan(args, dix, contigs, cfg["bins"], world, rank, dev, dist, oix, reps=args.steps)
+    out_j = {"metric": r.pop("metric"), "value": r.pop("value"), "unit": "bases/s",
+             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+             "ms_per_step": r.pop("ms_per_scan"), "higher_is_better": True,
+             "scaling": r.pop("scaling"), "vs_baseline": None, "dtype": "u8/u64 (integer)",
+             "data": "synthetic (tools/synth.py hg19-shaped genome)",
+             "config": {"workload": cfg["workload"], "genome": cfg["genome"],
+                        "bases": r.pop("bases"), "k": r.pop("k"), "bins": r.pop("bins"),
+                        "parallelism": "%d contiguous base ranges, all_reduce counts" % world}}
+    out_j.update(r)
     if rank == 0:
         print(json.dumps(out_j), flush=True)
     if world > 1:
@@ -264,12 +294,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--pairs", type=int, default=0, help="pairs per rank per step")
+    ap.add_argument("--batch", type=int, default=0, help="pairs per device batch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 scan on the same index")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.pairs:
         cfg["pairs"] = args.pairs
+    if args.batch:
+        cfg["batch"] = args.batch
 
     import torch
     import smashgpu as S
@@ -300,26 +334,39 @@ def main():
     tmpdir = tempfile.mkdtemp()
     starts = bin_starts_for(cfg, contigs, tmpdir)
     cs = chrom_sizes_for(cfg, contigs)
-    P = cfg["pairs"]
-    L = cfg["read_len"]
-    reads_h = make_reads(contigs, cfg, P, cfg["seed"] * 1000 + rank)
-    d_reads = torch.from_numpy(reads_h).to(dev)
-    log("reads: %d pairs x %d bp per rank (%.1fs since start)" % (P, L, time.time() - t0))
-    pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P)
+    P, L, B = cfg["pairs"], cfg["read_len"], min(cfg["batch"], cfg["pairs"])
+    # the rank's reads, generated on the device (tools/readgen.hip), resident
+    import readgen
+    gen = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000 + rank)
+    d_reads = gen.generate(P)
+    torch.cuda.synchronize()
+    log("reads: %d pairs x %d bp per rank in HBM (%.1f GB), batches of %d (%.1fs since start)"
+        % (P, L, d_reads.numel() / 1e9, B, time.time() - t0))
+    # the key set: every key of the run (single GPU), or the keys this rank
+    # owns (hash % world of all ranks' keys: ~P as well)
+    pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
     counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+    nb = (P + B - 1) // B
 
     if world > 1:
         from dist import ShardedCounter
         sc = ShardedCounter(pipe, rank, world, dev)
 
     def step(i):
+        """one run over the rank's P pairs: a fresh key set / adjacent-dup
+        state (a new smashMEM.py + varbin.py invocation), carried across
+        the batches"""
         counts.zero_()
         if world == 1:
             pipe.reset()
-            pipe.count_batch(d_reads, P, counts)
+            for b in range(nb):
+                b0, b1 = b * B, min(P, (b + 1) * B)
+                pipe.count_batch(d_reads[2 * b0:2 * b1], b1 - b0, counts)
         else:
             sc.reset()
-            sc.step(d_reads, P, 0, counts)
+            for b in range(nb):
+                b0, b1 = b * B, min(P, (b + 1) * B)
+                sc.step(d_reads[2 * b0:2 * b1], b1 - b0, b0 * world, counts)
             dist.all_reduce(counts)
 
     for i in range(args.warmup):
@@ -343,6 +390,8 @@ def main():
     mam_ms, launches, mam_reads = pipe.profile_read()
     pipe.profile(False)
     st = pipe.stats()
+    if st.error:
+        raise SystemExit("pipeline data error: %s" % S.ERRORS.get(st.error, st.error))
     same = bool(np.array_equal(counts.cpu().numpy(), ref_counts)) if args.warmup else True
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -350,8 +399,8 @@ def main():
         el = float(t.item())
     total_reads = 2 * P * world * args.steps
     value = total_reads / el
-    log("timed %d steps: %.3f s -> %.3e reads/s; k_mam %.1f ms/launch; stats %s; "
-        "deterministic=%s" % (args.steps, el, value, mam_ms / max(launches, 1),
+    log("timed %d steps: %.3f s -> %.3e reads/s; k_mam %.2f ms/launch (%d launches); stats %s; "
+        "deterministic=%s" % (args.steps, el, value, mam_ms / max(launches, 1), launches,
                               st.as_dict(), same))
 
     out = {
@@ -359,11 +408,13 @@ def main():
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64 (integer)",
-        "data": "synthetic (tools/synth.py genome + SMASH reads, seeded)",
+        "data": "synthetic (tools/synth.py hg19-shaped genome; SMASH reads generated on the "
+                "device, tools/readgen.hip, seeded)",
         "config": {"workload": cfg["workload"], "genome": cfg["genome"],
                    "genome_bp": int(sum(len(s) for _, s in contigs)),
                    "text_N": int(dix.info.N), "pairs_per_rank": P, "read_len": L,
-                   "reads_per_step": 2 * P * world, "bins": int(len(starts)),
+                   "reads_per_step": 2 * P * world, "batch_pairs": B, "batches_per_step": nb,
+                   "bins": int(len(starts)),
                    "parallelism": "dp%d: pair shards, all_to_all key de-dup, "
                                   "all_gather tails, all_reduce counts" % world
                    if world > 1 else "single GPU",
@@ -376,11 +427,13 @@ def main():
     reads_per_launch = mam_reads / max(launches, 1)
     roof = None
     cpu = None
+    oix = None
     if rank == 0:
         import oracle as O
         t2 = time.time()
         ns = min(4000, 2 * P)
-        oix, mp = host_index(S, O, dix, T, sp, sz, names, sample_reads=reads_h[:ns])
+        sample = d_reads[:ns].cpu().numpy()
+        oix, mp = host_index(S, O, dix, T, sp, sz, names, sample_reads=sample)
         log("host copy of the index for the oracle: %.1fs" % (time.time() - t2))
         # algorithmic bytes per read: 64 B x the 64-byte line transitions of
         # k_mam_sm's own probe sequence, counted by running the kernel's code
@@ -388,14 +441,15 @@ def main():
         # index and a sample of the same reads
         import sm_emu
         emu = sm_emu.Emu(oix, copy=False)
-        _, emu_it = emu.map(reads_h[:ns])
+        _, emu_it = emu.map(sample)
         lines = sum(v[1] for v in emu.counters.values())
         b_read = 64.0 * lines / ns
-        achieved = reads_per_launch * b_read / (avg_ms / 1e3) / 1e9
+        achieved = mam_reads * b_read / (mam_ms / 1e3) / 1e9
         roof = {"bound": "hbm", "kernel": "k_mam_sm", "achieved": round(achieved, 2),
                 "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
                 "traffic": None, "bytes_per_read": round(b_read, 1),
                 "avg_kernel_ms": round(avg_ms, 3), "reads_per_launch": int(reads_per_launch),
+                "launches": int(launches),
                 "lines_per_read": {k: round(v[1] / ns, 3) for k, v in emu.counters.items()},
                 "probes_per_read": {k: round(v[0] / ns, 3) for k, v in emu.counters.items()},
                 "loop_iterations_per_read": round(float(emu_it.mean()), 1),
@@ -404,62 +458,57 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
         if os.path.exists(pmc):
             try:
-                roof["traffic"] = json.load(open(pmc)).get("k_mam_bytes_per_launch")
+                j = json.load(open(pmc))
+                roof["traffic"] = j.get("k_mam_bytes_per_read", 0) * reads_per_launch or \
+                    j.get("k_mam_bytes_per_launch")
                 roof["traffic_source"] = os.path.relpath(pmc, ROOT)
             except Exception:
                 pass
         if world == 1 and not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
+            threads = os.cpu_count() or 1
             op = O.Pipeline(oix, mp, cs, starts)
-            # calibrate, then a bounded sample of ~cpu_seconds
-            n0 = min(P, 256 * threads)
+            # calibrate, then a bounded sample of ~cpu_seconds of the same reads
+            n0 = min(P, 64 * threads)
+            h0 = d_reads[:2 * n0].cpu().numpy()
             t3 = time.perf_counter()
-            op.run(reads_h[:2 * n0], threads=threads)
+            op.run(h0, threads=threads)
             dt0 = time.perf_counter() - t3
             n1 = int(min(P, max(n0, n0 * args.cpu_seconds / max(dt0, 1e-3))))
+            h1 = d_reads[:2 * n1].cpu().numpy()
             op = O.Pipeline(oix, mp, cs, starts)
             t3 = time.perf_counter()
-            err = op.run(reads_h[:2 * n1], threads=threads)
+            err = op.run(h1, threads=threads)
             dt = time.perf_counter() - t3
+            # the search alone (longSA::MAM, no resolve/tag/filter/bin)
+            nm = min(len(h1), 2 * n0 * 4)
+            t3 = time.perf_counter()
+            O.map_only(oix, h1[:nm], threads=threads)
+            dtm = time.perf_counter() - t3
             # device on the same sample must give the same counts
             pipe.reset()
             c2 = torch.zeros(len(starts), dtype=torch.int64, device=dev)
-            pipe.count_batch(d_reads[:2 * n1], n1, c2)
+            for b0 in range(0, n1, B):
+                b1 = min(n1, b0 + B)
+                pipe.count_batch(d_reads[2 * b0:2 * b1], b1 - b0, c2)
             dev_counts = c2.cpu().numpy().astype(np.uint64)
             exact = bool(err == 0 and np.array_equal(dev_counts, op.counts))
             cpu = {"value": 2 * n1 / dt, "unit": "reads/s", "cores": threads,
                    "kind": "port",
-                   "sample": "%d pairs (%d reads) of the same batch, whole chain "
-                             "(oracle/smash_oracle.c orc_run_pairs), %.1f s" % (n1, 2 * n1, dt),
+                   "sample": "%d pairs (%d reads) of the same reads, whole chain "
+                             "(oracle/smash_oracle.c orc_run_pairs, %d threads), %.1f s"
+                             % (n1, 2 * n1, threads, dt),
+                   "mapping_only_reads_per_s": round(nm / dtm, 1),
+                   "mapping_only_sample": "%d reads, longSA::MAM restated (orc_map_only), "
+                                          "%.1f s" % (nm, dtm),
+                   "end_to_end_reads_per_s": round(2 * n1 / dt, 1),
+                   "index_load_s": round(time.time() - t2 - dt - dtm - dt0, 1),
                    "bin_counts_identical_to_device": exact}
-            log("cpu baseline: %.3e reads/s on %d threads; device==oracle counts: %s"
-                % (cpu["value"], threads, exact))
+            log("cpu baseline: %.3e reads/s end to end, %.3e mapping only, on %d threads; "
+                "device==oracle counts: %s" % (cpu["value"], nm / dtm, threads, exact))
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
-    # host-buffer boundary: the same batch copied H2D from pinned memory
-    # (not part of `value`, whose inputs are resident in HBM)
-    try:
-        hb = torch.from_numpy(reads_h).pin_memory()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        d_reads.copy_(hb, non_blocking=True)
-        torch.cuda.synchronize()
-        e0.record()
-        for _ in range(3):
-            d_reads.copy_(hb, non_blocking=True)
-        e1.record()
-        torch.cuda.synchronize()
-        h2d_ms = e0.elapsed_time(e1) / 3
-        step_ms = 1000.0 * el / args.steps
-        out["host_boundary"] = {
-            "h2d_ms_per_step": round(h2d_ms, 3),
-            "h2d_GBps": round(reads_h.nbytes / h2d_ms / 1e6, 1),
-            "reads_per_s_h2d_serial": round(2 * P * world / ((step_ms + h2d_ms) / 1e3), 1),
-            "reads_per_s_h2d_overlapped": round(2 * P * world / (max(step_ms, h2d_ms) / 1e3), 1),
-            "note": "pinned host batch -> HBM per step; serial = copy then step, "
-                    "overlapped = copy of the next batch on another stream (estimate)"}
-        del hb
-    except Exception as ex:   # measurement extra only
-        out["host_boundary"] = {"error": str(ex)}
+    if cfg["genome"] == "hg19" and not args.no_c5:
+        out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)
     out["deterministic_counts"] = same
     out["stats_last_step"] = st.as_dict()
     if rank == 0:

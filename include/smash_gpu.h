@@ -286,6 +286,7 @@ int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_keep,
 /* tag = 1, appends mappability_tag's L<i>/R<i> columns (mappability_tag.cpp: */
 /* 93-124) to the same lines.                                                 */
 /* smash_sam_records: one record per match slot of smash_map_batch's output   */
+/* (read i of length d_lens[i], stride >= 255, or `len` when d_lens is NULL)  */
 /* (Alignment::resolve, query.cpp:68-97; XE of the match's diagonal,          */
 /* :270-274; map.bin L/R of its '=' block when d_tag_offsets, the u32         */
 /* sam_header offsets per forward contig, is given).  Asynchronous.           */
@@ -309,9 +310,10 @@ typedef struct {
   uint32_t reserved;       /* 40-byte record                                */
 } smash_sam_rec;
 int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
-                      uint32_t len, uint64_t n_reads, const uint64_t *d_match,
-                      uint32_t cap_per_read, const uint32_t *d_n_match,
-                      const uint32_t *d_tag_offsets, smash_sam_rec *d_out, void *stream);
+                      const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                      const uint64_t *d_match, uint32_t cap_per_read,
+                      const uint32_t *d_n_match, const uint32_t *d_tag_offsets,
+                      smash_sam_rec *d_out, void *stream);
 int smash_sam_format(const char *const *contigs, uint32_t n_contig,
                      const smash_sam_rec *h_rec,
                      const uint32_t *h_n, uint32_t cap_per_read, uint64_t n_reads,

@@ -428,6 +428,14 @@ class Pipeline:
             pass
 
 
+def map_only(ix: Index, reads: np.ndarray, min_len=20, threads=1):
+    """longSA::MAM over every read (the reference's own probe sequence), on
+    `threads` host threads; returns the number of matches."""
+    reads = np.ascontiguousarray(reads, np.uint8)
+    return int(lib().orc_map_only(C.byref(ix.c), _p(reads, u8p), reads.shape[1],
+                                  reads.shape[1], reads.shape[0], min_len, threads, None))
+
+
 def map_only_fast(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=False):
     """Accelerated search (device algorithm) on the CPU; counters = its lines."""
     reads = np.ascontiguousarray(reads, np.uint8)

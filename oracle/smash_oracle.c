@@ -972,9 +972,9 @@ int orc_run_pairs(const orc_pipeline *p, const uint8_t *reads, uint32_t L,
   const uint64_t chunk = n_pairs < PAIR_CHUNK * (uint64_t)threads ? (n_pairs ? n_pairs : 1)
                                                                     : PAIR_CHUNK * (uint64_t)threads;
   pair_out_t *out = (pair_out_t *)malloc(chunk * sizeof(pair_out_t));
-  pthread_t th[256];
-  job_t jobs[256];
-  if (threads > 256) threads = 256;
+  pthread_t th[1024];
+  job_t jobs[1024];
+  if (threads > 1024) threads = 1024;
   int err = 0;
   uint8_t key[PAIR_CAP * 12 + 4];
   int64_t pos0[PAIR_CAP], absp[PAIR_CAP];
@@ -1038,8 +1038,8 @@ uint64_t orc_map_only(const orc_index *ix, const uint8_t *reads, uint32_t L,
                       uint64_t stride, uint64_t n, uint32_t min_len,
                       int threads, orc_counters *ctr) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t th[256];
+  if (threads > 1024) threads = 1024;
+  pthread_t th[1024];
   mjob_t *jobs = (mjob_t *)calloc((size_t)threads, sizeof(mjob_t));
   for (int t = 0; t < threads; ++t) {
     jobs[t].ix = ix; jobs[t].reads = reads; jobs[t].L = L; jobs[t].min_len = min_len;
@@ -1223,8 +1223,8 @@ uint64_t orc_map_only_fast(const orc_index *ix, const orc_accel *acc,
                            uint64_t n, uint32_t min_len, int threads,
                            orc_counters *ctr) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t th[256];
+  if (threads > 1024) threads = 1024;
+  pthread_t th[1024];
   fjob_t *jobs = (fjob_t *)calloc((size_t)threads, sizeof(fjob_t));
   for (int t = 0; t < threads; ++t) {
     jobs[t].ix = ix; jobs[t].acc = acc; jobs[t].reads = reads; jobs[t].L = L;
@@ -1461,8 +1461,8 @@ uint64_t orc_map_only_v3(const orc_index *ix, const orc_accel *acc,
                          uint64_t n, uint32_t min_len, int threads,
                          orc_counters *ctr) {
   if (threads < 1) threads = 1;
-  if (threads > 256) threads = 256;
-  pthread_t th[256];
+  if (threads > 1024) threads = 1024;
+  pthread_t th[1024];
   v3job_t *jobs = (v3job_t *)calloc((size_t)threads, sizeof(v3job_t));
   for (int t = 0; t < threads; ++t) {
     jobs[t].ix = ix; jobs[t].acc = acc; jobs[t].reads = reads; jobs[t].L = L;

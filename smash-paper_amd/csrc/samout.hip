@@ -28,7 +28,8 @@ constexpr int kSB = 256;
 
 __global__ __launch_bounds__(kSB) void k_sam_recs(
     const uint64_t *__restrict__ match, const uint32_t *__restrict__ n_match, uint32_t cap,
-    uint64_t n_reads, const uint8_t *__restrict__ reads, uint64_t stride, uint32_t L,
+    uint64_t n_reads, const uint8_t *__restrict__ reads, uint64_t stride,
+    const uint16_t *__restrict__ lens, uint32_t L0,
     const uint8_t *__restrict__ text, uint64_t N, const uint64_t *__restrict__ startpos,
     const uint64_t *__restrict__ sizes, uint32_t n_seq, const uint32_t *__restrict__ tag_off,
     const uint8_t *__restrict__ map, uint64_t map_bytes, smash_sam_rec *__restrict__ out) {
@@ -38,6 +39,7 @@ __global__ __launch_bounds__(kSB) void k_sam_recs(
   if (r >= n_reads) return;
   const uint32_t nm = n_match[r];
   if (k >= nm) return;
+  const uint32_t L = lens ? lens[r] : L0;
   const uint64_t w = match[r * cap + k];
   const uint64_t ref = w & 0xFFFFFFFFFFFFull;
   const uint32_t q = uint32_t((w >> 48) & 0xFF), len = uint32_t(w >> 56);
@@ -257,12 +259,12 @@ using namespace smash;
 static_assert(sizeof(smash_sam_rec) == 40, "smash_sam_rec layout (smashgpu.SAM_REC)");
 
 extern "C" int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
-                                 uint32_t len, uint64_t n_reads, const uint64_t *d_match,
-                                 uint32_t cap_per_read, const uint32_t *d_n_match,
-                                 const uint32_t *d_tag_offsets, smash_sam_rec *d_out,
-                                 void *stream) {
-  if (!ix || !d_reads || !d_match || !d_n_match || !d_out || !cap_per_read || len == 0 ||
-      len > 255 || stride < len) {
+                                 const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                                 const uint64_t *d_match, uint32_t cap_per_read,
+                                 const uint32_t *d_n_match, const uint32_t *d_tag_offsets,
+                                 smash_sam_rec *d_out, void *stream) {
+  if (!ix || !d_reads || !d_match || !d_n_match || !d_out || !cap_per_read ||
+      (!d_lens && (len == 0 || len > 255 || stride < len)) || (d_lens && stride < 255)) {
     set_error("smash_sam_records: bad arguments");
     return SMASH_ERR_ARG;
   }
@@ -274,7 +276,7 @@ extern "C" int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, 
   const uint64_t slots = n_reads * cap_per_read;
   const hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_sam_recs, dim3(unsigned((slots + kSB - 1) / kSB)), dim3(kSB), 0, s,
-                     d_match, d_n_match, cap_per_read, n_reads, d_reads, stride, len,
+                     d_match, d_n_match, cap_per_read, n_reads, d_reads, stride, d_lens, len,
                      ix->d_text, ix->N, ix->d_startpos, ix->d_sizes, ix->n_seq, d_tag_offsets,
                      ix->d_map, ix->map_bytes, d_out);
   SMASH_HIP(hipGetLastError());

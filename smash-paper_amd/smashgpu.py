@@ -134,8 +134,8 @@ def lib():
                                       vp]
     L.smash_mappability_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32, vp, i64p, vp,
                                          C.c_uint32, vp, vp, vp]
-    L.smash_sam_records.argtypes = [vp, vp, C.c_uint64, C.c_uint32, C.c_uint64, vp, C.c_uint32,
-                                    vp, vp, vp, vp]
+    L.smash_sam_records.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_uint64, vp,
+                                    C.c_uint32, vp, vp, vp, vp]
     L.smash_sam_format.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, vp, u32p, C.c_uint32, C.c_uint64,
                                    C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
                                    C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int, C.c_int,
@@ -584,7 +584,7 @@ def sam_records(index: Index, d_reads, n, read_len, cap, tag_offsets=None, min_l
     d_off = None
     if tag_offsets is not None:
         d_off = torch.from_numpy(np.ascontiguousarray(tag_offsets, np.uint32).view(np.int32)).to(dev)
-    check(lib().smash_sam_records(index.h, _ptr(d_reads), read_len, read_len, n, _ptr(d_m), cap,
+    check(lib().smash_sam_records(index.h, _ptr(d_reads), read_len, None, read_len, n, _ptr(d_m), cap,
                                   _ptr(d_n), _ptr(d_off), _ptr(d_rec), vp(_stream(stream))),
           "smash_sam_records")
     torch.cuda.synchronize(dev)

@@ -1,0 +1,325 @@
+"""BASELINE.json's configurations on the device, each against an
+independent checker.
+
+C1  chr21-only reference, 10 k x 100 bp, sample_bins/500000: the device
+    index equals the REFERENCE's own index files byte for byte
+    (tests/golden/c1_index.sha256, oracle/_ref/mummer), and the device bin
+    counts equal the REAL varbin.py run on the reference's own mapout
+    (tests/golden/c1_varbin_*; tools/make_golden_c1.sh).
+hg19 (C2, C3, C5) no CPU suffix sort finishes here, so the device index is
+    pinned at full size by an independent device checker (tests/csrc/
+    index_check.hip: SA a permutation with ISA its inverse, every adjacent
+    pair of suffixes in order at its LCP with the first min(LCP, 255) bytes
+    equal, the overflow table exact, sampled overflow entries compared in
+    full) plus a host-side sample of the same properties; the oracle then
+    runs on that (now pinned) index:
+    C2  hg19, 1 M x 100 bp (all 500 k pairs), sample_bins/100000
+    C3  hg19, 150 bp, sample_bins/50000: a 100 k-pair sample of the bench's
+        workload through the oracle; the full 25 M-pair run by properties
+    C5  the map.bin self-scan of every forward base == the index build's
+        map.bin, and windows of it == the oracle's longSA::show restatement
+idx8 the whole count pipeline with 64-bit SA/ISA (the hg19 element width) on
+    the mid genome, against an oracle that builds its own index.
+"""
+import ctypes as C
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, gold
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import smashgpu as S  # noqa: E402
+import oracle as O  # noqa: E402
+import synth  # noqa: E402
+
+THREADS = min(16, os.cpu_count() or 1)   # the box's CPU share
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _reads(contigs, n_pairs, L, seed):
+    r1, r2 = synth.make_reads(contigs, n_pairs, L, seed=seed)
+    reads = np.empty((2 * n_pairs, L), np.uint8)
+    reads[0::2], reads[1::2] = r1, r2
+    return S.prepare_reads(reads)
+
+
+def _device_counts(dix, cs, starts, reads, batch):
+    n = reads.shape[0] // 2
+    pipe = S.Pipeline(dix, cs, starts, reads.shape[1], min(batch, n), dedup_capacity=n)
+    counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    pipe.reset()
+    for b0 in range(0, n, batch):
+        b1 = min(n, b0 + batch)
+        pipe.count_batch(torch.from_numpy(reads[2 * b0:2 * b1]).cuda(), b1 - b0, counts)
+    st = pipe.stats()
+    return counts.cpu().numpy().astype(np.uint64), st, pipe
+
+
+def _oracle_counts(oix, mp, cs, starts, reads):
+    op = O.Pipeline(oix, mp, cs, starts)
+    err = op.run(reads, threads=THREADS)
+    return op, err
+
+
+# ---------------------------------------------------------------------------
+# C1
+# ---------------------------------------------------------------------------
+def test_c1_chr21_index_and_counts_equal_reference():
+    contigs = synth.make_genome("chr21")
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    dix = S.Index.create(T, sp, sz, names)
+    i = dix.info
+    assert i.idx_bytes == 4 and i.N == 96259792
+    sums = {l.split()[0]: l.split()[1] for l in open(gold("c1_index.sha256"))}
+    assert _sha(S.download(i.d_text, i.N)) == sums["rc1.ref.seq.bin"]
+    assert _sha(S.download(i.d_sa, 4 * i.N)) == sums["rc1.i4.index.sa.bin"]
+    assert _sha(S.download(i.d_isa, 4 * i.N)) == sums["rc1.i4.index.isa.bin"]
+    assert _sha(S.download(i.d_lcp8, i.N)) == sums["rc1.i4.index.lcp.vec.bin"]
+    ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64)
+    assert _sha(ovf) == sums["rc1.i4.index.lcp.m.bin:masked"]
+    assert _sha(S.download(i.d_map, i.map_bytes)[2:]) == sums["map.bin[2:]"]
+    # 5 000 pairs x 100 bp through the device chain, 500 k bins, chr21 at
+    # its hg19 offset
+    reads = _reads(contigs, 5000, 100, seed=1)
+    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    rows = []
+    for line in open(src):
+        c = line.rstrip("\n").split("\t")
+        a, ab, b = int(c[1]), int(c[2]), int(c[3])
+        for k in range(10):
+            rows.append(ab + ((b - a) * k) // 10)
+    starts = np.array(rows, np.int64)
+    counts, st, _ = _device_counts(dix, {"chr21": 2781598825}, starts, reads, 5000)
+    assert st.error == 0
+    exp = np.zeros(len(starts), np.uint64)
+    lines = open(gold("c1_varbin_nonzero.txt")).read().splitlines()
+    assert lines[-1] == "rows %d" % len(starts)
+    for l in lines[:-1]:
+        b, c = l.split("\t")
+        exp[int(b)] = int(c)
+    assert np.array_equal(counts, exp)
+    g = open(gold("c1_varbin_stats_partial.txt")).read().splitlines()[1].split("\t")
+    assert (st.positions, st.dups, st.kept) == (int(g[0]), int(g[1]), int(g[2]))
+
+
+# ---------------------------------------------------------------------------
+# hg19: full-size index properties, then C2 / C3 / C5 against the oracle
+# ---------------------------------------------------------------------------
+class IchkResult(C.Structure):
+    _fields_ = [(n, C.c_ulonglong) for n in (
+        "perm_bad", "perm_first", "order_bad", "order_first", "ovf_bad", "ovf_first",
+        "full_bad", "full_first", "full_checked", "full_bytes", "rank0_ok")]
+
+
+def _ichk():
+    p = os.path.join(ROOT, "tests", "lib", "libindexcheck.so")
+    if not os.path.exists(p):
+        pytest.fail("tests/lib/libindexcheck.so not built (__graft_entry__.build())")
+    L = C.CDLL(p)
+    vp = C.c_void_p
+    L.ichk_run.argtypes = [vp, C.c_uint64, vp, vp, C.c_uint32, vp, vp, C.c_uint64, C.c_uint64,
+                           C.c_uint64, C.POINTER(IchkResult), C.POINTER(C.c_ulonglong)]
+    return L
+
+
+@pytest.fixture(scope="module")
+def hg19():
+    contigs = synth.make_genome("hg19")
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    dix = S.Index.create(T, sp, sz, names)
+    return contigs, (T, sp, sz, names), dix
+
+
+def test_hg19_device_index_properties_full_size(hg19):
+    """Every rank of the 6.2e9-suffix index (independent device checker)."""
+    _, _, dix = hg19
+    i = dix.info
+    assert i.idx_bytes == 8 and i.N > (1 << 32)
+    r = IchkResult()
+    n255 = C.c_ulonglong()
+    rc = _ichk().ichk_run(i.d_text, i.N, i.d_sa, i.d_isa, i.idx_bytes, i.d_lcp8, i.d_lcp_ovf,
+                          i.n_lcp_overflow, 1024, 1 << 16, C.byref(r), C.byref(n255))
+    assert rc == 0
+    assert r.rank0_ok == 1
+    assert r.perm_bad == 0, r.perm_first
+    assert r.order_bad == 0, r.order_first
+    assert r.ovf_bad == 0 and n255.value == i.n_lcp_overflow, (r.ovf_first, n255.value)
+    assert r.full_bad == 0 and r.full_checked > 100000, (r.full_first, r.full_checked)
+
+
+def test_hg19_device_index_host_sample(hg19):
+    """The same properties on 2 M random ranks, checked on the host from
+    gathered values (no device code involved in the comparison)."""
+    _, (T, sp, sz, names), dix = hg19
+    i = dix.info
+    N = i.N
+    rng = np.random.default_rng(19)
+    ranks = np.unique(rng.integers(1, N, size=2_000_000)).astype(np.int64)
+    SA = S.device_view(i.d_sa, 8 * N, torch.int64)
+    ISA = S.device_view(i.d_isa, 8 * N, torch.int64)
+    L8 = S.device_view(i.d_lcp8, N, torch.uint8)
+    r = torch.from_numpy(ranks).cuda()
+    a = SA.index_select(0, r - 1).cpu().numpy()
+    b = SA.index_select(0, r).cpu().numpy()
+    back = ISA.index_select(0, torch.from_numpy(b).cuda()).cpu().numpy()
+    l8 = L8.index_select(0, r).cpu().numpy().astype(np.int64)
+    assert np.array_equal(back, ranks)
+    ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
+    big = l8 == 255
+    pos = np.searchsorted(ovf[:, 0], ranks[big].astype(np.uint64))
+    assert np.array_equal(ovf[pos, 0], ranks[big].astype(np.uint64))
+    lcp = l8.copy()
+    lcp[big] = ovf[pos, 1].astype(np.int64)
+    for k in range(0, len(ranks), 997):   # byte compares on the host text
+        x, y, l = int(a[k]), int(b[k]), int(lcp[k])
+        m = min(l, 4096)
+        assert T[x:x + m].tobytes() == T[y:y + m].tobytes(), ranks[k]
+        assert np.int8(T[x + l]) < np.int8(T[y + l]), ranks[k]
+
+
+@pytest.fixture(scope="module")
+def hg19_oracle(hg19):
+    """The oracle over the device index (pinned by the two tests above)."""
+    contigs, (T, sp, sz, names), dix = hg19
+    i = dix.info
+    N = i.N
+    SA = S.download(i.d_sa, 8 * N, np.uint64)
+    ISA = S.download(i.d_isa, 8 * N, np.uint64)
+    L8 = S.download(i.d_lcp8, N)
+    ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
+    mp = S.download(i.d_map, i.map_bytes)
+    oix = O.Index(T, sp, sz, names, SA=SA, ISA=ISA, L8=L8, ovf=ovf)
+    return oix, mp
+
+
+def _chrom_sizes(contigs):
+    out, n = {}, 0
+    for name, s in contigs:
+        if "_" in name:
+            continue
+        out[name] = n
+        n += len(s)
+    return out
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, tmp_path):
+    contigs, _, dix = hg19
+    oix, mp = hg19_oracle
+    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    if cfg == "c2":     # all of C2: 1 M mates x 100 bp, the 100 000-bin split
+        n, L, seed = 500_000, 100, 2
+        path = str(tmp_path / "bins100k.txt")
+        synth.split_bins(src, 2, path)
+    else:               # a 100 k-pair sample of C3's 150 bp workload, 50 000 bins
+        n, L, seed, path = 100_000, 150, 3, src
+    starts = np.array([int(l.split("\t")[2]) for l in open(path)], np.int64)
+    reads = _reads(contigs, n, L, seed)
+    cs = _chrom_sizes(contigs)
+    counts, st, _ = _device_counts(dix, cs, starts, reads, 40_000)
+    assert st.error == 0
+    op, err = _oracle_counts(oix, mp, cs, starts, reads)
+    assert err == 0
+    assert np.array_equal(counts, op.counts)
+    assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
+    assert st.dupe_pairs == op.n_dupe.value
+    assert st.kept > n   # SMASH reads: several kept segments per pair
+
+
+def test_c3_full_run_properties(hg19):
+    """The C3 run as stated, 25 M pairs (50 M mates) in 13 batches with one
+    key set and the adjacent-dup state carried: the counts sum to ReadsKept,
+    every pair is accounted for, and the same reads in other batch splits
+    give the same counts (the oracle cannot run 50 M reads here)."""
+    contigs, _, dix = hg19
+    cs = _chrom_sizes(contigs)
+    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    starts = np.array([int(l.split("\t")[2]) for l in open(src)], np.int64)
+    import readgen
+    P = 25_000_000
+    g = readgen.Generator(dix, contigs, 150, seed=3)
+    d_reads = g.generate(P)
+    outs = []
+    for batch in (2_000_000, 1_700_000):
+        pipe = S.Pipeline(dix, cs, starts, 150, batch, dedup_capacity=P)
+        counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+        pipe.reset()
+        for b0 in range(0, P, batch):
+            b1 = min(P, b0 + batch)
+            pipe.count_batch(d_reads[2 * b0:2 * b1], b1 - b0, counts)
+        st = pipe.stats()
+        assert st.error == 0 and st.pairs == P
+        assert int(counts.sum().item()) == st.kept
+        assert st.positions == st.kept + st.dups
+        outs.append((counts.cpu().numpy(), st.as_dict()))
+        del pipe
+    assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+
+
+def test_c5_mappability_scan_full_genome(hg19, hg19_oracle):
+    contigs, _, dix = hg19
+    oix, mp = hg19_oracle
+    total = int(sum(dix.contig_sizes))
+    out = torch.empty(2 * total, dtype=torch.uint8, device="cuda")
+    cc = torch.zeros(len(dix.contigs), dtype=torch.int64, device="cuda")
+    S.mappability_scan(dix, 0, total, 36, out, None, None, 0, None, cc)
+    dev = out.cpu().numpy()
+    assert np.array_equal(dev, mp[2:])        # == the index build's map.bin
+    rng = np.random.default_rng(5)
+    n_uniq = 0
+    for g0 in [0] + [int(x) for x in rng.integers(0, total - 300_000, size=4)]:
+        m, u = oix.mappability_range(g0, g0 + 300_000, 36)
+        assert np.array_equal(m, dev[2 * g0:2 * (g0 + 300_000)]), g0
+        r = dev[2 * g0 + 1:2 * (g0 + 300_000):2]
+        assert u == int(((r >= 1) & (r <= 36)).sum())
+        n_uniq += u
+    assert int(cc.sum().item()) == int(((dev[1::2] >= 1) & (dev[1::2] <= 36)).sum())
+
+
+# ---------------------------------------------------------------------------
+# idx8 on the mid genome: the 64-bit search and chain vs an independent oracle
+# ---------------------------------------------------------------------------
+def test_idx8_pipeline_equals_independent_oracle(monkeypatch, tmp_path):
+    g = synth.make_genome("mid")
+    T, sp, sz, names = O.text_from_contigs(g)
+    oix = O.Index(T, sp, sz, names)            # the oracle's own suffix sort
+    monkeypatch.setenv("SMASH_IDX_BYTES", "8")
+    dix = S.Index.create(T, sp, sz, names)
+    monkeypatch.delenv("SMASH_IDX_BYTES")
+    i = dix.info
+    assert i.idx_bytes == 8
+    assert np.array_equal(S.download(i.d_sa, 8 * i.N, np.uint64), oix.SA.astype(np.uint64))
+    assert np.array_equal(S.download(i.d_isa, 8 * i.N, np.uint64), oix.ISA.astype(np.uint64))
+    reads = _reads(g, 6000, 150, seed=88)
+    # MAM triples of every 5th read
+    n = reads.shape[0]
+    cap = 150 - 20 + 1
+    d = torch.from_numpy(reads).cuda()
+    o = torch.zeros(n * cap, dtype=torch.int64, device="cuda")
+    nn = torch.zeros(n, dtype=torch.int32, device="cuda")
+    S.map_batch(dix, d, n, 150, o, cap, nn)
+    torch.cuda.synchronize()
+    w = o.cpu().numpy().view(np.uint64).reshape(n, cap)
+    k = nn.cpu().numpy()
+    for r in range(0, n, 5):
+        assert S.unpack_matches(w[r], k[r]) == oix.search(reads[r].tobytes()), r
+    bins_path = str(tmp_path / "bins.txt")
+    synth.make_bins(g, 16, bins_path)
+    synth.write_index_side_files(str(tmp_path), g)
+    cs = {l.split("\t")[0]: int(l.split("\t")[2]) for l in open(tmp_path / "chrom_sizes.txt")}
+    starts = np.array([int(l.split("\t")[2]) for l in open(bins_path)], np.int64)
+    counts, st, _ = _device_counts(dix, cs, starts, reads, 2500)
+    assert st.error == 0
+    op, err = _oracle_counts(oix, oix.mappability(), cs, starts, reads)
+    assert err == 0
+    assert np.array_equal(counts, op.counts)
+    assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
+    assert st.dupe_pairs == op.n_dupe.value

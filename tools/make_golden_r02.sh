@@ -51,7 +51,26 @@ done
 # the mapout header (fasta.cpp:243-252) of one output file
 cat mapout/*.txt | grep '^@' | LC_ALL=C sort -u > "$OUT/tiny_mapout_header.txt"
 
+# 3. the other query formats and search modes through -samout (the drop-in
+#    CLI's other paths): FASTQ (-fastq) and FASTA input of s150, and -maxmatch
+#    / -mum on the first 60 / 300 records of s100 (sorted full lines)
+Q="python3 $ROOT/tools/golden_queries.py"
+$Q "$OUT/s150_fastqs_to_sam.sam.gz" fastq q.fq
+$Q "$OUT/s150_fastqs_to_sam.sam.gz" fasta q.fa
+$Q "$OUT/s100_fastqs_to_sam.sam.gz" sam q300.sam 300
+$Q "$OUT/s100_fastqs_to_sam.sam.gz" sam q60.sam 60
+run() {   # $1 = output tag, rest = mummer arguments
+  local tag=$1; shift
+  rm -rf mapout
+  "$R/mummer" "$@" 2> /dev/null
+  cat mapout/*.txt | grep -v '^@' | LC_ALL=C sort > $tag.txt
+  gzip -9 -n -c $tag.txt > "$OUT/$tag.txt.gz"
+}
+run s150_mapout_fastq_full -rcref -qthreads 2 -fastq -nomap -samout tiny.fa q.fq
+run s150_mapout_fasta_full -rcref -qthreads 2 -nomap -samout tiny.fa q.fa
+run s100_60_mapout_MEM_full -rcref -qthreads 2 -maxmatch -nomap -samin -samout tiny.fa q60.sam
+run s100_300_mapout_MUM_full -rcref -qthreads 2 -mum -samin -samout tiny.fa q300.sam
 # (mummer without -samout writes only the header: print_matches' non-SAM
 # branch, query.cpp:404-412, never calls OutputSorter::end_line, so its
-# lines are dropped; checked here, nothing to record)
+# lines are dropped; nothing to record)
 echo "round-2 golden written to $OUT"

@@ -1,0 +1,90 @@
+// tools/readgen.hip -- synthetic SMASH read pairs generated ON THE DEVICE from
+// the resident doubled text (test / benchmark data, not part of the product).
+//
+// Same model as tools/synth.py make_reads: each mate is a
+// concatenation of segments of uniform length [20, 60] from independent
+// loci (intervals of non-N sequence >= 500 bp from N runs and contig ends,
+// weighted by length, chrM and '_' contigs excluded) on a random strand;
+// 1% uniform substitutions; 0.5% of mates carry one N; 1% of pairs are exact
+// copies of an earlier pair.  Reads come out already prepared as the
+// pipeline consumes them (lowercase, N -> 'z': fastqs_to_sam replaceN +
+// NewQuery::extend).  Counter-based hashing of (seed, pair, mate, segment)
+// makes every pair independent of the batch split: pair q is the same bytes
+// whether generated alone or in a batch of 25 M.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+__device__ __forceinline__ uint64_t mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t h4(uint64_t s, uint64_t a, uint64_t b, uint64_t c) {
+  return mix(mix(mix(s ^ a) ^ (b * 0xD6E8FEB86659FD93ull)) ^ (c * 0xA0761D6478BD642Full));
+}
+__device__ __forceinline__ double unit(uint64_t h) { return double(h >> 11) * 0x1.0p-53; }
+
+struct Iv {
+  uint64_t a, b;        // forward contig coordinates [a, b)
+  uint64_t fwd_base;    // text position of forward base 0 of the contig
+  uint64_t rc_end;      // text position of the rc copy + contig size
+};
+
+__global__ void k_gen(const uint8_t *__restrict__ text, const Iv *__restrict__ iv,
+                      const uint64_t *__restrict__ cum, uint32_t n_iv, uint64_t total,
+                      uint64_t seed, uint64_t q0, uint64_t n_pairs, uint32_t L,
+                      uint8_t *__restrict__ out) {
+  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= 2 * n_pairs) return;
+  const uint64_t q = q0 + t / 2, mate = t & 1;
+  uint64_t src = q;   // 1% exact duplicates of an earlier pair
+  if (q > 0 && unit(h4(seed, q, 0xD0, 0)) < 0.01) src = h4(seed, q, 0xD1, 0) % q;
+  uint8_t *o = out + t * L;
+  uint32_t pos = 0;
+  for (uint32_t k = 0; pos < L; ++k) {
+    const uint64_t hs = h4(seed, src, mate, 4 * k);
+    const uint32_t seglen = 20 + uint32_t(hs % 41);
+    const uint64_t u = h4(seed, src, mate, 4 * k + 1) % total;
+    uint32_t lo = 0, hi = n_iv;   // interval containing u (upper_bound of cum)
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (cum[m] <= u) lo = m + 1; else hi = m;
+    }
+    const Iv v = iv[lo < n_iv ? lo : n_iv - 1];
+    const uint64_t span = v.b - v.a > seglen ? v.b - v.a - seglen : 1;
+    const uint64_t S = v.a + uint64_t(unit(h4(seed, src, mate, 4 * k + 2)) * double(span));
+    const bool rc = h4(seed, src, mate, 4 * k + 3) & 1;
+    const uint64_t base = rc ? v.rc_end - S - seglen : v.fwd_base + S;
+    for (uint32_t j = 0; j < seglen && pos < L; ++j, ++pos) {
+      uint8_t c = text[base + j];
+      const uint64_t hm = h4(seed ^ 0x5B, src, mate, pos);
+      if (unit(hm) < 0.01) {   // substitution to one of the other three bases
+        const uint32_t ci = c == 'a' ? 0 : c == 'c' ? 1 : c == 'g' ? 2 : 3;
+        c = "acgt"[(ci + 1 + uint32_t((hm >> 7) % 3)) & 3];
+      }
+      o[pos] = c;
+    }
+  }
+  const uint64_t hn = h4(seed ^ 0x4E, src, mate, 0);
+  if (unit(hn) < 0.005) o[(hn >> 20) % L] = 'z';
+}
+
+}  // namespace
+
+// Pairs [q0, q0 + n_pairs) into d_out[2 * n_pairs * L] (mate 2i = read 1 of
+// pair q0 + i).  iv/cum are device arrays (rg_iv_bytes per interval).
+extern "C" int rg_generate(const uint8_t *d_text, const void *d_iv, const uint64_t *d_cum,
+                           uint32_t n_iv, uint64_t total, uint64_t seed, uint64_t q0,
+                           uint64_t n_pairs, uint32_t L, uint8_t *d_out, void *stream) {
+  if (!n_pairs) return 0;
+  const uint64_t n = 2 * n_pairs;
+  k_gen<<<unsigned((n + 255) / 256), 256, 0, static_cast<hipStream_t>(stream)>>>(
+      d_text, static_cast<const Iv *>(d_iv), d_cum, n_iv, total, seed, q0, n_pairs, L, d_out);
+  return int(hipGetLastError());
+}
+
+extern "C" uint32_t rg_iv_bytes(void) { return sizeof(Iv); }

@@ -39,8 +39,9 @@ def main():
     dix = S.Index.create(T, sp, sz, names, device=0)
     starts = bench.bin_starts_for(cfg, contigs, tempfile.mkdtemp())
     cs = bench.chrom_sizes_for(cfg, contigs)
-    P, L = cfg["pairs"], cfg["read_len"]
-    d_reads = torch.from_numpy(bench.make_reads(contigs, cfg, P, cfg["seed"] * 1000)).cuda()
+    P, L = cfg["batch"], cfg["read_len"]      # one batch of the config
+    import readgen
+    d_reads = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000).generate(P)
     pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P)
     counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
     ref = None
