@@ -23,7 +23,8 @@ Also reported: `roofline` of the dominant kernel (k_mam_sm: algorithmic bytes
 running the kernel source on the host (tools/sm_emu) over the downloaded index
 for a sample of the same reads, over the HIP-event-timed kernel duration),
 `cpu_baseline` (the C oracle of the whole chain and of the search alone, on
-all os.cpu_count() host threads, rank 0, N = 1, bounded sample of the same
+all the host CPUs the box grants (its cgroup quota = nproc), rank 0, N = 1,
+bounded sample of the same
 reads; the device's counts on that sample must be identical) and `c5`
 (BASELINE config C5 on the same resident index: the map.bin self-scan of
 every forward base with unique-36-mer counts, bases/s, its roofline and a CPU
@@ -65,6 +66,25 @@ CONFIGS = {
     "mid": dict(genome="mid", read_len=150, pairs=200_000, batch=200_000, bins="synthetic",
                 seed=2, workload="3.2 Mbp synthetic genome, 150 bp (functional check)"),
 }
+
+
+def host_cores():
+    """The host CPUs this process may use: the cgroup CPU quota when one is
+    set (the GPU box: 16 of the node's os.cpu_count() = 256, what `nproc`
+    reports there), else the affinity mask.  Returns (cores, note)."""
+    cpus = os.cpu_count() or 1
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = max(1, -(-int(q) // int(p)))
+            return n, "cgroup cpu.max %s/%s = %d CPUs (nproc); os.cpu_count() = %d" % (q, p, n, cpus)
+    except (OSError, ValueError):
+        pass
+    try:
+        n = len(os.sched_getaffinity(0))
+        return n, "affinity %d CPUs; os.cpu_count() = %d" % (n, cpus)
+    except AttributeError:
+        return cpus, "os.cpu_count() = %d" % cpus
 
 
 def log(*a):
@@ -230,7 +250,7 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
         # oracle/smash_oracle.c orc_mappability_range on every host thread,
         # contiguous sub-windows of one window in the middle of the genome
         from concurrent.futures import ThreadPoolExecutor
-        threads = os.cpu_count() or 1
+        threads, note = host_cores()
         n0 = 1 << 18
         t3 = time.perf_counter()
         oix.mappability_range(g0, g0 + n0, k)
@@ -250,6 +270,7 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
             "value": n1 / dt, "unit": "bases/s", "cores": threads, "kind": "port",
             "sample": "%d consecutive forward bases from %d (oracle/smash_oracle.c "
                       "orc_mappability_range, %d threads), %.1f s" % (n1, a, threads, dt),
+            "cores_note": note,
             "map_identical_to_device": exact}
         log("C5 cpu baseline: %.3e bases/s on %d threads; identical: %s"
             % (n1 / dt, threads, exact))
@@ -465,7 +486,7 @@ def main():
             except Exception:
                 pass
         if world == 1 and not args.no_cpu_baseline:
-            threads = os.cpu_count() or 1
+            threads, note = host_cores()
             op = O.Pipeline(oix, mp, cs, starts)
             # calibrate, then a bounded sample of ~cpu_seconds of the same reads
             n0 = min(P, 64 * threads)
@@ -501,6 +522,7 @@ def main():
                    "mapping_only_sample": "%d reads, longSA::MAM restated (orc_map_only), "
                                           "%.1f s" % (nm, dtm),
                    "end_to_end_reads_per_s": round(2 * n1 / dt, 1),
+                   "cores_note": note,
                    "index_load_s": round(time.time() - t2 - dt - dtm - dt0, 1),
                    "bin_counts_identical_to_device": exact}
             log("cpu baseline: %.3e reads/s end to end, %.3e mapping only, on %d threads; "

@@ -177,8 +177,11 @@ void prepare(Mate &m, const smash_sam_rec *rec, uint32_t n) {
       last_end = uint64_t(a.r.prefix) + a.r.len;   // merged away: n_matches stays 0
     }
   }
-  // to_print (query.cpp:219-229): qpos, then rc; stable over to_merge order
-  std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) {
+  // to_print (query.cpp:219-229): qpos, then rc.  Ties are common under
+  // -maxmatch (one segment, many loci) and the reference breaks them with
+  // std::sort's introsort over the to_merge order (query.cpp:292): the same
+  // std::sort over the same sequence reproduces its order exactly
+  std::sort(idx.begin(), idx.end(), [&](int x, int y) {
     const Al &a = m.al[x], &b = m.al[y];
     if (a.qpos != b.qpos) return a.qpos < b.qpos;
     return a.r.rc < b.r.rc;

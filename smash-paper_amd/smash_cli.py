@@ -327,6 +327,10 @@ def cmd_varbin(args):
 
 
 def cmd_search(args):
+    """mummer's match triples per read, in --batch chunks of one read length:
+    MAM / MUM emit at most L - l + 1 matches per read; MEM (-maxmatch) starts
+    at --cap records per read and re-runs a chunk with the largest count when
+    any read has more (smash_match_batch counts past the capacity)."""
     import torch
     ref = _ref(args)
     ix = load_index(ref, args.device)
@@ -341,23 +345,26 @@ def cmd_search(args):
     dev = torch.device("cuda", args.device)
     out = sys.stdout
     for L in sorted({len(s) for _, s in recs}):
-        sel = [(n, s) for n, s in recs if len(s) == L and L > 0]
-        if not sel:
-            continue
-        reads = S.prepare_reads(np.frombuffer(b"".join(s for _, s in sel), np.uint8).reshape(-1, L))
-        cap = args.cap
-        d = torch.from_numpy(np.ascontiguousarray(reads)).to(dev)
-        o = torch.zeros(len(sel) * cap * 2, dtype=torch.int64, device=dev)
-        nn = torch.zeros(len(sel), dtype=torch.int32, device=dev)
-        S.match_batch(ix, d, len(sel), L, o, cap, nn, mode=mode, min_len=args.l)
-        w = o.cpu().numpy().view(np.uint64).reshape(len(sel), 2 * cap)
-        k = nn.cpu().numpy()
-        for i, (name, _) in enumerate(sel):
-            if k[i] > cap:
-                raise SystemExit("%s: %d matches exceed --cap %d" % (name.decode(), k[i], cap))
-            ms = S.unpack_records(w[i], k[i], cap)
-            out.write(name.decode() + "\t" + str(int(k[i])) + "".join(
-                "\t%d,%d,%d" % m for m in ms) + "\n")
+        sel_all = [(n, s) for n, s in recs if len(s) == L and L > 0]
+        for c0 in range(0, len(sel_all), args.batch):
+            sel = sel_all[c0:c0 + args.batch]
+            reads = S.prepare_reads(np.frombuffer(b"".join(s for _, s in sel),
+                                                  np.uint8).reshape(-1, L))
+            d = torch.from_numpy(np.ascontiguousarray(reads)).to(dev)
+            cap = max(1, L - args.l + 1) if mode != "MEM" else args.cap
+            while True:
+                o = torch.zeros(len(sel) * cap * 2, dtype=torch.int64, device=dev)
+                nn = torch.zeros(len(sel), dtype=torch.int32, device=dev)
+                S.match_batch(ix, d, len(sel), L, o, cap, nn, mode=mode, min_len=args.l)
+                k = nn.cpu().numpy()
+                if int(k.max()) <= cap:
+                    break
+                cap = int(k.max())           # MEM: every occurrence is a record
+            w = o.cpu().numpy().view(np.uint64).reshape(len(sel), 2 * cap)
+            for i, (name, _) in enumerate(sel):
+                ms = S.unpack_records(w[i], k[i], cap)
+                out.write(name.decode() + "\t" + str(int(k[i])) + "".join(
+                    "\t%d,%d,%d" % m for m in ms) + "\n")
 
 
 def sam_records_in(path):
@@ -482,14 +489,17 @@ def main(argv=None):
     p.add_argument("-l", type=int, default=20, help="minimum match length (query.h:129)")
     p.add_argument("--tag", action="store_true", help="append mappability_tag L/R columns")
     p.add_argument("--out", default=None, help="default mapout/mapout.1.txt")
-    p.add_argument("--batch", type=int, default=1_000_000, help="pairs per device batch")
+    p.add_argument("--batch", type=int, default=250_000,
+                   help="pairs per device batch (device memory ~ batch x 2 x (L - l + 1) x 48 B)")
     p.add_argument("query", help="unmapped SAM (fastqs_to_sam output), FASTA or FASTQ")
     p.set_defaults(fn=cmd_memsam)
     p = sub.add_parser("search")
     p.add_argument("-mum", action="store_true")
     p.add_argument("-maxmatch", action="store_true")
     p.add_argument("-l", type=int, default=20, help="minimum match length (query.h:129)")
-    p.add_argument("--cap", type=int, default=65536, help="records per read")
+    p.add_argument("--cap", type=int, default=256,
+                   help="-maxmatch: initial records per read (grown when exceeded)")
+    p.add_argument("--batch", type=int, default=200_000, help="reads per device batch")
     p.add_argument("query")
     p.set_defaults(fn=cmd_search)
     args = ap.parse_args(argv)

@@ -233,3 +233,23 @@ def test_formatter_full_lines_equal_reference(tiny_ix, tables, s, tagged):
                               nomap=True, tag=tagged, small_chr=small)
     assert terr == 0
     assert sorted(text.decode().splitlines()) == _golden_full(s, tagged)
+
+
+@pytest.mark.parametrize("mode,n,golden,nomap", [("MEM", 60, "s100_60_mapout_MEM_full", True),
+                                                 ("MUM", 300, "s100_300_mapout_MUM_full", False)])
+def test_formatter_other_modes_equal_reference(tiny_ix, tables, mode, n, golden, nomap):
+    """-maxmatch / -mum through -samout: the reference's own triples (in the
+    order longSA::MEM / MUM emit them) formatted on the host == the
+    reference's full mapout lines.  Under -maxmatch many alignments tie in
+    to_print order (qpos, rc); the order of the tie is std::sort's over the
+    to_merge order, as in query.cpp:292."""
+    mapbin, offsets, small = tables
+    names, seqs, quals, opts, reads = load_sam_input("s100")
+    names, seqs, quals, opts, reads = names[:n], seqs[:n], quals[:n], opts[:n], reads[:n]
+    triples = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+               for l in read_gz_lines("s100_%s.txt.gz" % mode)][:n]
+    cap = max(1, max(len(t) for t in triples))
+    rec, cnt = py_records(tiny_ix, mapbin, offsets, reads, triples, cap)
+    text, terr = S.sam_format(tiny_ix.contigs, rec, cnt, cap, names, seqs, quals, opts,
+                              nomap=nomap, tag=False, small_chr=small)
+    assert sorted(text.decode().splitlines()) == sorted(read_gz_lines(golden + ".txt.gz"))
