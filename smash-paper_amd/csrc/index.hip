@@ -63,7 +63,7 @@ void upload_tables(smash_index *ix, hipStream_t s) {
 
 void account(smash_index *ix) {
   const uint64_t N = ix->N;
-  ix->device_bytes = (N + 64) + 2 * N * ix->idx_bytes + N + 16 * ix->n_ovf +
+  ix->device_bytes = (N + 64) + 2 * N * ix->idx_bytes + (N + 64) + 16 * ix->n_ovf +
                      ix->map_bytes + 16 * ix->n_seq + (N + 64) +
                      (ix->kmer_k ? 16ull << (2 * ix->kmer_k) : 0) +
                      (ix->bitmap_b ? (1ull << (2 * ix->bitmap_b)) / 8 : 0);
@@ -244,7 +244,8 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
     }
     if (!read_file(base + ".lcp.vec.bin", buf) || buf.size() != N)
       throw hip_failure{"cannot read lcp.vec.bin"};
-    ix->d_lcp8 = dalloc<uint8_t>(N);
+    ix->d_lcp8 = dalloc<uint8_t>(N + 64);   // zero pad: 16-byte probes at the last entry
+    SMASH_HIPX(hipMemset(ix->d_lcp8 + N, 0, 64));
     SMASH_HIPX(hipMemcpy(ix->d_lcp8, buf.data(), N, hipMemcpyHostToDevice));
     if (!read_file(base + ".lcp.m.bin", buf) || buf.size() != n_m * 16)
       throw hip_failure{"cannot read lcp.m.bin"};

@@ -199,7 +199,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
         {reinterpret_cast<uint64_t>(ix->d_text), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_sa), N * isz},
         {reinterpret_cast<uint64_t>(ix->d_isa), N * isz},
-        {reinterpret_cast<uint64_t>(ix->d_lcp8), N},
+        {reinterpret_cast<uint64_t>(ix->d_lcp8), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_uniq), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_kmer), 16ull << (2 * ix->kmer_k)},
         {reinterpret_cast<uint64_t>(ix->d_bitmap), 8 * (((1ull << (2 * ix->bitmap_b)) >> 6) + 1)},

@@ -24,8 +24,10 @@
 #pragma once
 #include "mam_device.hpp"
 
-// the 16-byte probe (the host emulation, tools/sm_emu, substitutes a checked
-// load here)
+// the 16-byte probe at byte address a (not necessarily aligned: gfx950's
+// global loads take any byte address, and a block that stays inside one
+// 64-byte line is one request).  The host emulation, tools/sm_emu,
+// substitutes a checked, counted load here.
 #ifndef PAD_KEEP
 #define PAD_KEEP(x) asm volatile("" : "+v"(x))
 #endif
@@ -36,11 +38,17 @@
 #define SM_HOOK_BS(size, depth)   // host emulation: interval statistics
 #endif
 #ifndef SM_LOAD16
-#define SM_LOAD16(a) (*reinterpret_cast<const uint4 *>((a) & ~uint64_t(15)))
+#define SM_LOAD16(a) ::smash::sm::load16u(a)
 #endif
 
 namespace smash {
 namespace sm {
+
+__device__ __forceinline__ uint4 load16u(uint64_t a) {
+  uint4 v;
+  __builtin_memcpy(&v, reinterpret_cast<const uint8_t *>(a), 16);
+  return v;
+}
 
 // record / LDS row geometry for a launch (reads up to max_len bases)
 struct Geom {
@@ -148,7 +156,11 @@ __global__ __launch_bounds__(256) void k_prep(const uint8_t *__restrict__ seqs, 
   for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) dst[k] = out[k];
 }
 
-// lane states: S_COPY and above own a pending 16-byte probe at `addr`
+// lane states: S_COPY and above own a pending 16-byte probe at `addr`.
+// S_BYTE and above probe byte arrays (text, U, L8) at the exact byte
+// address (the block holds bytes [addr, addr + 16)); the states below
+// probe aligned 16-byte blocks (records, bitmap words, k-mer entries,
+// SA / ISA elements) and find their element at addr & 15.
 enum : uint32_t { S_EXIT = 0, S_NEW, S_ALU, S_COPY, S_BM, S_KT, S_IDX, S_BYTE, S_CMP, S_USCAN,
                   S_EXL, S_EXR, S_EXB };
 // S_IDX ops (an SA / ISA element arrived; *2: a second one in v2)
@@ -367,17 +379,20 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   auto uscan_start = [&](uint64_t p, uint32_t d) {
     dch = d; j = 1;
     addr = reinterpret_cast<uint64_t>(c.U + p + 1);
-    addr2 = (addr & ~uint64_t(15)) + 16;
-    need2 = d - 1 > 16 - (uint32_t(addr) & 15);
+    addr2 = addr + 16;
+    need2 = d - 1 > 16;
     st = S_USCAN;
   };
   // a run [es, ee] grows within [lb, hb] while L8 >= xd: both sides' first
   // blocks in one iteration (S_EXB), or the one side with room; false: none
+  // left blocks are the 16 bytes ENDING at es (from 0 when es < 15), right
+  // blocks start at ee + 1
+  auto lblock = [&](uint64_t e) { return reinterpret_cast<uint64_t>(c.L8 + (e >= 15 ? e - 15 : 0)); };
   auto ex_start = [&](uint64_t lb, uint64_t hb) {
     const bool l = es > lb, r = ee < hb;
     nblk = 0;
     rdone = !r;
-    addr = reinterpret_cast<uint64_t>(c.L8 + (l ? es : ee + 1));
+    addr = l ? lblock(es) : reinterpret_cast<uint64_t>(c.L8 + ee + 1);
     addr2 = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
     need2 = l && r;
     st = l && r ? S_EXB : l ? S_EXL : S_EXR;
@@ -413,8 +428,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       need2 = false;
     }
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
-    if (st >= S_COPY) v = SM_LOAD16(addr);
-    if (need2) v2 = SM_LOAD16(addr2);
+    const uint64_t amask = st >= S_BYTE ? ~uint64_t(0) : ~uint64_t(15);
+    if (st >= S_COPY) v = SM_LOAD16(addr & amask);
+    if (need2) v2 = SM_LOAD16(addr2 & amask);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
     if (newm) {
       if (take) base = __shfl(base, int(__builtin_ctzll(newm)), 64);
@@ -447,7 +463,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
              depth, (unsigned long long)start, (unsigned long long)end, (unsigned long long)pos,
              int(have_pos));
 #endif
-    const uint32_t ao = uint32_t(addr) & 15;
+    const uint32_t ao = st >= S_BYTE ? 0u : uint32_t(addr) & 15;   // element offset in v
     uint32_t a = A_NONE;
 
     // ---------------- consume ----------------
@@ -555,9 +571,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           a = op == O_SAPOS ? A_TRAV : A_AFTER;
         } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
           sp = iv;
+          // 16 bytes first: a binary-search probe usually decides early
           addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
-          addr2 = (addr & ~uint64_t(15)) + 16;
-          need2 = cap - lc > 16 - (uint32_t(addr) & 15);
+          addr2 = addr + 16;
+          need2 = false;
           st = S_CMP; op = O_BS;
         } else if (op == O_ISAJ) {
           start = end = iv; have_pos = false;
@@ -582,21 +599,21 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
-        // bytes [ao, 16) of v, then (need2) the next block v2
+        // text bytes [addr, addr + 16) in v, then (need2) the next 16 in v2
         const uint32_t off = prefix + (op == O_BS ? cbase : depth) + lc;
         const uint32_t rem = op == O_BS ? cap - lc : L - off;
-        const uint32_t lim = rem < 16 - ao ? rem : 16 - ao;
-        uint32_t k = agree_block(v, ao, P, off, lim);
+        const uint32_t lim = rem < 16 ? rem : 16u;
+        uint32_t k = agree_block(v, 0, P, off, lim);
         if (need2 && k == lim && k < rem) {
           const uint32_t lim2 = rem - k < 16 ? rem - k : 16u;
           k += agree_block(v2, 0, P, off + k, lim2);
         }
-        const uint32_t got = need2 ? (rem < 32 - ao ? rem : 32 - ao) : lim;   // bytes available
+        const uint32_t got = need2 ? (rem < 32 ? rem : 32u) : lim;   // bytes available
         lc += k;
         if (k == got && k < rem) {                    // agreed on all loaded bytes: go on
           addr += k;
-          addr2 = (addr & ~uint64_t(15)) + 16;
-          need2 = rem - k > 16 - (uint32_t(addr) & 15);
+          addr2 = addr + 16;
+          need2 = rem - k > 16;
         } else if (op == O_EXT) {
           need2 = false;
           depth += lc; lc = 0;
@@ -607,8 +624,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           if (bsm == BS_INSERT) {
             // P' < S_m iff P' ran out (prefix of S_m) or the first differing
             // byte of P' is smaller (signed chars, like the reference)
-            const uint32_t tpos = ao + k;
-            const uint32_t tbyte = tpos < 16 ? byte_at(v, tpos) : byte_at(v2, tpos - 16);
+            const uint32_t tbyte = k < 16 ? byte_at(v, k) : byte_at(v2, k - 16);
             left = k == rem || int8_t(P[off + k]) < int8_t(tbyte);
             if (lc > best) { best = lc; bpos = sp; bi = m; }
           } else {                                    // in the run iff lcp reaches cap
@@ -621,19 +637,18 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_USCAN: {                                // (B) first j with U[pos+j] >= d-j
-        // bytes [ao, 16) of v, then (need2) the whole next block v2
+        // U bytes [addr, addr + 16) in v, then (need2) the next 16 in v2
         bool fin = false;
 #pragma unroll
         for (uint32_t h = 0; h < 2; ++h) {
           if (fin || (h == 1 && !need2)) break;
           const uint4 &u = h ? v2 : v;
-          const uint32_t o = h ? 0u : ao;
           const uint32_t D = dch - j;
-          const uint32_t lim = D < 16 - o ? D : 16 - o;
-          const uint32_t inr = ((1u << lim) - 1) << o;
-          const uint32_t hm = byte_mask(u, [&](uint32_t b, uint32_t i) { return b + i >= D + o; }) & inr;
+          const uint32_t lim = D < 16 ? D : 16u;
+          const uint32_t inr = (1u << lim) - 1;
+          const uint32_t hm = byte_mask(u, [&](uint32_t b, uint32_t i) { return b + i >= D; }) & inr;
           if (hm) {
-            j += uint32_t(__builtin_ctz(hm)) - o; hit = true; fin = true;
+            j += uint32_t(__builtin_ctz(hm)); hit = true; fin = true;
           } else {
             j += lim;
             if (j >= dch) { hit = false; fin = true; }
@@ -643,7 +658,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           need2 = false;
           a = A_CHAIN_DONE;
         } else {
-          addr = (addr & ~uint64_t(15)) + (need2 ? 32 : 16);
+          addr += need2 ? 32 : 16;
           addr2 = addr + 16;
           need2 = dch - j > 16;
         }
@@ -669,10 +684,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           return k;
         };
         bool moreL = false, moreR = false;
-        if (st != S_EXR) es -= side(v, ao, true, moreL);
+        // the left block ends at es (position es - its start), the right one
+        // starts at ee + 1 (position 0)
+        if (st != S_EXR)
+          es -= side(v, uint32_t(es - (addr - reinterpret_cast<uint64_t>(c.L8))), true, moreL);
         if (st != S_EXL) {
           const bool b2 = st == S_EXB;
-          ee += side(b2 ? v2 : v, b2 ? (uint32_t(addr2) & 15) : ao, false, moreR);
+          ee += side(b2 ? v2 : v, 0u, false, moreR);
           if (b2) rdone = !moreR;
         }
         need2 = false;
@@ -681,7 +699,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         if (!more) {
           a = left ? A_XL_DONE : A_RUN_DONE;
         } else if (++nblk < c.lin_blocks) {
-          addr = reinterpret_cast<uint64_t>(c.L8 + (left ? es : ee + 1));
+          addr = left ? lblock(es) : reinterpret_cast<uint64_t>(c.L8 + ee + 1);
           st = left ? S_EXL : S_EXR;
         } else {                                      // long run: bisect for its end
           bsm = left ? BS_LEFT : BS_RIGHT;
@@ -891,8 +909,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             st = S_IDX; op = O_SAPOS;
           } else {
             addr = reinterpret_cast<uint64_t>(c.T + pos + depth);
-            addr2 = (addr & ~uint64_t(15)) + 16;
-            need2 = L - prefix - depth > 16 - (uint32_t(addr) & 15);
+            addr2 = addr + 16;
+            need2 = L - prefix - depth > 16;
             st = S_CMP; op = O_EXT; lc = 0;
           }
         } else {                                     // search [start, end] for P'

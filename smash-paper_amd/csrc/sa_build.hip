@@ -516,7 +516,10 @@ uint32_t *build_lcp32(smash_index *ix, hipStream_t s) {
 
 void finish_lcp(smash_index *ix, const uint32_t *lcp, hipStream_t s) {
   const uint64_t N = ix->N;
-  if (!ix->d_lcp8) ix->d_lcp8 = dalloc<uint8_t>(N);
+  if (!ix->d_lcp8) {   // + 64 zero bytes: 16-byte probes may start at the last entry
+    ix->d_lcp8 = dalloc<uint8_t>(N + 64);
+    SMASH_HIPX(hipMemsetAsync(ix->d_lcp8 + N, 0, 64, s));
+  }
   uint8_t *flag = dalloc<uint8_t>(N);
   k_lcp8<<<grid_for(N, kBlock, 65536), kBlock, 0, s>>>(lcp, N, ix->d_lcp8, flag);
   uint64_t *d_nsel = dalloc<uint64_t>(1);

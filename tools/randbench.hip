@@ -64,6 +64,24 @@ __global__ __launch_bounds__(256) void k_chase_line(const uint4 *buf, uint64_t n
   if (acc == 0x123456789ull) sink[0] = acc;
 }
 
+// one 16-byte load per step at a random byte offset inside a random 64-byte
+// line (never crossing it): is an unaligned probe one request?
+__global__ __launch_bounds__(256) void k_chase_ua(const uint8_t *buf, uint64_t n64, int steps,
+                                                  uint64_t *sink, uint64_t seed) {
+  const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  uint64_t h = mix(t + seed);
+  uint64_t acc = 0;
+  for (int s = 0; s < steps; ++s) {
+    const uint64_t a = (h % n64) * 64 + (h >> 58) % 49;
+    uint4 v;
+    __builtin_memcpy(&v, buf + a, 16);
+    const uint32_t x = v.x ^ v.w;
+    acc += x;
+    h = mix(h + x + 1);
+  }
+  if (acc == 0x123456789ull) sink[0] = acc;
+}
+
 int main(int argc, char **argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -102,11 +120,12 @@ int main(int argc, char **argv) {
     if (lines) {
       const int wps = 4, steps = 64;
       const uint64_t threads = uint64_t(wps) * 4 * cus * 64;
-      for (int w : {1, 2, 4}) {
+      for (int w : {1, 2, 4, 0}) {   // 0: one unaligned 16-byte load inside the line
         hipEvent_t a, b;
         CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
         auto launch = [&](uint64_t seed) {
-          if (w == 1) k_chase_line<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
+          if (w == 0) k_chase_ua<<<unsigned(threads / 256), 256>>>((const uint8_t *)buf, n16 / 4, steps, sink, seed);
+          else if (w == 1) k_chase_line<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
           else if (w == 2) k_chase_line<2><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
           else k_chase_line<4><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, n16, steps, sink, seed);
         };
@@ -119,8 +138,10 @@ int main(int argc, char **argv) {
         float ms = 0;
         CK(hipEventElapsedTime(&ms, a, b));
         const double ln = 3.0 * threads * steps;
-        std::printf("footprint %8.3f GiB  waves/SIMD %d  %d x 16 B per line : %.3f G lines/s  %.3f G loads/s\n",
-                    g, wps, w, ln / (ms * 1e-3) * 1e-9, w * ln / (ms * 1e-3) * 1e-9);
+        std::printf("footprint %8.3f GiB  waves/SIMD %d  %s : %.3f G lines/s  %.3f G loads/s\n",
+                    g, wps, w == 0 ? "1 x 16 B unaligned" : w == 1 ? "1 x 16 B per line " :
+                    w == 2 ? "2 x 16 B per line " : "4 x 16 B per line ",
+                    ln / (ms * 1e-3) * 1e-9, (w ? w : 1) * ln / (ms * 1e-3) * 1e-9);
         std::fflush(stdout);
         CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
       }

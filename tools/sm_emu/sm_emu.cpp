@@ -16,22 +16,29 @@ static const uint64_t *emu_spans;
 static uint64_t emu_rec_lo, emu_rec_hi, emu_bad;
 static uint64_t emu_probes[8], emu_lines[8], emu_last[8];
 static unsigned long long emu_ws[64];   // the kernel's STATS counters of the last run
+// the 16 bytes at address a, exactly (the kernel aligns the blocks it wants
+// aligned); a block crossing a 64-byte line is two requests and touches two
+// lines
 static uint4 emu_load16(uint64_t a) {
   int arr = -1;
   if (a >= emu_rec_lo && a < emu_rec_hi) arr = 7;
   for (int k = 0; k < 7 && arr < 0; ++k)
     if (a >= emu_spans[2 * k] && a < emu_spans[2 * k + 1]) arr = k;
   if (arr < 0) { ++emu_bad; return uint4{0, 0, 0, 0}; }
-  ++emu_probes[arr];
-  if ((a >> 6) != emu_last[arr]) { ++emu_lines[arr]; emu_last[arr] = a >> 6; }
-  // the block may run past (or start before) the array: copy the valid bytes
-  const uint64_t lo = arr == 7 ? emu_rec_lo : emu_spans[2 * arr];
+  for (uint64_t line = a >> 6; line <= (a + 15) >> 6; ++line) {
+    ++emu_probes[arr];
+    if (line != emu_last[arr]) { ++emu_lines[arr]; emu_last[arr] = line; }
+  }
+  // the block may run past the array: copy the valid bytes
   const uint64_t hi = arr == 7 ? emu_rec_hi : emu_spans[2 * arr + 1];
-  const uint64_t b = a & ~uint64_t(15);
-  if (b >= lo && b + 16 <= hi) return *reinterpret_cast<const uint4 *>(b);
+  if (a + 16 <= hi) {
+    uint4 r;
+    std::memcpy(&r, reinterpret_cast<const void *>(a), 16);
+    return r;
+  }
   uint8_t buf[16] = {0};
   for (uint64_t k = 0; k < 16; ++k)
-    if (b + k >= lo && b + k < hi) buf[k] = *reinterpret_cast<const uint8_t *>(b + k);
+    if (a + k < hi) buf[k] = *reinterpret_cast<const uint8_t *>(a + k);
   uint4 r;
   std::memcpy(&r, buf, 16);
   return r;
