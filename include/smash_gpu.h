@@ -186,7 +186,8 @@ typedef struct {
   const int64_t *h_bin_starts;   /* [nbins] bins.txt col 3 (start abspos), ascending */
   int32_t min_excess;        /* smashMEM arg 5 (smash_mapping.sh:25: 4) */
   int64_t hit_window;        /* smashMEM arg 4 (10000) */
-  uint64_t dedup_capacity;   /* distinct pair keys the persistent set holds */
+  uint64_t dedup_capacity;   /* distinct pair keys the persistent set holds
+                                (exact keys: ~16 hit words per key of arena) */
 } smash_pipeline_cfg;
 
 int smash_pipeline_create(const smash_index *ix, const smash_pipeline_cfg *cfg,
@@ -204,15 +205,21 @@ int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
 
 /* Multi-GPU phases (one rank per GPU; the caller runs the collectives):
  *  1. smash_phase_map      -- map/resolve/tag/filter/hash + in-batch first-wins
- *  2. smash_phase_export   -- (key hash, global pair index) of in-batch-first
- *                             keys into d_send[n][3] grouped by owner rank
- *                             (hash % world); h_send_counts[world] filled
- *                             (synchronises the stream)
- *     caller: all_to_all(d_send) -> d_recv
- *  3. smash_dedup_owner    -- owner side: for received entries decide
- *                             first-wins against the persistent set (global
- *                             index order), insert winners, write one byte
- *                             per entry (1 = keep) into d_flags
+ *  2. smash_phase_export   -- the in-batch-first keys grouped by owner rank
+ *                             (hash % world): per key a 5-word header {hash hi,
+ *                             hash lo, global pair index, nk, word offset in
+ *                             its owner segment} in *d_send and the key's nk
+ *                             canonical hit words (tid << 48 | pos0) in
+ *                             *d_send_words (both pipeline-owned, valid until
+ *                             the next export); h_send_counts[world] /
+ *                             h_send_words[world] filled (synchronises)
+ *     caller: all_to_all of the counts, then of d_send (5 words per key) and
+ *             of d_send_words -> d_recv, d_recv_words (source-rank order)
+ *  3. smash_dedup_owner    -- owner side: first-wins in global index order
+ *                             over the EXACT keys, against the persistent set;
+ *                             inserts winners; one byte per received header
+ *                             into d_flags (1 = keep).  h_recv_counts /
+ *                             h_recv_words: per source rank (synchronises)
  *     caller: all_to_all(d_flags) back, in d_send order
  *  4. smash_phase_import   -- apply the returned flags
  *  5. smash_phase_positions-- emit kept positions; d_tail[2] = {count, last
@@ -222,9 +229,13 @@ int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
 int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                     void *stream);
 int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
-                       uint64_t *d_send, int64_t *h_send_counts, void *stream);
+                       int64_t *h_send_counts, int64_t *h_send_words,
+                       const uint64_t **d_send, const uint64_t **d_send_words,
+                       void *stream);
 int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint64_t n_recv,
-                      uint8_t *d_flags, void *stream);
+                      const uint64_t *d_recv_words, const int64_t *h_recv_counts,
+                      const int64_t *h_recv_words, int world, uint8_t *d_flags,
+                      void *stream);
 int smash_phase_import(smash_pipeline *p, const uint8_t *d_flags_back,
                        void *stream);
 int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *stream);

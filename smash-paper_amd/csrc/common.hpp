@@ -88,6 +88,7 @@ struct smash_index {
   uint8_t *d_map = nullptr;
   uint64_t map_bytes = 0;
   uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
+  mutable uint64_t *d_nsdir = nullptr;   // first U < 255 per 4096 positions (mappability.hip)
   uint64_t *d_kmer = nullptr;    // {lo,hi} per k-mer
   uint32_t kmer_k = 0;
   uint64_t *d_bitmap = nullptr;  // B-mer presence bits (aux_build.hip)

@@ -16,19 +16,35 @@
 // variable-width bin (abspos = chrom_sizes offset + i, bisect_right over the
 // bin starts, i = 0 lands in the last bin as in varbin.py:89-92).
 //
-// Memory: per forward base two sequential 8-byte ISA reads (forward and
-// reverse-complement strand, the latter walking down) and two random LCP
-// reads (adjacent bytes, one 64-B line each) -> ~146 B per base, HBM-bound.
-// Each block takes a tile of consecutive bases (coalesced ISA loads); the
-// bin counts of a tile, which spans few bins, go through LDS.
+// Streaming form.  U[x] = min(255, max(LCP[ISA[x]], LCP[ISA[x] + 1])) is
+// resident with the index (aux_build.hip), so m(x) = U[x] + 1 exactly when
+// U[x] < 255: the scan reads U at the forward position sp + i and at the
+// reverse-complement position sp + 2S - i, both sequentially, and writes the
+// two bytes -- 4 B per base, HBM-streaming -- instead of two ISA reads and
+// two random LCP lines per base.  When U[x] == 255 (m >= 256: N runs, long
+// repeats) the byte is 255 unless the edge rule zeroes it, and that rule is
+// decided without the exact m whenever possible:
+//   * m >= 256, so right is zeroed if i + 256 >= S, left if i <= 256;
+//   * m(x) <= m(y) + (y - x) for any y > x (the match that gives m(x), moved
+//     y - x positions on, is a match of the suffix at y), so with y the next
+//     text position holding U[y] < 255, m(x) <= U[y] + 1 + (y - x): right is
+//     kept when i + that bound < S, left when the bound < i.
+// Only the bases left undecided (saturated runs that reach a contig end)
+// take the exact path: ISA, then the LCP bytes and the overflow table.  The
+// next unsaturated position comes from the block's own U bytes, else from a
+// directory of the first unsaturated position per 4096 text positions
+// (built once per index, 12 MB at hg19).
 #include "common.hpp"
 
 namespace smash {
 namespace {
 
-constexpr int kMB = 256;          // threads per block
-constexpr int kMItems = 16;       // bases per thread per tile
-constexpr int kLdsBins = 32;      // bins of a tile counted in LDS
+constexpr int kMB = 256;                    // threads per block
+constexpr int kMPer = 16;                   // consecutive bases per thread
+constexpr uint64_t kMTile = uint64_t(kMB) * kMPer;
+constexpr int kDirShift = 12;               // directory: 4096 text positions per entry
+constexpr int kLdsBins = 32;                // bins of a tile counted in LDS
+constexpr uint64_t kNone = ~0ull;
 
 struct MapCtx {
   const uint8_t *L8;
@@ -55,14 +71,55 @@ __device__ __forceinline__ uint64_t min_len_at(const MapCtx &c, uint64_t r) {
   return (a > b ? a : b) + 1;
 }
 
-__device__ __forceinline__ uint32_t bin_of(const MapCtx &c, int64_t a) {
+__device__ __forceinline__ uint32_t bisect_right(const MapCtx &c, int64_t a) {
   uint32_t lo = 0, hi = c.nbins;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     if (a < c.bins[mid]) hi = mid;
     else lo = mid + 1;
   }
-  return lo == 0 ? c.nbins - 1 : lo - 1;
+  return lo;
+}
+
+__device__ __forceinline__ uint4 load16u(const uint8_t *p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ uint32_t byte_of(const uint4 &v, uint32_t q) {
+  const uint32_t w = q < 4 ? v.x : q < 8 ? v.y : q < 12 ? v.z : v.w;
+  return (w >> (8 * (q & 3))) & 0xFF;
+}
+
+// dir[t] = the first text position p in [t << 12, (t + 1) << 12) with
+// U[p] < 255, else kNone
+__global__ __launch_bounds__(kMB) void k_nsdir(const uint8_t *__restrict__ U, uint64_t N,
+                                               uint64_t *__restrict__ dir, uint64_t ndir) {
+  __shared__ unsigned long long s_first;
+  for (uint64_t t = blockIdx.x; t < ndir; t += gridDim.x) {
+    if (threadIdx.x == 0) s_first = kNone;
+    __syncthreads();
+    const uint64_t p0 = (t << kDirShift) + uint64_t(threadIdx.x) * kMPer;
+    uint64_t f = kNone;
+    if (p0 < N) {
+      const uint4 v = load16u(U + p0);
+      for (uint32_t q = 0; q < uint32_t(kMPer) && f == kNone; ++q)
+        if (p0 + q < N && byte_of(v, q) < 255) f = p0 + q;
+    }
+    if (f != kNone) atomicMin(&s_first, (unsigned long long)f);
+    __syncthreads();
+    if (threadIdx.x == 0) dir[t] = s_first;
+    __syncthreads();
+  }
+}
+
+// the first unsaturated text position >= p (kNone: none before N), from
+// the directory; p must be a multiple of 4096 or the caller must accept a
+// later (looser) position
+__device__ uint64_t next_unsat_dir(const uint64_t *dir, uint64_t ndir, uint64_t p) {
+  for (uint64_t t = (p + (uint64_t(1) << kDirShift) - 1) >> kDirShift; t < ndir; ++t)
+    if (dir[t] != kNone) return dir[t];
+  return kNone;
 }
 
 // bases [i0, i1) of one contig (text start sp, size S); out: map.bin bytes of
@@ -70,55 +127,152 @@ __device__ __forceinline__ uint32_t bin_of(const MapCtx &c, int64_t a) {
 // not binned)
 template <class IdxT>
 __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restrict__ ISA,
+                                                 const uint8_t *__restrict__ U,
+                                                 const uint64_t *__restrict__ dir, uint64_t ndir,
                                                  uint64_t sp, uint64_t S, uint64_t i0, uint64_t i1,
                                                  uint8_t *__restrict__ out, int64_t abs0,
                                                  unsigned long long *bin_counts,
                                                  unsigned long long *contig_count) {
-  __shared__ unsigned long long s_bin[kLdsBins];
+  __shared__ unsigned long long s_bin[kLdsBins + 1];
+  __shared__ int64_t s_bs[kLdsBins];
   __shared__ unsigned long long s_tot;
-  __shared__ uint32_t s_b0;
-  const uint64_t tile = uint64_t(kMB) * kMItems;
-  const uint64_t ntiles = (i1 - i0 + tile - 1) / tile;
+  __shared__ uint32_t s_o0;
+  __shared__ uint64_t s_f[kMB], s_r[kMB];   // per chunk: first unsaturated (fwd / rc text order)
+  __shared__ uint64_t s_ftail, s_rtail;
+  const uint64_t N = c.N;
+  const bool binned = abs0 >= 0 && c.nbins;
+  const uint64_t ntiles = (i1 - i0 + kMTile - 1) / kMTile;
   for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t t0 = i0 + t * tile;
-    if (threadIdx.x < kLdsBins) s_bin[threadIdx.x] = 0;
+    const uint64_t t0 = i0 + t * kMTile;
+    if (threadIdx.x <= kLdsBins) s_bin[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       s_tot = 0;
-      s_b0 = (abs0 >= 0 && c.nbins) ? bin_of(c, abs0 + int64_t(t0)) : 0;
+      s_o0 = binned ? bisect_right(c, abs0 + int64_t(t0)) : 0;
     }
     __syncthreads();
-    const uint32_t b0 = s_b0;
-    unsigned long long mine = 0;
-#pragma unroll 4
-    for (int j = 0; j < kMItems; ++j) {
-      const uint64_t i = t0 + uint64_t(j) * kMB + threadIdx.x;
-      if (i >= i1) break;
-      const uint64_t sapos = ISA[sp + i];
-      const uint64_t rcsapos = ISA[sp + 2 * S - i];
-      uint64_t right = min_len_at(c, sapos);
-      uint64_t left = min_len_at(c, rcsapos);
-      if (right + i >= S) right = 0;
-      if (left >= i) left = 0;
-      if (out) {
-        const uint64_t o = 2 * (i - i0);
-        out[o] = uint8_t(left < 255 ? left : 255);
-        out[o + 1] = uint8_t(right < 255 ? right : 255);
+    const uint32_t o0 = s_o0;
+    if (binned && threadIdx.x < kLdsBins)
+      s_bs[threadIdx.x] = o0 + threadIdx.x < c.nbins ? c.bins[o0 + threadIdx.x] : INT64_MAX;
+    // this thread's 16 bases: U at the forward positions (ascending) and at
+    // the reverse-complement positions (descending; byte 15 - q is base q)
+    const uint64_t ib = t0 + uint64_t(threadIdx.x) * kMPer;
+    const uint64_t xf = sp + ib, xr = sp + 2 * S - ib;   // xr - q: base ib + q
+    const uint4 fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    const uint4 rw = xr >= 15 ? load16u(U + xr - 15) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    uint32_t satf = 0, satr = 0;   // bit q: U == 255 at base ib + q
+    uint64_t ff = kNone, fr = kNone;
+#pragma unroll
+    for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
+      const bool sf = byte_of(fw, q) == 255 || xf + q >= N;
+      const bool sr = byte_of(rw, 15 - q) == 255 || xr < q;
+      satf |= uint32_t(sf) << q;
+      satr |= uint32_t(sr) << q;
+      if (!sf && ff == kNone) ff = xf + q;                 // lowest fwd text position
+      if (!sr) fr = xr - q;                                // lowest rc text position (largest q)
+    }
+    const bool any_sat = __syncthreads_or((satf | satr) != 0);
+    uint64_t fnext = kNone, rnext = kNone;   // first unsaturated chunk after / before mine
+    if (any_sat) {
+      // suffix-min of the forward chunk heads over later chunks, prefix-min of
+      // the rc chunk heads over earlier chunks (higher text positions)
+      s_f[threadIdx.x] = ff;
+      s_r[threadIdx.x] = fr;
+      if (threadIdx.x == 0) {
+        s_ftail = next_unsat_dir(dir, ndir, sp + t0 + kMTile);
+        s_rtail = next_unsat_dir(dir, ndir, xr + 1);       // above the tile's rc range
       }
-      const uint64_t rb = right < 255 ? right : 255;
+      __syncthreads();
+      for (uint32_t d = 1; d < uint32_t(kMB); d <<= 1) {
+        const uint64_t a = threadIdx.x + d < uint32_t(kMB) ? s_f[threadIdx.x + d] : kNone;
+        const uint64_t b = threadIdx.x >= d ? s_r[threadIdx.x - d] : kNone;
+        __syncthreads();
+        s_f[threadIdx.x] = a < s_f[threadIdx.x] ? a : s_f[threadIdx.x];
+        s_r[threadIdx.x] = b < s_r[threadIdx.x] ? b : s_r[threadIdx.x];
+        __syncthreads();
+      }
+      fnext = threadIdx.x + 1 < uint32_t(kMB) ? s_f[threadIdx.x + 1] : kNone;
+      rnext = threadIdx.x > 0 ? s_r[threadIdx.x - 1] : kNone;
+      if (fnext == kNone) fnext = s_ftail;
+      if (rnext == kNone) rnext = s_rtail;
+    }
+    uint32_t ob[2 * kMPer / 4] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long mine = 0;
+    uint32_t d = 0;   // bin ordinal offset from o0 (monotone over the thread's bases)
+#pragma unroll 4
+    for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
+      const uint64_t i = ib + q;
+      if (i >= i1) break;
+      // right: m at the forward position, zeroed when m + i >= S (:666)
+      uint64_t right;
+      if (!((satf >> q) & 1)) {
+        right = byte_of(fw, q) + 1;
+        if (right + i >= S) right = 0;
+      } else if (i + 256 >= S) {
+        right = 0;
+      } else {
+        uint64_t y = kNone;   // next unsaturated text position after xf + q
+        for (uint32_t q2 = q + 1; q2 < uint32_t(kMPer) && y == kNone; ++q2)
+          if (!((satf >> q2) & 1)) y = xf + q2;
+        if (y == kNone) y = fnext;
+        const uint64_t ub = y == kNone ? kNone : U[y] + 1 + (y - (xf + q));
+        if (ub != kNone && i + ub < S) right = 255;
+        else {
+          right = min_len_at(c, uint64_t(ISA[xf + q]));
+          if (right + i >= S) right = 0;
+        }
+      }
+      // left: m at the reverse-complement position, zeroed when m >= i (:667)
+      uint64_t left;
+      if (!((satr >> q) & 1)) {
+        left = byte_of(rw, 15 - q) + 1;
+        if (left >= i) left = 0;
+      } else if (i <= 256) {
+        left = 0;
+      } else {
+        uint64_t y = kNone;   // next unsaturated text position above xr - q
+        for (uint32_t q2 = q; q2-- > 0 && y == kNone;)
+          if (!((satr >> q2) & 1)) y = xr - q2;
+        if (y == kNone) y = rnext;
+        const uint64_t ub = y == kNone ? kNone : U[y] + 1 + (y - (xr - q));
+        if (ub != kNone && ub < i) left = 255;
+        else {
+          left = min_len_at(c, uint64_t(ISA[xr - q]));
+          if (left >= i) left = 0;
+        }
+      }
+      const uint32_t lb = uint32_t(left < 255 ? left : 255), rb = uint32_t(right < 255 ? right : 255);
+      ob[q >> 1] |= (lb | (rb << 8)) << (16 * (q & 1));
       if (rb >= 1 && rb <= c.k) {
         ++mine;
-        if (abs0 >= 0 && c.nbins) {
-          const uint32_t b = bin_of(c, abs0 + int64_t(i));
-          const uint32_t d = b - b0;
-          if (d < uint32_t(kLdsBins)) atomicAdd(&s_bin[d], 1ull);
-          else atomicAdd(&bin_counts[b], 1ull);
+        if (binned) {
+          const int64_t a = abs0 + int64_t(i);
+          while (d < uint32_t(kLdsBins) && a >= s_bs[d]) ++d;
+          if (d < uint32_t(kLdsBins)) {
+            atomicAdd(&s_bin[d], 1ull);
+          } else {
+            const uint32_t o = bisect_right(c, a);
+            atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], 1ull);
+          }
+        }
+      }
+    }
+    if (out && ib < i1) {
+      uint8_t *o = out + 2 * (ib - i0);
+      if (ib + kMPer <= i1) {   // 32 bytes (the caller's pointer need not be aligned)
+        __builtin_memcpy(o, ob, 32);
+      } else {
+        for (uint32_t q = 0; q < uint32_t(i1 - ib); ++q) {
+          o[2 * q] = uint8_t(ob[q >> 1] >> (16 * (q & 1)));
+          o[2 * q + 1] = uint8_t(ob[q >> 1] >> (16 * (q & 1) + 8));
         }
       }
     }
     if (mine) atomicAdd(&s_tot, mine);
     __syncthreads();
-    if (threadIdx.x < kLdsBins && s_bin[threadIdx.x] && c.nbins)
-      atomicAdd(&bin_counts[(b0 + threadIdx.x) % c.nbins], s_bin[threadIdx.x]);
+    if (binned && threadIdx.x <= kLdsBins && s_bin[threadIdx.x]) {
+      const uint32_t o = o0 + threadIdx.x;   // ordinal o counts into bin o - 1 (0: the last)
+      atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], s_bin[threadIdx.x]);
+    }
     if (threadIdx.x == 0 && s_tot && contig_count) atomicAdd(contig_count, s_tot);
     __syncthreads();
   }
@@ -136,17 +290,24 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
   c.bins = d_bins;
   c.nbins = d_bins ? nbins : 0;
   c.k = k;
+  // the directory of unsaturated U positions, once per index
+  const uint64_t ndir = (ix->N + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
+  if (!ix->d_nsdir) {
+    SMASH_HIP(hipMalloc(&ix->d_nsdir, 8 * ndir));
+    k_nsdir<<<unsigned(ndir < 65536 ? ndir : 65536), kMB, 0, s>>>(ix->d_uniq, ix->N, ix->d_nsdir,
+                                                                   ndir);
+    SMASH_HIP(hipGetLastError());
+  }
   uint64_t g = 0;   // forward-base coordinate of the contig's first base
   for (uint32_t q = 0; q < ix->n_seq; q += 2) {
     const uint64_t S = ix->sizes[q], sp = ix->startpos[q];
     const uint64_t a = begin > g ? begin - g : 0;
     const uint64_t b = end < g + S ? end - g : S;
     if (a < b && g < end) {
-      const uint64_t n = b - a;
-      const uint64_t tiles = (n + uint64_t(kMB) * kMItems - 1) / (uint64_t(kMB) * kMItems);
+      const uint64_t tiles = (b - a + kMTile - 1) / kMTile;
       const unsigned grid = unsigned(tiles < 65536 ? tiles : 65536);
       k_mapscan<IdxT><<<grid, kMB, 0, s>>>(
-          c, static_cast<const IdxT *>(ix->d_isa), sp, S, a, b,
+          c, static_cast<const IdxT *>(ix->d_isa), ix->d_uniq, ix->d_nsdir, ndir, sp, S, a, b,
           out ? out + 2 * (g + a - begin) : nullptr, h_chrom_off ? h_chrom_off[q / 2] : -1,
           reinterpret_cast<unsigned long long *>(d_bin_counts),
           d_contig_counts ? reinterpret_cast<unsigned long long *>(d_contig_counts + q / 2)
@@ -179,6 +340,10 @@ extern "C" int smash_mappability_scan(const smash_index *ix, uint64_t begin, uin
     return SMASH_ERR_ARG;
   }
   if (begin == end) return SMASH_OK;
+  if (!ix->d_uniq) {
+    set_error("smash_mappability_scan: index lacks U (aux_build)");
+    return SMASH_ERR_ARG;
+  }
   SMASH_HIP(hipSetDevice(ix->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (ix->idx_bytes == 4)

@@ -52,8 +52,11 @@ struct smash_pipeline {
   uint32_t *d_v[2] = {nullptr, nullptr};
   void *d_temp = nullptr;
   size_t temp_bytes = 0;
-  uint64_t *d_table = nullptr;
+  uint64_t *d_table = nullptr;   // {hash hi, arena ref + 1} slots, 0 = empty
   uint64_t table_mask = 0;
+  uint64_t *d_arena = nullptr;   // canonical keys: [lo, nk, hit words...] per key
+  uint64_t arena_cap = 0;        // words
+  unsigned long long *d_arena_top = nullptr;
   uint32_t *d_posoff = nullptr;   // [max_pairs + 1]
   uint32_t *d_cnt = nullptr;      // [max_pairs]
   int64_t *d_pos0 = nullptr, *d_abs = nullptr;
@@ -61,10 +64,16 @@ struct smash_pipeline {
   unsigned long long *d_stats = nullptr;
   uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast -> k_post pair list
   uint8_t *d_post_ws = nullptr;   // k_post workspace: kPostThreads slices
+  uint64_t hash_mask = ~0ull;
   bool post_fast = false;
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
-  unsigned long long *d_owner = nullptr;  // per-owner counters (<= 64 ranks)
+  unsigned long long *d_owner = nullptr;  // per owner: [0,64) entries [64,128) entry cursors
+                                          // [128,192) words [192,256) word cursors
+  uint64_t *d_send_hdr = nullptr; // [n_export][5] {hi, lo, global index, nk, word offset}
+  uint64_t *d_send_words = nullptr;   // the exported keys' hit words, grouped by owner
+  uint64_t send_words_cap = 0;
+  uint64_t *d_recv_base = nullptr;    // [2 * 65] owner side: header / word prefix per source
   uint64_t n_pairs = 0, n_export = 0;
   hipStream_t last = nullptr;
   // profiling (smash_pipeline_profile)
@@ -87,6 +96,8 @@ struct PostCfg {
   int32_t min_excess;
   int64_t window;
   uint32_t fast_cap;   // k_post_fast: mates with more matches go to k_post
+  uint64_t hash_mask;  // ~0; tests shorten the key hash (SMASH_KEY_HASH_BITS) so
+                       // that the exact key comparison meets real collisions
 };
 
 struct Aln {
@@ -264,8 +275,8 @@ __device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restr
         }
         if (!close) put(h2[b].tid, h2[b].pos);
       }
-      hh = mix64(hh ^ uint64_t(nk)) | 1;
-      hl = mix64(hl + uint64_t(nk)) | 1;
+      hh = (mix64(hh ^ uint64_t(nk)) & c.hash_mask) | 1;
+      hl = (mix64(hl + uint64_t(nk)) & c.hash_mask) | 1;
     }
     nk_out[q] = nk;
     nmajor_out[q] = nmaj;
@@ -478,8 +489,8 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
           }
           if (!close) put(H2[b]);
         }
-        hh = mix64(hh ^ uint64_t(nk)) | 1;
-        hl = mix64(hl + uint64_t(nk)) | 1;
+        hh = (mix64(hh ^ uint64_t(nk)) & c.hash_mask) | 1;
+        hl = (mix64(hl + uint64_t(nk)) & c.hash_mask) | 1;
       }
       nk_out[q] = nk;
       nmajor_out[q] = nmaj;
@@ -498,29 +509,69 @@ __global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n
   val[q] = uint32_t(q);
 }
 
-// 128-bit key set, open addressing, slot = {hi, lo}, 0 = empty.
-// returns true if the key was already present; inserts it otherwise.
-__device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi,
-                                uint64_t lo, bool insert, bool *full) {
+// The persistent pair-key set of smashMEM.py:149,217-228 (dupeSet), exact:
+// a key is the pair's kept hit list (tid << 48 | pos0 per hit, r1 then r2 in
+// HI order, smashMEM.py:122-131).  Open addressing on the 64-bit hash `hi`;
+// slot = {hi, ref}, ref = 1 + arena offset of the key record [lo, nk, words]
+// (0: the inserting thread has not published it yet).  A hash match counts
+// as the same key only when lo, nk and every hit word agree, so a hash
+// collision is a different key (it goes on probing), never a false duplicate.
+struct KeyRef {
+  const uint64_t *w;   // the key's hit words
+  uint32_t nk;
+  uint64_t lo;
+};
+
+__device__ bool same_key(const uint64_t *rec, const KeyRef &k) {
+  if (rec[0] != k.lo || rec[1] != k.nk) return false;
+  for (uint32_t i = 0; i < k.nk; ++i)
+    if (rec[2 + i] != k.w[i]) return false;
+  return true;
+}
+
+__device__ bool same_key(const KeyRef &a, const KeyRef &b) {
+  if (a.lo != b.lo || a.nk != b.nk) return false;
+  for (uint32_t i = 0; i < a.nk; ++i)
+    if (a.w[i] != b.w[i]) return false;
+  return true;
+}
+
+// true if the key was already present; inserts it otherwise (*full: the
+// table or the arena ran out -- an error the caller reports)
+__device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, const KeyRef &k,
+                                uint64_t *arena, uint64_t arena_cap,
+                                unsigned long long *arena_top, bool *full) {
   uint64_t i = (hi ^ (hi >> 31)) & mask;
   for (uint64_t probe = 0; probe <= mask; ++probe) {
     unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
     unsigned long long cur = __hip_atomic_load(sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == 0) {
-      if (!insert) return false;
       const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
       if (prev == 0) {
+        const uint64_t need = 2 + uint64_t(k.nk);
+        const uint64_t off = atomicAdd(arena_top, (unsigned long long)need);
+        if (off + need > arena_cap) {
+          *full = true;
+          return false;
+        }
+        uint64_t *rec = arena + off;
+        rec[0] = k.lo;
+        rec[1] = k.nk;
+        for (uint32_t j = 0; j < k.nk; ++j) rec[2 + j] = k.w[j];
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * i + 1]),
-                           (unsigned long long)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                           (unsigned long long)(off + 1), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
       cur = prev;
     }
     if (cur == hi) {
-      const unsigned long long l = __hip_atomic_load(
-          reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_RELAXED,
+      // ref 0: a key being inserted by this launch, which holds distinct keys
+      // only (the in-batch pass ran first): not ours
+      const unsigned long long ref = __hip_atomic_load(
+          reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_ACQUIRE,
           __HIP_MEMORY_SCOPE_AGENT);
-      if (l == lo) return true;
+      if (ref && same_key(arena + (ref - 1), k)) return true;
     }
     i = (i + 1) & mask;
   }
@@ -529,10 +580,14 @@ __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi,
 }
 
 // mode 0: single GPU (test+insert the persistent set); mode 1: mark
-// in-batch first occurrences only (multi-GPU export)
+// in-batch first occurrences only (multi-GPU export).  key/val: the batch's
+// pairs sorted (stably) by hash hi; a pair is first unless an earlier pair
+// of its hi group has the same key.
 __global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                               uint64_t n, const int32_t *nk, const uint64_t *hash,
-                              uint64_t *table, uint64_t mask, int mode, uint8_t *keep,
+                              const uint64_t *hits, uint32_t slots, uint64_t *table,
+                              uint64_t mask, uint64_t *arena, uint64_t arena_cap,
+                              unsigned long long *arena_top, int mode, uint8_t *keep,
                               uint8_t *first, unsigned long long *stats) {
   const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   unsigned long long kp = 0, dp = 0;
@@ -545,14 +600,15 @@ __global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *
     } else {
       kp = 1;
       bool f = true;
-      const uint64_t lo = hash[2 * q + 1];
+      const KeyRef me{hits + uint64_t(q) * 2 * slots, uint32_t(nk[q]), hash[2 * q + 1]};
       for (uint64_t t = s; t-- > 0 && key[t] == key[s];) {
         const uint32_t q2 = val[t];
-        if (hash[2 * q2 + 1] == lo) { f = false; break; }
+        const KeyRef other{hits + uint64_t(q2) * 2 * slots, uint32_t(nk[q2]), hash[2 * q2 + 1]};
+        if (same_key(me, other)) { f = false; break; }
       }
       first[q] = f ? 1 : 0;
       if (mode == 0) {
-        bool k = f && !set_test_insert(table, mask, key[s], lo, true, &full);
+        bool k = f && !set_test_insert(table, mask, key[s], me, arena, arena_cap, arena_top, &full);
         keep[q] = k ? 1 : 0;
         dp = k ? 0 : 1;
       }
@@ -672,6 +728,7 @@ PostCfg post_cfg(const smash_pipeline *p) {
   c.min_excess = p->min_excess;
   c.window = p->hit_window;
   c.fast_cap = p->post_cap;
+  c.hash_mask = p->hash_mask;
   return c;
 }
 
@@ -748,6 +805,13 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->table_mask = pw - 1;
     p->d_table = dalloc<uint64_t>(2 * pw);
     SMASH_HIPX(hipMemset(p->d_table, 0, 16 * pw));
+    // key records: 2 + nk words each; SMASH reads keep ~7 hits per pair, the
+    // arena holds 16 words per key of the capacity (an exhausted arena is a
+    // reported error, SMASH_ERR_NOMEM, never a silent cut)
+    p->arena_cap = 16 * std::max<uint64_t>(cfg->dedup_capacity, P) + (1u << 20);
+    p->d_arena = dalloc<uint64_t>(p->arena_cap);
+    p->d_arena_top = dalloc<unsigned long long>(1);
+    SMASH_HIPX(hipMemset(p->d_arena_top, 0, 8));
     p->d_pos0 = dalloc<int64_t>(P * 2 * p->slots);
     p->d_abs = dalloc<int64_t>(P * 2 * p->slots);
     p->d_prev = dalloc<int64_t>(2);
@@ -768,7 +832,13 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       const uint32_t cap = pc && *pc ? uint32_t(atoi(pc)) : uint32_t(FCAP);
       p->post_cap = std::min<uint32_t>({cap, uint32_t(FCAP), p->slots});
     }
-    p->d_owner = dalloc<unsigned long long>(2 * 64);
+    if (const char *hb = getenv("SMASH_KEY_HASH_BITS")) {   // tests: force collisions
+      const int b = atoi(hb);
+      if (b > 0 && b < 64) p->hash_mask = (1ull << b) - 1;
+    }
+    p->d_owner = dalloc<unsigned long long>(4 * 64);
+    p->d_send_hdr = dalloc<uint64_t>(5 * P);
+    p->d_recv_base = dalloc<uint64_t>(2 * 65);
     SMASH_HIPX(hipMemset(p->d_posoff, 0, 4));
   } catch (hip_failure &f) {
     set_error(f.what);
@@ -792,7 +862,8 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
                   (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb,
-                  (void *)p->d_post_ws})
+                  (void *)p->d_post_ws, (void *)p->d_arena, (void *)p->d_arena_top,
+                  (void *)p->d_send_hdr, (void *)p->d_send_words, (void *)p->d_recv_base})
     dfree(q);
   delete p;
 }
@@ -858,8 +929,9 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
 static int dedup_local(smash_pipeline *p, hipStream_t s) {
   if (!p->n_pairs) return SMASH_OK;
   k_dedup_first<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, s>>>(
-      p->d_k[0], p->d_v[0], p->n_pairs, p->d_nk, p->d_hash, p->d_table,
-      p->table_mask, 0, p->d_keep, p->d_first, p->d_stats);
+      p->d_k[0], p->d_v[0], p->n_pairs, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
+      p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 0, p->d_keep, p->d_first,
+      p->d_stats);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }
@@ -909,48 +981,80 @@ extern "C" int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
 }
 
 // ---- multi-GPU de-dup exchange ------------------------------------------------
+// Each rank exports its in-batch-first keys to owner = hash hi % world: a
+// 5-word header {hi, lo, global pair index, nk, word offset} per key and the
+// key's nk hit words (hash + canonical key bytes + index).
+// The owner decides first-wins over the exact keys and answers one byte per
+// header.
 namespace smash {
 namespace {
 __global__ void k_export_count(const uint8_t *first, const int32_t *nk,
                                const uint64_t *hash, uint64_t n, int world,
                                unsigned long long *cnt) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (q < n && nk[q] >= 0 && first[q]) atomicAdd(&cnt[hash[2 * q] % uint64_t(world)], 1ull);
+  if (q < n && nk[q] >= 0 && first[q]) {
+    const uint64_t o = hash[2 * q] % uint64_t(world);
+    atomicAdd(&cnt[o], 1ull);
+    atomicAdd(&cnt[128 + o], (unsigned long long)nk[q]);
+  }
 }
 __global__ void k_export_fill(const uint8_t *first, const int32_t *nk,
-                              const uint64_t *hash, uint64_t n, int world,
-                              uint64_t gbase, unsigned long long *cursor,
-                              uint64_t *send, uint32_t *send_q) {
+                              const uint64_t *hash, const uint64_t *hits, uint32_t slots,
+                              uint64_t n, int world, uint64_t gbase, unsigned long long *cnt,
+                              uint64_t *hdr, uint64_t *words, uint32_t *send_q) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= n || nk[q] < 0 || !first[q]) return;
-  const uint64_t o = atomicAdd(&cursor[hash[2 * q] % uint64_t(world)], 1ull);
-  send[3 * o] = hash[2 * q];
-  send[3 * o + 1] = hash[2 * q + 1];
-  send[3 * o + 2] = gbase + q;
+  const uint64_t ow = hash[2 * q] % uint64_t(world);
+  const uint64_t o = atomicAdd(&cnt[64 + ow], 1ull);             // entry slot
+  const uint64_t k = uint64_t(nk[q]);
+  const uint64_t w = atomicAdd(&cnt[192 + ow], (unsigned long long)k);   // word slot
+  hdr[5 * o] = hash[2 * q];
+  hdr[5 * o + 1] = hash[2 * q + 1];
+  hdr[5 * o + 2] = gbase + q;
+  hdr[5 * o + 3] = k;
+  hdr[5 * o + 4] = w - cnt[128 + 64 + ow];   // offset in this owner's word segment
+  const uint64_t *src = hits + q * 2 * uint64_t(slots);
+  for (uint64_t i = 0; i < k; ++i) words[w + i] = src[i];
   send_q[o] = uint32_t(q);
 }
 __global__ void k_owner_keys(const uint64_t *recv, uint64_t n, uint64_t *key, uint32_t *val) {
   const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j < n) { key[j] = recv[3 * j]; val[j] = uint32_t(j); }
+  if (j < n) { key[j] = recv[5 * j]; val[j] = uint32_t(j); }
+}
+// base[0..world]: header prefix per source rank; base[65..65+world]: word
+// prefix per source rank
+__device__ __forceinline__ KeyRef recv_key(const uint64_t *recv, const uint64_t *words,
+                                           const uint64_t *base, int world, uint32_t j) {
+  int r = 0;
+  while (r + 1 < world && j >= base[r + 1]) ++r;
+  return KeyRef{words + base[65 + r] + recv[5 * j + 4], uint32_t(recv[5 * j + 3]),
+                recv[5 * j + 1]};
 }
 __global__ void k_owner_decide(const uint64_t *key, const uint32_t *val, const uint64_t *recv,
-                               uint64_t n, uint64_t *table, uint64_t mask, uint8_t *flags,
-                               unsigned long long *stats) {
+                               const uint64_t *words, const uint64_t *base, int world,
+                               uint64_t n, uint64_t *table, uint64_t mask, uint64_t *arena,
+                               uint64_t arena_cap, unsigned long long *arena_top,
+                               uint8_t *flags, unsigned long long *stats) {
   const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const uint32_t j = val[s];
-  const uint64_t lo = recv[3 * j + 1], g = recv[3 * j + 2];
-  bool win = true;
+  const KeyRef me = recv_key(recv, words, base, world, j);
+  const uint64_t g = recv[5 * j + 2];
+  bool win = true;   // no same key with a smaller global pair index
   for (uint64_t t = s; t-- > 0 && key[t] == key[s];) {
     const uint32_t j2 = val[t];
-    if (recv[3 * j2 + 1] == lo && recv[3 * j2 + 2] < g) { win = false; break; }
+    if (recv[5 * j2 + 2] < g && same_key(me, recv_key(recv, words, base, world, j2))) {
+      win = false;
+      break;
+    }
   }
   for (uint64_t t = s + 1; win && t < n && key[t] == key[s]; ++t) {
     const uint32_t j2 = val[t];
-    if (recv[3 * j2 + 1] == lo && recv[3 * j2 + 2] < g) win = false;
+    if (recv[5 * j2 + 2] < g && same_key(me, recv_key(recv, words, base, world, j2))) win = false;
   }
   bool full = false;
-  const bool keep = win && !set_test_insert(table, mask, key[s], lo, true, &full);
+  const bool keep =
+      win && !set_test_insert(table, mask, key[s], me, arena, arena_cap, arena_top, &full);
   flags[j] = keep ? 1 : 0;
   if (full) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
 }
@@ -971,9 +1075,11 @@ __global__ void k_import_stats(const uint8_t *keep, const int32_t *nk, uint64_t 
 }  // namespace smash
 
 extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
-                                  uint64_t *d_send, int64_t *h_send_counts,
+                                  int64_t *h_send_counts, int64_t *h_send_words,
+                                  const uint64_t **d_send, const uint64_t **d_send_words,
                                   void *stream) {
-  if (!p || world < 1 || world > 64 || !d_send || !h_send_counts) {
+  if (!p || world < 1 || world > 64 || !h_send_counts || !h_send_words || !d_send ||
+      !d_send_words) {
     set_error("smash_phase_export: bad arguments");
     return SMASH_ERR_ARG;
   }
@@ -984,43 +1090,78 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
   if (n) {
     // in-batch first occurrences (mode 1: no persistent-set probe)
     k_dedup_first<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
-        p->d_k[0], p->d_v[0], n, p->d_nk, p->d_hash, p->d_table, p->table_mask, 1,
-        p->d_keep, p->d_first, p->d_stats);
+        p->d_k[0], p->d_v[0], n, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
+        p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 1, p->d_keep, p->d_first,
+        p->d_stats);
   }
-  SMASH_HIP(hipMemsetAsync(p->d_owner, 0, 2 * 64 * 8, s));
+  SMASH_HIP(hipMemsetAsync(p->d_owner, 0, 4 * 64 * 8, s));
   if (n)
     k_export_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_first, p->d_nk, p->d_hash, n,
                                                            world, p->d_owner);
-  unsigned long long cnt[64];
-  SMASH_HIP(hipMemcpyAsync(cnt, p->d_owner, 8 * world, hipMemcpyDeviceToHost, s));
+  unsigned long long cnt[256];
+  SMASH_HIP(hipMemcpyAsync(cnt, p->d_owner, 8 * 256, hipMemcpyDeviceToHost, s));
   SMASH_HIP(hipStreamSynchronize(s));
-  unsigned long long off[64];
-  uint64_t tot = 0;
-  for (int r = 0; r < world; ++r) {
-    off[r] = tot;
+  uint64_t tot = 0, wtot = 0;
+  for (int r = 0; r < world; ++r) {   // cursors: entry and word offsets per owner
+    cnt[64 + r] = tot;
+    cnt[192 + r] = wtot;
     tot += cnt[r];
+    wtot += cnt[128 + r];
     h_send_counts[r] = int64_t(cnt[r]);
+    h_send_words[r] = int64_t(cnt[128 + r]);
   }
   p->n_export = tot;
-  SMASH_HIP(hipMemcpyAsync(p->d_owner + 64, off, 8 * world, hipMemcpyHostToDevice, s));
+  if (wtot > p->send_words_cap) {
+    SMASH_HIP(hipStreamSynchronize(s));
+    if (p->d_send_words) SMASH_HIP(hipFree(p->d_send_words));
+    p->send_words_cap = wtot + wtot / 4 + 1024;
+    SMASH_HIP(hipMalloc(&p->d_send_words, 8 * p->send_words_cap));
+  }
+  // word-segment starts again at [128 + 64 + r] for the relative offsets
+  for (int r = 0; r < world; ++r) cnt[128 + 64 + r] = cnt[192 + r];
+  SMASH_HIP(hipMemcpyAsync(p->d_owner, cnt, 8 * 256, hipMemcpyHostToDevice, s));
   if (n)
-    k_export_fill<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_first, p->d_nk, p->d_hash, n,
-                                                          world, global_base, p->d_owner + 64,
-                                                          d_send, p->d_send_q);
+    k_export_fill<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
+        p->d_first, p->d_nk, p->d_hash, p->d_hits, p->slots, n, world, global_base, p->d_owner,
+        p->d_send_hdr, p->d_send_words, p->d_send_q);
   SMASH_HIP(hipGetLastError());
+  SMASH_HIP(hipStreamSynchronize(s));   // cnt is a host local read by the copy above
+  *d_send = p->d_send_hdr;
+  *d_send_words = p->d_send_words;
   return SMASH_OK;
 }
 
-extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv,
-                                 uint64_t n_recv, uint8_t *d_flags, void *stream) {
-  if (!p || (n_recv && (!d_recv || !d_flags))) return SMASH_ERR_ARG;
+extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint64_t n_recv,
+                                 const uint64_t *d_recv_words, const int64_t *h_recv_counts,
+                                 const int64_t *h_recv_words, int world, uint8_t *d_flags,
+                                 void *stream) {
+  if (!p || world < 1 || world > 64 || !h_recv_counts || !h_recv_words ||
+      (n_recv && (!d_recv || !d_flags))) {
+    set_error("smash_dedup_owner: bad arguments");
+    return SMASH_ERR_ARG;
+  }
   if (n_recv > 2 * p->max_pairs) {
     set_error("smash_dedup_owner: more keys than 2 * cfg.max_pairs");
     return SMASH_ERR_ARG;
   }
+  uint64_t base[2 * 65] = {0};
+  uint64_t hs = 0, ws = 0;
+  for (int r = 0; r < world; ++r) {
+    base[r] = hs;
+    base[65 + r] = ws;
+    hs += uint64_t(h_recv_counts[r]);
+    ws += uint64_t(h_recv_words[r]);
+  }
+  if (hs != n_recv || (ws && !d_recv_words)) {
+    set_error("smash_dedup_owner: per-source counts do not add up to n_recv");
+    return SMASH_ERR_ARG;
+  }
+  base[world] = hs;
+  base[65 + world] = ws;
   hipStream_t s = static_cast<hipStream_t>(stream);
   p->last = s;
   if (!n_recv) return SMASH_OK;
+  SMASH_HIP(hipMemcpyAsync(p->d_recv_base, base, sizeof(base), hipMemcpyHostToDevice, s));
   // reuse the sort buffers (phase_map's sorted keys are no longer needed)
   k_owner_keys<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(d_recv, n_recv, p->d_k[0], p->d_v[0]);
   hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
@@ -1028,9 +1169,10 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv,
   size_t tb = p->temp_bytes;
   SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_recv, 0, 64, s));
   k_owner_decide<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(
-      kb.Current(), vb.Current(), d_recv, n_recv, p->d_table, p->table_mask, d_flags,
-      p->d_stats);
+      kb.Current(), vb.Current(), d_recv, d_recv_words, p->d_recv_base, world, n_recv,
+      p->d_table, p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, d_flags, p->d_stats);
   SMASH_HIP(hipGetLastError());
+  SMASH_HIP(hipStreamSynchronize(s));   // `base` is a host local read by the copy above
   return SMASH_OK;
 }
 
@@ -1087,6 +1229,7 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   SMASH_HIP(hipSetDevice(p->device));
   SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * (p->table_mask + 1), s));
+  SMASH_HIP(hipMemsetAsync(p->d_arena_top, 0, 8, s));
   SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * S_N, s));
   k_reset_prev<<<1, 1, 0, s>>>(p->d_prev);   // no host source: stays asynchronous
   SMASH_HIP(hipGetLastError());

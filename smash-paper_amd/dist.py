@@ -6,9 +6,11 @@ SURVEY.md Appendix A.11) is (step, rank, pair).  Everything is per-rank except
 the two dependencies the reference's sequential scripts carry:
 
 * smashMEM.py's global first-wins pair de-dup (smashMEM.py:149,217-228): the
-  in-batch-first keys are sent to owner rank = hash % world (all_to_all), the
-  owner decides first-wins by global pair index against its persistent key set
-  and returns one flag per key (all_to_all back);
+  in-batch-first keys -- a header {hash, global pair index, length} plus the
+  key's canonical hit words -- are sent to owner rank = hash % world
+  (all_to_all of the counts, the headers and the words), the owner decides
+  first-wins by global pair index over the exact keys against its persistent
+  key set and returns one flag per key (all_to_all back);
 * varbin.py's adjacent de-dup (varbin.py:56-58) compares with the previous
   emitted position: all_gather of every rank's {count, last pos0} gives each
   rank the last position emitted before its shard.
@@ -44,19 +46,23 @@ class ShardedCounter:
         dev, W, r = self.device, self.world, self.rank
         p = self.pipe
         p.phase_map(d_reads, n_pairs)
-        send = torch.empty((max(n_pairs, 1), 3), dtype=torch.int64, device=dev)
-        cnt = p.phase_export(W, step_base + r * n_pairs, send)
-        sc = torch.as_tensor(cnt, dtype=torch.int64).to(dev)
+        hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * n_pairs)
+        sc = torch.as_tensor([[int(a), int(b)] for a, b in zip(cnt, wcnt)],
+                             dtype=torch.int64).to(dev)
         rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        rcv = rc.cpu().tolist()
-        snd = [int(x) for x in cnt]
-        n_recv = sum(rcv)
-        recv = torch.empty((max(n_recv, 1), 3), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(recv[:n_recv], send[:sum(snd)], output_split_sizes=rcv,
+        dist.all_to_all_single(rc, sc, group=self.group)   # row s: what rank s sends me
+        rcl = rc.cpu().tolist()
+        rcv, rcw = [x[0] for x in rcl], [x[1] for x in rcl]
+        snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
+        n_recv, n_words = sum(rcv), sum(rcw)
+        recv = torch.empty((max(n_recv, 1), 5), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv[:n_recv], hdr[:sum(snd)], output_split_sizes=rcv,
                                input_split_sizes=snd, group=self.group)
+        recv_words = torch.empty(max(n_words, 1), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(recv_words[:n_words], words[:sum(sndw)], output_split_sizes=rcw,
+                               input_split_sizes=sndw, group=self.group)
         flags = torch.empty(max(n_recv, 1), dtype=torch.uint8, device=dev)
-        p.dedup_owner(recv, n_recv, flags)
+        p.dedup_owner(recv, n_recv, recv_words, rcv, rcw, flags)
         back = torch.empty(max(sum(snd), 1), dtype=torch.uint8, device=dev)
         dist.all_to_all_single(back[:sum(snd)], flags[:n_recv], output_split_sizes=snd,
                                input_split_sizes=rcv, group=self.group)

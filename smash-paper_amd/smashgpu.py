@@ -119,8 +119,9 @@ def lib():
     L.smash_pipeline_free.restype = None
     L.smash_count_batch.argtypes = [vp, vp, C.c_uint64, vp, vp]
     L.smash_phase_map.argtypes = [vp, vp, C.c_uint64, vp]
-    L.smash_phase_export.argtypes = [vp, C.c_int, C.c_uint64, vp, i64p, vp]
-    L.smash_dedup_owner.argtypes = [vp, vp, C.c_uint64, vp, vp]
+    L.smash_phase_export.argtypes = [vp, C.c_int, C.c_uint64, i64p, i64p, C.POINTER(vp),
+                                     C.POINTER(vp), vp]
+    L.smash_dedup_owner.argtypes = [vp, vp, C.c_uint64, vp, i64p, i64p, C.c_int, vp, vp]
     L.smash_phase_import.argtypes = [vp, vp, vp]
     L.smash_phase_positions.argtypes = [vp, vp, vp]
     L.smash_phase_bin.argtypes = [vp, vp, vp, vp]
@@ -368,15 +369,30 @@ class Pipeline:
         check(lib().smash_phase_map(self.h, _ptr(d_reads), n_pairs, vp(_stream(stream))),
               "smash_phase_map")
 
-    def phase_export(self, world, global_base, d_send, stream=None):
+    def phase_export(self, world, global_base, stream=None):
+        """(headers [n, 5] int64, words [w] int64, per-owner key counts,
+        per-owner word counts) -- the tensors alias pipeline-owned device
+        memory, valid until the next export."""
+        import torch
         counts = np.zeros(world, np.int64)
-        check(lib().smash_phase_export(self.h, world, global_base, _ptr(d_send),
-                                       _p(counts, i64p), vp(_stream(stream))),
-              "smash_phase_export")
-        return counts
+        wcounts = np.zeros(world, np.int64)
+        ds, dw = vp(), vp()
+        check(lib().smash_phase_export(self.h, world, global_base, _p(counts, i64p),
+                                       _p(wcounts, i64p), C.byref(ds), C.byref(dw),
+                                       vp(_stream(stream))), "smash_phase_export")
+        n, w = int(counts.sum()), int(wcounts.sum())
+        hdr = device_view(ds.value, 40 * n, torch.int64).view(n, 5) if n else \
+            torch.zeros((0, 5), dtype=torch.int64, device="cuda")
+        words = device_view(dw.value, 8 * w, torch.int64) if w else \
+            torch.zeros(0, dtype=torch.int64, device="cuda")
+        return hdr, words, counts, wcounts
 
-    def dedup_owner(self, d_recv, n_recv, d_flags, stream=None):
-        check(lib().smash_dedup_owner(self.h, _ptr(d_recv), n_recv, _ptr(d_flags),
+    def dedup_owner(self, d_recv, n_recv, d_recv_words, recv_counts, recv_words, d_flags,
+                    stream=None):
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        rw = np.ascontiguousarray(recv_words, np.int64)
+        check(lib().smash_dedup_owner(self.h, _ptr(d_recv), n_recv, _ptr(d_recv_words),
+                                      _p(rc, i64p), _p(rw, i64p), len(rc), _ptr(d_flags),
                                       vp(_stream(stream))), "smash_dedup_owner")
 
     def phase_import(self, d_flags_back, stream=None):

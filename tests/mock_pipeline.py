@@ -60,29 +60,45 @@ class OraclePhasePipeline:
             self.hashes.append(key_hash(tuple(k)) if k is not None else None)
         self.n = n_pairs
 
-    def phase_export(self, world, gbase, d_send):
+    def phase_export(self, world, gbase):
+        """smash_phase_export's layout: per owner, 5-word headers {hi, lo,
+        global index, nk, word offset in the owner segment} and the keys'
+        hit words (tid << 48 | pos0)."""
         first = {}
-        for q, h in enumerate(self.hashes):
-            if h is not None and h not in first:
-                first[h] = q
+        for q, k in enumerate(self.kept_hits):
+            if k is not None and tuple(k) not in first:
+                first[tuple(k)] = q
         groups = [[] for _ in range(world)]
-        for h, q in first.items():
-            groups[h[0] % world].append((h, q))
+        for k, q in first.items():
+            groups[self.hashes[q][0] % world].append((k, q))
         self.order = []
-        rows = []
+        rows, words, counts, wcounts = [], [], [], []
         for w in range(world):
-            for h, q in sorted(groups[w], key=lambda t: t[1]):
-                rows.append((to_i64(h[0]), to_i64(h[1]), gbase + q))
+            seg = []
+            for k, q in sorted(groups[w], key=lambda t: t[1]):
+                h = self.hashes[q]
+                rows.append((to_i64(h[0]), to_i64(h[1]), gbase + q, len(k), len(seg)))
+                seg += [to_i64((tid << 48) | pos) for tid, pos in k]
                 self.order.append(q)
-        if rows:
-            d_send[:len(rows)] = torch.tensor(rows, dtype=torch.int64)
-        return np.array([len(g) for g in groups], np.int64)
+            words += seg
+            counts.append(len(groups[w]))
+            wcounts.append(len(seg))
+        hdr = torch.tensor(rows, dtype=torch.int64).reshape(-1, 5)
+        return (hdr, torch.tensor(words, dtype=torch.int64), np.array(counts, np.int64),
+                np.array(wcounts, np.int64))
 
-    def dedup_owner(self, d_recv, n_recv, d_flags):
+    def dedup_owner(self, d_recv, n_recv, d_recv_words, recv_counts, recv_words, d_flags):
         rows = d_recv[:n_recv].tolist()
+        words = d_recv_words.tolist()
+        hb = np.cumsum([0] + list(recv_counts))
+        wb = np.cumsum([0] + list(recv_words))
         best = {}
-        for j, (hi, lo, g) in enumerate(rows):
-            k = (to_u64(hi), to_u64(lo))
+        keys = []
+        for j, (hi, lo, g, nk, off) in enumerate(rows):
+            src = int(np.searchsorted(hb, j, side="right")) - 1
+            a = int(wb[src]) + off
+            k = tuple((to_u64(w) >> 48, to_u64(w) & 0xFFFFFFFFFFFF) for w in words[a:a + nk])
+            keys.append(k)
             if k not in best or g < rows[best[k]][2]:
                 best[k] = j
         flags = np.zeros(n_recv, np.uint8)

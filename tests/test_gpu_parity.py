@@ -289,3 +289,23 @@ def test_post_paths_agree(gix, s, env, monkeypatch):
     assert a[0] == b[0] and a[1] == b[1]
     assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
     assert a[4] == b[4]
+
+
+@pytest.mark.parametrize("bits", [2, 9])
+def test_key_set_exact_under_hash_collisions(gix, tiny_ix, bits, monkeypatch):
+    """The pair-key set compares the canonical hit words, not the hash: with
+    the key hash cut to `bits` bits (most keys collide) the counts, stats and
+    keep flags still equal the oracle's, whose set holds the full keys."""
+    reads = interleaved_reads("s100")
+    n = reads.shape[0] // 2
+    monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
+    pipe, starts = make_pipe(gix, reads.shape[1], 700)
+    monkeypatch.delenv("SMASH_KEY_HASH_BITS")
+    counts, st = run_pipeline(pipe, reads, len(starts), batch=700)
+    assert st.error == 0
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    op = O.Pipeline(tiny_ix, tiny_ix.mappability(), cs, starts)
+    assert op.run(reads, threads=4) == 0
+    assert counts.tolist() == op.counts.tolist()
+    assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
+    assert st.dupe_pairs == op.n_dupe.value

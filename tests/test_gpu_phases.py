@@ -33,30 +33,37 @@ def run_emulated(ix, reads, W, per_rank, steps, starts, cs):
     carried = torch.full((1,), -1, dtype=torch.int64, device=dev)
     for s in range(steps):
         base = s * W * per_rank
-        sends, cnts = [], []
+        sends = []
         for r in range(W):
             lo = base + r * per_rank
             d = torch.from_numpy(np.ascontiguousarray(reads[2 * lo:2 * (lo + per_rank)])).to(dev)
             pipes[r].phase_map(d, per_rank)
-            send = torch.empty((per_rank, 3), dtype=torch.int64, device=dev)
-            cnt = pipes[r].phase_export(W, base + r * per_rank, send)
-            sends.append(send)
-            cnts.append([int(c) for c in cnt])
-        offs = [np.cumsum([0] + c) for c in cnts]
+            hdr, words, cnt, wcnt = pipes[r].phase_export(W, base + r * per_rank)
+            # copies: the export buffers are the pipeline's own
+            sends.append((hdr.clone(), words.clone(), [int(c) for c in cnt],
+                          [int(c) for c in wcnt]))
         # all_to_all: owner o receives segment o of every rank, rank order
         flags_back = [[None] * W for _ in range(W)]
         for o in range(W):
-            parts = [sends[r][offs[r][o]:offs[r][o + 1]] for r in range(W)]
-            recv = torch.cat(parts) if parts else torch.empty((0, 3), dtype=torch.int64, device=dev)
-            n = recv.shape[0]
+            hparts, wparts, rc, rw = [], [], [], []
+            for r in range(W):
+                hdr, words, cnt, wcnt = sends[r]
+                h0, w0 = sum(cnt[:o]), sum(wcnt[:o])
+                hparts.append(hdr[h0:h0 + cnt[o]])
+                wparts.append(words[w0:w0 + wcnt[o]])
+                rc.append(cnt[o])
+                rw.append(wcnt[o])
+            recv = torch.cat(hparts) if sum(rc) else torch.zeros((1, 5), dtype=torch.int64, device=dev)
+            rwords = torch.cat(wparts) if sum(rw) else torch.zeros(1, dtype=torch.int64, device=dev)
+            n = sum(rc)
             flags = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-            pipes[o].dedup_owner(recv if n else torch.empty((1, 3), dtype=torch.int64, device=dev),
-                                 n, flags)
+            pipes[o].dedup_owner(recv, n, rwords, rc, rw, flags)
             k = 0
             for r in range(W):
-                m = cnts[r][o]
+                m = rc[r]
                 flags_back[r][o] = flags[k:k + m]
                 k += m
+        cnts = [x[2] for x in sends]
         tails = []
         for r in range(W):
             back = torch.cat(flags_back[r]) if sum(cnts[r]) else torch.zeros(1, dtype=torch.uint8, device=dev)
@@ -74,8 +81,13 @@ def run_emulated(ix, reads, W, per_rank, steps, starts, cs):
                    sum(x.kept for x in st), sum(x.dupe_pairs for x in st))
 
 
-@pytest.mark.parametrize("W,per_rank,steps", [(2, 500, 2), (3, 111, 3), (4, 250, 1)])
-def test_phases_equal_single_pipeline(gix, W, per_rank, steps):
+@pytest.mark.parametrize("W,per_rank,steps,bits", [(2, 500, 2, 0), (3, 111, 3, 0),
+                                                   (4, 250, 1, 0), (3, 200, 2, 3)])
+def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, monkeypatch):
+    """bits > 0: the key hash cut to `bits` bits, so owners see colliding
+    keys and must compare the exchanged key words."""
+    if bits:
+        monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
     reads = interleaved_reads("s100")
     n = W * per_rank * steps
     _, starts = load_bins(gold("tiny_bins.txt"))
