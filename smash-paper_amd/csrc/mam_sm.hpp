@@ -40,6 +40,18 @@
 #ifndef SM_LOAD16
 #define SM_LOAD16(a) ::smash::sm::load16u(a)
 #endif
+// speculative loads of a binary search's next SA elements (both children of
+// the probe being compared; one of them is used): the emulation does not
+// count them as probes, SM_HOOK_PF counts the one that is used
+#ifndef SM_LOADPF16
+#define SM_LOADPF16(a) ::smash::sm::load16u(a)
+#endif
+#ifndef SM_LOADIDX
+#define SM_LOADIDX(p, i) uint64_t((p)[i])
+#endif
+#ifndef SM_HOOK_PF
+#define SM_HOOK_PF(a)
+#endif
 
 namespace smash {
 namespace sm {
@@ -371,6 +383,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint32_t fm = 0;        // (F) probe mode (bm_dual 2)
   FlagRef ktr_set{fl, 7};   // a passed window's k-mer code is in m
   FlagRef clean{fl, 8};     // the read has no bad base (bad mask all zero)
+  // binary-search prefetch: the S_CMP O_BS probe in flight also loads the SA
+  // elements of its two children, SA[(lo+m)/2] (v2, when need2) and
+  // SA[(m+1+hi)/2] (v3, when pfr), so the next probe's text compare issues
+  // one iteration later instead of two
+  FlagRef pf{fl, 9}, pfr{fl, 10};
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
@@ -387,6 +404,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // blocks in one iteration (S_EXB), or the one side with room; false: none
   // left blocks are the 16 bytes ENDING at es (from 0 when es < 15), right
   // blocks start at ee + 1
+  auto bs_probe = [&]() {   // compare P' with T[sp + cbase + lc ...] (sp = SA[m])
+    addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
+    addr2 = ia(c.SA, (lo + m) >> 1);
+    need2 = lo < m;
+    pfr = m + 1 < hi;
+    pf = true;
+    st = S_CMP; op = O_BS;
+  };
   auto lblock = [&](uint64_t e) { return reinterpret_cast<uint64_t>(c.L8 + (e >= 15 ? e - 15 : 0)); };
   auto ex_start = [&](uint64_t lb, uint64_t hb) {
     const bool l = es > lb, r = ee < hb;
@@ -425,12 +450,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         c.viol[5] = prefix; c.viol[6] = depth; c.viol[7] = start; c.viol[8] = end; c.viol[9] = rd;
       }
       st = S_EXIT;
-      need2 = false;
+      need2 = false; pfr = false;
     }
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
+    uint64_t v3 = 0;
     const uint64_t amask = st >= S_BYTE ? ~uint64_t(0) : ~uint64_t(15);
     if (st >= S_COPY) v = SM_LOAD16(addr & amask);
-    if (need2) v2 = SM_LOAD16(addr2 & amask);
+    if (need2) {
+      if (pf) v2 = SM_LOADPF16(addr2 & ~uint64_t(15));
+      else v2 = SM_LOAD16(addr2 & amask);
+    }
+    if (pfr) v3 = SM_LOADIDX(c.SA, (m + 1 + hi) >> 1);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
     if (newm) {
       if (take) base = __shfl(base, int(__builtin_ctzll(newm)), 64);
@@ -445,6 +475,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           addr = reinterpret_cast<uint64_t>(c.rec + rd * c.chunks);
           addr2 = addr + 16;
           need2 = c.chunks > 1;
+          pf = false; pfr = false;
           kc = 0;
           st = S_COPY;
         }
@@ -572,10 +603,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
           sp = iv;
           // 16 bytes first: a binary-search probe usually decides early
-          addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
-          addr2 = addr + 16;
-          need2 = false;
-          st = S_CMP; op = O_BS;
+          bs_probe();
         } else if (op == O_ISAJ) {
           start = end = iv; have_pos = false;
           a = A_EXPAND;
@@ -599,16 +627,20 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
-        // text bytes [addr, addr + 16) in v, then (need2) the next 16 in v2
+        // text bytes [addr, addr + 16) in v, then (tn2) the next 16 in v2
+        // (pf: v2 / v3 hold the children's SA elements instead)
+        const bool tn2 = need2 && !pf;
         const uint32_t off = prefix + (op == O_BS ? cbase : depth) + lc;
         const uint32_t rem = op == O_BS ? cap - lc : L - off;
         const uint32_t lim = rem < 16 ? rem : 16u;
         uint32_t k = agree_block(v, 0, P, off, lim);
-        if (need2 && k == lim && k < rem) {
+        if (tn2 && k == lim && k < rem) {
           const uint32_t lim2 = rem - k < 16 ? rem - k : 16u;
           k += agree_block(v2, 0, P, off + k, lim2);
         }
-        const uint32_t got = need2 ? (rem < 32 ? rem : 32u) : lim;   // bytes available
+        const uint32_t got = tn2 ? (rem < 32 ? rem : 32u) : lim;   // bytes available
+        const bool had_pf = pf;
+        pf = false; pfr = false;
         lc += k;
         if (k == got && k < rem) {                    // agreed on all loaded bytes: go on
           addr += k;
@@ -632,7 +664,15 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           }
           if (left) { hi = m; lR = lc; }
           else { lo = m + 1; lL = lc; }
-          a = A_BS;
+          if (had_pf && lo < hi) {                    // the next probe's SA element is here
+            m = (lo + hi) >> 1;
+            SM_HOOK_PF(ia(c.SA, m));
+            sp = left ? idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15) : v3;
+            lc = lL < lR ? lL : lR;
+            bs_probe();
+          } else {
+            a = A_BS;
+          }
         }
         break;
       }

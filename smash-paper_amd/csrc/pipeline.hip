@@ -57,6 +57,7 @@ struct smash_pipeline {
   uint64_t *d_arena = nullptr;   // canonical keys: [lo, nk, hit words...] per key
   uint64_t arena_cap = 0;        // words
   unsigned long long *d_arena_top = nullptr;
+  uint64_t epoch = 0;             // launches of the set's insert kernels (ref tags)
   uint32_t *d_posoff = nullptr;   // [max_pairs + 1]
   uint32_t *d_cnt = nullptr;      // [max_pairs]
   int64_t *d_pos0 = nullptr, *d_abs = nullptr;
@@ -69,7 +70,8 @@ struct smash_pipeline {
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
   unsigned long long *d_owner = nullptr;  // per owner: [0,64) entries [64,128) entry cursors
-                                          // [128,192) words [192,256) word cursors
+                                          // [128,192) words (for the fill: word-segment
+                                          // starts) [192,256) word cursors
   uint64_t *d_send_hdr = nullptr; // [n_export][5] {hi, lo, global index, nk, word offset}
   uint64_t *d_send_words = nullptr;   // the exported keys' hit words, grouped by owner
   uint64_t send_words_cap = 0;
@@ -512,10 +514,20 @@ __global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n
 // The persistent pair-key set of smashMEM.py:149,217-228 (dupeSet), exact:
 // a key is the pair's kept hit list (tid << 48 | pos0 per hit, r1 then r2 in
 // HI order, smashMEM.py:122-131).  Open addressing on the 64-bit hash `hi`;
-// slot = {hi, ref}, ref = 1 + arena offset of the key record [lo, nk, words]
-// (0: the inserting thread has not published it yet).  A hash match counts
-// as the same key only when lo, nk and every hit word agree, so a hash
-// collision is a different key (it goes on probing), never a false duplicate.
+// slot = {hi, ref}, ref = epoch << 40 | (1 + arena offset of the key record
+// [lo, nk, words]) (0: the inserting thread has not published it yet).  A
+// hash match counts as the same key only when lo, nk and every hit word
+// agree, so a hash collision is a different key (it goes on probing), never a
+// false duplicate.
+//
+// The threads of one insert launch hold distinct keys (the in-batch pass ran
+// first), so a slot published by this launch (ref 0 or tagged with this
+// launch's epoch) is never the probing thread's key, and its record need not
+// be read; records of earlier launches are visible across the kernel
+// boundary.  Hence relaxed slot accesses, no per-key release / acquire
+// (agent-scope fences write back / invalidate the XCD's L2 on gfx950 and
+// made this kernel 5 ms per 2 M pairs).  Epochs wrap after 2^24 launches.
+constexpr int kRefShift = 40;
 struct KeyRef {
   const uint64_t *w;   // the key's hit words
   uint32_t nk;
@@ -536,11 +548,32 @@ __device__ bool same_key(const KeyRef &a, const KeyRef &b) {
   return true;
 }
 
-// true if the key was already present; inserts it otherwise (*full: the
-// table or the arena ran out -- an error the caller reports)
+// arena space for the wave's keys with ONE atomic per wave (an atomic per
+// key serialises ~2 M same-address atomics per batch on one L2 channel):
+// every lane of the wave calls it, need = 0 for lanes without a key; the
+// lane gets the offset of its `need` words.  A key that turns out present
+// leaves its reserved words unused.
+__device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t x = need;   // inclusive prefix over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= uint32_t(d)) x += y;
+  }
+  const uint32_t total = __shfl(x, 63, 64);
+  unsigned long long base = 0;
+  if (lane == 63 && total) base = atomicAdd(top, (unsigned long long)total);
+  base = __shfl(base, 63, 64);
+  return uint64_t(base) + x - need;
+}
+
+// true if the key was already present; inserts it otherwise, its record at
+// arena[off] (wave_alloc) (*full: the table or the arena ran out -- an error
+// the caller reports)
 __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, const KeyRef &k,
-                                uint64_t *arena, uint64_t arena_cap,
-                                unsigned long long *arena_top, bool *full) {
+                                uint64_t *arena, uint64_t arena_cap, uint64_t off,
+                                uint64_t epoch, bool *full) {
   uint64_t i = (hi ^ (hi >> 31)) & mask;
   for (uint64_t probe = 0; probe <= mask; ++probe) {
     unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
@@ -549,7 +582,6 @@ __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, con
       const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
       if (prev == 0) {
         const uint64_t need = 2 + uint64_t(k.nk);
-        const uint64_t off = atomicAdd(arena_top, (unsigned long long)need);
         if (off + need > arena_cap) {
           *full = true;
           return false;
@@ -559,19 +591,20 @@ __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, con
         rec[1] = k.nk;
         for (uint32_t j = 0; j < k.nk; ++j) rec[2 + j] = k.w[j];
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * i + 1]),
-                           (unsigned long long)(off + 1), __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_AGENT);
+                           (unsigned long long)((epoch << kRefShift) | (off + 1)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
       cur = prev;
     }
     if (cur == hi) {
-      // ref 0: a key being inserted by this launch, which holds distinct keys
-      // only (the in-batch pass ran first): not ours
+      // ref 0 or this epoch: a key of this launch, not ours
       const unsigned long long ref = __hip_atomic_load(
-          reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_ACQUIRE,
+          reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_RELAXED,
           __HIP_MEMORY_SCOPE_AGENT);
-      if (ref && same_key(arena + (ref - 1), k)) return true;
+      if (ref && (ref >> kRefShift) != epoch &&
+          same_key(arena + ((ref & ((1ull << kRefShift) - 1)) - 1), k))
+        return true;
     }
     i = (i + 1) & mask;
   }
@@ -587,11 +620,13 @@ __global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *
                               uint64_t n, const int32_t *nk, const uint64_t *hash,
                               const uint64_t *hits, uint32_t slots, uint64_t *table,
                               uint64_t mask, uint64_t *arena, uint64_t arena_cap,
-                              unsigned long long *arena_top, int mode, uint8_t *keep,
-                              uint8_t *first, unsigned long long *stats) {
+                              unsigned long long *arena_top, uint64_t epoch, int mode,
+                              uint8_t *keep, uint8_t *first, unsigned long long *stats) {
   const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   unsigned long long kp = 0, dp = 0;
   bool full = false;
+  const bool act = mode == 0 && s < n && nk[val[s]] >= 0;
+  const uint64_t off = wave_alloc(arena_top, act ? 2u + uint32_t(nk[val[s]]) : 0u);
   if (s < n) {
     const uint32_t q = val[s];
     if (nk[q] < 0) {
@@ -608,7 +643,7 @@ __global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *
       }
       first[q] = f ? 1 : 0;
       if (mode == 0) {
-        bool k = f && !set_test_insert(table, mask, key[s], me, arena, arena_cap, arena_top, &full);
+        bool k = f && !set_test_insert(table, mask, key[s], me, arena, arena_cap, off, epoch, &full);
         keep[q] = k ? 1 : 0;
         dp = k ? 0 : 1;
       }
@@ -926,11 +961,18 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
   return SMASH_OK;
 }
 
+// 1 .. 2^24 - 1, never 0 (an unpublished slot)
+static uint64_t next_epoch(smash_pipeline *p) {
+  p->epoch = p->epoch % ((1ull << (64 - smash::kRefShift)) - 1) + 1;
+  return p->epoch;
+}
+
 static int dedup_local(smash_pipeline *p, hipStream_t s) {
   if (!p->n_pairs) return SMASH_OK;
   k_dedup_first<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, s>>>(
       p->d_k[0], p->d_v[0], p->n_pairs, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
-      p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 0, p->d_keep, p->d_first,
+      p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, next_epoch(p), 0, p->d_keep,
+      p->d_first,
       p->d_stats);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
@@ -1012,7 +1054,7 @@ __global__ void k_export_fill(const uint8_t *first, const int32_t *nk,
   hdr[5 * o + 1] = hash[2 * q + 1];
   hdr[5 * o + 2] = gbase + q;
   hdr[5 * o + 3] = k;
-  hdr[5 * o + 4] = w - cnt[128 + 64 + ow];   // offset in this owner's word segment
+  hdr[5 * o + 4] = w - cnt[128 + ow];   // offset in this owner's word segment
   const uint64_t *src = hits + q * 2 * uint64_t(slots);
   for (uint64_t i = 0; i < k; ++i) words[w + i] = src[i];
   send_q[o] = uint32_t(q);
@@ -1034,8 +1076,10 @@ __global__ void k_owner_decide(const uint64_t *key, const uint32_t *val, const u
                                const uint64_t *words, const uint64_t *base, int world,
                                uint64_t n, uint64_t *table, uint64_t mask, uint64_t *arena,
                                uint64_t arena_cap, unsigned long long *arena_top,
-                               uint8_t *flags, unsigned long long *stats) {
+                               uint64_t epoch, uint8_t *flags, unsigned long long *stats) {
   const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t off =
+      wave_alloc(arena_top, s < n ? 2u + uint32_t(recv[5 * val[s] + 3]) : 0u);
   if (s >= n) return;
   const uint32_t j = val[s];
   const KeyRef me = recv_key(recv, words, base, world, j);
@@ -1054,7 +1098,7 @@ __global__ void k_owner_decide(const uint64_t *key, const uint32_t *val, const u
   }
   bool full = false;
   const bool keep =
-      win && !set_test_insert(table, mask, key[s], me, arena, arena_cap, arena_top, &full);
+      win && !set_test_insert(table, mask, key[s], me, arena, arena_cap, off, epoch, &full);
   flags[j] = keep ? 1 : 0;
   if (full) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
 }
@@ -1091,7 +1135,7 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
     // in-batch first occurrences (mode 1: no persistent-set probe)
     k_dedup_first<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
         p->d_k[0], p->d_v[0], n, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
-        p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 1, p->d_keep, p->d_first,
+        p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 0, 1, p->d_keep, p->d_first,
         p->d_stats);
   }
   SMASH_HIP(hipMemsetAsync(p->d_owner, 0, 4 * 64 * 8, s));
@@ -1117,8 +1161,9 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
     p->send_words_cap = wtot + wtot / 4 + 1024;
     SMASH_HIP(hipMalloc(&p->d_send_words, 8 * p->send_words_cap));
   }
-  // word-segment starts again at [128 + 64 + r] for the relative offsets
-  for (int r = 0; r < world; ++r) cnt[128 + 64 + r] = cnt[192 + r];
+  // [128 + r] (the word counts, read above) now holds owner r's word-segment
+  // start, for the offsets relative to it (the cursors at [192 + r] move)
+  for (int r = 0; r < world; ++r) cnt[128 + r] = cnt[192 + r];
   SMASH_HIP(hipMemcpyAsync(p->d_owner, cnt, 8 * 256, hipMemcpyHostToDevice, s));
   if (n)
     k_export_fill<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
@@ -1170,7 +1215,8 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_recv, 0, 64, s));
   k_owner_decide<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(
       kb.Current(), vb.Current(), d_recv, d_recv_words, p->d_recv_base, world, n_recv,
-      p->d_table, p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, d_flags, p->d_stats);
+      p->d_table, p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, next_epoch(p), d_flags,
+      p->d_stats);
   SMASH_HIP(hipGetLastError());
   SMASH_HIP(hipStreamSynchronize(s));   // `base` is a host local read by the copy above
   return SMASH_OK;

@@ -5,7 +5,7 @@
 # body every iteration, so the static counts track per-iteration cost.
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
-K=${1:-'k_mam_smImLi128ELb1ELb0EE'}
+K=${1:-'k_mam_smImLi64ELb1ELb0EE'}
 T=$(mktemp -d)
 cd "$T"
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -I"$R/include" -c \

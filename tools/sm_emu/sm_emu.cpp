@@ -19,16 +19,23 @@ static unsigned long long emu_ws[64];   // the kernel's STATS counters of the la
 // the 16 bytes at address a, exactly (the kernel aligns the blocks it wants
 // aligned); a block crossing a 64-byte line is two requests and touches two
 // lines
-static uint4 emu_load16(uint64_t a) {
+static int emu_array(uint64_t a) {
   int arr = -1;
   if (a >= emu_rec_lo && a < emu_rec_hi) arr = 7;
   for (int k = 0; k < 7 && arr < 0; ++k)
     if (a >= emu_spans[2 * k] && a < emu_spans[2 * k + 1]) arr = k;
-  if (arr < 0) { ++emu_bad; return uint4{0, 0, 0, 0}; }
-  for (uint64_t line = a >> 6; line <= (a + 15) >> 6; ++line) {
+  return arr;
+}
+static void emu_count(int arr, uint64_t a, uint64_t n) {
+  for (uint64_t line = a >> 6; line <= (a + n - 1) >> 6; ++line) {
     ++emu_probes[arr];
     if (line != emu_last[arr]) { ++emu_lines[arr]; emu_last[arr] = line; }
   }
+}
+static uint4 emu_load16(uint64_t a, bool count = true) {
+  const int arr = emu_array(a);
+  if (arr < 0) { ++emu_bad; return uint4{0, 0, 0, 0}; }
+  if (count) emu_count(arr, a, 16);
   // the block may run past the array: copy the valid bytes
   const uint64_t hi = arr == 7 ? emu_rec_hi : emu_spans[2 * arr + 1];
   if (a + 16 <= hi) {
@@ -44,6 +51,20 @@ static uint4 emu_load16(uint64_t a) {
   return r;
 }
 #define SM_LOAD16(a) emu_load16(a)
+// speculative SA prefetches: checked, not counted; the element the search
+// goes on with is counted (one 8- or 4-byte probe) by SM_HOOK_PF
+#define SM_LOADPF16(a) emu_load16(a, false)
+template <class IdxT>
+static uint64_t emu_loadidx(const IdxT *p, uint64_t i) {
+  if (emu_array(reinterpret_cast<uint64_t>(p + i)) < 0) { ++emu_bad; return 0; }
+  return uint64_t(p[i]);
+}
+#define SM_LOADIDX(p, i) emu_loadidx(p, i)
+static void emu_hook_pf(uint64_t a, uint64_t n) {
+  const int arr = emu_array(a);
+  if (arr < 0) ++emu_bad; else emu_count(arr, a, n);
+}
+#define SM_HOOK_PF(a) emu_hook_pf(a, sizeof(IdxT))
 #define PAD_KEEP(x) ((void)(x))
 // traverse binary searches by interval size (1..63, 64 = larger) and start depth
 static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
