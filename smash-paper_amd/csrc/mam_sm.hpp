@@ -52,6 +52,11 @@
 #ifndef SM_HOOK_PF
 #define SM_HOOK_PF(a)
 #endif
+// n 16-byte record chunks from src into the LDS row dst, asynchronously
+// (LDS-DMA: lanes 0..n-1 each move one chunk; dst wave-uniform)
+#ifndef SM_DMA_ROW
+#define SM_DMA_ROW(dst, src, n, lane) ::smash::sm::dma_row(dst, src, n, lane)
+#endif
 
 namespace smash {
 namespace sm {
@@ -62,11 +67,22 @@ __device__ __forceinline__ uint4 load16u(uint64_t a) {
   return v;
 }
 
+#ifndef SM_DMA_ROW_HOST
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void glb_void_t;
+__device__ __forceinline__ void dma_row(uint32_t *dst, const uint4 *src, uint32_t n, uint32_t lane) {
+  if (lane < n)
+    __builtin_amdgcn_global_load_lds((glb_void_t *)(src + lane), (lds_void_t *)dst, 16, 0, 0);
+}
+#endif
+
 // record / LDS row geometry for a launch (reads up to max_len bases)
 struct Geom {
   uint32_t w_raw;    // read bytes + lds_load8 over-read, in words
-  uint32_t w_row;    // LDS row words (= w_raw: lanes read their rows at
-                     // unrelated offsets, so no padding against bank conflicts)
+  uint32_t w_row;    // LDS row words: w_raw rounded up to whole 16-byte chunks
+                     // (the row is one LDS-DMA of the record's raw chunks; lanes
+                     // read their rows at unrelated offsets, so no padding
+                     // against bank conflicts)
   uint32_t c_bad;    // record chunks holding the bad mask (1 or 2)
   uint32_t chunks;   // 16-byte record chunks per read
 };
@@ -74,7 +90,7 @@ struct Geom {
 inline Geom make_geom(uint32_t max_len) {
   Geom g;
   g.w_raw = (max_len + 11) / 4;      // lds_load8 at offset <= L-1 reads 3 words
-  g.w_row = g.w_raw;
+  g.w_row = (g.w_raw + 3) & ~3u;
   g.c_bad = max_len > 128 ? 2 : 1;
   g.chunks = g.c_bad + (g.w_row + 3) / 4;
   return g;
@@ -84,8 +100,7 @@ inline Geom make_geom(uint32_t max_len) {
 // Record of read r (g.chunks * 4 words), built by k_prep:
 //   [0, 4*c_bad)          bad mask, bit i of word i/32: base i is not ACGT
 //                         or does not occur in the text
-//   [4*c_bad, +w_raw)     the read bytes, zero padded
-//   rest                  zero
+//   [4*c_bad, +w_row)     the read bytes, zero padded (w_row = whole chunks)
 // The 2-bit base codes the B-mer / k-mer lookups need are derived from the
 // bytes where they are used (codes_raw), which keeps the LDS row at the
 // read's bytes (occupancy: 4 waves per SIMD at 150 bp).
@@ -368,7 +383,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint32_t fl = 0;
   FlagRef need2{fl, 0};
   uint64_t rd = 0;
-  uint32_t L = 0, nem = 0, kc = 0;
+  uint32_t L = 0, nem = 0;
   Bad bad{0, 0, 0, 0, 0, 0, 0, 0};
   // search state (longSA.h interval_t + prefix)
   uint32_t prefix = 0, depth = 0;
@@ -472,16 +487,27 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           st = S_EXIT;
         } else {
           L = c.lens ? c.lens[rd] : c.len0;
+          // the lane loads the bad-mask chunks; the read's bytes go to its
+          // LDS row by DMA (below)
           addr = reinterpret_cast<uint64_t>(c.rec + rd * c.chunks);
           addr2 = addr + 16;
-          need2 = c.chunks > 1;
+          need2 = c.c_bad > 1;
           pf = false; pfr = false;
-          kc = 0;
           st = S_COPY;
         }
       }
       if (take) { q_next = base + (need - avail); q_end = base + take; }
       else q_next += need;
+      // LDS-DMA of the raw chunks of each newly assigned read into its row;
+      // the lane's own loads of the next iteration (its bad mask) wait for
+      // it (vmcnt retires in order) before any row read
+      uint64_t fm_ = __ballot(fresh && st == S_COPY);
+      while (fm_) {
+        const uint32_t ln = uint32_t(__builtin_ctzll(fm_));
+        fm_ &= fm_ - 1;
+        const uint64_t rl = __shfl(rd, int(ln), 64);
+        SM_DMA_ROW(ldsw + ln * c.w_row, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
+      }
     }
     if (st < S_ALU || fresh) continue;
     if (STATS) {
@@ -502,33 +528,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       case S_ALU:
         a = pend;
         break;
-      case S_COPY: {                                 // record chunks kc (v), kc+1 (v2)
-#pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-          const uint4 &u = h ? v2 : v;
-          const uint32_t k = kc + h;
-          if (k >= c.chunks) break;
-          if (k < c.c_bad) {
-            if (k == 0) { bad.w0 = u.x; bad.w1 = u.y; bad.w2 = u.z; bad.w3 = u.w; }
-            else { bad.w4 = u.x; bad.w5 = u.y; bad.w6 = u.z; bad.w7 = u.w; }
-          } else {
-            const uint32_t q = 4 * (k - c.c_bad);
-            if (q + 0 < c.w_row) row[q + 0] = u.x;
-            if (q + 1 < c.w_row) row[q + 1] = u.y;
-            if (q + 2 < c.w_row) row[q + 2] = u.z;
-            if (q + 3 < c.w_row) row[q + 3] = u.w;
-          }
-        }
-        kc += 2;
-        if (kc < c.chunks) {
-          addr += 32; addr2 = addr + 16; need2 = kc + 1 < c.chunks;
-        } else {
-          need2 = false;
-          prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
-          skip_f = false; fm = 0; ktr_set = false;
-          clean = (bad.w0 | bad.w1 | bad.w2 | bad.w3 | bad.w4 | bad.w5 | bad.w6 | bad.w7) == 0;
-          a = A_TOP;
-        }
+      case S_COPY: {                                 // bad-mask chunks 0 (v), 1 (v2)
+        bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
+        bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
+        need2 = false;
+        prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
+        skip_f = false; fm = 0; ktr_set = false;
+        clean = (bad.w0 | bad.w1 | bad.w2 | bad.w3 | bad.w4 | bad.w5 | bad.w6 | bad.w7) == 0;
+        a = A_TOP;
         break;
       }
       case S_BM: {                                   // (F) last, then first B-mer present?

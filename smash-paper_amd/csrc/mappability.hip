@@ -29,11 +29,24 @@
 //     y - x positions on, is a match of the suffix at y), so with y the next
 //     text position holding U[y] < 255, m(x) <= U[y] + 1 + (y - x): right is
 //     kept when i + that bound < S, left when the bound < i.
-// Only the bases left undecided (saturated runs that reach a contig end)
-// take the exact path: ISA, then the LCP bytes and the overflow table.  The
+// Only the bases left undecided (saturated runs that reach a contig end:
+// the N runs at chromosome ends) take the exact path: ISA, then the LCP
+// bytes and the overflow table (a ~30-load bisection at hg19).  Their m is
+// >= 256 > k, so the byte is 0 or 255 and the unique counts do not depend on
+// it: the scan writes 255, lists {text position, byte index, zero threshold}
+// and k_mapfix settles the listed bytes with one thread each, all in flight
+// together, instead of a serial chain on the thread (and the launch tail) of
+// the tile that meets them.  (k >= 255, or no map output, or a full list:
+// the exact path runs inline as before.)  The
 // next unsaturated position comes from the block's own U bytes, else from a
-// directory of the first unsaturated position per 4096 text positions
-// (built once per index, 12 MB at hg19).
+// directory holding, per 4096 text positions, the first unsaturated position
+// at or after them (built once per index, 12 MB at hg19: one load per
+// lookup, also inside N runs).
+//
+// Latency: a block's fixed work is one tile's loads and its LDS bin counts;
+// the bin ordinal of each tile's first base comes from k_tilebins (one thread
+// per tile, all bisections in flight at once) instead of a 16-load bisection
+// on the block's critical path.
 #include "common.hpp"
 
 namespace smash {
@@ -52,7 +65,11 @@ struct MapCtx {
   uint64_t n_ovf, N;
   const int64_t *bins;
   uint32_t nbins, k;
+  uint64_t *fix;                 // [fix_cap][3] {x, byte index in the scan's output, threshold}
+  unsigned long long *nfix;
+  uint64_t fix_cap;
 };
+constexpr uint64_t kFixCap = uint64_t(1) << 23;
 
 __device__ __forceinline__ uint64_t lcp_exact(const MapCtx &c, uint64_t r) {
   const uint32_t v = c.L8[r];
@@ -113,13 +130,19 @@ __global__ __launch_bounds__(kMB) void k_nsdir(const uint8_t *__restrict__ U, ui
   }
 }
 
-// the first unsaturated text position >= p (kNone: none before N), from
-// the directory; p must be a multiple of 4096 or the caller must accept a
-// later (looser) position
-__device__ uint64_t next_unsat_dir(const uint64_t *dir, uint64_t ndir, uint64_t p) {
-  for (uint64_t t = (p + (uint64_t(1) << kDirShift) - 1) >> kDirShift; t < ndir; ++t)
-    if (dir[t] != kNone) return dir[t];
-  return kNone;
+// an unsaturated text position >= p (kNone: none before N): the first one
+// at or after the next multiple of 4096 (exact when p is a multiple; a later,
+// looser bound otherwise, which the callers accept).  dir is the suffix-min
+// directory (scan_t).
+__device__ __forceinline__ uint64_t next_unsat_dir(const uint64_t *dir, uint64_t ndir, uint64_t p) {
+  const uint64_t t = (p + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
+  return t < ndir ? dir[t] : kNone;
+}
+
+// bin ordinal (bisect_right of abs0 + the tile's first base) per tile
+__global__ void k_tilebins(MapCtx c, int64_t abs0, uint64_t i0, uint64_t ntiles, uint32_t *o0) {
+  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t < ntiles) o0[t] = bisect_right(c, abs0 + int64_t(i0 + t * kMTile));
 }
 
 // bases [i0, i1) of one contig (text start sp, size S); out: map.bin bytes of
@@ -131,8 +154,10 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
                                                  const uint64_t *__restrict__ dir, uint64_t ndir,
                                                  uint64_t sp, uint64_t S, uint64_t i0, uint64_t i1,
                                                  uint8_t *__restrict__ out, int64_t abs0,
+                                                 const uint32_t *__restrict__ tile_o0,
                                                  unsigned long long *bin_counts,
-                                                 unsigned long long *contig_count) {
+                                                 unsigned long long *contig_count,
+                                                 uint64_t out_base) {
   __shared__ unsigned long long s_bin[kLdsBins + 1];
   __shared__ int64_t s_bs[kLdsBins];
   __shared__ unsigned long long s_tot;
@@ -147,7 +172,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     if (threadIdx.x <= kLdsBins) s_bin[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       s_tot = 0;
-      s_o0 = binned ? bisect_right(c, abs0 + int64_t(t0)) : 0;
+      s_o0 = binned ? tile_o0[t] : 0;
     }
     __syncthreads();
     const uint32_t o0 = s_o0;
@@ -196,6 +221,8 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       if (rnext == kNone) rnext = s_rtail;
     }
     uint32_t ob[2 * kMPer / 4] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t fixr = 0, fixl = 0;   // bases whose right / left byte k_mapfix settles
+    const bool defer = out && c.fix && c.k < 255;
     unsigned long long mine = 0;
     uint32_t d = 0;   // bin ordinal offset from o0 (monotone over the thread's bases)
 #pragma unroll 4
@@ -216,7 +243,10 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         if (y == kNone) y = fnext;
         const uint64_t ub = y == kNone ? kNone : U[y] + 1 + (y - (xf + q));
         if (ub != kNone && i + ub < S) right = 255;
-        else {
+        else if (defer) {
+          right = 255;
+          fixr |= 1u << q;
+        } else {
           right = min_len_at(c, uint64_t(ISA[xf + q]));
           if (right + i >= S) right = 0;
         }
@@ -235,7 +265,10 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         if (y == kNone) y = rnext;
         const uint64_t ub = y == kNone ? kNone : U[y] + 1 + (y - (xr - q));
         if (ub != kNone && ub < i) left = 255;
-        else {
+        else if (defer) {
+          left = 255;
+          fixl |= 1u << q;
+        } else {
           left = min_len_at(c, uint64_t(ISA[xr - q]));
           if (left >= i) left = 0;
         }
@@ -253,6 +286,37 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
             const uint32_t o = bisect_right(c, a);
             atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], 1ull);
           }
+        }
+      }
+    }
+    if (c.fix) {   // list the deferred bytes: one atomic per wave
+      const uint32_t nf = uint32_t(__popc(fixr) + __popc(fixl));
+      const uint32_t lane = threadIdx.x & 63;
+      uint32_t x = nf;
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t y = __shfl_up(x, dd, 64);
+        if (lane >= uint32_t(dd)) x += y;
+      }
+      const uint32_t tot = __shfl(x, 63, 64);
+      unsigned long long fb = 0;
+      if (lane == 63 && tot) fb = atomicAdd(c.nfix, (unsigned long long)tot);
+      fb = __shfl(fb, 63, 64) + (x - nf);
+      for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
+        for (uint32_t side = 0; side < 2; ++side) {
+          if (!(((side ? fixl : fixr) >> q) & 1)) continue;
+          const uint64_t i = ib + q;
+          const uint64_t x = side ? xr - q : xf + q;
+          const uint64_t bi = out_base + 2 * (i - i0) + (side ? 0 : 1);
+          const uint64_t thr = side ? i : S - i;   // zeroed when m >= thr
+          if (fb < c.fix_cap) {
+            c.fix[3 * fb] = x; c.fix[3 * fb + 1] = bi; c.fix[3 * fb + 2] = thr;
+          } else {                                 // list full: exact path here
+            const uint64_t mm = min_len_at(c, uint64_t(ISA[x]));
+            const uint32_t byte = mm >= thr ? 0u : (mm < 255 ? uint32_t(mm) : 255u);
+            const uint32_t sh = 16 * (q & 1) + (side ? 0 : 8);
+            ob[q >> 1] = (ob[q >> 1] & ~(0xFFu << sh)) | (byte << sh);
+          }
+          ++fb;
         }
       }
     }
@@ -278,6 +342,17 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
   }
 }
 
+// settle the listed bytes: exact m, zeroed at its threshold, else min(m, 255)
+template <class IdxT>
+__global__ void k_mapfix(MapCtx c, const IdxT *__restrict__ ISA, uint8_t *out) {
+  const uint64_t n = *c.nfix < c.fix_cap ? *c.nfix : c.fix_cap;
+  for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < n;
+       e += uint64_t(gridDim.x) * blockDim.x) {
+    const uint64_t m = min_len_at(c, uint64_t(ISA[c.fix[3 * e]]));
+    out[c.fix[3 * e + 1]] = uint8_t(m >= c.fix[3 * e + 2] ? 0 : (m < 255 ? m : 255));
+  }
+}
+
 template <class IdxT>
 int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint8_t *out,
            const int64_t *h_chrom_off, const int64_t *d_bins, uint32_t nbins,
@@ -290,13 +365,38 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
   c.bins = d_bins;
   c.nbins = d_bins ? nbins : 0;
   c.k = k;
-  // the directory of unsaturated U positions, once per index
+  c.fix = nullptr;
+  c.nfix = nullptr;
+  c.fix_cap = 0;
+  if (out && k < 255) {
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&c.fix), 24 * kFixCap, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&c.nfix), 8, s));
+    SMASH_HIP(hipMemsetAsync(c.nfix, 0, 8, s));
+    c.fix_cap = kFixCap;
+  }
+  // the directory of unsaturated U positions, once per index: first one per
+  // 4096 positions, then the suffix minimum (host side, 12 MB at hg19)
   const uint64_t ndir = (ix->N + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
   if (!ix->d_nsdir) {
     SMASH_HIP(hipMalloc(&ix->d_nsdir, 8 * ndir));
     k_nsdir<<<unsigned(ndir < 65536 ? ndir : 65536), kMB, 0, s>>>(ix->d_uniq, ix->N, ix->d_nsdir,
                                                                    ndir);
     SMASH_HIP(hipGetLastError());
+    std::vector<uint64_t> h(ndir);
+    SMASH_HIP(hipMemcpyAsync(h.data(), ix->d_nsdir, 8 * ndir, hipMemcpyDeviceToHost, s));
+    SMASH_HIP(hipStreamSynchronize(s));
+    for (uint64_t t = ndir - 1; t-- > 0;)
+      if (h[t] == kNone) h[t] = h[t + 1];
+    SMASH_HIP(hipMemcpyAsync(ix->d_nsdir, h.data(), 8 * ndir, hipMemcpyHostToDevice, s));
+    SMASH_HIP(hipStreamSynchronize(s));   // h is a host local
+  }
+  // per-tile bin ordinals (largest contig's tile count)
+  uint32_t *d_o0 = nullptr;
+  if (c.nbins) {
+    uint64_t maxt = 1;
+    for (uint32_t q = 0; q < ix->n_seq; q += 2)
+      maxt = std::max<uint64_t>(maxt, (ix->sizes[q] + kMTile - 1) / kMTile);
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_o0), 4 * maxt, s));
   }
   uint64_t g = 0;   // forward-base coordinate of the contig's first base
   for (uint32_t q = 0; q < ix->n_seq; q += 2) {
@@ -306,15 +406,28 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     if (a < b && g < end) {
       const uint64_t tiles = (b - a + kMTile - 1) / kMTile;
       const unsigned grid = unsigned(tiles < 65536 ? tiles : 65536);
+      const int64_t abs0 = h_chrom_off ? h_chrom_off[q / 2] : -1;
+      if (c.nbins && abs0 >= 0) {
+        k_tilebins<<<unsigned((tiles + 255) / 256), 256, 0, s>>>(c, abs0, a, tiles, d_o0);
+        SMASH_HIP(hipGetLastError());
+      }
       k_mapscan<IdxT><<<grid, kMB, 0, s>>>(
           c, static_cast<const IdxT *>(ix->d_isa), ix->d_uniq, ix->d_nsdir, ndir, sp, S, a, b,
-          out ? out + 2 * (g + a - begin) : nullptr, h_chrom_off ? h_chrom_off[q / 2] : -1,
+          out ? out + 2 * (g + a - begin) : nullptr, abs0, d_o0,
           reinterpret_cast<unsigned long long *>(d_bin_counts),
           d_contig_counts ? reinterpret_cast<unsigned long long *>(d_contig_counts + q / 2)
-                          : nullptr);
+                          : nullptr,
+          2 * (g + a - begin));
       SMASH_HIP(hipGetLastError());
     }
     g += S;
+  }
+  if (d_o0) SMASH_HIP(hipFreeAsync(d_o0, s));
+  if (c.fix) {
+    k_mapfix<IdxT><<<4096, 256, 0, s>>>(c, static_cast<const IdxT *>(ix->d_isa), out);
+    SMASH_HIP(hipGetLastError());
+    SMASH_HIP(hipFreeAsync(c.fix, s));
+    SMASH_HIP(hipFreeAsync(c.nfix, s));
   }
   return SMASH_OK;
 }

@@ -63,7 +63,8 @@ struct smash_pipeline {
   int64_t *d_pos0 = nullptr, *d_abs = nullptr;
   int64_t *d_prev = nullptr;      // [2] carried {last pos0 or -1, -}
   unsigned long long *d_stats = nullptr;
-  uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast -> k_post pair list
+  uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast<16> -> k_post pair list
+  uint32_t *d_l16 = nullptr;      // [1 + max_pairs]: k_post_fast<8> -> k_post_fast<16>
   uint8_t *d_post_ws = nullptr;   // k_post workspace: kPostThreads slices
   uint64_t hash_mask = ~0ull;
   bool post_fast = false;
@@ -354,6 +355,18 @@ __device__ __forceinline__ void cx(uint64_t &a, uint64_t &b) {
   b = hi;
 }
 
+// append v to list (counter *n) for the lanes with pred: one atomic per
+// wave (all lanes of the wave call it)
+__device__ __forceinline__ void wave_push(uint32_t *list, uint32_t *n, bool pred, uint32_t v) {
+  const uint64_t b = __ballot(pred);
+  if (!b) return;
+  const uint32_t lane = threadIdx.x & 63, leader = uint32_t(__builtin_ctzll(b));
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(n, uint32_t(__popcll(b)));
+  base = __shfl(base, int(leader), 64);
+  if (pred) list[base + uint32_t(__popcll(b & ((1ull << lane) - 1)))] = v;
+}
+
 // Batcher odd-even merge sort, N a power of two (fully unrolled)
 template <int N>
 __device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
@@ -369,15 +382,16 @@ __device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
             cx(v[i + j], v[i + j + k]);
 }
 
+template <int CAP>
 __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *sp, const uint64_t *m,
-                                          uint32_t n, uint64_t (&H)[FCAP], int32_t &err) {
+                                          uint32_t n, uint64_t (&H)[CAP], int32_t &err) {
   const uint32_t L = c.L;
-  uint64_t A[FCAP];
-  uint64_t w[FCAP];
+  uint64_t A[CAP];
+  uint64_t w[CAP];
 #pragma unroll
-  for (int k = 0; k < FCAP; ++k) w[k] = uint32_t(k) < n ? m[k] : 0;
+  for (int k = 0; k < CAP; ++k) w[k] = uint32_t(k) < n ? m[k] : 0;
 #pragma unroll
-  for (int k = 0; k < FCAP; ++k) {
+  for (int k = 0; k < CAP; ++k) {
     const uint64_t ref = w[k] & 0xFFFFFFFFFFFFull;
     const uint32_t q = uint32_t((w[k] >> 48) & 0xFF), len = uint32_t(w[k] >> 56);
     uint32_t lo = 0, hi = c.n_seq;          // upper_bound(startpos, ref), LDS copy
@@ -401,14 +415,14 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *sp, 
   uint32_t g_prefix = 0, g_qmin = 0;
   int32_t g_l0 = 0, g_r0 = 0;
 #pragma unroll
-  for (int i = 0; i < FCAP; ++i) {
+  for (int i = 0; i < CAP; ++i) {
     const uint64_t a = A[i];
     const bool valid = a != ~0ull;
     const uint32_t rc = uint32_t(a >> 63), tid = valid ? uint32_t(a >> 48) & 0x7FFF : 0u;
     const uint32_t pos = uint32_t(a >> 16), prefix = uint32_t(a >> 8) & 0xFF, len = uint32_t(a) & 0xFF;
     const uint32_t qpos = rc ? L - len - prefix : prefix;
     const bool start = i == 0 || (A[i - 1] >> 16) != (a >> 16);
-    const bool endg = i + 1 == FCAP || (A[i + 1 < FCAP ? i + 1 : i] >> 16) != (a >> 16);
+    const bool endg = i + 1 == CAP || (A[i + 1 < CAP ? i + 1 : i] >> 16) != (a >> 16);
     const uint32_t abspos = c.tag_off[tid] + pos + 1;
     const uint32_t li = abspos + prefix + len - 1, ri = abspos + prefix - 1;
     const unsigned lm = valid ? mapb(c, 2 + uint64_t(li) * 2) : 0u;
@@ -434,36 +448,47 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *sp, 
 
 __device__ __forceinline__ bool hit_kept(uint64_t h) { return h != ~0ull && ((h >> 54) & 1); }
 
+// CAP words per mate (8: the common case; a pair with a mate above `lim`
+// goes to the `up` list, for k_post_fast<16> or, past 16, k_post).  Pairs:
+// all n_pairs (list == nullptr) or the *n_list listed ones (grid-stride).
+template <int CAP>
 __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__restrict__ match,
                                                   const uint32_t *__restrict__ nmatch,
-                                                  uint64_t n_pairs, uint32_t *fb_list,
-                                                  uint32_t *fb_n, int32_t *nk_out,
-                                                  uint32_t *nmajor_out, uint64_t *hits_out,
-                                                  uint64_t *hash_out,
+                                                  uint64_t n_pairs, const uint32_t *list,
+                                                  const uint32_t *n_list, uint32_t lim,
+                                                  uint32_t *up_list, uint32_t *up_n,
+                                                  int32_t *nk_out, uint32_t *nmajor_out,
+                                                  uint64_t *hits_out, uint64_t *hash_out,
                                                   unsigned long long *stats) {
   __shared__ uint64_t sp[kSeqLds];
   for (uint32_t i = threadIdx.x; i < c.n_seq; i += blockDim.x) sp[i] = c.startpos[i];
   __syncthreads();
-  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t n = list ? *n_list : n_pairs;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const uint64_t t0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   int32_t err = 0;
   unsigned long long nm = 0, np = 0;
-  if (q < n_pairs) {
-    const uint32_t n1 = nmatch[2 * q], n2 = nmatch[2 * q + 1];
-    if (n1 > c.fast_cap || n2 > c.fast_cap) {
-      fb_list[atomicAdd(fb_n, 1u)] = uint32_t(q);   // general path
-    } else {
-      nm = n1 + n2;
-      np = 1;
-      uint64_t H1[FCAP], H2[FCAP];
-      mate_fast(c, sp, match + (2 * q) * c.slots, n1, H1, err);
-      mate_fast(c, sp, match + (2 * q + 1) * c.slots, n2, H2, err);
+  // every lane runs the same trip count (wave_push is wave-wide)
+  for (uint64_t base = t0 - threadIdx.x % 64; base < n; base += stride) {
+    const uint64_t i = base + threadIdx.x % 64;
+    const bool in = i < n;
+    const uint64_t q = in ? (list ? list[i] : i) : 0;
+    const uint32_t n1 = in ? nmatch[2 * q] : 0, n2 = in ? nmatch[2 * q + 1] : 0;
+    const bool over = in && (n1 > lim || n2 > lim);
+    wave_push(up_list, up_n, over, uint32_t(q));
+    if (in && !over) {
+      nm += n1 + n2;
+      ++np;
+      uint64_t H1[CAP], H2[CAP];
+      mate_fast<CAP>(c, sp, match + (2 * q) * c.slots, n1, H1, err);
+      mate_fast<CAP>(c, sp, match + (2 * q + 1) * c.slots, n2, H2, err);
       uint64_t *ho = hits_out + q * (2 * uint64_t(c.slots));
       int32_t nk = -1;
       uint32_t nmaj = 0;
       uint64_t hh = 0x9E3779B97F4A7C15ull, hl = 0xD1B54A32D192ED03ull;
       bool any = false;
 #pragma unroll
-      for (int i = 0; i < FCAP; ++i) any = any || hit_kept(H1[i]) || hit_kept(H2[i]);
+      for (int i = 0; i < CAP; ++i) any = any || hit_kept(H1[i]) || hit_kept(H2[i]);
       if (any) {                              // smashMEM.py:162
         nk = 0;
         auto put = [&](uint64_t h) {
@@ -476,14 +501,14 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
           if (c.chrom_off[tid] >= 0) ++nmaj;
         };
 #pragma unroll
-        for (int i = 0; i < FCAP; ++i)
+        for (int i = 0; i < CAP; ++i)
           if (hit_kept(H1[i])) put(H1[i]);
 #pragma unroll
-        for (int b = 0; b < FCAP; ++b) {      // hit window (smashMEM.py:193-200)
+        for (int b = 0; b < CAP; ++b) {      // hit window (smashMEM.py:193-200)
           if (!hit_kept(H2[b])) continue;
           bool close = false;
 #pragma unroll
-          for (int i = 0; i < FCAP; ++i) {
+          for (int i = 0; i < CAP; ++i) {
             int64_t d = int64_t(uint32_t(H1[i])) - int64_t(uint32_t(H2[b]));
             d = d < 0 ? -d : d;
             close |= hit_kept(H1[i]) && ((H1[i] >> 32) & 0xFFFF) == ((H2[b] >> 32) & 0xFFFF) &&
@@ -856,6 +881,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * S_N));
     p->d_send_q = dalloc<uint32_t>(P);
     p->d_fb = dalloc<uint32_t>(P + 1);
+    p->d_l16 = dalloc<uint32_t>(P + 1);
     p->d_post_ws = dalloc<uint8_t>(uint64_t(kPostThreads) * post_ws_bytes(p->slots));
     {
       bool ok = ix->n_seq <= kSeqLds && p->n_contig < 0x7FFF;
@@ -896,7 +922,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
-                  (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb,
+                  (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb, (void *)p->d_l16,
                   (void *)p->d_post_ws, (void *)p->d_arena, (void *)p->d_arena_top,
                   (void *)p->d_send_hdr, (void *)p->d_send_words, (void *)p->d_recv_base})
     dfree(q);
@@ -933,10 +959,18 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
     p->prof_reads += 2 * n_pairs;
   }
   if (p->post_fast) {
+    // mates of <= 8 matches (most pairs) in 8-word networks, <= 16 in
+    // 16-word ones, the rest in the general kernel
     SMASH_HIP(hipMemsetAsync(p->d_fb, 0, 4, s));
-    k_post_fast<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
-        post_cfg(p), p->d_match, p->d_nmatch, n_pairs, p->d_fb + 1, p->d_fb, p->d_nk,
-        p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+    SMASH_HIP(hipMemsetAsync(p->d_l16, 0, 4, s));
+    const PostCfg pc = post_cfg(p);
+    k_post_fast<8><<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
+        pc, p->d_match, p->d_nmatch, n_pairs, nullptr, nullptr, std::min(8u, p->post_cap),
+        p->d_l16 + 1, p->d_l16, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+    SMASH_HIP(hipGetLastError());
+    k_post_fast<FCAP><<<grid_for(n_pairs, kB, 1024), kB, 0, s>>>(
+        pc, p->d_match, p->d_nmatch, n_pairs, p->d_l16 + 1, p->d_l16, p->post_cap,
+        p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
     SMASH_HIP(hipGetLastError());
     k_post<<<kPostBlocks, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs,
                                       p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, p->d_hits,

@@ -65,6 +65,18 @@ static void emu_hook_pf(uint64_t a, uint64_t n) {
   if (arr < 0) ++emu_bad; else emu_count(arr, a, n);
 }
 #define SM_HOOK_PF(a) emu_hook_pf(a, sizeof(IdxT))
+// the row DMA: every chunk a counted record probe; the lane's own load of
+// the record's first chunks (next iteration) lies on the line the DMA's
+// first chunk opened: the record's 192 bytes are 3 line transitions
+static void emu_dma_row(uint32_t *dst, const uint4 *src, uint32_t n, const uint4 *rec0) {
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint4 v = emu_load16(reinterpret_cast<uint64_t>(src + k));
+    std::memcpy(dst + 4 * k, &v, 16);
+  }
+  emu_last[7] = reinterpret_cast<uint64_t>(rec0) >> 6;   // chunks 0, 1: the line chunk 2 opened
+}
+#define SM_DMA_ROW(dst, src, n, lane) emu_dma_row(dst, src, n, (src) - c.c_bad)
+#define SM_DMA_ROW_HOST
 #define PAD_KEEP(x) ((void)(x))
 // traverse binary searches by interval size (1..63, 64 = larger) and start depth
 static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
@@ -87,7 +99,12 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
                uint64_t *viol, uint32_t lin_blocks, uint64_t *counters) {
   const sm::Geom g = sm::make_geom(L);
   if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
-  std::vector<uint4> rec(n * g.chunks);
+  // 64-byte aligned, as the device's allocation (records are whole lines)
+  std::vector<uint4> rec_mem(n * g.chunks + 4);
+  uint4 *rec_p = rec_mem.data();
+  while (reinterpret_cast<uint64_t>(rec_p) & 63) ++rec_p;
+  struct { uint4 *p; size_t n; uint4 *data() { return p; } size_t size() const { return n; } } rec{
+      rec_p, size_t(n * g.chunks)};
   const uint32_t per = sm::prep_per_block(g, stride);
   if (sm::prep_lds_bytes(g, stride, per) > sizeof(sm::prep_lds)) return -1;
   blockDim.x = 1;
