@@ -311,6 +311,73 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def feed_bench(S, dix, cs, starts, L, d_reads, P, dev, tmpdir, n_plain=1000000,
+               n_gz=250000, batch=250000):
+    """The file-fed rate (smash_count_fastq, csrc/feed.hip): the first pairs
+    of the same reads written as FASTQ (names in sort -n order) to local disk,
+    then counted from the files with parse / H2D / compute overlapped, plain
+    and gzip; the counts must equal the device-resident path's on the same
+    pairs.  Also the pinned H2D copy rate."""
+    import torch
+    import readgen
+    res = {}
+    n_plain = min(P, n_plain)
+    n_gz = min(n_plain, n_gz)
+    h = d_reads[:2 * n_plain].cpu().numpy()
+    # resident reference counts on the same pairs and batches
+    pipe = S.Pipeline(dix, cs, starts, L, batch, dedup_capacity=n_plain + (1 << 16))
+
+    def resident(n):
+        pipe.reset()
+        c = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+        for b0 in range(0, n, batch):
+            b1 = min(n, b0 + batch)
+            pipe.count_batch(d_reads[2 * b0:2 * b1], b1 - b0, c)
+        return c.cpu().numpy()
+
+    for kind, n in (("plain", n_plain), ("gz", n_gz)):
+        ext = ".fq.gz" if kind == "gz" else ".fq"
+        p1, p2 = os.path.join(tmpdir, "r1" + ext), os.path.join(tmpdir, "r2" + ext)
+        t0 = time.perf_counter()
+        readgen.write_fastq(h[:2 * n], p1, p2, gz=kind == "gz")
+        wr = time.perf_counter() - t0
+        nbytes = os.path.getsize(p1) + os.path.getsize(p2)
+        exp = resident(n)
+        pipe.reset()
+        c = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        fs = pipe.count_fastq([p1], [p2], c, sort_names=False)
+        same = bool(np.array_equal(c.cpu().numpy(), exp))
+        res[kind] = {"reads_per_s": round(2 * fs["pairs"] / fs["wall_s"], 1),
+                     "pairs": int(fs["pairs"]), "batches": int(fs["batches"]),
+                     "wall_s": round(fs["wall_s"], 3), "ingest_s": round(fs["ingest_s"], 3),
+                     "device_waited_s": round(fs["wait_s"], 3), "file_bytes": int(nbytes),
+                     "counts_identical_to_resident": same}
+        log("file-fed %s: %d pairs, %.3f s -> %.3e reads/s (ingest %.3f s, device waited %.3f s, "
+            "%.1f MB, written in %.1f s); counts == resident: %s"
+            % (kind, fs["pairs"], fs["wall_s"], 2 * fs["pairs"] / fs["wall_s"], fs["ingest_s"],
+               fs["wait_s"], nbytes / 1e6, wr, same))
+        for q in (p1, p2):
+            os.remove(q)
+    # the pinned host -> device copy rate of one batch of reads
+    hp = torch.from_numpy(h[:2 * min(n_plain, batch)]).pin_memory()
+    dd = torch.empty_like(hp, device=dev)
+    dd.copy_(hp, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        dd.copy_(hp, non_blocking=True)
+    torch.cuda.synchronize()
+    gbs = 5 * hp.numel() / (time.perf_counter() - t0) / 1e9
+    res["h2d_pinned_GBps"] = round(gbs, 2)
+    res["h2d_reads_per_s"] = round(gbs * 1e9 / L, 1)
+    res["method"] = ("smash_count_fastq (csrc/feed.hip): 2 parse threads (one per mate list), "
+                     "3 pinned slots, 2 device buffers, H2D on its own stream; batches of %d "
+                     "pairs; FASTQ on local disk, names in sort -n order (streamed)" % batch)
+    del pipe
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -322,6 +389,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 scan on the same index")
+    ap.add_argument("--no-feed", action="store_true", help="skip the file-fed measurement")
+    ap.add_argument("--feed-pairs", type=int, default=1000000)
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.pairs:
@@ -503,8 +572,8 @@ def main():
             t3 = time.perf_counter()
             err = op.run(h1, threads=threads)
             dt = time.perf_counter() - t3
-            # the search alone (longSA::MAM, no resolve/tag/filter/bin)
-            nm = min(len(h1), 2 * n0 * 4)
+            # the search alone (longSA::MAM, no resolve/tag/filter/bin), ~5 s
+            nm = int(min(len(h1), max(2 * n0, 5.0 * 2 * n1 / max(dt, 1e-3))))
             t3 = time.perf_counter()
             O.map_only(oix, h1[:nm], threads=threads)
             dtm = time.perf_counter() - t3
@@ -532,6 +601,9 @@ def main():
                 "device==oracle counts: %s" % (cpu["value"], nm / dtm, threads, exact))
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
+    if rank == 0 and world == 1 and not args.no_feed:
+        out["host_boundary"] = feed_bench(S, dix, cs, starts, L, d_reads, P, dev, tmpdir,
+                                          n_plain=args.feed_pairs)
     if cfg["genome"] == "hg19" and not args.no_c5:
         out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)
     out["deterministic_counts"] = same

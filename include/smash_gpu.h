@@ -355,6 +355,35 @@ int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *len,
 void smash_fastq_close(smash_fastq *f);
 int smash_strnum_order(const char *names, uint32_t stride, uint64_t n, uint64_t *perm);
 
+/* ========================================================================== */
+/* File-fed counting: smash_mapping.sh:19-25's front (zcat | fastqs_to_sam |  */
+/* samtools sort -n) feeding the pipeline, as the reference's reader threads  */
+/* feed its workers (query.cpp:614-740).  The two mate lists (gzip or plain)  */
+/* are parsed on two threads into pinned host batches of cfg.max_pairs pairs  */
+/* (`threads` workers convert / check them: replaceN + lowercase, pairs as    */
+/* smash_fastq_read, every mate of cfg.read_len bases), copied H2D on an own  */
+/* stream into two device buffers, and counted with smash_count_batch on      */
+/* `stream`: parse, copy and compute of consecutive batches overlap.          */
+/*  sort_names = 0: the input is in samtools sort -n order already (checked   */
+/*                  on the read-1 names; SMASH_ERR_ARG if not, counts then    */
+/*                  partial); 1: all pairs are read, ordered by strnum_cmp    */
+/*                  (stable), then streamed.                                  */
+/* Adds into d_counts like smash_count_batch (the caller resets the pipeline  */
+/* when a new run starts).  Synchronises `stream` before returning.           */
+/* ========================================================================== */
+typedef struct {
+  uint64_t pairs;     /* pairs counted */
+  uint64_t batches;
+  double wall_s;      /* call start to the last batch's counts */
+  double ingest_s;    /* host time parsing / converting / ordering */
+  double wait_s;      /* time the device side waited for a parsed batch */
+  uint32_t read_len;
+} smash_feed_stats;
+int smash_count_fastq(smash_pipeline *p, const char *const *r1_paths, uint32_t n1,
+                      const char *const *r2_paths, uint32_t n2, int sort_names,
+                      uint32_t threads, uint64_t *d_counts, smash_feed_stats *stats,
+                      void *stream);
+
 #ifdef __cplusplus
 }
 #endif

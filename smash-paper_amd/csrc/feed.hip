@@ -1,0 +1,412 @@
+// smash-paper_amd/csrc/feed.hip -- file-fed counting: the FASTQ/FASTA read
+// lists of both mates -> pinned host batches -> H2D -> smash_count_batch,
+// with parsing, copies and compute overlapped.
+//
+// This is the front of smash_mapping.sh:19-25 (zcat | fastqs_to_sam |
+// samtools sort -n | memsam ...) feeding the device pipeline, organised like
+// the reference's reader threads feeding its workers (query.cpp:614-740):
+//   * producer: the two mate lists are parsed on two threads (ingest.hpp,
+//     zlib for gzip), zipped into a pinned host batch by `threads` workers
+//     (replaceN + lowercasing, pair checks as smash_fastq_read);
+//   * consumer (the calling thread): per batch, an H2D copy on a copy stream
+//     into one of two device buffers, then smash_count_batch on the compute
+//     stream once the copy's event fires; the copy of batch b+1 runs under
+//     the compute of batch b, the parse of b+2 under both.
+// Pair order: the pipeline wants pairs in `samtools sort -n` order.  With
+// sort_names = 0 the input must already be in that order (checked on the
+// read-1 names as they stream; an out-of-order pair is SMASH_ERR_ARG, counts
+// then partial); with sort_names = 1 every pair is read first (host memory),
+// ordered by strnum_cmp (stable), and then streamed through the same
+// copy / compute overlap.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <numeric>
+#include <thread>
+
+#include "common.hpp"
+#include "ingest.hpp"
+
+using smash::ingest::Chunk;
+using smash::ingest::Reader;
+using smash::ingest::strnum_cmp;
+
+namespace smash {
+uint32_t pipe_read_len(const smash_pipeline *p);
+uint64_t pipe_max_pairs(const smash_pipeline *p);
+int pipe_device(const smash_pipeline *p);
+}  // namespace smash
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double secs(Clock::time_point a, Clock::time_point b) {
+  return std::chrono::duration<double>(b - a).count();
+}
+
+// run f(lo, hi) over [0, n) on up to T threads
+template <class F>
+void par_for(uint64_t n, uint32_t T, F f) {
+  if (T <= 1 || n < 4096) {
+    f(uint64_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < T; ++t) {
+    const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+    th.emplace_back([&, lo, hi] { f(lo, hi); });
+  }
+  for (auto &x : th) x.join();
+}
+
+struct Slot {
+  uint8_t *h = nullptr;   // pinned [2 * max_pairs * L]
+  uint64_t n = 0;
+  bool last = false;
+  int state = 0;          // 0 free, 1 filled
+};
+
+struct Feed {
+  smash_pipeline *p;
+  uint32_t L, T;
+  uint64_t B;
+  Reader r1, r2;
+  Chunk c1, c2;
+  std::string prev_name;   // read-1 name of the last pair streamed (order check)
+  bool have_prev = false;
+  // shared state
+  std::mutex mu;
+  std::condition_variable cv;
+  Slot slot[3];
+  int err = 0;
+  std::string msg;
+  double ingest_s = 0;
+
+  void fail(int e, const std::string &m) {
+    std::lock_guard<std::mutex> g(mu);
+    if (!err) {
+      err = e;
+      msg = m;
+    }
+    cv.notify_all();
+  }
+  bool failed() {
+    std::lock_guard<std::mutex> g(mu);
+    return err != 0;
+  }
+
+  // parse up to `want` pairs (both lists on two threads); n pairs ready in
+  // c1 / c2; false at error
+  bool parse(uint64_t want, uint64_t &n, bool &end) {
+    std::thread t([&] { c2.parse(r2, want, false); });
+    c1.parse(r1, want, true);
+    t.join();
+    if (c1.err || c2.err) {
+      fail(c1.err ? c1.err : c2.err, c1.err ? r1.msg : r2.msg);
+      return false;
+    }
+    n = std::min(c1.size(), c2.size());
+    end = c1.end || c2.end;   // zip(): the shorter list ends the pairs
+    return true;
+  }
+
+  // pair checks of pairs [0, n) of c1 / c2 (both mates empty: dropped, one
+  // empty: error, other lengths: error); keep[i] = pair kept
+  bool check_pairs(uint64_t n, std::vector<uint8_t> &keep) {
+    keep.assign(n, 1);
+    std::atomic<int> bad{0};
+    std::atomic<uint64_t> where{~0ull};
+    par_for(n, T, [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) {
+        const uint64_t la = c1.boff[i + 1] - c1.boff[i], lb = c2.boff[i + 1] - c2.boff[i];
+        int e = 0;
+        if (la == 0 && lb == 0) keep[i] = 0;
+        else if (la == 0 || lb == 0) e = 1;
+        else if (la != L || lb != L) e = 2;
+        if (e) {
+          uint64_t w = where.load();
+          while (i < w && !where.compare_exchange_weak(w, i)) {
+          }
+          bad = 1;
+        }
+      }
+    });
+    if (!bad) return true;
+    const uint64_t i = where.load();
+    const std::string na(c1.names.data() + c1.noff[i], c1.noff[i + 1] - c1.noff[i]);
+    const uint64_t la = c1.boff[i + 1] - c1.boff[i], lb = c2.boff[i + 1] - c2.boff[i];
+    if (la == 0 || lb == 0)
+      fail(SMASH_ERR_ARG, "smash_count_fastq: one mate of a pair has no bases (" + na + ")");
+    else
+      fail(SMASH_ERR_ARG, "smash_count_fastq: every mate must have the pipeline's read length (" +
+                              na + ")");
+    return false;
+  }
+
+  // streaming producer (input already in name order)
+  void produce_stream() {
+    const uint8_t *lut = smash::ingest::lut();
+    std::vector<uint8_t> keep;
+    std::vector<uint64_t> dst;
+    for (uint64_t b = 0;; ++b) {
+      Slot &s = slot[b % 3];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return s.state == 0 || err; });
+        if (err) return;
+      }
+      const auto t0 = Clock::now();
+      uint64_t n = 0;
+      bool end = false;
+      if (!parse(B, n, end) || !check_pairs(n, keep)) return;
+      // destination pair index of each kept pair, and the order check
+      dst.resize(n);
+      uint64_t k = 0;
+      for (uint64_t i = 0; i < n; ++i) dst[i] = keep[i] ? k++ : ~0ull;
+      std::atomic<uint64_t> disorder{~0ull};
+      par_for(n, T, [&](uint64_t lo, uint64_t hi) {
+        const char *prev = nullptr;
+        size_t pn = 0;
+        for (uint64_t i = lo; i < hi; ++i) {
+          if (!keep[i]) continue;
+          const char *nm = c1.names.data() + c1.noff[i];
+          const size_t nn = c1.noff[i + 1] - c1.noff[i];
+          if (!prev && i > 0) {   // the kept pair before this range
+            for (uint64_t j = i; j-- > 0;)
+              if (keep[j]) {
+                prev = c1.names.data() + c1.noff[j];
+                pn = c1.noff[j + 1] - c1.noff[j];
+                break;
+              }
+          }
+          if (!prev && have_prev) {
+            prev = prev_name.data();
+            pn = prev_name.size();
+          }
+          if (prev && strnum_cmp(prev, pn, nm, nn) > 0) {
+            uint64_t w = disorder.load();
+            while (i < w && !disorder.compare_exchange_weak(w, i)) {
+            }
+            break;
+          }
+          prev = nm;
+          pn = nn;
+          const uint8_t *a = reinterpret_cast<const uint8_t *>(c1.bases.data() + c1.boff[i]);
+          const uint8_t *bb = reinterpret_cast<const uint8_t *>(c2.bases.data() + c2.boff[i]);
+          uint8_t *d = s.h + dst[i] * 2 * L;
+          for (uint32_t j = 0; j < L; ++j) d[j] = lut[a[j]];
+          for (uint32_t j = 0; j < L; ++j) d[L + j] = lut[bb[j]];
+        }
+      });
+      if (disorder.load() != ~0ull) {
+        const uint64_t i = disorder.load();
+        fail(SMASH_ERR_ARG,
+             "smash_count_fastq: pairs are not in samtools sort -n order at read " +
+                 std::string(c1.names.data() + c1.noff[i], c1.noff[i + 1] - c1.noff[i]) +
+                 " (use sort_names = 1)");
+        return;
+      }
+      for (uint64_t i = n; i-- > 0;)
+        if (keep[i]) {
+          prev_name.assign(c1.names.data() + c1.noff[i], c1.noff[i + 1] - c1.noff[i]);
+          have_prev = true;
+          break;
+        }
+      {
+        std::lock_guard<std::mutex> g(mu);
+        ingest_s += secs(t0, Clock::now());
+        s.n = k;
+        s.last = end;
+        s.state = 1;
+      }
+      cv.notify_all();
+      if (end) return;
+    }
+  }
+
+  // buffered producer: read all, order by name, stream batches
+  void produce_sorted() {
+    const uint8_t *lut = smash::ingest::lut();
+    const auto t0 = Clock::now();
+    std::vector<uint8_t> reads;        // [2 * pairs * L], converted
+    std::vector<char> names;
+    std::vector<uint64_t> noff(1, 0);
+    std::vector<uint8_t> keep;
+    for (;;) {
+      uint64_t n = 0;
+      bool end = false;
+      if (!parse(B, n, end) || !check_pairs(n, keep)) return;
+      for (uint64_t i = 0; i < n; ++i) {
+        if (!keep[i]) continue;
+        const size_t o = reads.size();
+        reads.resize(o + 2 * L);
+        const uint8_t *a = reinterpret_cast<const uint8_t *>(c1.bases.data() + c1.boff[i]);
+        const uint8_t *bb = reinterpret_cast<const uint8_t *>(c2.bases.data() + c2.boff[i]);
+        for (uint32_t j = 0; j < L; ++j) reads[o + j] = lut[a[j]];
+        for (uint32_t j = 0; j < L; ++j) reads[o + L + j] = lut[bb[j]];
+        names.insert(names.end(), c1.names.data() + c1.noff[i], c1.names.data() + c1.noff[i + 1]);
+        noff.push_back(names.size());
+      }
+      if (end) break;
+    }
+    const uint64_t np = noff.size() - 1;
+    std::vector<uint64_t> perm(np);
+    std::iota(perm.begin(), perm.end(), uint64_t(0));
+    std::stable_sort(perm.begin(), perm.end(), [&](uint64_t x, uint64_t y) {
+      return strnum_cmp(names.data() + noff[x], noff[x + 1] - noff[x], names.data() + noff[y],
+                        noff[y + 1] - noff[y]) < 0;
+    });
+    {
+      std::lock_guard<std::mutex> g(mu);
+      ingest_s += secs(t0, Clock::now());
+    }
+    for (uint64_t b = 0, q0 = 0;; ++b) {
+      Slot &s = slot[b % 3];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return s.state == 0 || err; });
+        if (err) return;
+      }
+      const auto t1 = Clock::now();
+      const uint64_t k = std::min(B, np - q0);
+      par_for(k, T, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i)
+          memcpy(s.h + i * 2 * L, reads.data() + perm[q0 + i] * 2 * L, 2 * L);
+      });
+      q0 += k;
+      const bool end = q0 >= np;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        ingest_s += secs(t1, Clock::now());
+        s.n = k;
+        s.last = end;
+        s.state = 1;
+      }
+      cv.notify_all();
+      if (end) return;
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint32_t n1,
+                                 const char *const *r2, uint32_t n2, int sort_names,
+                                 uint32_t threads, uint64_t *d_counts, smash_feed_stats *st,
+                                 void *stream) {
+  if (!p || !r1 || !r2 || n1 == 0 || n2 == 0 || !d_counts) {
+    smash::set_error("smash_count_fastq: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  const auto t_start = Clock::now();
+  auto f = std::make_unique<Feed>();
+  f->p = p;
+  f->L = smash::pipe_read_len(p);
+  f->B = smash::pipe_max_pairs(p);
+  f->T = threads ? threads : 1;
+  for (uint32_t i = 0; i < n1; ++i) f->r1.paths.emplace_back(r1[i]);
+  for (uint32_t i = 0; i < n2; ++i) f->r2.paths.emplace_back(r2[i]);
+  const uint64_t bytes = 2 * f->B * f->L;
+  SMASH_HIP(hipSetDevice(smash::pipe_device(p)));
+  hipStream_t cs = static_cast<hipStream_t>(stream), xs = nullptr;
+  uint8_t *dbuf[2] = {nullptr, nullptr};
+  hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+  int rc = SMASH_OK;
+  uint64_t pairs = 0, batches = 0;
+  double wait_s = 0;
+  std::thread prod;
+  auto cleanup = [&] {
+    if (prod.joinable()) {
+      f->fail(f->err ? f->err : SMASH_ERR_IO, f->msg.empty() ? "stopped" : f->msg);
+      prod.join();
+    }
+    if (xs) (void)hipStreamSynchronize(xs);
+    if (cs) (void)hipStreamSynchronize(cs);
+    for (int k = 0; k < 2; ++k) {
+      if (dbuf[k]) (void)hipFree(dbuf[k]);
+      if (copied[k]) (void)hipEventDestroy(copied[k]);
+      if (done[k]) (void)hipEventDestroy(done[k]);
+    }
+    for (Slot &s : f->slot)
+      if (s.h) (void)hipHostFree(s.h);
+    if (xs) (void)hipStreamDestroy(xs);
+  };
+  do {
+    if (hipStreamCreateWithFlags(&xs, hipStreamNonBlocking) != hipSuccess) {
+      rc = SMASH_ERR_HIP;
+      break;
+    }
+    bool ok = true;
+    for (int k = 0; k < 2 && ok; ++k)
+      ok = hipMalloc(&dbuf[k], bytes) == hipSuccess &&
+           hipEventCreateWithFlags(&copied[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+    for (Slot &s : f->slot)
+      ok = ok && hipHostMalloc(reinterpret_cast<void **>(&s.h), bytes, hipHostMallocDefault) == hipSuccess;
+    if (!ok) {
+      smash::set_error("smash_count_fastq: cannot allocate the batch buffers");
+      rc = SMASH_ERR_NOMEM;
+      break;
+    }
+    prod = std::thread([&] {
+      if (sort_names) f->produce_sorted();
+      else f->produce_stream();
+    });
+    for (uint64_t b = 0;; ++b) {
+      Slot &s = f->slot[b % 3];
+      const auto w0 = Clock::now();
+      {
+        std::unique_lock<std::mutex> g(f->mu);
+        f->cv.wait(g, [&] { return s.state == 1 || f->err; });
+        if (f->err) break;
+      }
+      wait_s += secs(w0, Clock::now());
+      const int d = int(b & 1);
+      if (s.n) {
+        // the copy into dbuf[d] waits for the compute that last read it
+        if (b >= 2 && hipStreamWaitEvent(xs, done[d], 0) != hipSuccess) { rc = SMASH_ERR_HIP; break; }
+        if (hipMemcpyAsync(dbuf[d], s.h, 2 * s.n * f->L, hipMemcpyHostToDevice, xs) != hipSuccess ||
+            hipEventRecord(copied[d], xs) != hipSuccess ||
+            hipStreamWaitEvent(cs, copied[d], 0) != hipSuccess) {
+          rc = SMASH_ERR_HIP;
+          break;
+        }
+        if ((rc = smash_count_batch(p, dbuf[d], s.n, d_counts, cs)) != SMASH_OK) break;
+        if (hipEventRecord(done[d], cs) != hipSuccess ||
+            hipEventSynchronize(copied[d]) != hipSuccess) {   // the pinned slot is free again
+          rc = SMASH_ERR_HIP;
+          break;
+        }
+        pairs += s.n;
+        ++batches;
+      }
+      const bool last = s.last;
+      {
+        std::lock_guard<std::mutex> g(f->mu);
+        s.state = 0;
+        s.n = 0;
+      }
+      f->cv.notify_all();
+      if (last) break;
+    }
+    if (rc == SMASH_OK && hipStreamSynchronize(cs) != hipSuccess) rc = SMASH_ERR_HIP;
+    if (prod.joinable()) prod.join();
+    if (rc == SMASH_OK && f->err) {
+      smash::set_error(f->msg);
+      rc = f->err;
+    }
+  } while (false);
+  if (rc == SMASH_ERR_HIP) smash::set_error("smash_count_fastq: HIP error");
+  cleanup();
+  if (st) {
+    st->pairs = pairs;
+    st->batches = batches;
+    st->wall_s = secs(t_start, Clock::now());
+    st->ingest_s = f->ingest_s;
+    st->wait_s = wait_s;
+    st->read_len = f->L;
+  }
+  return rc;
+}

@@ -12,8 +12,6 @@
 //    the caller's (pinned) mate matrix: mate 2q = read 1, 2q + 1 = read 2.
 //  * smash_strnum_order: the pair order of `samtools sort -n` (strnum_cmp:
 //    digit runs compare as numbers), stable, so read 1 stays before read 2.
-#include <zlib.h>
-
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -22,179 +20,19 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/smash_gpu.h"
+#include "ingest.hpp"
 
 namespace smash {
 void set_error(const std::string &msg);
 }
 using smash::set_error;
-
-namespace {
-
-struct Reader {
-  std::vector<std::string> paths;
-  size_t next_path = 0;
-  gzFile f = nullptr;
-  std::vector<char> buf = std::vector<char>(1 << 22);
-  size_t beg = 0, fill = 0;   // unread bytes buf[beg, fill)
-  std::string msg;   // error text (set_error is per thread; the caller reports it)
-
-  ~Reader() {
-    if (f) gzclose(f);
-  }
-  // refill from the current file (opening the next at EOF); false at the end
-  bool more(int &err) {
-    for (;;) {
-      if (!f) {
-        if (next_path >= paths.size()) return false;
-        f = gzopen(paths[next_path].c_str(), "rb");
-        if (!f) {
-          msg = ("cannot open " + paths[next_path]);
-          err = SMASH_ERR_IO;
-          return false;
-        }
-        gzbuffer(f, 1 << 20);
-        ++next_path;
-      }
-      if (beg) {
-        memmove(buf.data(), buf.data() + beg, fill - beg);
-        fill -= beg;
-        beg = 0;
-      }
-      if (fill == buf.size()) buf.resize(buf.size() * 2);
-      const int n = gzread(f, buf.data() + fill, unsigned(buf.size() - fill));
-      if (n < 0) {
-        msg = ("read error in " + paths[next_path - 1]);
-        err = SMASH_ERR_IO;
-        return false;
-      }
-      if (n > 0) {
-        fill += size_t(n);
-        return true;
-      }
-      gzclose(f);
-      f = nullptr;
-      // a file that does not end in '\n' ends its last line (as getline does)
-      if (fill > beg && buf[fill - 1] != '\n') {
-        if (fill == buf.size()) buf.resize(buf.size() * 2);
-        buf[fill++] = '\n';
-        return true;
-      }
-    }
-  }
-  // one line without the trailing \r\n; false at the end of the last file
-  bool line(std::string &out, int &err) {
-    out.clear();
-    size_t scan = beg;
-    for (;;) {
-      const char *nl = static_cast<const char *>(memchr(buf.data() + scan, '\n', fill - scan));
-      if (nl) {
-        size_t e = size_t(nl - buf.data());
-        out.assign(buf.data() + beg, e - beg);
-        beg = e + 1;
-        while (!out.empty() && out.back() == '\r') out.pop_back();
-        return true;
-      }
-      scan = fill - beg;   // offset after the memmove in more()
-      if (!more(err)) {
-        if (fill > beg) {   // unreachable: more() terminates a last line
-          out.assign(buf.data() + beg, fill - beg);
-          beg = fill;
-          return true;
-        }
-        return false;
-      }
-    }
-  }
-  // fastqs_to_sam record: name, bases; false at the end
-  bool record(std::string &name, std::string &bases, int &err) {
-    std::string l;
-    for (;;) {
-      if (!line(l, err)) return false;
-      size_t b = 0, e = l.size();
-      while (b < e && isspace(uint8_t(l[b]))) ++b;
-      while (e > b && isspace(uint8_t(l[e - 1]))) --e;
-      if (b == e) continue;
-      const char mark = l[b];
-      if (mark != '@' && mark != '>') {
-        msg = ("Fastq @ parse error: " + l.substr(0, 40));
-        err = SMASH_ERR_IO;
-        return false;
-      }
-      size_t t = b + 1;
-      while (t < e && isspace(uint8_t(l[t]))) ++t;
-      size_t te = t;
-      while (te < e && !isspace(uint8_t(l[te]))) ++te;
-      if (t == te) {
-        msg = ("Problem reading read name");
-        err = SMASH_ERR_IO;
-        return false;
-      }
-      name.assign(l, t, te - t);
-      if (!line(bases, err)) bases.clear();
-      if (err) return false;
-      if (mark == '@') {
-        std::string plus, qual;
-        if (!line(plus, err) || plus.find_first_not_of(" \t") == std::string::npos ||
-            plus[plus.find_first_not_of(" \t")] != '+') {
-          if (!err) {
-            msg = ("Fastq + parse error");
-            err = SMASH_ERR_IO;
-          }
-          return false;
-        }
-        line(qual, err);
-        if (err) return false;
-      }
-      return true;
-    }
-  }
-};
-
-// samtools sort -n (bam_sort.c strnum_cmp; samtools is absent from the
-// reference and unpinned: this follows samtools 1.x): bytes compare one by
-// one; where both sides are at a digit, leading zeros are skipped, matching
-// digits walked, and the longer digit run wins, else the first differing
-// digit; a non-digit on either side compares the two bytes.  Names are
-// NUL-terminated within their n bytes.
-int strnum_cmp(const char *a, size_t na, const char *b, size_t nb) {
-  auto at = [](const char *s, size_t n, size_t i) -> int {
-    return i < n ? static_cast<unsigned char>(s[i]) : 0;
-  };
-  auto isd = [](int c) { return c >= '0' && c <= '9'; };
-  size_t i = 0, j = 0;
-  while (at(a, na, i) && at(b, nb, j)) {
-    const int ca = at(a, na, i), cb = at(b, nb, j);
-    if (!isd(ca) || !isd(cb)) {
-      if (ca != cb) return ca - cb;
-      ++i;
-      ++j;
-    } else {
-      while (at(a, na, i) == '0') ++i;
-      while (at(b, nb, j) == '0') ++j;
-      while (isd(at(a, na, i)) && at(a, na, i) == at(b, nb, j)) ++i, ++j;
-      const int diff = at(a, na, i) - at(b, nb, j);
-      while (isd(at(a, na, i)) && isd(at(b, nb, j))) ++i, ++j;
-      if (isd(at(a, na, i))) return 1;
-      if (isd(at(b, nb, j))) return -1;
-      if (diff) return diff;
-    }
-  }
-  return at(a, na, i) ? 1 : at(b, nb, j) ? -1 : 0;
-}
-
-uint8_t g_lut[256];
-struct LutInit {
-  LutInit() {
-    for (int c = 0; c < 256; ++c) g_lut[c] = uint8_t(c >= 'A' && c <= 'Z' ? c + 32 : c);
-    g_lut[uint8_t('N')] = uint8_t('z');   // replaceN, then lowercase
-  }
-} g_lut_init;
-
-}  // namespace
+using smash::ingest::Chunk;
+using smash::ingest::Reader;
+using smash::ingest::strnum_cmp;
 
 struct smash_fastq {
   Reader r1, r2;
+  Chunk c1, c2;   // parse buffers, reused
   uint32_t L = 0;
   bool done = false;
 };
@@ -212,34 +50,6 @@ extern "C" int smash_fastq_open(const char *const *r1, uint32_t n1, const char *
   return SMASH_OK;
 }
 
-namespace {
-// up to `want` records of one mate list: names (read 1 only) and bases, flat
-struct Chunk {
-  std::vector<char> bases, names;
-  std::vector<uint64_t> boff, noff;   // n + 1 offsets each
-  bool end = false;
-  int err = 0;
-  void parse(Reader &r, uint64_t want, bool keep_names) {
-    bases.clear();
-    names.clear();
-    boff.assign(1, 0);
-    noff.assign(1, 0);
-    end = false;
-    std::string nm, b;
-    for (uint64_t i = 0; i < want; ++i) {
-      if (!r.record(nm, b, err)) {
-        end = true;
-        return;
-      }
-      bases.insert(bases.end(), b.begin(), b.end());
-      boff.push_back(bases.size());
-      if (keep_names) names.insert(names.end(), nm.begin(), nm.end());
-      noff.push_back(names.size());
-    }
-  }
-  uint64_t size() const { return boff.size() - 1; }
-};
-}  // namespace
 
 extern "C" int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *len,
                                 uint8_t *h_reads, char *h_names, uint32_t name_stride,
@@ -250,7 +60,8 @@ extern "C" int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *le
   }
   *n_pairs = 0;
   uint64_t q = 0;
-  Chunk c1, c2;
+  Chunk &c1 = f->c1, &c2 = f->c2;
+  const uint8_t *lut = smash::ingest::lut();
   // the two mate lists are parsed (and inflated) on two threads, then zipped
   while (q < max_pairs && !f->done) {
     const uint64_t want = max_pairs - q;
@@ -288,8 +99,8 @@ extern "C" int smash_fastq_read(smash_fastq *f, uint64_t max_pairs, uint32_t *le
       }
       const char *a = c1.bases.data() + c1.boff[i], *b = c2.bases.data() + c2.boff[i];
       uint8_t *d = h_reads + q * 2 * *len;
-      for (uint32_t j = 0; j < *len; ++j) d[j] = g_lut[uint8_t(a[j])];
-      for (uint32_t j = 0; j < *len; ++j) d[*len + j] = g_lut[uint8_t(b[j])];
+      for (uint32_t j = 0; j < *len; ++j) d[j] = lut[uint8_t(a[j])];
+      for (uint32_t j = 0; j < *len; ++j) d[*len + j] = lut[uint8_t(b[j])];
       if (h_names) {
         if (na.size() >= name_stride) {
           set_error("smash_fastq_read: read name longer than name_stride - 1: " + na);

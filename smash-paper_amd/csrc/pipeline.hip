@@ -910,6 +910,12 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
   return SMASH_OK;
 }
 
+namespace smash {
+uint32_t pipe_read_len(const smash_pipeline *p) { return p->read_len; }
+uint64_t pipe_max_pairs(const smash_pipeline *p) { return p->max_pairs; }
+int pipe_device(const smash_pipeline *p) { return p->device; }
+}  // namespace smash
+
 extern "C" void smash_pipeline_free(smash_pipeline *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);

@@ -49,6 +49,7 @@ EXPORTS = [
     "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
+    "smash_count_fastq",
 ]
 
 
@@ -69,6 +70,14 @@ class PipelineCfg(C.Structure):
                 ("h_chrom_off", i64p), ("nbins", C.c_uint32),
                 ("h_bin_starts", i64p), ("min_excess", C.c_int32),
                 ("hit_window", C.c_int64), ("dedup_capacity", C.c_uint64)]
+
+
+class FeedStats(C.Structure):
+    _fields_ = [("pairs", C.c_uint64), ("batches", C.c_uint64), ("wall_s", C.c_double),
+                ("ingest_s", C.c_double), ("wait_s", C.c_double), ("read_len", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class Stats(C.Structure):
@@ -149,6 +158,9 @@ def lib():
     L.smash_fastq_close.argtypes = [vp]
     L.smash_fastq_close.restype = None
     L.smash_strnum_order.argtypes = [vp, C.c_uint32, C.c_uint64, u64p]
+    L.smash_count_fastq.argtypes = [vp, C.POINTER(C.c_char_p), C.c_uint32,
+                                    C.POINTER(C.c_char_p), C.c_uint32, C.c_int, C.c_uint32, vp,
+                                    C.POINTER(FeedStats), vp]
     _LIB = L
     return L
 
@@ -364,6 +376,21 @@ class Pipeline:
         """d_reads: device uint8 [2*n_pairs, read_len] (torch tensor or ptr)."""
         check(lib().smash_count_batch(self.h, _ptr(d_reads), n_pairs, _ptr(d_counts),
                                       vp(_stream(stream))), "smash_count_batch")
+
+    def count_fastq(self, r1_paths, r2_paths, d_counts, sort_names=True, threads=0,
+                    stream=None):
+        """File-fed counting (smash_count_fastq): the two mate lists parsed,
+        batched in pinned memory, copied and counted with overlap.
+        sort_names=False: the input is in samtools sort -n order already.
+        Returns the feed statistics (pairs, batches, wall_s, ingest_s, wait_s)."""
+        arr1 = _cstrs([os.fsencode(x) for x in r1_paths])
+        arr2 = _cstrs([os.fsencode(x) for x in r2_paths])
+        st = FeedStats()
+        T = threads or min(16, os.cpu_count() or 1)
+        check(lib().smash_count_fastq(self.h, arr1, len(r1_paths), arr2, len(r2_paths),
+                                      int(bool(sort_names)), T, _ptr(d_counts), C.byref(st),
+                                      vp(_stream(stream))), "smash_count_fastq")
+        return st.as_dict()
 
     def phase_map(self, d_reads, n_pairs, stream=None):
         check(lib().smash_phase_map(self.h, _ptr(d_reads), n_pairs, vp(_stream(stream))),

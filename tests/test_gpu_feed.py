@@ -1,0 +1,127 @@
+"""File-fed counting (smash_count_fastq, csrc/feed.hip): FASTQ lists ->
+pinned batches -> H2D -> count, overlapped.  Its counts and statistics must
+equal the batch path (smash_fastq_read + samtools sort -n order +
+smash_count_batch) on the same pairs, for gzip and plain input, one and many
+batches, input in name order (streamed) and not (buffered + ordered); and it
+must refuse what the batch path refuses."""
+import gzip
+
+import numpy as np
+import pytest
+
+from conftest import gold, load_bins, load_chrom_sizes
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+import smashgpu as S  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def gix(tiny_fa):
+    return S.Index.from_fasta(tiny_fa)
+
+
+@pytest.fixture(scope="module")
+def setup():
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    return cs, starts
+
+
+def _batch_path(gix, cs, starts, names, reads, batch):
+    """smash_cli's batch path: samtools sort -n order, smash_count_batch."""
+    order = S.strnum_order(names)
+    n = len(names)
+    reads = reads.reshape(n, -1)[order].reshape(2 * n, -1)
+    pipe = S.Pipeline(gix, cs, starts, reads.shape[1], batch, dedup_capacity=n)
+    pipe.reset()
+    c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    for b0 in range(0, n, batch):
+        b1 = min(n, b0 + batch)
+        pipe.count_batch(torch.from_numpy(np.ascontiguousarray(reads[2 * b0:2 * b1])).cuda(),
+                         b1 - b0, c)
+    st = pipe.stats()
+    return c.cpu().numpy().tolist(), (st.pairs, st.key_pairs, st.dupe_pairs, st.positions,
+                                      st.dups, st.kept)
+
+
+def _feed_path(gix, cs, starts, r1, r2, L, batch, sort_names, n):
+    pipe = S.Pipeline(gix, cs, starts, L, batch, dedup_capacity=n)
+    pipe.reset()
+    c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    fs = pipe.count_fastq(r1, r2, c, sort_names=sort_names, threads=3)
+    st = pipe.stats()
+    return c.cpu().numpy().tolist(), (st.pairs, st.key_pairs, st.dupe_pairs, st.positions,
+                                      st.dups, st.kept), fs
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+@pytest.mark.parametrize("batch", [5000, 37])
+def test_feed_sorted_equals_batch_path(gix, setup, s, batch):
+    """sort_names=1 reads every pair, orders them and streams the batches
+    (gzip input)."""
+    cs, starts = setup
+    r1, r2 = [gold("%s_r1.fq.gz" % s)], [gold("%s_r2.fq.gz" % s)]
+    names, reads = S.read_fastq_pairs(r1, r2)
+    exp = _batch_path(gix, cs, starts, names, reads, batch)
+    got_c, got_s, fs = _feed_path(gix, cs, starts, r1, r2, reads.shape[1], batch, True,
+                                  len(names))
+    assert (got_c, got_s) == exp
+    assert fs["pairs"] == len(names)
+    assert fs["batches"] == -(-len(names) // batch)
+
+
+@pytest.mark.parametrize("gz", [False, True])
+def test_feed_streams_input_in_name_order(gix, setup, tmp_path, gz):
+    """Pairs rewritten in name order (tools/readgen.py write_fastq): the
+    streaming mode (sort_names=0) over many small batches, so the two device
+    buffers and three pinned slots cycle."""
+    import readgen
+    cs, starts = setup
+    names, reads = S.read_fastq_pairs([gold("s100_r1.fq.gz")], [gold("s100_r2.fq.gz")])
+    n = len(names)
+    order = S.strnum_order(names)
+    srt = reads.reshape(n, -1)[order].reshape(2 * n, -1)
+    ext = ".fq.gz" if gz else ".fq"
+    p1, p2 = str(tmp_path / ("a" + ext)), str(tmp_path / ("b" + ext))
+    readgen.write_fastq(srt, p1, p2, gz=gz)
+    new_names = np.array([b"r%012d/1" % i for i in range(n)], "S16")
+    exp = _batch_path(gix, cs, starts, new_names, srt, 29)
+    got_c, got_s, fs = _feed_path(gix, cs, starts, [p1], [p2], srt.shape[1], 29, False, n)
+    assert (got_c, got_s) == exp
+    assert fs["batches"] == -(-n // 29)
+
+
+def test_feed_refuses_unsorted_stream_and_bad_lengths(gix, setup, tmp_path):
+    cs, starts = setup
+    r1, r2 = [gold("s100_r1.fq.gz")], [gold("s100_r2.fq.gz")]
+    names, reads = S.read_fastq_pairs(r1, r2)
+    # the first 200 pairs with names in descending order: r10 > r9 numerically
+    u1, u2 = tmp_path / "u1.fq", tmp_path / "u2.fq"
+    for path, mate in ((u1, 0), (u2, 1)):
+        path.write_bytes(b"".join(b"@r%d\n%s\n+\n%s\n" % (
+            200 - q, bytes(reads[2 * q + mate]).upper().replace(b"Z", b"N"),
+            b"I" * reads.shape[1]) for q in range(200)))
+    pipe = S.Pipeline(gix, cs, starts, reads.shape[1], 64, dedup_capacity=len(names))
+    c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    with pytest.raises(S.SmashError, match="sort -n order"):
+        pipe.count_fastq([str(u1)], [str(u2)], c, sort_names=False)
+    # ordered (sort_names=1), the same pairs count as the batch path does
+    exp = _batch_path(gix, cs, starts, np.array([b"r%d" % (200 - q) for q in range(200)], "S8"),
+                      reads[:400], 64)
+    got_c, got_s, _ = _feed_path(gix, cs, starts, [str(u1)], [str(u2)], reads.shape[1], 64,
+                                 True, 200)
+    assert (got_c, got_s) == exp
+    pipe2 = S.Pipeline(gix, cs, starts, reads.shape[1] + 1, 64, dedup_capacity=len(names))
+    with pytest.raises(S.SmashError, match="read length"):
+        pipe2.count_fastq(r1, r2, c, sort_names=True)
+    a, b = tmp_path / "a.fq", tmp_path / "b.fq"
+    a.write_bytes(b"@p1\n" + b"A" * reads.shape[1] + b"\n+\n\n@p2\n\n+\n\n")
+    b.write_bytes(b"@p1\n" + b"C" * reads.shape[1] + b"\n+\n\n@p2\n" + b"C" * reads.shape[1] +
+                  b"\n+\n\n")
+    with pytest.raises(S.SmashError, match="no bases"):
+        pipe.count_fastq([str(a)], [str(b)], c, sort_names=True)
+    with pytest.raises(S.SmashError, match="cannot open"):
+        pipe.count_fastq(["/nonexistent.fq"], r2, c)
+    with gzip.open(gold("s100_r1.fq.gz")) as f:
+        assert f.read(1) == b"@"

@@ -12,8 +12,12 @@
 // makes every pair independent of the batch split: pair q is the same bytes
 // whether generated alone or in a batch of 25 M.
 #include <hip/hip_runtime.h>
+#include <zlib.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
 
 namespace {
 
@@ -88,3 +92,47 @@ extern "C" int rg_generate(const uint8_t *d_text, const void *d_iv, const uint64
 }
 
 extern "C" uint32_t rg_iv_bytes(void) { return sizeof(Iv); }
+
+// Host side: pairs [0, n_pairs) of h_reads (prepared bytes, as rg_generate
+// writes them) as two FASTQ files (read 1, read 2) with names r<q0 + i>
+// zero-padded to 12 digits (already in samtools sort -n order), bases upper
+// case with 'z' -> 'N' (what ingest's replaceN + lowercasing turns back into
+// the same bytes), qualities 'I'.  gz: gzip level 1, else plain.  0 = ok.
+extern "C" int rg_write_fastq(const uint8_t *h_reads, uint64_t n_pairs, uint32_t L, uint64_t q0,
+                              const char *path1, const char *path2, int gz) {
+  const char *paths[2] = {path1, path2};
+  for (int mate = 0; mate < 2; ++mate) {
+    std::vector<char> out;
+    out.reserve(size_t(n_pairs) * (2 * L + 24));
+    char head[40];
+    for (uint64_t i = 0; i < n_pairs; ++i) {
+      const int h = snprintf(head, sizeof(head), "@r%012llu/%d\n", (unsigned long long)(q0 + i),
+                             mate + 1);
+      out.insert(out.end(), head, head + h);
+      const uint8_t *r = h_reads + (2 * i + mate) * L;
+      for (uint32_t j = 0; j < L; ++j) out.push_back(r[j] == 'z' ? 'N' : char(r[j] - 32));
+      out.push_back('\n');
+      out.push_back('+');
+      out.push_back('\n');
+      out.insert(out.end(), L, 'I');
+      out.push_back('\n');
+    }
+    if (gz) {
+      gzFile f = gzopen(paths[mate], "wb1");
+      if (!f) return 1;
+      size_t o = 0;
+      while (o < out.size()) {
+        const unsigned k = unsigned(std::min<size_t>(out.size() - o, size_t(1) << 30));
+        if (gzwrite(f, out.data() + o, k) != int(k)) { gzclose(f); return 2; }
+        o += k;
+      }
+      if (gzclose(f) != Z_OK) return 3;
+    } else {
+      FILE *f = fopen(paths[mate], "wb");
+      if (!f) return 1;
+      const bool ok = fwrite(out.data(), 1, out.size(), f) == out.size();
+      if (fclose(f) != 0 || !ok) return 2;
+    }
+  }
+  return 0;
+}

@@ -26,6 +26,8 @@ def lib():
         L.rg_generate.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                                   C.c_uint64, C.c_uint32, vp, vp]
         L.rg_iv_bytes.restype = C.c_uint32
+        L.rg_write_fastq.argtypes = [vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_char_p,
+                                     C.c_char_p, C.c_int]
         _LIB = L
     return _LIB
 
@@ -65,6 +67,17 @@ class Generator:
         if rc:
             raise RuntimeError("rg_generate: hip error %d" % rc)
         return out
+
+
+def write_fastq(h_reads, path1, path2, gz=False, q0=0):
+    """pairs of h_reads (numpy uint8 [2n, L], prepared bytes) as a FASTQ pair
+    of files in name order (rg_write_fastq)."""
+    h = np.ascontiguousarray(h_reads)
+    n, L = h.shape[0] // 2, h.shape[1]
+    rc = lib().rg_write_fastq(h.ctypes.data, n, L, q0, os.fsencode(path1), os.fsencode(path2),
+                              int(gz))
+    if rc:
+        raise RuntimeError("rg_write_fastq failed (%d)" % rc)
 
 
 def S_startpos(index):
