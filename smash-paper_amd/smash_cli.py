@@ -291,8 +291,34 @@ def cmd_map(args):
         o.write("%d dupes\t%d non-dupes\n" % (st.dupe_pairs, st.key_pairs - st.dupe_pairs))
 
 
+def _count_files(args, bins):
+    """count from the FASTQ lists through the file-fed pipeline
+    (smash_count_fastq: parse / H2D / compute overlapped, pairs ordered by
+    name first unless --presorted)"""
+    import torch
+    ref = _ref(args)
+    ix = load_index(ref, args.device)
+    cs = S.read_chrom_sizes(args.chrom_sizes or ref + ".bin/chrom_sizes.txt")
+    rows, starts = S.read_bins(bins)
+    r1, r2 = args.reads1.split(), args.reads2.split()
+    L = S.first_read_length(r1)
+    pipe = S.Pipeline(ix, cs, starts, L, args.batch, dedup_capacity=args.dedup_capacity)
+    counts = torch.zeros(len(starts), dtype=torch.int64, device=torch.device("cuda", args.device))
+    pipe.reset()
+    pipe.count_fastq(r1, r2, counts, sort_names=not args.presorted)
+    st = pipe.stats()
+    if st.error:
+        raise SystemExit("mappability_tag: %s" % S.ERRORS.get(st.error, st.error))
+    return rows, counts.cpu().numpy(), st
+
+
 def cmd_count(args):
     bins = os.path.join(args.bindir, "bins.txt")
+    if not args.sam and args.reads1:
+        rows, counts, st = _count_files(args, bins)
+        write_varbin(rows, counts, st.positions, st.dups, st.kept,
+                     args.out or args.id + ".varbin.txt", args.id + ".stats.txt")
+        return
     run = _Run(args, bins)
     counts, st = run.run(lambda pipe: None)
     write_varbin(run.bins_rows, counts, st.positions, st.dups, st.kept,
@@ -477,6 +503,11 @@ def main(argv=None):
         p.add_argument("--sam", default=None, help="unmapped SAM input instead (mummer -samin)")
         p.add_argument("--chrom-sizes", default=None)
         p.add_argument("--batch", type=int, default=2_000_000, help="pairs per device batch")
+        if name == "count":
+            p.add_argument("--presorted", action="store_true",
+                           help="FASTQ pairs already in samtools sort -n order: stream them")
+            p.add_argument("--dedup-capacity", type=int, default=1 << 24,
+                           help="distinct pair keys the de-dup set holds")
         p.set_defaults(fn=fn)
     p = sub.add_parser("varbin")
     for a in ("positions", "bins", "out", "stats", "chrom_sizes"):

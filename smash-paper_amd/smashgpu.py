@@ -682,6 +682,24 @@ def read_fastq_pairs(r1_paths, r2_paths, batch_pairs=1 << 20, name_stride=64):
     return np.concatenate(names), np.concatenate(reads)
 
 
+def first_read_length(paths):
+    """bases in the first record of the first file (FASTQ / FASTA, gzip or
+    plain): the read length a file-fed pipeline is built for."""
+    import gzip
+    with open(paths[0], "rb") as f:
+        magic = f.read(2)
+    op = gzip.open if magic == b"\x1f\x8b" else open
+    with op(paths[0], "rb") as f:
+        for line in f:
+            t = line.strip()
+            if not t:
+                continue
+            if t[:1] not in (b"@", b">"):
+                raise SmashError("%s: not FASTQ / FASTA" % paths[0])
+            return len(next(f).rstrip(b"\r\n"))
+    raise SmashError("%s: no records" % paths[0])
+
+
 def strnum_order(names):
     """Stable `samtools sort -n` order of a fixed-width bytes array
     (smash_strnum_order)."""

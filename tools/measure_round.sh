@@ -13,9 +13,9 @@ mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 python3 "$R/bench.py" > "$O/bench.json" 2> "$O/bench.log"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv \
-    -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$O/prof.log" 2>&1
+    -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-feed --no-c5 > "$O/prof.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_mam_sm -d "$O/pmc" -o pmc \
-    --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline \
+    --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-feed --no-c5 \
     > "$O/pmc.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$O/calib" -o pmc --output-format csv \
     -- "$R/tools/randbench" calib > "$O/calib.log" 2>&1

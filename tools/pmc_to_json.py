@@ -29,8 +29,14 @@ def main(mdir, pdir, config="c3"):
     per_probe = ckb * 1024 / loads
     scale = 64.0 / per_probe
     bench = json.load(open(os.path.join(mdir, "bench.json")))
+    # the counted dispatch is the step's last batch: P - (nb - 1) * B pairs
+    cfg = bench["config"]
+    P, B, nb = cfg["pairs_per_rank"], cfg["batch_pairs"], cfg["batches_per_step"]
+    reads_last = 2 * (P - (nb - 1) * B)
     out = {
         "k_mam_bytes_per_launch": int(round(kb * 1024 * scale)),
+        "k_mam_bytes_per_read": round(kb * 1024 * scale / reads_last, 1),
+        "reads_counted_dispatch": reads_last,
         "kernel": name.split("(")[0].replace("void smash::sm::", ""),
         "reads_per_launch": bench["roofline"]["reads_per_launch"],
         "fetch_size_kb": kb,

@@ -14,5 +14,5 @@ for SET in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   i=$((i+1))
   timeout -k 10 420 rocprofv3 --pmc $SET --kernel-include-regex k_mam -d "$R/$OUT/p$i" -o pmc \
       --output-format csv -- python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 \
-      --no-cpu-baseline > "$R/$OUT/p$i.json" 2> "$R/$OUT/p$i.log"
+      --no-cpu-baseline --no-feed --no-c5 > "$R/$OUT/p$i.json" 2> "$R/$OUT/p$i.log"
 done
