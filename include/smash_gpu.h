@@ -202,6 +202,13 @@ void smash_pipeline_free(smash_pipeline *p);
  * d_counts[nbins] (u64).  Asynchronous on `stream`. */
 int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
                       uint64_t n_pairs, uint64_t *d_counts, void *stream);
+/* n_pairs resident pairs in batches of batch_pairs (<= cfg.max_pairs), the
+ * same chain and result as smash_count_batch per batch in order; the search
+ * of each batch runs on one of two pipeline streams, so batch b + 1's search
+ * starts under the tail of batch b's.  Asynchronous on `stream` (every batch's
+ * reads must be ready by the work already on `stream`). */
+int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                        uint64_t batch_pairs, uint64_t *d_counts, void *stream);
 
 /* Multi-GPU phases (one rank per GPU; the caller runs the collectives):
  *  1. smash_phase_map      -- map/resolve/tag/filter/hash + in-batch first-wins
@@ -262,6 +269,10 @@ int smash_pipeline_stats(smash_pipeline *p, smash_stats *out);
 int smash_pipeline_profile(smash_pipeline *p, int enable);
 int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
                                 uint64_t *launches, uint64_t *reads);
+/* The time at least one profiled search launch was running (the union of
+ * the launches' event intervals; launches on the two search streams of
+ * smash_count_batches overlap).  Synchronises. */
+int smash_pipeline_profile_active(smash_pipeline *p, double *active_ms);
 
 /* Start a new run: clears the pair-key set, the carried adjacent-dup state
  * and the stats (a fresh smashMEM.py + varbin.py invocation). */

@@ -117,10 +117,24 @@ void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // ma
 void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
 // mam.hip: smash_map_batch without the per-launch synchronisation of the
 // probe check (sync_check = false: the caller runs probe_check later)
+// caller-owned search workspace (the pipeline's double-buffered sets): the
+// read records and the work counter of one k_mam_sm launch, so two launches
+// on different streams can run at once; null: the index's own
+struct SearchWs {
+  uint8_t *rec = nullptr;
+  uint64_t rec_bytes = 0;
+  unsigned long long *work = nullptr;
+};
 int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
                    uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
                    uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out, void *stream,
-                   bool sync_check);
+                   bool sync_check, const SearchWs *ws = nullptr);
+// record bytes of n reads of up to max_len bases (k_prep)
+uint64_t search_rec_bytes(uint64_t n_reads, uint32_t max_len);
+// one pipeline batch whose search waits for in_ev (null: for all earlier
+// work on s) instead of for everything on s (pipeline.hip)
+int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                   uint64_t *d_counts, hipStream_t s, hipEvent_t in_ev);
 int probe_check(const smash_index *ix);   // synchronous; SMASH_OK or the probe error
 // mem.hip: smash_map_batch's MUM mode (MAM, then cleanMUMcand per read)
 int map_batch_mum(const smash_index *ix, uint32_t min_len, const uint8_t *seqs, uint64_t stride,

@@ -368,12 +368,14 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
         // the copy into dbuf[d] waits for the compute that last read it
         if (b >= 2 && hipStreamWaitEvent(xs, done[d], 0) != hipSuccess) { rc = SMASH_ERR_HIP; break; }
         if (hipMemcpyAsync(dbuf[d], s.h, 2 * s.n * f->L, hipMemcpyHostToDevice, xs) != hipSuccess ||
-            hipEventRecord(copied[d], xs) != hipSuccess ||
-            hipStreamWaitEvent(cs, copied[d], 0) != hipSuccess) {
+            hipEventRecord(copied[d], xs) != hipSuccess) {
           rc = SMASH_ERR_HIP;
           break;
         }
-        if ((rc = smash_count_batch(p, dbuf[d], s.n, d_counts, cs)) != SMASH_OK) break;
+        // the batch's search waits for its copy only (not for the previous
+        // batch's post stage on cs): it can start under that batch's search
+        if ((rc = smash::count_batch_ev(p, dbuf[d], s.n, d_counts, cs, copied[d])) != SMASH_OK)
+          break;
         if (hipEventRecord(done[d], cs) != hipSuccess ||
             hipEventSynchronize(copied[d]) != hipSuccess) {   // the pinned slot is free again
           rc = SMASH_ERR_HIP;

@@ -93,14 +93,14 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   std::vector<uint32_t> h_iters;
   if (STATS) {
     SMASH_HIP(hipMalloc(&c.iters, n_reads * sizeof(uint32_t)));
-    SMASH_HIP(hipMalloc(&c.wave_stats, 64 * 8));
-    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 64 * 8, s));
+    SMASH_HIP(hipMalloc(&c.wave_stats, 128 * 8));
+    SMASH_HIP(hipMemsetAsync(c.wave_stats, 0, 128 * 8, s));
   }
   // d_work[1..10]: sticky probe-check record (zeroed at index creation,
   // never reset): the pipeline reads it at stats time, so a batch does not
   // synchronise the stream (smash::probe_check)
   c.viol = reinterpret_cast<unsigned long long *>(ix->d_work) + 1;
-  SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
+  SMASH_HIP(hipMemsetAsync(c.work, 0, 8, s));
   if (ix->kev[0]) SMASH_HIP(hipEventRecord(ix->kev[0], s));
   kern<<<unsigned(blocks), B, lds, s>>>(c);
   SMASH_HIP(hipGetLastError());
@@ -111,9 +111,9 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   }
   if (STATS) {
     std::vector<uint32_t> hv(n_reads);
-    unsigned long long ws[64];
+    unsigned long long ws[128];
     SMASH_HIP(hipMemcpy(hv.data(), c.iters, n_reads * 4, hipMemcpyDeviceToHost));
-    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 64 * 8, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipMemcpy(ws, c.wave_stats, 128 * 8, hipMemcpyDeviceToHost));
     SMASH_HIP(hipFree(c.iters));
     SMASH_HIP(hipFree(c.wave_stats));
     std::vector<uint32_t> srt(hv);
@@ -142,6 +142,17 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
     for (int k = 0; k < 2; ++k)
       if (ws[42 + k]) std::fprintf(stderr, " CMP.%s %.1f", k ? "SCAN" : "EXT", double(ws[42 + k]) / n_reads);
     std::fprintf(stderr, "\n");
+    // SM_REGION counters: share of wave iterations each code region ran in
+    static const char *regions[] = {
+        "consume", "S_ALU", "S_COPY", "S_BM", "S_KT", "S_IDX", "S_BYTE", "S_CMP", "S_USCAN",
+        "S_EX", "A_BS", "A_BS_DONE", "A_XL_DONE", "A_RUN_DONE", "A_CHAIN_DONE", "A_EXPAND",
+        "A_AFTER", "A_TOP", "A_TRAV", "A_DONE", "TOP.!clean", "TOP.codes1", "TOP.codes2",
+        "TOP.kt", "TOP.filter", "-", "dma"};
+    std::fprintf(stderr, "[k_mam_sm] wave iterations running each region (%%):");
+    for (int k = 0; k < 27; ++k)
+      if (ws[64 + k])
+        std::fprintf(stderr, " %s %.1f", regions[k], 100.0 * double(ws[64 + k]) / double(ws[0] ? ws[0] : 1));
+    std::fprintf(stderr, "\n");
   }
   return SMASH_OK;
 }
@@ -150,12 +161,17 @@ template <class IdxT>
 int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
               uint64_t stride, const uint16_t *lens, uint32_t len,
               uint64_t n_reads, uint64_t *out, uint32_t cap, uint32_t *n_out,
-              hipStream_t s, bool sync_check) {
+              hipStream_t s, bool sync_check, const SearchWs *ws) {
   constexpr int B = kSmBlock;
   const sm::Geom g = sm::make_geom(lens ? 255 : len);
-  // read records (k_prep)
+  // read records (k_prep): the caller's workspace, else the index's buffer
   const uint64_t need = n_reads * g.chunks * 16;
-  if (need > ix->rec_bytes) {
+  uint32_t *rec = ws ? reinterpret_cast<uint32_t *>(ws->rec) : nullptr;
+  if (ws && need > ws->rec_bytes) {
+    set_error("k_mam_sm: search workspace too small");
+    return SMASH_ERR_ARG;
+  }
+  if (!ws && need > ix->rec_bytes) {
     SMASH_HIP(hipStreamSynchronize(s));
     if (ix->d_rec) SMASH_HIP(hipFree(ix->d_rec));
     ix->d_rec = nullptr;
@@ -164,12 +180,13 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
     SMASH_HIP(hipMalloc(&ix->d_rec, bytes));
     ix->rec_bytes = bytes;
   }
+  if (!ws) rec = ix->d_rec;
   {
     const uint32_t per = sm::prep_per_block(g, stride);
     const size_t plds = sm::prep_lds_bytes(g, stride, per);
     sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
         seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
-        ix->in_text[3], g, per, ix->d_rec);
+        ix->in_text[3], g, per, rec);
     SMASH_HIP(hipGetLastError());
   }
   sm::Ctx<IdxT> c;
@@ -177,7 +194,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.T = x.T; c.SA = x.SA; c.ISA = x.ISA; c.L8 = x.L8; c.U = x.U; c.KT = x.KT; c.BM = x.BM;
   c.N = x.N; c.logN = uint32_t(x.logN); c.K = uint32_t(x.K); c.B = uint32_t(x.B);
   c.min_len = min_len;
-  c.rec = reinterpret_cast<const uint4 *>(ix->d_rec);
+  c.rec = reinterpret_cast<const uint4 *>(rec);
   c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
   c.lin_blocks = 8;
   c.pad = 0;
@@ -189,7 +206,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   if (const char *e = std::getenv("SMASH_SM_LIN")) c.lin_blocks = uint32_t(std::max(1, std::atoi(e)));
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
   c.out = out; c.n_out = n_out;
-  c.work = reinterpret_cast<unsigned long long *>(ix->d_work);
+  c.work = ws ? ws->work : reinterpret_cast<unsigned long long *>(ix->d_work);
   for (int k = 0; k < 4; ++k) c.in_text[k] = ix->in_text[k];
   c.iters = nullptr;
   c.wave_stats = nullptr;
@@ -203,7 +220,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
         {reinterpret_cast<uint64_t>(ix->d_uniq), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_kmer), 16ull << (2 * ix->kmer_k)},
         {reinterpret_cast<uint64_t>(ix->d_bitmap), 8 * (((1ull << (2 * ix->bitmap_b)) >> 6) + 1)},
-        {reinterpret_cast<uint64_t>(ix->d_rec), n_reads * g.chunks * 16}};
+        {reinterpret_cast<uint64_t>(rec), n_reads * g.chunks * 16}};
     c.lo = ~0ull; c.hi = 0;
     for (int k = 0; k < 8; ++k) {
       c.lo = std::min<uint64_t>(c.lo, spans[k][0]);
@@ -272,10 +289,14 @@ int probe_check(const smash_index *ix) {
   return SMASH_ERR_HIP;
 }
 
+uint64_t search_rec_bytes(uint64_t n_reads, uint32_t max_len) {
+  return n_reads * sm::make_geom(max_len).chunks * 16;
+}
+
 int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
                    uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
                    uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out, void *stream,
-                   bool sync_check) {
+                   bool sync_check, const SearchWs *ws) {
   if (!ix || !d_seqs || !d_out || !d_n_out || cap_per_read == 0) {
     set_error("smash_map_batch: bad arguments");
     return SMASH_ERR_ARG;
@@ -314,9 +335,9 @@ int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint
   if (!plain && !use_direct()) {
     if (ix->idx_bytes == 4)
       return launch_sm<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
-                                 cap_per_read, d_n_out, s, sync_check);
+                                 cap_per_read, d_n_out, s, sync_check, ws);
     return launch_sm<uint64_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
-                               cap_per_read, d_n_out, s, sync_check);
+                               cap_per_read, d_n_out, s, sync_check, ws);
   }
   if (ix->idx_bytes == 4)
     return plain ? launch<uint32_t, true>(ix, min_len, d_seqs, stride, d_lens, len, n_reads,

@@ -52,6 +52,17 @@
 #ifndef SM_HOOK_PF
 #define SM_HOOK_PF(a)
 #endif
+// STATS builds: count the wave iterations in which a code region runs (any
+// lane active in it), wave_stats[64 + k]; the regions' costs are paid per
+// such iteration (tools/isa_regions.py gives their static VALU)
+#define SM_REGION(k)                                                              \
+  do {                                                                            \
+    if (STATS) {                                                                  \
+      const uint64_t am_ = __ballot(1);                                           \
+      if (lane == uint32_t(__builtin_ctzll(am_))) atomicAdd(c.wave_stats + 64 + (k), 1ull); \
+    }                                                                             \
+  } while (0)
+
 // n 16-byte record chunks from src into the LDS row dst, asynchronously
 // (LDS-DMA: lanes 0..n-1 each move one chunk; dst wave-uniform)
 #ifndef SM_DMA_ROW
@@ -502,6 +513,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       // the lane's own loads of the next iteration (its bad mask) wait for
       // it (vmcnt retires in order) before any row read
       uint64_t fm_ = __ballot(fresh && st == S_COPY);
+      if (fm_) SM_REGION(26);
       while (fm_) {
         const uint32_t ln = uint32_t(__builtin_ctzll(fm_));
         fm_ &= fm_ - 1;
@@ -522,13 +534,16 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
 #endif
     const uint32_t ao = st >= S_BYTE ? 0u : uint32_t(addr) & 15;   // element offset in v
     uint32_t a = A_NONE;
+    SM_REGION(0);
 
     // ---------------- consume ----------------
     switch (st) {
       case S_ALU:
+        SM_REGION(1);
         a = pend;
         break;
       case S_COPY: {                                 // bad-mask chunks 0 (v), 1 (v2)
+        SM_REGION(2);
         bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
         bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
         need2 = false;
@@ -539,6 +554,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_BM: {                                   // (F) last, then first B-mer present?
+        SM_REGION(3);
         // The last B-mer [q1, q1+B) (q1 = prefix+min_len-B) is probed first:
         // absent, it lies inside every window starting in [prefix, q1], so
         // all of them are skipped at once; an absent first B-mer rules out
@@ -596,12 +612,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_KT: {                                   // (C)
+        SM_REGION(4);
         const uint64_t l0 = lo64(v), h0 = hi64(v);
         if (l0 <= h0) { depth = c.K; start = l0; end = h0; have_pos = false; }
         a = A_TRAV;
         break;
       }
       case S_IDX: {
+        SM_REGION(5);
         const uint64_t iv = idx_val<IdxT>(v, ao);
         const uint64_t iv2 = idx_val<IdxT>(v2, uint32_t(addr2) & 15);
         if (op == O_SAPOS || op == O_SAPOS2) {
@@ -626,6 +644,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_BYTE: {                                 // is_leftmaximal: T[pos-1]
+        SM_REGION(6);
         if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
           if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
           ++nem;
@@ -634,6 +653,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
+        SM_REGION(7);
         // text bytes [addr, addr + 16) in v, then (tn2) the next 16 in v2
         // (pf: v2 / v3 hold the children's SA elements instead)
         const bool tn2 = need2 && !pf;
@@ -684,6 +704,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       }
       case S_USCAN: {                                // (B) first j with U[pos+j] >= d-j
+        SM_REGION(8);
         // U bytes [addr, addr + 16) in v, then (need2) the next 16 in v2
         bool fin = false;
 #pragma unroll
@@ -714,6 +735,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       case S_EXL:                                    // L8 runs: expand_link (xrun = 0)
       case S_EXR:                                    // or the traverse's final run (1);
       case S_EXB: {                                  // S_EXB: both sides in one iteration
+        SM_REGION(9);
         const uint64_t lb = xrun ? start : 0, hb = xrun ? end : N - 1;
         // run members before the stop in one block, walking down (left:
         // bytes (o-lim, o]) or up (right: bytes [o, o+lim)); *more: no stop
@@ -772,6 +794,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
 
     // ---------------- decide ----------------
     if (a == A_BS) {                                  // next probe of a binary search
+      SM_REGION(10);
       if (lo < hi) {
         m = (lo + hi) >> 1;
         lc = lL < lR ? lL : lR;
@@ -783,6 +806,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_BS_DONE) {
+      SM_REGION(11);
       lc = 0;
       if (bsm == BS_LEFT) {
         es = lo;                                      // first suffix of the run
@@ -800,6 +824,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_XL_DONE) {                             // left end known: right side
+      SM_REGION(12);
       const uint64_t hb = xrun ? end : N - 1;
       nblk = 0;
       if (!xrun && start - es >= thresh) {            // expand_link gives up (longSA.h:164)
@@ -814,6 +839,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_RUN_DONE) {
+      SM_REGION(13);
       if (xrun) {                                     // traverse result
         start = es; end = ee; depth = xd; pos = bpos; have_pos = start == end;
         a = A_AFTER;
@@ -826,6 +852,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_CHAIN_DONE) {
+      SM_REGION(14);
       prefix += j;
       if (!hit) {
         depth = 0; start = 0; end = N - 1; have_pos = false;
@@ -838,6 +865,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_EXPAND) {                              // expand_link (longSA.h:158-174)
+      SM_REGION(15);
       // the run around [start, end] with L8 >= depth = the suffixes sharing
       // P[prefix, prefix+depth); it fails iff it holds >= thresh more
       thresh = 2u * depth * c.logN;
@@ -847,6 +875,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       a = ex_start(0, N - 1) ? A_NONE : A_RUN_DONE;
     }
     if (a == A_AFTER) {
+      SM_REGION(16);
       if (depth <= 1) {
         depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
         a = A_TOP;
@@ -872,6 +901,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_TOP) {
+      SM_REGION(17);
       // (F) runs while the state is shallow, once per prefix (skip_f: this
       // prefix's window already passed the bitmap)
       bool proceed = skip_f || depth >= c.min_len;
@@ -880,6 +910,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       if (prefix >= L || (!proceed && prefix + c.min_len > L)) {
         a = A_DONE;
       } else if (!proceed) {
+        SM_REGION(24);
         // bad-mask work only for reads holding a bad base (clean: none)
         int32_t kb = -1;
         const uint32_t B = c.B;
@@ -888,6 +919,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         bool okP = true, okQ = true;                // [p, p+B), [p+D, p+D+B): inside the read
         bool okP1 = prefix + 1 + B <= L, okM = sM + B <= L;
         if (!clean) {
+          SM_REGION(20);
           kb = bad.last(prefix, c.min_len);
           while (kb >= 0 && in_text(P[kb]))
             kb = bad.last(prefix, uint32_t(kb) - prefix);
@@ -916,11 +948,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;
           const uint32_t span = hi_s + B - lo_s;
           if (span <= 21) {
+            SM_REGION(21);
             const uint64_t X = codes_raw(row, lo_s, span);
             const uint64_t mk = (1ull << (2 * B)) - 1;
             c1 = (X >> (2 * (lo_s + span - s1 - B))) & mk;
             c0 = (X >> (2 * (lo_s + span - s2 - B))) & mk;
           } else {
+            SM_REGION(22);
             c0 = codes_raw(row, s2, B);
             c1 = codes_raw(row, s1, B);
           }
@@ -936,6 +970,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       if (a == A_TOP && proceed) {                     // (C) from the root
         if (depth == 0 && prefix + c.K <= L && (clean || bad.bits(prefix, c.K) == 0)) {
           // the window's first B-mer code (c.B >= c.K) from the filter pass
+          SM_REGION(23);
           const uint64_t kc = ktr ? m : codes_raw(row, prefix, c.K);
           addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
           st = S_KT;
@@ -946,6 +981,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_TRAV) {
+      SM_REGION(18);
       if (depth >= L || prefix + depth >= L) {
         a = A_AFTER;                                  // (backwards: parks in S_ALU)
       } else {
@@ -972,6 +1008,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
     }
     if (a == A_DONE) {
+      SM_REGION(19);
       c.n_out[rd] = nem;
       if (STATS && c.iters) c.iters[rd] = it;
       it = 0;

@@ -40,8 +40,21 @@ struct smash_pipeline {
   uint8_t *d_small = nullptr;
   int64_t *d_chrom_off = nullptr;
   int64_t *d_bins = nullptr;
-  uint64_t *d_match = nullptr;
+  uint64_t *d_match = nullptr;    // the current search set's (below)
   uint32_t *d_nmatch = nullptr;
+  // two search sets: the k_mam_sm launch of batch b + 1 runs on its own
+  // stream under the tail of batch b's (the slowest reads of a launch leave
+  // most CUs idle for ~1.6 ms); set k is free again once the post stage of
+  // its last batch has read it (ev_free)
+  uint64_t *d_match_s[2] = {nullptr, nullptr};
+  uint32_t *d_nmatch_s[2] = {nullptr, nullptr};
+  uint8_t *d_rec_s[2] = {nullptr, nullptr};
+  unsigned long long *d_work_s[2] = {nullptr, nullptr};
+  uint64_t rec_bytes = 0;
+  hipStream_t xs[2] = {nullptr, nullptr};
+  hipEvent_t ev_in = nullptr, ev_found[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+  bool set_used[2] = {false, false};
+  int set = 1;
   int32_t *d_nk = nullptr;
   uint32_t *d_nmajor = nullptr;
   uint64_t *d_hits = nullptr;
@@ -834,8 +847,19 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     SMASH_HIPX(hipMemcpy(p->d_small, cfg->h_small_chr, p->n_contig, hipMemcpyHostToDevice));
     SMASH_HIPX(hipMemcpy(p->d_chrom_off, cfg->h_chrom_off, 8 * p->n_contig, hipMemcpyHostToDevice));
     SMASH_HIPX(hipMemcpy(p->d_bins, cfg->h_bin_starts, 8 * p->nbins, hipMemcpyHostToDevice));
-    p->d_match = dalloc<uint64_t>(2 * P * p->slots);
-    p->d_nmatch = dalloc<uint32_t>(2 * P);
+    p->rec_bytes = search_rec_bytes(2 * P, p->read_len);
+    for (int k = 0; k < 2; ++k) {
+      p->d_match_s[k] = dalloc<uint64_t>(2 * P * p->slots);
+      p->d_nmatch_s[k] = dalloc<uint32_t>(2 * P);
+      p->d_rec_s[k] = dalloc<uint8_t>(p->rec_bytes);
+      p->d_work_s[k] = dalloc<unsigned long long>(1);
+      SMASH_HIPX(hipStreamCreateWithFlags(&p->xs[k], hipStreamNonBlocking));
+      SMASH_HIPX(hipEventCreateWithFlags(&p->ev_found[k], hipEventDisableTiming));
+      SMASH_HIPX(hipEventCreateWithFlags(&p->ev_free[k], hipEventDisableTiming));
+    }
+    SMASH_HIPX(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
+    p->d_match = p->d_match_s[0];
+    p->d_nmatch = p->d_nmatch_s[0];
     p->d_nk = dalloc<int32_t>(P);
     p->d_nmajor = dalloc<uint32_t>(P);
     p->d_hits = dalloc<uint64_t>(P * 2 * p->slots);
@@ -920,8 +944,20 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  for (int k = 0; k < 2; ++k) {
+    if (p->xs[k]) {
+      (void)hipStreamSynchronize(p->xs[k]);
+      (void)hipStreamDestroy(p->xs[k]);
+    }
+    if (p->ev_found[k]) (void)hipEventDestroy(p->ev_found[k]);
+    if (p->ev_free[k]) (void)hipEventDestroy(p->ev_free[k]);
+    for (void *q : {(void *)p->d_match_s[k], (void *)p->d_nmatch_s[k], (void *)p->d_rec_s[k],
+                    (void *)p->d_work_s[k]})
+      dfree(q);
+  }
+  if (p->ev_in) (void)hipEventDestroy(p->ev_in);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
-                  (void *)p->d_bins, (void *)p->d_match, (void *)p->d_nmatch,
+                  (void *)p->d_bins,
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
                   (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_first,
                   (void *)p->d_k[0], (void *)p->d_k[1], (void *)p->d_v[0],
@@ -935,15 +971,28 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
   delete p;
 }
 
-extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
-                               uint64_t n_pairs, void *stream) {
+// map -> resolve/tag/filter/hash -> in-batch order.  The search runs on the
+// next set's stream once `in_ev` (the reads are ready) and the set's previous
+// post stage have completed; the rest runs on s after the search.  in_ev
+// null: recorded on s now (everything before this call on s).
+static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                          hipStream_t s, hipEvent_t in_ev) {
   int rc = check_pipe(p, n_pairs);
   if (rc) return rc;
-  hipStream_t s = static_cast<hipStream_t>(stream);
   p->last = s;
   p->n_pairs = n_pairs;
   if (!n_pairs) return SMASH_OK;
   SMASH_HIP(hipSetDevice(p->device));
+  const int k = p->set ^= 1;
+  p->d_match = p->d_match_s[k];
+  p->d_nmatch = p->d_nmatch_s[k];
+  hipStream_t xs = p->xs[k];
+  if (!in_ev) {
+    in_ev = p->ev_in;
+    SMASH_HIP(hipEventRecord(in_ev, s));
+  }
+  SMASH_HIP(hipStreamWaitEvent(xs, in_ev, 0));
+  if (p->set_used[k]) SMASH_HIP(hipStreamWaitEvent(xs, p->ev_free[k], 0));
   if (p->prof) {
     if (2 * p->n_ev + 2 > p->ev.size()) {
       for (int k = 0; k < 64; ++k) {
@@ -955,11 +1004,14 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
     p->ix->kev[0] = p->ev[2 * p->n_ev];          // recorded around k_mam_sm itself
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
+  const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k]};
   rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
-                      p->read_len, 2 * n_pairs, p->d_match, p->slots, p->d_nmatch, stream,
-                      false);   // no per-batch sync: the probe check runs at stats time
+                      p->read_len, 2 * n_pairs, p->d_match, p->slots, p->d_nmatch, xs,
+                      false, &ws);   // no per-batch sync: the probe check runs at stats time
   p->ix->kev[0] = p->ix->kev[1] = nullptr;
   if (rc) return rc;
+  SMASH_HIP(hipEventRecord(p->ev_found[k], xs));
+  SMASH_HIP(hipStreamWaitEvent(s, p->ev_found[k], 0));
   if (p->prof) {
     ++p->n_ev;
     p->prof_reads += 2 * n_pairs;
@@ -987,6 +1039,8 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
                                       p->d_stats, p->d_post_ws);
   }
   SMASH_HIP(hipGetLastError());
+  SMASH_HIP(hipEventRecord(p->ev_free[k], s));   // the set's matches are read
+  p->set_used[k] = true;
   // in-batch ordering for de-dup: stable radix sort of key hi, value = pair
   k_dedup_keys<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_nk, p->d_hash, n_pairs,
                                                              p->d_k[0], p->d_v[0]);
@@ -999,6 +1053,11 @@ extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
     std::swap(p->d_v[0], p->d_v[1]);
   }
   return SMASH_OK;
+}
+
+extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
+                               uint64_t n_pairs, void *stream) {
+  return phase_map_impl(p, d_reads, n_pairs, static_cast<hipStream_t>(stream), nullptr);
 }
 
 // 1 .. 2^24 - 1, never 0 (an unpublished slot)
@@ -1052,14 +1111,46 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
   return SMASH_OK;
 }
 
+namespace smash {
+// one batch, its search after in_ev (null: after everything on s so far)
+int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                   uint64_t *d_counts, hipStream_t s, hipEvent_t in_ev) {
+  int rc = phase_map_impl(p, d_reads, n_pairs, s, in_ev);
+  if (rc) return rc;
+  if ((rc = dedup_local(p, s))) return rc;
+  if ((rc = smash_phase_positions(p, nullptr, s))) return rc;
+  return smash_phase_bin(p, nullptr, d_counts, s);
+}
+}  // namespace smash
+
 extern "C" int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
                                  uint64_t n_pairs, uint64_t *d_counts, void *stream) {
-  int rc = smash_phase_map(p, d_reads, n_pairs, stream);
-  if (rc) return rc;
+  return smash::count_batch_ev(p, d_reads, n_pairs, d_counts, static_cast<hipStream_t>(stream),
+                               nullptr);
+}
+
+extern "C" int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                                   uint64_t batch_pairs, uint64_t *d_counts, void *stream) {
+  if (!p || (n_pairs && !d_reads) || !d_counts || batch_pairs == 0 ||
+      batch_pairs > p->max_pairs) {
+    set_error("smash_count_batches: bad arguments");
+    return SMASH_ERR_ARG;
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if ((rc = dedup_local(p, s))) return rc;
-  if ((rc = smash_phase_positions(p, nullptr, stream))) return rc;
-  return smash_phase_bin(p, nullptr, d_counts, stream);
+  SMASH_HIP(hipSetDevice(p->device));
+  // every batch's reads are ready once the work before this call on s is:
+  // one input event for all, so batch b + 1's search can start under the
+  // tail of batch b's
+  hipEvent_t in_ev = nullptr;
+  SMASH_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
+  int rc = hipEventRecord(in_ev, s) == hipSuccess ? SMASH_OK : SMASH_ERR_HIP;
+  const uint64_t L2 = 2 * uint64_t(p->read_len);
+  for (uint64_t b0 = 0; rc == SMASH_OK && b0 < n_pairs; b0 += batch_pairs) {
+    const uint64_t n = std::min(batch_pairs, n_pairs - b0);
+    rc = smash::count_batch_ev(p, d_reads + b0 * L2, n, d_counts, s, in_ev);
+  }
+  (void)hipEventDestroy(in_ev);   // released once the waits on it have completed
+  return rc;
 }
 
 // ---- multi-GPU de-dup exchange ------------------------------------------------
@@ -1344,6 +1435,36 @@ extern "C" int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
   if (search_ms) *search_ms = ms;
   if (launches) *launches = p->n_ev;
   if (reads) *reads = p->prof_reads;
+  return SMASH_OK;
+}
+
+// The time at least one profiled k_mam_sm launch was running: the union of
+// the launches' [start, end] event intervals (launches on the two search
+// streams overlap, so their summed durations count the overlap twice).
+extern "C" int smash_pipeline_profile_active(smash_pipeline *p, double *active_ms) {
+  if (!p || !active_ms) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  std::vector<std::pair<double, double>> iv;
+  for (uint64_t i = 0; i < p->n_ev; ++i) {
+    SMASH_HIP(hipEventSynchronize(p->ev[2 * i + 1]));
+    float a = 0, b = 0;
+    SMASH_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[2 * i]));
+    SMASH_HIP(hipEventElapsedTime(&b, p->ev[0], p->ev[2 * i + 1]));
+    iv.emplace_back(a, b);
+  }
+  std::sort(iv.begin(), iv.end());
+  double tot = 0, cs = 0, ce = -1e300;
+  for (const auto &x : iv) {
+    if (x.first > ce) {
+      if (ce > cs) tot += ce - cs;
+      cs = x.first;
+      ce = x.second;
+    } else if (x.second > ce) {
+      ce = x.second;
+    }
+  }
+  if (!iv.empty() && ce > cs) tot += ce - cs;
+  *active_ms = tot;
   return SMASH_OK;
 }
 

@@ -49,7 +49,7 @@ EXPORTS = [
     "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
-    "smash_count_fastq",
+    "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
 ]
 
 
@@ -127,6 +127,8 @@ def lib():
     L.smash_pipeline_free.argtypes = [vp]
     L.smash_pipeline_free.restype = None
     L.smash_count_batch.argtypes = [vp, vp, C.c_uint64, vp, vp]
+    L.smash_count_batches.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp]
+    L.smash_pipeline_profile_active.argtypes = [vp, C.POINTER(C.c_double)]
     L.smash_phase_map.argtypes = [vp, vp, C.c_uint64, vp]
     L.smash_phase_export.argtypes = [vp, C.c_int, C.c_uint64, i64p, i64p, C.POINTER(vp),
                                      C.POINTER(vp), vp]
@@ -392,6 +394,13 @@ class Pipeline:
                                       vp(_stream(stream))), "smash_count_fastq")
         return st.as_dict()
 
+    def count_batches(self, d_reads, n_pairs, batch_pairs, d_counts, stream=None):
+        """n_pairs resident pairs in batches (smash_count_batches): one batch's
+        search overlaps the previous one's tail."""
+        check(lib().smash_count_batches(self.h, _ptr(d_reads), n_pairs, batch_pairs,
+                                        _ptr(d_counts), vp(_stream(stream))),
+              "smash_count_batches")
+
     def phase_map(self, d_reads, n_pairs, stream=None):
         check(lib().smash_phase_map(self.h, _ptr(d_reads), n_pairs, vp(_stream(stream))),
               "smash_phase_map")
@@ -453,6 +462,13 @@ class Pipeline:
         check(lib().smash_pipeline_profile_read(self.h, C.byref(ms), C.byref(n), C.byref(r)),
               "smash_pipeline_profile_read")
         return ms.value, n.value, r.value
+
+    def profile_active(self):
+        """milliseconds during which at least one profiled search launch ran"""
+        ms = C.c_double()
+        check(lib().smash_pipeline_profile_active(self.h, C.byref(ms)),
+              "smash_pipeline_profile_active")
+        return ms.value
 
     def positions(self):
         """(pos0, abspos) int64 arrays of the positions the last batch emitted

@@ -100,3 +100,28 @@ def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, monkeypatch
     total, st = run_emulated(gix, reads, W, per_rank, steps, starts, cs)
     assert total.tolist() == c1.cpu().numpy().astype(np.uint64).tolist()
     assert st == (s1.positions, s1.dups, s1.kept, s1.dupe_pairs)
+
+
+@pytest.mark.parametrize("batch", [97, 500, 2000])
+def test_count_batches_equals_batch_by_batch(gix, batch):
+    """smash_count_batches (searches on two alternating streams, each batch's
+    search under the previous one's tail) == smash_count_batch per batch."""
+    reads = interleaved_reads("s150")
+    n = reads.shape[0] // 2
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    d = torch.from_numpy(np.ascontiguousarray(reads)).cuda()
+    out = []
+    for together in (False, True):
+        pipe = S.Pipeline(gix, cs, starts, reads.shape[1], batch, dedup_capacity=n)
+        pipe.reset()
+        c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+        if together:
+            pipe.count_batches(d, n, batch, c)
+        else:
+            for b0 in range(0, n, batch):
+                b1 = min(n, b0 + batch)
+                pipe.count_batch(d[2 * b0:2 * b1], b1 - b0, c)
+        st = pipe.stats()
+        out.append((c.cpu().numpy().tolist(), st.positions, st.dups, st.kept, st.dupe_pairs))
+    assert out[0] == out[1]

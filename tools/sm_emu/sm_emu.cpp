@@ -130,7 +130,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   unsigned long long work = 0;
   c.work = &work;
   for (int k = 0; k < 4; ++k) c.in_text[k] = in_text[k];
-  unsigned long long ws[64] = {0};
+  unsigned long long ws[128] = {0};
   c.iters = iters; c.wave_stats = ws;
   // the emulator checks every probe against its own array (the device checks
   // the span of all of them)
