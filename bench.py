@@ -457,7 +457,9 @@ def main():
             sc.reset()
             for b in range(nb):
                 b0, b1 = b * B, min(P, (b + 1) * B)
-                sc.step(d_reads[2 * b0:2 * b1], b1 - b0, b0 * world, counts)
+                n0, n1 = b1, min(P, b1 + B)   # the next batch, searched under this one's exchange
+                sc.step(d_reads[2 * b0:2 * b1], b1 - b0, b0 * world, counts,
+                        d_reads[2 * n0:2 * n1] if n1 > n0 else None, n1 - n0)
             dist.all_reduce(counts)
 
     for i in range(args.warmup):

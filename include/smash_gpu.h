@@ -235,6 +235,12 @@ int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pa
  *  6. smash_phase_bin      -- adjacent de-dup against *d_prev, bin, add. */
 int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                     void *stream);
+/* smash_phase_map, then the search of the NEXT batch (d_next, n_next pairs,
+ * its reads ready by the work already on `stream`) issued at once on the
+ * pipeline's other search stream: it runs while the caller exchanges this
+ * batch's keys; the next smash_phase_map[_ahead] with the same reads uses it. */
+int smash_phase_map_ahead(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                          const uint8_t *d_next, uint64_t n_next, void *stream);
 int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
                        int64_t *h_send_counts, int64_t *h_send_words,
                        const uint64_t **d_send, const uint64_t **d_send_words,

@@ -54,6 +54,10 @@ struct smash_pipeline {
   hipStream_t xs[2] = {nullptr, nullptr};
   hipEvent_t ev_in = nullptr, ev_found[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
   bool set_used[2] = {false, false};
+  // a search already issued into a set (smash_phase_map_ahead): its reads
+  const uint8_t *pref_reads[2] = {nullptr, nullptr};
+  uint64_t pref_n[2] = {0, 0};
+  bool searched[2] = {false, false};
   int set = 1;
   int32_t *d_nk = nullptr;
   uint32_t *d_nmajor = nullptr;
@@ -971,31 +975,16 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
   delete p;
 }
 
-// map -> resolve/tag/filter/hash -> in-batch order.  The search runs on the
-// next set's stream once `in_ev` (the reads are ready) and the set's previous
-// post stage have completed; the rest runs on s after the search.  in_ev
-// null: recorded on s now (everything before this call on s).
-static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
-                          hipStream_t s, hipEvent_t in_ev) {
-  int rc = check_pipe(p, n_pairs);
-  if (rc) return rc;
-  p->last = s;
-  p->n_pairs = n_pairs;
-  if (!n_pairs) return SMASH_OK;
-  SMASH_HIP(hipSetDevice(p->device));
-  const int k = p->set ^= 1;
-  p->d_match = p->d_match_s[k];
-  p->d_nmatch = p->d_nmatch_s[k];
+// the search of n_pairs pairs into set k on its stream, after in_ev (the
+// reads are ready) and after the post stage that last read the set
+static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_t n_pairs,
+                       hipEvent_t in_ev) {
   hipStream_t xs = p->xs[k];
-  if (!in_ev) {
-    in_ev = p->ev_in;
-    SMASH_HIP(hipEventRecord(in_ev, s));
-  }
   SMASH_HIP(hipStreamWaitEvent(xs, in_ev, 0));
   if (p->set_used[k]) SMASH_HIP(hipStreamWaitEvent(xs, p->ev_free[k], 0));
   if (p->prof) {
     if (2 * p->n_ev + 2 > p->ev.size()) {
-      for (int k = 0; k < 64; ++k) {
+      for (int q = 0; q < 64; ++q) {
         hipEvent_t e;
         SMASH_HIP(hipEventCreate(&e));
         p->ev.push_back(e);
@@ -1005,17 +994,52 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
   const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k]};
-  rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
-                      p->read_len, 2 * n_pairs, p->d_match, p->slots, p->d_nmatch, xs,
-                      false, &ws);   // no per-batch sync: the probe check runs at stats time
+  const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
+                                p->read_len, 2 * n_pairs, p->d_match_s[k], p->slots,
+                                p->d_nmatch_s[k], xs, false, &ws);   // probe check at stats time
   p->ix->kev[0] = p->ix->kev[1] = nullptr;
   if (rc) return rc;
-  SMASH_HIP(hipEventRecord(p->ev_found[k], xs));
-  SMASH_HIP(hipStreamWaitEvent(s, p->ev_found[k], 0));
   if (p->prof) {
     ++p->n_ev;
     p->prof_reads += 2 * n_pairs;
   }
+  SMASH_HIP(hipEventRecord(p->ev_found[k], xs));
+  p->pref_reads[k] = d_reads;
+  p->pref_n[k] = n_pairs;
+  p->searched[k] = true;
+  return SMASH_OK;
+}
+
+// map -> resolve/tag/filter/hash -> in-batch order.  The search runs on the
+// next set's stream once `in_ev` (the reads are ready) and the set's previous
+// post stage have completed (unless smash_phase_map_ahead already searched
+// these reads into that set); the rest runs on s after the search.  in_ev
+// null: recorded on s now (everything before this call on s).  d_next: the
+// next batch's search is issued into the other set right after this one's,
+// before this batch's post stage is queued, so it runs while the caller
+// works on this batch.
+static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                          hipStream_t s, hipEvent_t in_ev, const uint8_t *d_next = nullptr,
+                          uint64_t n_next = 0) {
+  int rc = check_pipe(p, n_pairs);
+  if (rc) return rc;
+  if (d_next && (rc = check_pipe(p, n_next))) return rc;
+  p->last = s;
+  p->n_pairs = n_pairs;
+  if (!n_pairs) return SMASH_OK;
+  SMASH_HIP(hipSetDevice(p->device));
+  const int k = p->set ^= 1;
+  p->d_match = p->d_match_s[k];
+  p->d_nmatch = p->d_nmatch_s[k];
+  const bool have = p->searched[k] && p->pref_reads[k] == d_reads && p->pref_n[k] == n_pairs;
+  if (!in_ev && (!have || (d_next && n_next))) {
+    in_ev = p->ev_in;
+    SMASH_HIP(hipEventRecord(in_ev, s));
+  }
+  if (!have && (rc = search_into(p, k, d_reads, n_pairs, in_ev))) return rc;
+  p->searched[k] = false;   // consumed by this batch
+  if (d_next && n_next && (rc = search_into(p, k ^ 1, d_next, n_next, in_ev))) return rc;
+  SMASH_HIP(hipStreamWaitEvent(s, p->ev_found[k], 0));
   if (p->post_fast) {
     // mates of <= 8 matches (most pairs) in 8-word networks, <= 16 in
     // 16-word ones, the rest in the general kernel
@@ -1058,6 +1082,13 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
 extern "C" int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads,
                                uint64_t n_pairs, void *stream) {
   return phase_map_impl(p, d_reads, n_pairs, static_cast<hipStream_t>(stream), nullptr);
+}
+
+extern "C" int smash_phase_map_ahead(smash_pipeline *p, const uint8_t *d_reads,
+                                     uint64_t n_pairs, const uint8_t *d_next, uint64_t n_next,
+                                     void *stream) {
+  return phase_map_impl(p, d_reads, n_pairs, static_cast<hipStream_t>(stream), nullptr, d_next,
+                        n_next);
 }
 
 // 1 .. 2^24 - 1, never 0 (an unpublished slot)

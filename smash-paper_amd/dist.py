@@ -40,12 +40,17 @@ class ShardedCounter:
         self.pipe.reset()
         self.carried.fill_(-1)
 
-    def step(self, d_reads, n_pairs, step_base, d_counts):
+    def step(self, d_reads, n_pairs, step_base, d_counts, next_reads=None, next_pairs=0):
         """One batch: this rank's n_pairs pairs start at global index
-        step_base + rank * n_pairs (every rank passes the same n_pairs)."""
+        step_base + rank * n_pairs (every rank passes the same n_pairs).
+        next_reads / next_pairs: the rank's next batch, whose search the
+        pipeline starts now, so it runs under this batch's exchanges."""
         dev, W, r = self.device, self.world, self.rank
         p = self.pipe
-        p.phase_map(d_reads, n_pairs)
+        if next_pairs:
+            p.phase_map_ahead(d_reads, n_pairs, next_reads, next_pairs)
+        else:
+            p.phase_map(d_reads, n_pairs)
         hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * n_pairs)
         sc = torch.as_tensor([[int(a), int(b)] for a, b in zip(cnt, wcnt)],
                              dtype=torch.int64).to(dev)

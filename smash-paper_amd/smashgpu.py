@@ -50,6 +50,7 @@ EXPORTS = [
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
     "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
+    "smash_phase_map_ahead",
 ]
 
 
@@ -128,6 +129,7 @@ def lib():
     L.smash_pipeline_free.restype = None
     L.smash_count_batch.argtypes = [vp, vp, C.c_uint64, vp, vp]
     L.smash_count_batches.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp]
+    L.smash_phase_map_ahead.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp]
     L.smash_pipeline_profile_active.argtypes = [vp, C.POINTER(C.c_double)]
     L.smash_phase_map.argtypes = [vp, vp, C.c_uint64, vp]
     L.smash_phase_export.argtypes = [vp, C.c_int, C.c_uint64, i64p, i64p, C.POINTER(vp),
@@ -404,6 +406,13 @@ class Pipeline:
     def phase_map(self, d_reads, n_pairs, stream=None):
         check(lib().smash_phase_map(self.h, _ptr(d_reads), n_pairs, vp(_stream(stream))),
               "smash_phase_map")
+
+    def phase_map_ahead(self, d_reads, n_pairs, d_next, n_next, stream=None):
+        """phase_map, and the next batch's search issued at once on the
+        pipeline's other search stream (smash_phase_map_ahead)."""
+        check(lib().smash_phase_map_ahead(self.h, _ptr(d_reads), n_pairs,
+                                          _ptr(d_next) if n_next else None, n_next,
+                                          vp(_stream(stream))), "smash_phase_map_ahead")
 
     def phase_export(self, world, global_base, stream=None):
         """(headers [n, 5] int64, words [w] int64, per-owner key counts,

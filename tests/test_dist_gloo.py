@@ -49,7 +49,12 @@ def _worker(rank, world, port, per_rank, steps, out_q):
         base = s * world * per_rank
         lo = base + rank * per_rank
         d_reads = torch.from_numpy(reads[2 * lo:2 * (lo + per_rank)].copy())
-        sc.step(d_reads, per_rank, base, counts)
+        if s + 1 < steps and s % 2 == 0:   # the look-ahead form (next batch's search issued now)
+            nlo = lo + world * per_rank
+            nxt = torch.from_numpy(reads[2 * nlo:2 * (nlo + per_rank)].copy())
+            sc.step(d_reads, per_rank, base, counts, nxt, per_rank)
+        else:
+            sc.step(d_reads, per_rank, base, counts)
     dist.all_reduce(counts)
     st = torch.tensor([pipe.total, pipe.dups, pipe.kept], dtype=torch.int64)
     dist.all_reduce(st)

@@ -24,20 +24,31 @@ def _prev(tails, carried):
     return ShardedCounter._prev(tails, carried)
 
 
-def run_emulated(ix, reads, W, per_rank, steps, starts, cs):
+def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False):
     dev = torch.device("cuda")
     pipes = [S.Pipeline(ix, cs, starts, reads.shape[1], per_rank) for _ in range(W)]
     for p in pipes:
         p.reset()
     counts = [torch.zeros(len(starts), dtype=torch.int64, device=dev) for _ in range(W)]
     carried = torch.full((1,), -1, dtype=torch.int64, device=dev)
+    keep_alive, prev_next = [], [None] * W
     for s in range(steps):
         base = s * W * per_rank
         sends = []
         for r in range(W):
             lo = base + r * per_rank
             d = torch.from_numpy(np.ascontiguousarray(reads[2 * lo:2 * (lo + per_rank)])).to(dev)
-            pipes[r].phase_map(d, per_rank)
+            # ahead: this batch was searched by the previous step's look-ahead
+            cur = prev_next[r] if (ahead and s > 0) else d
+            if ahead and s + 1 < steps:
+                # the rank's next batch searched now, on the other search stream
+                nlo = lo + W * per_rank
+                nxt = torch.from_numpy(np.ascontiguousarray(reads[2 * nlo:2 * (nlo + per_rank)])).to(dev)
+                keep_alive.append(nxt)
+                pipes[r].phase_map_ahead(cur, per_rank, nxt, per_rank)
+                prev_next[r] = nxt
+            else:
+                pipes[r].phase_map(cur, per_rank)
             hdr, words, cnt, wcnt = pipes[r].phase_export(W, base + r * per_rank)
             # copies: the export buffers are the pipeline's own
             sends.append((hdr.clone(), words.clone(), [int(c) for c in cnt],
@@ -81,9 +92,13 @@ def run_emulated(ix, reads, W, per_rank, steps, starts, cs):
                    sum(x.kept for x in st), sum(x.dupe_pairs for x in st))
 
 
-@pytest.mark.parametrize("W,per_rank,steps,bits", [(2, 500, 2, 0), (3, 111, 3, 0),
-                                                   (4, 250, 1, 0), (3, 200, 2, 3)])
-def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, monkeypatch):
+@pytest.mark.parametrize("W,per_rank,steps,bits,ahead", [(2, 500, 2, 0, False),
+                                                         (3, 111, 3, 0, False),
+                                                         (4, 250, 1, 0, False),
+                                                         (3, 200, 2, 3, False),
+                                                         (3, 111, 3, 0, True),
+                                                         (2, 300, 3, 2, True)])
+def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, ahead, monkeypatch):
     """bits > 0: the key hash cut to `bits` bits, so owners see colliding
     keys and must compare the exchanged key words."""
     if bits:
@@ -97,7 +112,7 @@ def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, monkeypatch
     c1 = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
     one.count_batch(torch.from_numpy(np.ascontiguousarray(reads[:2 * n])).cuda(), n, c1)
     s1 = one.stats()
-    total, st = run_emulated(gix, reads, W, per_rank, steps, starts, cs)
+    total, st = run_emulated(gix, reads, W, per_rank, steps, starts, cs, ahead)
     assert total.tolist() == c1.cpu().numpy().astype(np.uint64).tolist()
     assert st == (s1.positions, s1.dups, s1.kept, s1.dupe_pairs)
 
