@@ -58,6 +58,7 @@ constexpr uint64_t kMTile = uint64_t(kMB) * kMPer;
 constexpr int kDirShift = 12;               // directory: 4096 text positions per entry
 constexpr int kLdsBins = 32;                // bins of a tile counted in LDS
 constexpr uint64_t kNone = ~0ull;
+constexpr int kMaxSegLds = 128;             // segment tables up to this size live in LDS
 
 struct MapCtx {
   const uint8_t *L8;
@@ -139,40 +140,91 @@ __device__ __forceinline__ uint64_t next_unsat_dir(const uint64_t *dir, uint64_t
   return t < ndir ? dir[t] : kNone;
 }
 
-// bin ordinal (bisect_right of abs0 + the tile's first base) per tile
-__global__ void k_tilebins(MapCtx c, int64_t abs0, uint64_t i0, uint64_t ntiles, uint32_t *o0) {
-  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t < ntiles) o0[t] = bisect_right(c, abs0 + int64_t(i0 + t * kMTile));
+// one contig's part of the scan: bases [i0, i1) of the contig at text
+// position sp (size S); its map.bin bytes at out + out_off; abs0 = its
+// chrom_sizes offset (< 0: not binned); tiles [tile0, tile0 + tiles of it)
+// of the launch
+struct Seg {
+  uint64_t sp, S, i0, i1, out_off, tile0;
+  int64_t abs0;
+  uint64_t contig;
+};
+
+// the segment holding launch tile T (segs ascending by tile0)
+__device__ __forceinline__ uint32_t seg_of(const Seg *segs, uint32_t nseg, uint64_t T) {
+  uint32_t lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (segs[mid].tile0 <= T) lo = mid;
+    else hi = mid;
+  }
+  return lo;
 }
 
-// bases [i0, i1) of one contig (text start sp, size S); out: map.bin bytes of
-// base i0 onwards (or null); abs0 = chrom_sizes offset of the contig (< 0:
-// not binned)
+// bit i (0..15): byte i of the block is 0xFF
+__device__ __forceinline__ uint32_t sat_mask16(const uint4 &v) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t w = ~(k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w);
+    // 0x80 in each byte of w that is non-zero (exact, no borrows)
+    const uint32_t nz = (((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;
+    const uint32_t z = ~nz & 0x80808080u;                 // bytes of v equal to 0xFF
+    m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+  }
+  return m;
+}
+// the 16-bit mask reversed (byte 15 - q of the rc block is base q)
+__device__ __forceinline__ uint32_t rev16(uint32_t m) { return __brev(m) >> 16; }
+
+// bin ordinal (bisect_right of abs0 + the tile's first base) per tile
+__global__ void k_tilebins(MapCtx c, const Seg *segs, uint32_t nseg, uint64_t ntiles,
+                           uint32_t *o0) {
+  const uint64_t T = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (T >= ntiles) return;
+  const Seg g = segs[seg_of(segs, nseg, T)];
+  o0[T] = g.abs0 >= 0 ? bisect_right(c, g.abs0 + int64_t(g.i0 + (T - g.tile0) * kMTile)) : 0;
+}
+
+// every contig's bases in ONE launch (per-contig launches and their tails
+// dominated the scan): block-stride over the tiles of all segments; out: the
+// scan's map.bin bytes (or null)
 template <class IdxT>
 __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restrict__ ISA,
                                                  const uint8_t *__restrict__ U,
                                                  const uint64_t *__restrict__ dir, uint64_t ndir,
-                                                 uint64_t sp, uint64_t S, uint64_t i0, uint64_t i1,
-                                                 uint8_t *__restrict__ out, int64_t abs0,
+                                                 const Seg *__restrict__ segs, uint32_t nseg,
+                                                 uint64_t ntiles_all, uint8_t *__restrict__ out,
                                                  const uint32_t *__restrict__ tile_o0,
                                                  unsigned long long *bin_counts,
-                                                 unsigned long long *contig_count,
-                                                 uint64_t out_base) {
+                                                 unsigned long long *contig_counts) {
   __shared__ unsigned long long s_bin[kLdsBins + 1];
   __shared__ int64_t s_bs[kLdsBins];
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_o0;
   __shared__ uint64_t s_f[kMB], s_r[kMB];   // per chunk: first unsaturated (fwd / rc text order)
   __shared__ uint64_t s_ftail, s_rtail;
+  __shared__ uint32_t s_seg;
+  __shared__ Seg s_segs[kMaxSegLds];   // the segment table, once per block
   const uint64_t N = c.N;
-  const bool binned = abs0 >= 0 && c.nbins;
-  const uint64_t ntiles = (i1 - i0 + kMTile - 1) / kMTile;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint64_t t0 = i0 + t * kMTile;
+  const bool lds_segs = nseg <= uint32_t(kMaxSegLds);
+  if (lds_segs)
+    for (uint32_t k = threadIdx.x; k < nseg; k += blockDim.x) s_segs[k] = segs[k];
+  __syncthreads();
+  const Seg *tab = lds_segs ? s_segs : segs;
+  for (uint64_t T = blockIdx.x; T < ntiles_all; T += gridDim.x) {
+    if (threadIdx.x == 0) s_seg = seg_of(tab, nseg, T);
+    __syncthreads();
+    const Seg g = tab[s_seg];
+    const uint64_t sp = g.sp, S = g.S, i0 = g.i0, i1 = g.i1;
+    const int64_t abs0 = g.abs0;
+    const bool binned = abs0 >= 0 && c.nbins;
+    unsigned long long *contig_count = contig_counts ? contig_counts + g.contig : nullptr;
+    const uint64_t t0 = i0 + (T - g.tile0) * kMTile;
     if (threadIdx.x <= kLdsBins) s_bin[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       s_tot = 0;
-      s_o0 = binned ? tile_o0[t] : 0;
+      s_o0 = binned ? tile_o0[T] : 0;
     }
     __syncthreads();
     const uint32_t o0 = s_o0;
@@ -184,17 +236,16 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     const uint64_t xf = sp + ib, xr = sp + 2 * S - ib;   // xr - q: base ib + q
     const uint4 fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
     const uint4 rw = xr >= 15 ? load16u(U + xr - 15) : make_uint4(~0u, ~0u, ~0u, ~0u);
-    uint32_t satf = 0, satr = 0;   // bit q: U == 255 at base ib + q
-    uint64_t ff = kNone, fr = kNone;
-#pragma unroll
-    for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
-      const bool sf = byte_of(fw, q) == 255 || xf + q >= N;
-      const bool sr = byte_of(rw, 15 - q) == 255 || xr < q;
-      satf |= uint32_t(sf) << q;
-      satr |= uint32_t(sr) << q;
-      if (!sf && ff == kNone) ff = xf + q;                 // lowest fwd text position
-      if (!sr) fr = xr - q;                                // lowest rc text position (largest q)
-    }
+    // bit q: U == 255 at base ib + q (or past the text), 4 bytes per step:
+    // a byte is 0xFF iff its complement is zero
+    uint32_t satf = sat_mask16(fw), satr = rev16(sat_mask16(rw));
+    if (xf + 16 > N)
+      for (uint32_t q = 0; q < uint32_t(kMPer); ++q) satf |= uint32_t(xf + q >= N) << q;
+    if (xr < 15)
+      for (uint32_t q = 0; q < uint32_t(kMPer); ++q) satr |= uint32_t(xr < q) << q;
+    // lowest unsaturated fwd text position, lowest rc one (largest q)
+    const uint64_t ff = (~satf & 0xFFFFu) ? xf + __builtin_ctz(~satf & 0xFFFFu) : kNone;
+    const uint64_t fr = (~satr & 0xFFFFu) ? xr - (31 - __builtin_clz(~satr & 0xFFFFu)) : kNone;
     const bool any_sat = __syncthreads_or((satf | satr) != 0);
     uint64_t fnext = kNone, rnext = kNone;   // first unsaturated chunk after / before mine
     if (any_sat) {
@@ -225,8 +276,49 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     const bool defer = out && c.fix && c.k < 255;
     unsigned long long mine = 0;
     uint32_t d = 0;   // bin ordinal offset from o0 (monotone over the thread's bases)
+    // fast path (most chunks): no saturated byte and every base inside
+    // [i0, i1): straight-line selects, the unique bases as a mask, and their
+    // bin counted with one LDS atomic when the 16 bases share a bin
+    const bool fast = (satf | satr) == 0 && ib + kMPer <= i1;
+    uint32_t umask = 0;
+    if (fast) {
+      // away from the contig ends (m <= 255) the edge rules cannot zero a byte
+      const bool edge = ib < 272 || ib + kMPer + 256 > S;
+#pragma unroll
+      for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
+        const uint64_t i = ib + q;
+        uint32_t rb = byte_of(fw, q) + 1;                  // <= 255: U < 255 here
+        uint32_t lb = byte_of(rw, 15 - q) + 1;
+        if (edge) {
+          rb = uint64_t(rb) + i >= S ? 0u : rb;
+          lb = uint64_t(lb) >= i ? 0u : lb;
+        }
+        ob[q >> 1] |= (lb | (rb << 8)) << (16 * (q & 1));
+        umask |= uint32_t(rb - 1u < c.k) << q;             // 1 <= rb <= k
+      }
+      mine = uint32_t(__popc(umask));
+      if (binned && umask) {
+        const int64_t a0 = abs0 + int64_t(ib) + __builtin_ctz(umask);
+        const int64_t a1 = abs0 + int64_t(ib) + 31 - __builtin_clz(umask);
+        while (d < uint32_t(kLdsBins) && a0 >= s_bs[d]) ++d;
+        if (d < uint32_t(kLdsBins) && a1 < s_bs[d]) {       // [a0, a1] in one bin
+          atomicAdd(&s_bin[d], (unsigned long long)__popc(umask));
+        } else {
+          for (uint32_t m = umask; m; m &= m - 1) {
+            const int64_t a = abs0 + int64_t(ib) + __builtin_ctz(m);
+            while (d < uint32_t(kLdsBins) && a >= s_bs[d]) ++d;
+            if (d < uint32_t(kLdsBins)) {
+              atomicAdd(&s_bin[d], 1ull);
+            } else {
+              const uint32_t o = bisect_right(c, a);
+              atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], 1ull);
+            }
+          }
+        }
+      }
+    }
 #pragma unroll 4
-    for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
+    for (uint32_t q = 0; q < uint32_t(kMPer) && !fast; ++q) {
       const uint64_t i = ib + q;
       if (i >= i1) break;
       // right: m at the forward position, zeroed when m + i >= S (:666)
@@ -306,7 +398,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
           if (!(((side ? fixl : fixr) >> q) & 1)) continue;
           const uint64_t i = ib + q;
           const uint64_t x = side ? xr - q : xf + q;
-          const uint64_t bi = out_base + 2 * (i - i0) + (side ? 0 : 1);
+          const uint64_t bi = g.out_off + 2 * (i - i0) + (side ? 0 : 1);
           const uint64_t thr = side ? i : S - i;   // zeroed when m >= thr
           if (fb < c.fix_cap) {
             c.fix[3 * fb] = x; c.fix[3 * fb + 1] = bi; c.fix[3 * fb + 2] = thr;
@@ -321,7 +413,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       }
     }
     if (out && ib < i1) {
-      uint8_t *o = out + 2 * (ib - i0);
+      uint8_t *o = out + g.out_off + 2 * (ib - i0);
       if (ib + kMPer <= i1) {   // 32 bytes (the caller's pointer need not be aligned)
         __builtin_memcpy(o, ob, 32);
       } else {
@@ -390,38 +482,48 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     SMASH_HIP(hipMemcpyAsync(ix->d_nsdir, h.data(), 8 * ndir, hipMemcpyHostToDevice, s));
     SMASH_HIP(hipStreamSynchronize(s));   // h is a host local
   }
-  // per-tile bin ordinals (largest contig's tile count)
-  uint32_t *d_o0 = nullptr;
-  if (c.nbins) {
-    uint64_t maxt = 1;
-    for (uint32_t q = 0; q < ix->n_seq; q += 2)
-      maxt = std::max<uint64_t>(maxt, (ix->sizes[q] + kMTile - 1) / kMTile);
-    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_o0), 4 * maxt, s));
-  }
-  uint64_t g = 0;   // forward-base coordinate of the contig's first base
+  // the segments of [begin, end): one per contig part, tiles numbered across
+  std::vector<Seg> segs;
+  uint64_t ntiles = 0, g0 = 0;
   for (uint32_t q = 0; q < ix->n_seq; q += 2) {
-    const uint64_t S = ix->sizes[q], sp = ix->startpos[q];
-    const uint64_t a = begin > g ? begin - g : 0;
-    const uint64_t b = end < g + S ? end - g : S;
-    if (a < b && g < end) {
-      const uint64_t tiles = (b - a + kMTile - 1) / kMTile;
-      const unsigned grid = unsigned(tiles < 65536 ? tiles : 65536);
-      const int64_t abs0 = h_chrom_off ? h_chrom_off[q / 2] : -1;
-      if (c.nbins && abs0 >= 0) {
-        k_tilebins<<<unsigned((tiles + 255) / 256), 256, 0, s>>>(c, abs0, a, tiles, d_o0);
-        SMASH_HIP(hipGetLastError());
-      }
-      k_mapscan<IdxT><<<grid, kMB, 0, s>>>(
-          c, static_cast<const IdxT *>(ix->d_isa), ix->d_uniq, ix->d_nsdir, ndir, sp, S, a, b,
-          out ? out + 2 * (g + a - begin) : nullptr, abs0, d_o0,
-          reinterpret_cast<unsigned long long *>(d_bin_counts),
-          d_contig_counts ? reinterpret_cast<unsigned long long *>(d_contig_counts + q / 2)
-                          : nullptr,
-          2 * (g + a - begin));
+    const uint64_t S = ix->sizes[q];
+    const uint64_t a = begin > g0 ? begin - g0 : 0;
+    const uint64_t b = end < g0 + S ? end - g0 : S;
+    if (a < b && g0 < end) {
+      Seg sg;
+      sg.sp = ix->startpos[q]; sg.S = S; sg.i0 = a; sg.i1 = b;
+      sg.out_off = 2 * (g0 + a - begin);
+      sg.tile0 = ntiles;
+      sg.abs0 = h_chrom_off ? h_chrom_off[q / 2] : -1;
+      sg.contig = q / 2;
+      segs.push_back(sg);
+      ntiles += (b - a + kMTile - 1) / kMTile;
+    }
+    g0 += S;
+  }
+  uint32_t *d_o0 = nullptr;
+  Seg *d_segs = nullptr;
+  if (!segs.empty()) {
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_segs), sizeof(Seg) * segs.size(), s));
+    SMASH_HIP(hipMemcpyAsync(d_segs, segs.data(), sizeof(Seg) * segs.size(), hipMemcpyHostToDevice,
+                             s));
+    SMASH_HIP(hipStreamSynchronize(s));   // segs is a host local: copied before the launches
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_o0), 4 * ntiles, s));
+    const uint32_t nseg = uint32_t(segs.size());
+    if (c.nbins) {
+      k_tilebins<<<unsigned((ntiles + 255) / 256), 256, 0, s>>>(c, d_segs, nseg, ntiles, d_o0);
       SMASH_HIP(hipGetLastError());
     }
-    g += S;
+    int cus = 0;
+    SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
+    const uint64_t grid = std::min<uint64_t>(ntiles, uint64_t(cus) * 8);   // resident blocks
+    k_mapscan<IdxT><<<unsigned(grid), kMB, 0, s>>>(
+        c, static_cast<const IdxT *>(ix->d_isa), ix->d_uniq, ix->d_nsdir, ndir, d_segs, nseg,
+        ntiles, out, d_o0, reinterpret_cast<unsigned long long *>(d_bin_counts),
+        reinterpret_cast<unsigned long long *>(d_contig_counts));
+    SMASH_HIP(hipGetLastError());
   }
+  if (d_segs) SMASH_HIP(hipFreeAsync(d_segs, s));
   if (d_o0) SMASH_HIP(hipFreeAsync(d_o0, s));
   if (c.fix) {
     k_mapfix<IdxT><<<4096, 256, 0, s>>>(c, static_cast<const IdxT *>(ix->d_isa), out);
