@@ -326,6 +326,7 @@ int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_keep,
 /* (query.cpp:153-156).  *out_text is malloc'ed (smash_sam_free) and holds    */
 /* the SAM lines without the header; *tag_error gets the first                */
 /* SMASH_ERR_TAG_* that mappability_tag would throw (0 = none).               */
+/* cap_per_read 0: h_rec is packed (smash_sam_records_packed).               */
 /* ========================================================================== */
 typedef struct {
   int64_t pos;             /* 0-based on the forward contig (< 0: erased)   */
@@ -342,6 +343,16 @@ int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t st
                       const uint64_t *d_match, uint32_t cap_per_read,
                       const uint32_t *d_n_match, const uint32_t *d_tag_offsets,
                       smash_sam_rec *d_out, void *stream);
+/* smash_sam_records_packed: the same records without the per-read slots of   */
+/* cap_per_read: read i's min(d_n_match[i], cap) records go to                */
+/* d_out[d_rec_off[i] ...] (d_rec_off = exclusive prefix sum of the counts),  */
+/* so the table is as large as the matches, not n_reads * cap.  Format them   */
+/* with smash_sam_format(..., cap_per_read = 0, ...).                         */
+int smash_sam_records_packed(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
+                             const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                             const uint64_t *d_match, uint32_t cap_per_read,
+                             const uint32_t *d_n_match, const uint64_t *d_rec_off,
+                             const uint32_t *d_tag_offsets, smash_sam_rec *d_out, void *stream);
 int smash_sam_format(const char *const *contigs, uint32_t n_contig,
                      const smash_sam_rec *h_rec,
                      const uint32_t *h_n, uint32_t cap_per_read, uint64_t n_reads,

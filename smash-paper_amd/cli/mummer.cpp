@@ -363,7 +363,9 @@ struct Device {
   smash_match *mrec = nullptr;
   uint32_t *n = nullptr;
   smash_sam_rec *rec = nullptr;
-  size_t reads_cap = 0, lens_cap = 0, match_cap = 0, mrec_cap = 0, n_cap = 0, rec_cap = 0;
+  uint64_t *off = nullptr;
+  size_t reads_cap = 0, lens_cap = 0, match_cap = 0, mrec_cap = 0, n_cap = 0, rec_cap = 0,
+         off_cap = 0;
   template <class T>
   static void grow(T *&p, size_t &cap, size_t want) {
     if (want <= cap) return;
@@ -374,7 +376,7 @@ struct Device {
   }
   ~Device() {
     for (void *p : {(void *)reads, (void *)lens, (void *)match, (void *)mrec, (void *)n,
-                    (void *)rec})
+                    (void *)rec, (void *)off})
       if (p) (void)hipFree(p);
   }
 };
@@ -446,17 +448,28 @@ void run_batch(const Args &a, const Index &ix, Device &d, Sorter &out,
                        cap, d.n, nullptr),
        "smash_map_batch");
   }
-  Device::grow(d.rec, d.rec_cap, n * cap);
-  ck(smash_sam_records(ix.h, d.reads, stride, dl, fixed ? L : 0, n, d.match, cap, d.n, nullptr,
-                       d.rec, nullptr),
-     "smash_sam_records");
+  // records packed read after read (smash_sam_records_packed): the table is
+  // as large as the matches found, not n * cap
+  std::vector<uint32_t> cnt(n);
+  hk(hipMemcpy(cnt.data(), d.n, 4 * n, hipMemcpyDeviceToHost), "hipMemcpy");
+  std::vector<uint64_t> off(n);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (cnt[i] > cap) throw Fail("a query has more matches than the record cap");
+    off[i] = total;
+    total += cnt[i];
+  }
+  Device::grow(d.off, d.off_cap, n);
+  hk(hipMemcpy(d.off, off.data(), 8 * n, hipMemcpyHostToDevice), "hipMemcpy");
+  Device::grow(d.rec, d.rec_cap, total ? total : 1);
+  ck(smash_sam_records_packed(ix.h, d.reads, stride, dl, fixed ? L : 0, n, d.match, cap, d.n,
+                              d.off, nullptr, d.rec, nullptr),
+     "smash_sam_records_packed");
   hk(hipDeviceSynchronize(), "hipDeviceSynchronize");
   if (!a.sam_out) return;   // query.cpp:404-412: the non-SAM lines are never ended
-  std::vector<smash_sam_rec> rec(n * cap);
-  std::vector<uint32_t> cnt(n);
-  hk(hipMemcpy(rec.data(), d.rec, rec.size() * sizeof(smash_sam_rec), hipMemcpyDeviceToHost),
+  std::vector<smash_sam_rec> rec(total);
+  hk(hipMemcpy(rec.data(), d.rec, total * sizeof(smash_sam_rec), hipMemcpyDeviceToHost),
      "hipMemcpy");
-  hk(hipMemcpy(cnt.data(), d.n, 4 * n, hipMemcpyDeviceToHost), "hipMemcpy");
   std::vector<const char *> names(n), seqs(n), quals(n), opts(n);
   for (uint64_t i = 0; i < n; ++i) {
     names[i] = qs[i].name.c_str();
@@ -467,7 +480,7 @@ void run_batch(const Args &a, const Index &ix, Device &d, Sorter &out,
   char *text = nullptr;
   uint64_t len = 0;
   int32_t terr = 0;
-  ck(smash_sam_format(contigs.data(), uint32_t(contigs.size()), rec.data(), cnt.data(), cap, n,
+  ck(smash_sam_format(contigs.data(), uint32_t(contigs.size()), rec.data(), cnt.data(), 0, n,
                       names.data(), seqs.data(), quals.data(), opts.data(), a.nomap ? 1 : 0, 0,
                       nullptr, &text, &len, &terr),
      "smash_sam_format");

@@ -32,7 +32,8 @@ __global__ __launch_bounds__(kSB) void k_sam_recs(
     const uint16_t *__restrict__ lens, uint32_t L0,
     const uint8_t *__restrict__ text, uint64_t N, const uint64_t *__restrict__ startpos,
     const uint64_t *__restrict__ sizes, uint32_t n_seq, const uint32_t *__restrict__ tag_off,
-    const uint8_t *__restrict__ map, uint64_t map_bytes, smash_sam_rec *__restrict__ out) {
+    const uint8_t *__restrict__ map, uint64_t map_bytes, const uint64_t *__restrict__ off,
+    smash_sam_rec *__restrict__ out) {
   const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t r = t / cap;
   const uint32_t k = uint32_t(t % cap);
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(kSB) void k_sam_recs(
   o.pad = 0;
   o.spare = 0;
   o.reserved = 0;
-  out[r * cap + k] = o;
+  out[(off ? off[r] : r * cap) + k] = o;   // packed: read r's records from off[r]
 }
 
 // ---- host side: one Aligner's prepare_matches + print_matches ------------
@@ -261,11 +262,11 @@ using namespace smash;
 
 static_assert(sizeof(smash_sam_rec) == 40, "smash_sam_rec layout (smashgpu.SAM_REC)");
 
-extern "C" int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
-                                 const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
-                                 const uint64_t *d_match, uint32_t cap_per_read,
-                                 const uint32_t *d_n_match, const uint32_t *d_tag_offsets,
-                                 smash_sam_rec *d_out, void *stream) {
+static int sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
+                       const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                       const uint64_t *d_match, uint32_t cap_per_read, const uint32_t *d_n_match,
+                       const uint64_t *d_rec_off, const uint32_t *d_tag_offsets,
+                       smash_sam_rec *d_out, void *stream) {
   if (!ix || !d_reads || !d_match || !d_n_match || !d_out || !cap_per_read ||
       (!d_lens && (len == 0 || len > 255 || stride < len)) || (d_lens && stride < 255)) {
     set_error("smash_sam_records: bad arguments");
@@ -281,9 +282,32 @@ extern "C" int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, 
   hipLaunchKernelGGL(k_sam_recs, dim3(unsigned((slots + kSB - 1) / kSB)), dim3(kSB), 0, s,
                      d_match, d_n_match, cap_per_read, n_reads, d_reads, stride, d_lens, len,
                      ix->d_text, ix->N, ix->d_startpos, ix->d_sizes, ix->n_seq, d_tag_offsets,
-                     ix->d_map, ix->map_bytes, d_out);
+                     ix->d_map, ix->map_bytes, d_rec_off, d_out);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
+}
+
+extern "C" int smash_sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t stride,
+                                 const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
+                                 const uint64_t *d_match, uint32_t cap_per_read,
+                                 const uint32_t *d_n_match, const uint32_t *d_tag_offsets,
+                                 smash_sam_rec *d_out, void *stream) {
+  return sam_records(ix, d_reads, stride, d_lens, len, n_reads, d_match, cap_per_read, d_n_match,
+                     nullptr, d_tag_offsets, d_out, stream);
+}
+
+extern "C" int smash_sam_records_packed(const smash_index *ix, const uint8_t *d_reads,
+                                        uint64_t stride, const uint16_t *d_lens, uint32_t len,
+                                        uint64_t n_reads, const uint64_t *d_match,
+                                        uint32_t cap_per_read, const uint32_t *d_n_match,
+                                        const uint64_t *d_rec_off, const uint32_t *d_tag_offsets,
+                                        smash_sam_rec *d_out, void *stream) {
+  if (!d_rec_off) {
+    set_error("smash_sam_records_packed: no record offsets");
+    return SMASH_ERR_ARG;
+  }
+  return sam_records(ix, d_reads, stride, d_lens, len, n_reads, d_match, cap_per_read, d_n_match,
+                     d_rec_off, d_tag_offsets, d_out, stream);
 }
 
 extern "C" int smash_sam_format(const char *const *contigs, uint32_t n_contig,
@@ -293,20 +317,27 @@ extern "C" int smash_sam_format(const char *const *contigs, uint32_t n_contig,
                                 const char *const *quals, const char *const *optionals,
                                 int nomap, int tag, const uint8_t *h_small_chr,
                                 char **out_text, uint64_t *out_len, int32_t *tag_error) {
-  if (!contigs || !h_rec || !h_n || !names || !seqs || !out_text || !out_len || !cap_per_read) {
+  if (!contigs || !h_rec || !h_n || !names || !seqs || !out_text || !out_len) {
     set_error("smash_sam_format: bad arguments");
     return SMASH_ERR_ARG;
+  }
+  // cap_per_read 0: packed records (smash_sam_records_packed), read r's
+  // h_n[r] records follow read r-1's; else read r's start at r * cap_per_read
+  std::vector<uint64_t> roff(n_reads);
+  for (uint64_t r = 0, acc = 0; r < n_reads; ++r) {
+    roff[r] = cap_per_read ? r * cap_per_read : acc;
+    acc += h_n[r];
   }
   if (tag_error) *tag_error = 0;
   std::string o;
   o.reserve(n_reads * 256);
   for (uint64_t r = 0; r < n_reads; ++r) {   // every record's contig must be named
-    if (h_n[r] > cap_per_read) {
+    if (cap_per_read && h_n[r] > cap_per_read) {
       set_error("smash_sam_format: a read has more matches than cap_per_read");
       return SMASH_ERR_ARG;
     }
     for (uint32_t k = 0; k < h_n[r]; ++k)
-      if (h_rec[r * cap_per_read + k].tid >= n_contig) {
+      if (h_rec[roff[r] + k].tid >= n_contig) {
         set_error("smash_sam_format: record contig out of range");
         return SMASH_ERR_ARG;
       }
@@ -323,7 +354,7 @@ extern "C" int smash_sam_format(const char *const *contigs, uint32_t n_contig,
       const size_t nl = strlen(nm);
       if (nl >= 2 && nm[nl - 2] == ':' && (nm[nl - 1] == '0' || nm[nl - 1] == '1'))
         m.flag = nm[nl - 1] == '0' ? 65u : 129u;   // Aligner::reset (query.cpp:186-199)
-      prepare(m, h_rec + (i + k) * cap_per_read, h_n[i + k]);
+      prepare(m, h_rec + roff[i + k], h_n[i + k]);
       if (m.printed.empty() && nomap) {   // set_nomap (query.cpp:308-320)
         m.unmapped = true;
         m.flag |= 4u;

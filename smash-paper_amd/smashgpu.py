@@ -50,7 +50,7 @@ EXPORTS = [
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
     "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
-    "smash_phase_map_ahead",
+    "smash_phase_map_ahead", "smash_sam_records_packed",
 ]
 
 
@@ -150,6 +150,8 @@ def lib():
                                          C.c_uint32, vp, vp, vp]
     L.smash_sam_records.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_uint64, vp,
                                     C.c_uint32, vp, vp, vp, vp]
+    L.smash_sam_records_packed.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_uint64, vp,
+                                           C.c_uint32, vp, vp, vp, vp, vp]
     L.smash_sam_format.argtypes = [C.POINTER(C.c_char_p), C.c_uint32, vp, u32p, C.c_uint32, C.c_uint64,
                                    C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
                                    C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int, C.c_int,
@@ -619,10 +621,13 @@ def _cstrs(xs):
 def sam_format(contigs, h_rec, h_n, cap, names, seqs, quals=None, optionals=None, nomap=True,
                tag=False, small_chr=None):
     """Host half of the mapout writer (smash_sam_format, query.cpp:231-415):
-    SAM lines from the per-match records; returns (bytes, tag_error)."""
+    SAM lines from the per-match records (read r's at r * cap, or packed read
+    after read when cap is 0, as sam_records returns them); returns
+    (bytes, tag_error)."""
     h_rec = np.ascontiguousarray(h_rec)
     h_n = np.ascontiguousarray(h_n, np.uint32)
-    assert h_rec.nbytes >= len(names) * cap * SAM_REC.itemsize and len(h_n) == len(names)
+    need = len(names) * cap if cap else int(h_n.astype(np.int64).sum())
+    assert h_rec.nbytes >= need * SAM_REC.itemsize and len(h_n) == len(names)
     sm = None if small_chr is None else np.ascontiguousarray(small_chr, np.uint8)
     out = C.c_void_p()
     olen = C.c_uint64()
@@ -642,21 +647,30 @@ def sam_format(contigs, h_rec, h_n, cap, names, seqs, quals=None, optionals=None
 def sam_records(index: Index, d_reads, n, read_len, cap, tag_offsets=None, min_len=20,
                 stream=None):
     """MAM search + per-match records on the device (smash_map_batch ->
-    smash_sam_records); returns host copies (SAM_REC[n*cap], counts[n])."""
+    smash_sam_records_packed); returns host copies (SAM_REC[sum(counts)] packed
+    read after read, counts[n]).  The record table is sized by the matches
+    found (an exclusive scan of the counts), not by n * cap."""
     import torch
     dev = d_reads.device
     d_m = torch.empty(n * cap, dtype=torch.int64, device=dev)
     d_n = torch.empty(n, dtype=torch.int32, device=dev)
     map_batch(index, d_reads, n, read_len, d_m, cap, d_n, min_len=min_len, stream=stream)
-    d_rec = torch.zeros(n * cap * SAM_REC.itemsize, dtype=torch.uint8, device=dev)
-    d_off = None
+    cnt = d_n.to(torch.int64).clamp_(max=cap)
+    d_off = torch.cumsum(cnt, 0) - cnt
+    total = int(cnt.sum().item()) if n else 0
+    d_rec = torch.empty(max(total, 1) * SAM_REC.itemsize, dtype=torch.uint8, device=dev)
+    d_tag = None
     if tag_offsets is not None:
-        d_off = torch.from_numpy(np.ascontiguousarray(tag_offsets, np.uint32).view(np.int32)).to(dev)
-    check(lib().smash_sam_records(index.h, _ptr(d_reads), read_len, None, read_len, n, _ptr(d_m), cap,
-                                  _ptr(d_n), _ptr(d_off), _ptr(d_rec), vp(_stream(stream))),
-          "smash_sam_records")
+        d_tag = torch.from_numpy(np.ascontiguousarray(tag_offsets, np.uint32).view(np.int32)).to(dev)
+    check(lib().smash_sam_records_packed(index.h, _ptr(d_reads), read_len, None, read_len, n, _ptr(d_m),
+                                         cap, _ptr(d_n), _ptr(d_off), _ptr(d_tag), _ptr(d_rec),
+                                         vp(_stream(stream))),
+          "smash_sam_records_packed")
     torch.cuda.synchronize(dev)
-    return d_rec.cpu().numpy().view(SAM_REC), d_n.cpu().numpy().view(np.uint32).copy()
+    h_n = d_n.cpu().numpy().view(np.uint32).copy()
+    if (h_n > cap).any():
+        raise SmashError("sam_records: a read has more matches than cap")
+    return d_rec[:total * SAM_REC.itemsize].cpu().numpy().view(SAM_REC), h_n
 
 
 def sam_lines(index: Index, d_reads, read_len, names, seqs, quals=None, optionals=None,
@@ -671,7 +685,7 @@ def sam_lines(index: Index, d_reads, read_len, names, seqs, quals=None, optional
     if cap is None:
         cap = read_len - min_len + 1
     h_rec, h_n = sam_records(index, d_reads, n, read_len, cap, tag_offsets, min_len, stream)
-    return sam_format(index.contigs, h_rec, h_n, cap, names, seqs, quals, optionals, nomap,
+    return sam_format(index.contigs, h_rec, h_n, 0, names, seqs, quals, optionals, nomap,
                       tag_offsets is not None, small_chr)
 
 

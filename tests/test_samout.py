@@ -207,8 +207,10 @@ def test_device_records_equal_restatement(tiny_fa, tiny_ix, tables, s):
     d = torch.from_numpy(np.ascontiguousarray(reads)).cuda()
     got, cnt = S.sam_records(gix, d, reads.shape[0], reads.shape[1], cap, tag_offsets=offsets)
     assert cnt.tolist() == ecnt.tolist()
+    off = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))])   # packed, read after read
+    assert len(got) == off[-1]
     for r in range(reads.shape[0]):
-        a, b = got[r * cap:r * cap + cnt[r]], exp[r * cap:r * cap + cnt[r]]
+        a, b = got[off[r]:off[r + 1]], exp[r * cap:r * cap + cnt[r]]
         assert a.tobytes() == b.tobytes(), (r, a, b)
 
 
@@ -233,6 +235,11 @@ def test_formatter_full_lines_equal_reference(tiny_ix, tables, s, tagged):
                               nomap=True, tag=tagged, small_chr=small)
     assert terr == 0
     assert sorted(text.decode().splitlines()) == _golden_full(s, tagged)
+    # the packed layout (cap 0, smash_sam_records_packed) formats identically
+    packed = np.concatenate([rec[r * cap:r * cap + cnt[r]] for r in range(len(cnt))])
+    text0, terr0 = S.sam_format(tiny_ix.contigs, packed, cnt, 0, names, seqs, quals, opts,
+                                nomap=True, tag=tagged, small_chr=small)
+    assert (text0, terr0) == (text, terr)
 
 
 @pytest.mark.parametrize("mode,n,golden,nomap", [("MEM", 60, "s100_60_mapout_MEM_full", True),
