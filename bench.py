@@ -560,6 +560,14 @@ def main():
                 "lines_per_read": {k: round(v[1] / ns, 3) for k, v in emu.counters.items()},
                 "probes_per_read": {k: round(v[0] / ns, 3) for k, v in emu.counters.items()},
                 "loop_iterations_per_read": round(float(emu_it.mean()), 1),
+                # the memory requests the kernel issues (every 16-byte load, the
+                # binary search's speculative SA elements included): with the
+                # lines they bring, the figures of the request-rate ceiling
+                # (tools/randbench req)
+                "requests_per_read": round(emu.requests[0] / ns, 2),
+                "speculative_requests_per_read": round(emu.requests[1] / ns, 2),
+                "requests_G_per_s": round(mam_reads * emu.requests[0] / ns / (active_ms / 1e3) / 1e9, 2),
+                "lines_G_per_s": round(mam_reads * lines / ns / (active_ms / 1e3) / 1e9, 2),
                 "bytes_method": "64 B x line transitions of the kernel's probe sequence "
                                 "(tools/sm_emu on the downloaded index, %d reads)" % ns}
         pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)

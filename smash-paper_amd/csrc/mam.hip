@@ -200,6 +200,10 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.pad = 0;
   c.grab = 16;
   c.bm_dual = 2;
+  c.pf = 1;
+  c.u32 = 1;
+  if (const char *e = std::getenv("SMASH_SM_PF")) c.pf = uint32_t(std::atoi(e));
+  if (const char *e = std::getenv("SMASH_SM_U32")) c.u32 = uint32_t(std::atoi(e));
   if (const char *e = std::getenv("SMASH_SM_BM_DUAL")) c.bm_dual = uint32_t(std::atoi(e));
   if (const char *e = std::getenv("SMASH_SM_GRAB")) c.grab = uint32_t(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("SMASH_SM_PAD")) c.pad = uint32_t(std::atoi(e));

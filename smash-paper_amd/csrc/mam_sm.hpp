@@ -52,6 +52,13 @@
 #ifndef SM_HOOK_PF
 #define SM_HOOK_PF(a)
 #endif
+// byte permute (v_perm_b32): byte i of the result is byte sel_i of the pair
+// {s0 (bytes 4-7), s1 (bytes 0-3)} (8-11: the sign of byte 1/3/5/7 spread,
+// 12: zero); the host emulation substitutes its own
+#ifndef SM_PERM
+#define SM_PERM(s0, s1, sel) __builtin_amdgcn_perm(s0, s1, sel)
+#endif
+
 // STATS builds: count the wave iterations in which a code region runs (any
 // lane active in it), wave_stats[64 + k]; the regions' costs are paid per
 // such iteration (tools/isa_regions.py gives their static VALU)
@@ -102,6 +109,7 @@ inline Geom make_geom(uint32_t max_len) {
   Geom g;
   g.w_raw = (max_len + 11) / 4;      // lds_load8 at offset <= L-1 reads 3 words
   g.w_row = (g.w_raw + 3) & ~3u;
+  if (g.w_row < 8) g.w_row = 8;      // codes_raw reads 6 words from q <= w_row - 6
   g.c_bad = max_len > 128 ? 2 : 1;
   g.chunks = g.c_bad + (g.w_row + 3) / 4;
   return g;
@@ -207,7 +215,7 @@ enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
 enum : uint32_t { O_EXT = 0, O_BS };
 // ALU continuations, in the order the decide chain runs them
 enum : uint32_t { A_NONE = 0, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE, A_EXPAND,
-                  A_AFTER, A_TOP, A_TRAV, A_DONE };
+                  A_AFTER, A_ROOT, A_TOP, A_TRAV, A_DONE };
 // binary-search modes: 0 where P' sorts (traverse); 1 / 2 the left / right
 // end of a run of suffixes sharing `cap` characters (from `cbase`) with P
 enum : uint32_t { BS_INSERT = 0, BS_LEFT, BS_RIGHT };
@@ -245,6 +253,48 @@ __device__ __forceinline__ uint32_t byte_mask(const uint4 &v, F f) {
     m |= uint32_t(f(b, i)) << i;
   }
   return m;
+}
+
+// packed 16-bit subtract (v_pk_sub_u16): both halves, no borrow between them
+#ifndef SM_PK_SUB16
+typedef unsigned short sm_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(sm_u16x2, a) - __builtin_bit_cast(sm_u16x2, b));
+}
+#define SM_PK_SUB16(a, b) ::smash::sm::pk_sub16(a, b)
+#endif
+
+// 4-bit mask, bit j: (t_j - byte j of w) is negative, for 16-bit thresholds
+// t_j in [-32768, 32767] given as packed halves te = (t0, t2), to = (t1, t3).
+// The bytes go to 16-bit lanes by two byte permutes, two packed subtracts
+// compare them, a third permute spreads the four sign bits to bytes (selectors
+// 8-11) and one multiply gathers them: 9 VALU per 4 bytes instead of a
+// compare and a select per byte.
+__device__ __forceinline__ uint32_t gt4(uint32_t w, uint32_t te, uint32_t to) {
+  const uint32_t e = SM_PERM(w, w, 0x0c020c00u), o = SM_PERM(w, w, 0x0c030c01u);
+  const uint32_t r = SM_PERM(SM_PK_SUB16(to, o), SM_PK_SUB16(te, e), 0x0b090a08u);
+  return ((r & 0x80808080u) * 0x00204081u) >> 28;
+}
+// mask bit i (0..15): byte i of the block > t_i = base - i (base <= 255 + 16)
+__device__ __forceinline__ uint32_t gt_desc_mask(const uint4 &v, uint32_t base) {
+  const uint32_t bp = base * 0x00010001u;
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t te = bp - ((4 * k) | ((4 * k + 2) << 16));
+    const uint32_t to = bp - ((4 * k + 1) | ((4 * k + 3) << 16));
+    m |= gt4(dword_at(v, k), te, to) << (4 * k);
+  }
+  return m;
+}
+// mask bit i (0..15): byte i of the block < t (t <= 255)
+__device__ __forceinline__ uint32_t lt_mask(const uint4 &v, uint32_t t) {
+  // b < t  <=>  b > t - 1  is false: the complement of gt with t - 1
+  const uint32_t tp = (t - 1) * 0x00010001u;
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) m |= gt4(dword_at(v, k), tp, tp) << (4 * k);
+  return ~m & 0xFFFFu;
 }
 
 // one bit of a lane's flag word, used like a bool
@@ -289,22 +339,31 @@ struct Bad {   // the read's bad mask (registers; named, never an array)
 };
 
 // 2-bit codes (a0 c1 g2 t3) of the 4 lowercase bytes of w, first byte most
-// significant: code = ((b >> 1) ^ (b >> 2)) & 3 for a c g t, and one
-// multiply gathers the four 2-bit fields (no carries: the partial products
-// land on disjoint bits).  Other bytes give garbage (callers check `bad`).
+// significant.  The low 3 bits of a c g t are 1 3 7 4, so one byte permute
+// over an 8-entry table {1: 0, 3: 1, 7: 2, 4: 3} turns each byte into its
+// code, and one multiply gathers the four 2-bit fields (no carries: the
+// partial products land on disjoint bits).  Other bytes give garbage
+// (callers check `bad`).
 __device__ __forceinline__ uint32_t byte4_codes(uint32_t w) {
-  return ((((w >> 1) ^ (w >> 2)) & 0x03030303u) * 0x40100401u) >> 24;
+  const uint32_t cb = SM_PERM(0x02000003u, 0x01000000u, w & 0x07070707u);
+  return (cb * 0x40100401u) >> 24;
 }
 
-// 2n code bits of bases [p, p+n) of the LDS row R (first base most
-// significant), n <= 20; reads only the words holding those bases
-__device__ __forceinline__ uint64_t codes_raw(const uint32_t *R, uint32_t p, uint32_t n) {
-  const uint32_t q = p >> 2, sh = p & 3, nw = (sh + n + 3) >> 2;
-  uint64_t x = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 6; ++k)
-    if (k < nw) x = (x << 8) | byte4_codes(R[q + k]);
-  return (x >> (8 * nw - 2 * (sh + n))) & ((1ull << (2 * n)) - 1);
+// 2n code bits of bases [p, p+n) of the LDS row R of w_row words (first base
+// most significant), n <= 21: always the 6 words from q (24 bases, no
+// branches), q clamped so that they stay inside the row (p + n <= L <=
+// 4 w_row - 8 keeps [p, p+n) inside them: sh + n <= 24)
+__device__ __forceinline__ uint64_t codes_raw(const uint32_t *R, uint32_t w_row, uint32_t p,
+                                              uint32_t n) {
+  const uint32_t q0 = p >> 2, qm = w_row - 6;
+  const uint32_t q = q0 < qm ? q0 : qm, sh = p - 4 * q;
+  uint32_t hi = byte4_codes(R[q]);
+  hi = (hi << 8) | byte4_codes(R[q + 1]);
+  hi = (hi << 8) | byte4_codes(R[q + 2]);
+  hi = (hi << 8) | byte4_codes(R[q + 3]);
+  const uint32_t lo = (byte4_codes(R[q + 4]) << 8) | byte4_codes(R[q + 5]);
+  const uint64_t x = (uint64_t(hi) << 16) | lo;
+  return (x >> (48 - 2 * (sh + n))) & ((1ull << (2 * n)) - 1);
 }
 
 template <class IdxT>
@@ -324,6 +383,8 @@ struct Ctx {
   uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
   uint32_t bm_dual;       // (F): 0 one B-mer word per iteration, 1 last + first in one,
                           // 2 the cover policy (two words per iteration chosen by mode)
+  uint32_t pf;            // binary-search compares also load the children's SA elements
+  uint32_t u32;           // (B) U scans load 32 bytes per iteration (else 16)
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -423,7 +484,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     dch = d; j = 1;
     addr = reinterpret_cast<uint64_t>(c.U + p + 1);
     addr2 = addr + 16;
-    need2 = d - 1 > 16;
+    need2 = c.u32 && d - 1 > 16;
     st = S_USCAN;
   };
   // a run [es, ee] grows within [lb, hb] while L8 >= xd: both sides' first
@@ -433,9 +494,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   auto bs_probe = [&]() {   // compare P' with T[sp + cbase + lc ...] (sp = SA[m])
     addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
-    need2 = lo < m;
-    pfr = m + 1 < hi;
-    pf = true;
+    need2 = c.pf && lo < m;
+    pfr = c.pf && m + 1 < hi;
+    pf = c.pf != 0;
     st = S_CMP; op = O_BS;
   };
   auto lblock = [&](uint64_t e) { return reinterpret_cast<uint64_t>(c.L8 + (e >= 15 ? e - 15 : 0)); };
@@ -547,10 +608,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
         bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
         need2 = false;
-        prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
+        prefix = 0; nem = 0;
         skip_f = false; fm = 0; ktr_set = false;
         clean = (bad.w0 | bad.w1 | bad.w2 | bad.w3 | bad.w4 | bad.w5 | bad.w6 | bad.w7) == 0;
-        a = A_TOP;
+        a = A_ROOT;
         break;
       }
       case S_BM: {                                   // (F) last, then first B-mer present?
@@ -593,15 +654,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             ktr_set = true;
           } else {
             fm = nfm;
-            if (adv) { depth = 0; start = 0; end = N - 1; have_pos = false; prefix += adv; }
+            prefix += adv;
           }
-          a = A_TOP;
+          a = adv ? A_ROOT : A_TOP;
         } else if (!pa && !bm2) {
-          depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix += c.min_len - c.B + 1;
-          a = A_TOP;
+          a = A_ROOT;
         } else if (!pa || !pb) {
-          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
+          ++prefix; a = A_ROOT;
         } else if (!bm2 && !c.bm_dual) {
           bm2 = true;
           addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
@@ -638,8 +698,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {                                      // O_NS_ISA2
           start = iv; end = iv2; need2 = false;
           ++prefix; have_pos = false;
-          if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
-          else a = A_EXPAND;
+          a = depth == 0 ? A_ROOT : A_EXPAND;
         }
         break;
       }
@@ -714,7 +773,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           const uint32_t D = dch - j;
           const uint32_t lim = D < 16 ? D : 16u;
           const uint32_t inr = (1u << lim) - 1;
-          const uint32_t hm = byte_mask(u, [&](uint32_t b, uint32_t i) { return b + i >= D; }) & inr;
+          const uint32_t hm = gt_desc_mask(u, D - 1) & inr;   // U[.+i] + i >= D
           if (hm) {
             j += uint32_t(__builtin_ctz(hm)); hit = true; fin = true;
           } else {
@@ -728,7 +787,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {
           addr += need2 ? 32 : 16;
           addr2 = addr + 16;
-          need2 = dch - j > 16;
+          need2 = c.u32 && dch - j > 16;
         }
         break;
       }
@@ -744,7 +803,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           const uint64_t room = left ? es - lb : hb - ee;
           const uint32_t w = left ? o + 1 : 16 - o;
           const uint32_t lim = room < uint64_t(w) ? uint32_t(room) : w;
-          const uint32_t below = byte_mask(u, [&](uint32_t b, uint32_t) { return b < xd; });
+          const uint32_t below = lt_mask(u, xd);
           const uint32_t win = left ? (((1u << lim) - 1) << (o + 1 - lim)) : (((1u << lim) - 1) << o);
           const uint32_t sm = below & win;
           const uint32_t k = sm ? (left ? o - (31 - __builtin_clz(sm)) : uint32_t(__builtin_ctz(sm)) - o)
@@ -828,8 +887,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       const uint64_t hb = xrun ? end : N - 1;
       nblk = 0;
       if (!xrun && start - es >= thresh) {            // expand_link gives up (longSA.h:164)
-        depth = 0; start = 0; end = N - 1; have_pos = false;
-        a = A_TOP;
+        a = A_ROOT;
       } else if (ee < hb && !rdone) {
         addr = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
         st = S_EXR;
@@ -844,8 +902,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         start = es; end = ee; depth = xd; pos = bpos; have_pos = start == end;
         a = A_AFTER;
       } else if ((start - es) + (ee - end) >= thresh) {
-        depth = 0; start = 0; end = N - 1; have_pos = false;
-        a = A_TOP;
+        a = A_ROOT;
       } else {                                        // expand_link succeeded
         start = es; end = ee;
         a = A_TOP;
@@ -855,8 +912,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       SM_REGION(14);
       prefix += j;
       if (!hit) {
-        depth = 0; start = 0; end = N - 1; have_pos = false;
-        a = A_TOP;
+        a = A_ROOT;
       } else {
         depth = dch - j;
         addr = ia(c.ISA, pos + j);
@@ -877,8 +933,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     if (a == A_AFTER) {
       SM_REGION(16);
       if (depth <= 1) {
-        depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
-        a = A_TOP;
+        ++prefix;
+        a = A_ROOT;
       } else {
         a = A_NONE;
         if (start != end) {                          // non-singleton suffix link
@@ -899,6 +955,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           uscan_start(pos, depth);
         }
       }
+    }
+    if (a == A_ROOT) {                                // a new search from the root at prefix
+      depth = 0; start = 0; end = N - 1; have_pos = false;
+      a = A_TOP;
     }
     if (a == A_TOP) {
       SM_REGION(17);
@@ -940,23 +1000,23 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           fm = 0;
         }
         if (kb >= 0) {                                // absent byte: next window
-          depth = 0; start = 0; end = N - 1; have_pos = false;
-          prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
+          prefix = uint32_t(kb) + 1;                  // (A_ROOT, A_TOP again: parks in S_ALU)
           fm = 0;
+          a = A_ROOT;
         } else if (B > 0 && B <= c.min_len && ok) {
           // both codes from one pass over the row when the span allows
           const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;
           const uint32_t span = hi_s + B - lo_s;
           if (span <= 21) {
             SM_REGION(21);
-            const uint64_t X = codes_raw(row, lo_s, span);
+            const uint64_t X = codes_raw(row, c.w_row, lo_s, span);
             const uint64_t mk = (1ull << (2 * B)) - 1;
             c1 = (X >> (2 * (lo_s + span - s1 - B))) & mk;
             c0 = (X >> (2 * (lo_s + span - s2 - B))) & mk;
           } else {
             SM_REGION(22);
-            c0 = codes_raw(row, s2, B);
-            c1 = codes_raw(row, s1, B);
+            c0 = codes_raw(row, c.w_row, s2, B);
+            c1 = codes_raw(row, c.w_row, s1, B);
           }
           addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
           st = S_BM; bm2 = false;
@@ -971,7 +1031,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         if (depth == 0 && prefix + c.K <= L && (clean || bad.bits(prefix, c.K) == 0)) {
           // the window's first B-mer code (c.B >= c.K) from the filter pass
           SM_REGION(23);
-          const uint64_t kc = ktr ? m : codes_raw(row, prefix, c.K);
+          const uint64_t kc = ktr ? m : codes_raw(row, c.w_row, prefix, c.K);
           addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
           st = S_KT;
           a = A_NONE;

@@ -83,3 +83,21 @@ def test_state_machine_on_mid_genome():
         got, _ = emu.map(reads, lin_blocks=lin)
         for i in range(len(reads)):
             assert got[i] == ix.search(reads[i].tobytes()), (lin, i)
+
+
+@pytest.mark.parametrize("pf", ["0", "1"])
+def test_request_accounting(emu, pf, monkeypatch):
+    """tools/sm_emu's request count (bench.py roofline: requests_per_read):
+    every probe is at least one request, every line transition one of them,
+    speculative loads only with the binary-search prefetch (SMASH_SM_PF)."""
+    monkeypatch.setenv("SMASH_SM_PF", pf)
+    e = emu[1]
+    got, _ = e.map(interleaved_reads("s150"))
+    lines = sum(v[1] for v in e.counters.values())
+    probes = sum(v[0] for v in e.counters.values())
+    allr, spec = e.requests
+    assert lines <= allr and spec <= allr
+    assert (spec > 0) == (pf == "1")
+    assert allr <= probes + spec + len(got) * 4   # + the record lines per read
+    print("requests/read %.1f (spec %.1f) probes/read %.1f lines/read %.1f" % (
+        allr / len(got), spec / len(got), probes / len(got), lines / len(got)))

@@ -2,7 +2,7 @@
 // as a function of the footprint (the access pattern of the MAM search:
 // every lane follows its own chain of dependent probes into a ~144 GB index).
 //
-//   randbench <GiB list...>
+//   randbench <GiB list...>  |  randbench lines <GiB...>  |  randbench req  |  randbench calib
 // For each footprint: lanes = waves_per_simd * 4 * CUs * 64 chains, each doing
 // `steps` dependent 16-byte loads at hashed addresses; prints loads/s and the
 // 64-B-line rate.  Also an "ilp" variant with 4 independent chains per lane.
@@ -82,6 +82,32 @@ __global__ __launch_bounds__(256) void k_chase_ua(const uint8_t *buf, uint64_t n
   if (acc == 0x123456789ull) sink[0] = acc;
 }
 
+// the request-rate ceilings without a modulo in the address math (power-of-
+// two footprints, a multiply-shift hash): per step one 16-byte load at a
+// random line (a miss beyond the caches) and W - 1 more 16-byte loads to the
+// SAME line (requests that hit): the cost of a miss and of a hit request,
+// the two kinds the MAM search issues (new lines; re-probes of a line it
+// just touched, second blocks, prefetch elements)
+template <int W>
+__global__ __launch_bounds__(256) void k_req(const uint4 *buf, uint64_t mask16, int steps,
+                                             uint64_t *sink, uint64_t seed) {
+  const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+  uint64_t h = mix(t + seed);
+  uint32_t acc = 0;
+  for (int s = 0; s < steps; ++s) {
+    const uint64_t i = ((h >> 17) & mask16) & ~uint64_t(3);
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const uint4 v = buf[i + (k & 3)];
+      x += v.x ^ v.w;
+    }
+    acc += x;
+    h = (h + x + 1) * 0x9E3779B97F4A7C15ull;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main(int argc, char **argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -100,6 +126,45 @@ int main(int argc, char **argv) {
     CK(hipDeviceSynchronize());
     std::printf("calib: %llu random 16-byte loads (%llu threads x %d) over 64 GiB\n",
                 (unsigned long long)(threads * steps), (unsigned long long)threads, steps);
+    return 0;
+  }
+  if (argc > 1 && std::string(argv[1]) == "req") {
+    uint64_t *sink;
+    CK(hipMalloc(&sink, 8));
+    for (int lg : {-5, -2, 2, 6, 7}) {   // 32 MiB (L2-sized), 256 MiB (Infinity Cache), 4-128 GiB
+      const uint64_t bytes = lg < 0 ? (1ull << 30) >> -lg : (1ull << 30) << lg;
+      void *buf = nullptr;
+      CK(hipMalloc(&buf, bytes));
+      CK(hipMemset(buf, 0, bytes));
+      for (int wps : {4, 8}) {
+        for (int w : {1, 2, 3}) {
+          const uint64_t threads = uint64_t(wps) * 4 * cus * 64;
+          const int steps = 64;
+          auto launch = [&](uint64_t seed) {
+            if (w == 1) k_req<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
+            else if (w == 2) k_req<2><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
+            else k_req<3><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
+          };
+          hipEvent_t a, b;
+          CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+          launch(1);
+          CK(hipDeviceSynchronize());
+          CK(hipEventRecord(a));
+          for (int r = 0; r < 3; ++r) launch(100 + r);
+          CK(hipEventRecord(b));
+          CK(hipEventSynchronize(b));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, a, b));
+          const double lines = 3.0 * threads * steps;
+          std::printf("req footprint %9.4f GiB  waves/SIMD %d  %d x 16 B per random line : %7.3f G lines/s  %7.3f G requests/s  %.3f ns per line\n",
+                      double(bytes) / (1ull << 30), wps, w, lines / (ms * 1e-3) * 1e-9,
+                      w * lines / (ms * 1e-3) * 1e-9, ms * 1e6 / lines);
+          std::fflush(stdout);
+          CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
+        }
+      }
+      CK(hipFree(buf));
+    }
     return 0;
   }
   std::vector<double> gib;

@@ -16,6 +16,15 @@ static const uint64_t *emu_spans;
 static uint64_t emu_rec_lo, emu_rec_hi, emu_bad;
 static uint64_t emu_probes[8], emu_lines[8], emu_last[8];
 static unsigned long long emu_ws[64];   // the kernel's STATS counters of the last run
+// every request the device issues: each 16-byte load (one per 64-byte line it
+// touches), speculative ones included ([1] counts those), the row DMA one per
+// line of its chunks
+static uint64_t emu_req[2];
+static void emu_reqs(uint64_t a, uint64_t n, bool spec) {
+  const uint64_t k = ((a + n - 1) >> 6) - (a >> 6) + 1;
+  emu_req[0] += k;
+  if (spec) emu_req[1] += k;
+}
 // the 16 bytes at address a, exactly (the kernel aligns the blocks it wants
 // aligned); a block crossing a 64-byte line is two requests and touches two
 // lines
@@ -34,6 +43,7 @@ static void emu_count(int arr, uint64_t a, uint64_t n) {
 }
 static uint4 emu_load16(uint64_t a, bool count = true) {
   const int arr = emu_array(a);
+  if (arr != 7) emu_reqs(a, 16, !count);   // (record chunks: counted by the DMA / below)
   if (arr < 0) { ++emu_bad; return uint4{0, 0, 0, 0}; }
   if (count) emu_count(arr, a, 16);
   // the block may run past the array: copy the valid bytes
@@ -57,6 +67,7 @@ static uint4 emu_load16(uint64_t a, bool count = true) {
 template <class IdxT>
 static uint64_t emu_loadidx(const IdxT *p, uint64_t i) {
   if (emu_array(reinterpret_cast<uint64_t>(p + i)) < 0) { ++emu_bad; return 0; }
+  emu_reqs(reinterpret_cast<uint64_t>(p + i), sizeof(IdxT), true);
   return uint64_t(p[i]);
 }
 #define SM_LOADIDX(p, i) emu_loadidx(p, i)
@@ -69,6 +80,10 @@ static void emu_hook_pf(uint64_t a, uint64_t n) {
 // the record's first chunks (next iteration) lies on the line the DMA's
 // first chunk opened: the record's 192 bytes are 3 line transitions
 static void emu_dma_row(uint32_t *dst, const uint4 *src, uint32_t n, const uint4 *rec0) {
+  // one instruction: its lanes' chunks coalesce per line; the lane's own
+  // bad-mask load next iteration is one more request per line it touches
+  emu_req[0] += ((reinterpret_cast<uint64_t>(src + n) - 1) >> 6) - (reinterpret_cast<uint64_t>(src) >> 6) + 1;
+  emu_req[0] += ((reinterpret_cast<uint64_t>(src) - 1) >> 6) - (reinterpret_cast<uint64_t>(rec0) >> 6) + 1;
   for (uint32_t k = 0; k < n; ++k) {
     const uint4 v = emu_load16(reinterpret_cast<uint64_t>(src + k));
     std::memcpy(dst + 4 * k, &v, 16);
@@ -78,6 +93,27 @@ static void emu_dma_row(uint32_t *dst, const uint4 *src, uint32_t n, const uint4
 #define SM_DMA_ROW(dst, src, n, lane) emu_dma_row(dst, src, n, (src) - c.c_bad)
 #define SM_DMA_ROW_HOST
 #define PAD_KEEP(x) ((void)(x))
+// v_perm_b32 on the host: byte i of the result from selector byte i (0-7 a
+// byte of {s0:s1}, 8-11 the sign of byte 1/3/5/7 spread, 12 zero, 13+ 0xFF)
+static uint32_t emu_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t v = (uint64_t(s0) << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t b = (sel >> (8 * i)) & 0xFF;
+    uint32_t o = 0;
+    if (b < 8) o = uint32_t(v >> (8 * b)) & 0xFF;
+    else if (b < 12) o = ((v >> (16 * (b - 8) + 15)) & 1) ? 0xFF : 0;
+    else if (b > 12) o = 0xFF;
+    r |= o << (8 * i);
+  }
+  return r;
+}
+#define SM_PERM(s0, s1, sel) emu_perm(s0, s1, sel)
+// v_pk_sub_u16 on the host: both 16-bit halves, no borrow between them
+static uint32_t emu_pk_sub16(uint32_t a, uint32_t b) {
+  return ((a - b) & 0xFFFFu) | (((a >> 16) - (b >> 16)) << 16);
+}
+#define SM_PK_SUB16(a, b) emu_pk_sub16(a, b)
 // traverse binary searches by interval size (1..63, 64 = larger) and start depth
 static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
 #define SM_HOOK_BM(mode, a1, a2) (++emu_bm[4 * (mode) + 2 * (a1) + (a2)])
@@ -125,6 +161,8 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   c.pad = 0;
   c.grab = 1;
   c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 2;   // = the device default (mam.hip)
+  c.pf = std::getenv("SMASH_SM_PF") ? uint32_t(std::atoi(std::getenv("SMASH_SM_PF"))) : 1;
+  c.u32 = std::getenv("SMASH_SM_U32") ? uint32_t(std::atoi(std::getenv("SMASH_SM_U32"))) : 1;
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
   c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
@@ -143,6 +181,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   emu_rec_hi = emu_rec_lo + rec.size() * sizeof(uint4);
   emu_bad = 0;
   for (int k = 0; k < 8; ++k) { emu_probes[k] = emu_lines[k] = 0; emu_last[k] = ~0ull; }
+  emu_req[0] = emu_req[1] = 0;
   sm::k_mam_sm<IdxT, 1, true, true>(c);
   for (int k = 0; k < 10; ++k) viol[k] = v[k];
   viol[0] += emu_bad;
@@ -156,6 +195,9 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
 extern "C" void sm_emu_ws(uint64_t *out) {
   for (int k = 0; k < 64; ++k) out[k] = emu_ws[k];
 }
+
+// device requests of the last sm_emu_map: [0] all, [1] speculative
+extern "C" void sm_emu_requests(uint64_t *out) { out[0] = emu_req[0]; out[1] = emu_req[1]; }
 
 // binary-search start histograms since the last reset (size[65], depth[256])
 extern "C" void sm_emu_bs_hist(uint64_t *size, uint64_t *depth, int reset) {

@@ -120,6 +120,9 @@ class Emu:
             w = out[i * cap:i * cap + k]
             res.append([(int(x & 0xFFFFFFFFFFFF), int((x >> 48) & 0xFF), int(x >> 56)) for x in w])
         self.counters = {name: (int(ctr[k]), int(ctr[8 + k])) for k, name in enumerate(ARRAYS)}
+        rq = np.zeros(2, np.uint64)
+        lib().sm_emu_requests(rq.ctypes.data_as(C.c_void_p))
+        self.requests = (int(rq[0]), int(rq[1]))   # device requests (all, speculative)
         ws = np.zeros(64, np.uint64)
         lib().sm_emu_ws(ws.ctypes.data_as(C.c_void_p))
         self.states = {}
