@@ -215,7 +215,7 @@ enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
 enum : uint32_t { O_EXT = 0, O_BS };
 // ALU continuations, in the order the decide chain runs them
 enum : uint32_t { A_NONE = 0, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE, A_EXPAND,
-                  A_AFTER, A_ROOT, A_TOP, A_TRAV, A_DONE };
+                  A_AFTER, A_TOP, A_TRAV, A_DONE };
 // binary-search modes: 0 where P' sorts (traverse); 1 / 2 the left / right
 // end of a run of suffixes sharing `cap` characters (from `cbase`) with P
 enum : uint32_t { BS_INSERT = 0, BS_LEFT, BS_RIGHT };
@@ -275,26 +275,21 @@ __device__ __forceinline__ uint32_t gt4(uint32_t w, uint32_t te, uint32_t to) {
   const uint32_t r = SM_PERM(SM_PK_SUB16(to, o), SM_PK_SUB16(te, e), 0x0b090a08u);
   return ((r & 0x80808080u) * 0x00204081u) >> 28;
 }
-// mask bit i (0..15): byte i of the block > t_i = base - i (base <= 255 + 16)
-__device__ __forceinline__ uint32_t gt_desc_mask(const uint4 &v, uint32_t base) {
-  const uint32_t bp = base * 0x00010001u;
+// mask bit i (0..15): byte i of the block > t_i, with t_i = base - i (desc)
+// or base; thresholds below -32768 or above 32767 do not occur (base <= 271)
+__device__ __forceinline__ uint32_t thr_mask(const uint4 &v, uint32_t base, bool desc) {
+  const uint32_t bp = base * 0x00010001u, s4 = desc ? 0x00040004u : 0u;
+  // (a lane below zero borrows from its upper neighbour, whose index is larger:
+  // both lie past the bytes the callers keep)
+  uint32_t te = bp - (desc ? 0x00020000u : 0u), to = bp - (desc ? 0x00030001u : 0u);
   uint32_t m = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t te = bp - ((4 * k) | ((4 * k + 2) << 16));
-    const uint32_t to = bp - ((4 * k + 1) | ((4 * k + 3) << 16));
     m |= gt4(dword_at(v, k), te, to) << (4 * k);
+    te -= s4;
+    to -= s4;
   }
   return m;
-}
-// mask bit i (0..15): byte i of the block < t (t <= 255)
-__device__ __forceinline__ uint32_t lt_mask(const uint4 &v, uint32_t t) {
-  // b < t  <=>  b > t - 1  is false: the complement of gt with t - 1
-  const uint32_t tp = (t - 1) * 0x00010001u;
-  uint32_t m = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) m |= gt4(dword_at(v, k), tp, tp) << (4 * k);
-  return ~m & 0xFFFFu;
 }
 
 // one bit of a lane's flag word, used like a bool
@@ -596,6 +591,18 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     const uint32_t ao = st >= S_BYTE ? 0u : uint32_t(addr) & 15;   // element offset in v
     uint32_t a = A_NONE;
     SM_REGION(0);
+    // the scan states' byte masks, one computation shared by all four (their
+    // bodies would otherwise each pay for it): bit i of mv / mv2 is byte i of
+    // v / v2 > t_i, t_i = D - 1 - i for the U scan (U[.+i] + i >= D, D =
+    // dch - j; v2 continues at D - 16) and xd - 1 for L8 runs (the complement:
+    // L8 < xd, a stop)
+    uint32_t mv = 0, mv2 = 0;
+    if (st >= S_USCAN) {
+      const bool us = st == S_USCAN;
+      const uint32_t base = us ? dch - j - 1 : xd - 1;
+      mv = thr_mask(v, base, us);
+      mv2 = thr_mask(v2, us ? base - 16 : base, us);
+    }
 
     // ---------------- consume ----------------
     switch (st) {
@@ -608,10 +615,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
         bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
         need2 = false;
-        prefix = 0; nem = 0;
+        prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
         skip_f = false; fm = 0; ktr_set = false;
         clean = (bad.w0 | bad.w1 | bad.w2 | bad.w3 | bad.w4 | bad.w5 | bad.w6 | bad.w7) == 0;
-        a = A_ROOT;
+        a = A_TOP;
         break;
       }
       case S_BM: {                                   // (F) last, then first B-mer present?
@@ -654,14 +661,15 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             ktr_set = true;
           } else {
             fm = nfm;
-            prefix += adv;
+            if (adv) { depth = 0; start = 0; end = N - 1; have_pos = false; prefix += adv; }
           }
-          a = adv ? A_ROOT : A_TOP;
+          a = A_TOP;
         } else if (!pa && !bm2) {
+          depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix += c.min_len - c.B + 1;
-          a = A_ROOT;
+          a = A_TOP;
         } else if (!pa || !pb) {
-          ++prefix; a = A_ROOT;
+          depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
         } else if (!bm2 && !c.bm_dual) {
           bm2 = true;
           addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
@@ -698,7 +706,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {                                      // O_NS_ISA2
           start = iv; end = iv2; need2 = false;
           ++prefix; have_pos = false;
-          a = depth == 0 ? A_ROOT : A_EXPAND;
+          if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
+          else a = A_EXPAND;
         }
         break;
       }
@@ -769,11 +778,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
 #pragma unroll
         for (uint32_t h = 0; h < 2; ++h) {
           if (fin || (h == 1 && !need2)) break;
-          const uint4 &u = h ? v2 : v;
           const uint32_t D = dch - j;
           const uint32_t lim = D < 16 ? D : 16u;
           const uint32_t inr = (1u << lim) - 1;
-          const uint32_t hm = gt_desc_mask(u, D - 1) & inr;   // U[.+i] + i >= D
+          const uint32_t hm = (h ? mv2 : mv) & inr;   // U[.+i] + i >= D
           if (hm) {
             j += uint32_t(__builtin_ctz(hm)); hit = true; fin = true;
           } else {
@@ -799,11 +807,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         // run members before the stop in one block, walking down (left:
         // bytes (o-lim, o]) or up (right: bytes [o, o+lim)); *more: no stop
         // in the window and room beyond it
-        auto side = [&](const uint4 &u, uint32_t o, bool left, bool &more) {
+        auto side = [&](uint32_t mask, uint32_t o, bool left, bool &more) {
           const uint64_t room = left ? es - lb : hb - ee;
           const uint32_t w = left ? o + 1 : 16 - o;
           const uint32_t lim = room < uint64_t(w) ? uint32_t(room) : w;
-          const uint32_t below = lt_mask(u, xd);
+          const uint32_t below = ~mask & 0xFFFFu;      // L8 < xd
           const uint32_t win = left ? (((1u << lim) - 1) << (o + 1 - lim)) : (((1u << lim) - 1) << o);
           const uint32_t sm = below & win;
           const uint32_t k = sm ? (left ? o - (31 - __builtin_clz(sm)) : uint32_t(__builtin_ctz(sm)) - o)
@@ -815,10 +823,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         // the left block ends at es (position es - its start), the right one
         // starts at ee + 1 (position 0)
         if (st != S_EXR)
-          es -= side(v, uint32_t(es - (addr - reinterpret_cast<uint64_t>(c.L8))), true, moreL);
+          es -= side(mv, uint32_t(es - (addr - reinterpret_cast<uint64_t>(c.L8))), true, moreL);
         if (st != S_EXL) {
           const bool b2 = st == S_EXB;
-          ee += side(b2 ? v2 : v, 0u, false, moreR);
+          ee += side(b2 ? mv2 : mv, 0u, false, moreR);
           if (b2) rdone = !moreR;
         }
         need2 = false;
@@ -887,7 +895,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       const uint64_t hb = xrun ? end : N - 1;
       nblk = 0;
       if (!xrun && start - es >= thresh) {            // expand_link gives up (longSA.h:164)
-        a = A_ROOT;
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        a = A_TOP;
       } else if (ee < hb && !rdone) {
         addr = reinterpret_cast<uint64_t>(c.L8 + ee + 1);
         st = S_EXR;
@@ -902,7 +911,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         start = es; end = ee; depth = xd; pos = bpos; have_pos = start == end;
         a = A_AFTER;
       } else if ((start - es) + (ee - end) >= thresh) {
-        a = A_ROOT;
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        a = A_TOP;
       } else {                                        // expand_link succeeded
         start = es; end = ee;
         a = A_TOP;
@@ -912,7 +922,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       SM_REGION(14);
       prefix += j;
       if (!hit) {
-        a = A_ROOT;
+        depth = 0; start = 0; end = N - 1; have_pos = false;
+        a = A_TOP;
       } else {
         depth = dch - j;
         addr = ia(c.ISA, pos + j);
@@ -933,8 +944,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     if (a == A_AFTER) {
       SM_REGION(16);
       if (depth <= 1) {
-        ++prefix;
-        a = A_ROOT;
+        depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
+        a = A_TOP;
       } else {
         a = A_NONE;
         if (start != end) {                          // non-singleton suffix link
@@ -955,10 +966,6 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           uscan_start(pos, depth);
         }
       }
-    }
-    if (a == A_ROOT) {                                // a new search from the root at prefix
-      depth = 0; start = 0; end = N - 1; have_pos = false;
-      a = A_TOP;
     }
     if (a == A_TOP) {
       SM_REGION(17);
@@ -1000,9 +1007,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           fm = 0;
         }
         if (kb >= 0) {                                // absent byte: next window
-          prefix = uint32_t(kb) + 1;                  // (A_ROOT, A_TOP again: parks in S_ALU)
+          depth = 0; start = 0; end = N - 1; have_pos = false;
+          prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
           fm = 0;
-          a = A_ROOT;
         } else if (B > 0 && B <= c.min_len && ok) {
           // both codes from one pass over the row when the span allows
           const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;

@@ -40,6 +40,11 @@ struct smash_pipeline {
   uint8_t *d_small = nullptr;
   int64_t *d_chrom_off = nullptr;
   int64_t *d_bins = nullptr;
+  // bin directory: cell c = [c << cshift, (c + 1) << cshift) of the absolute
+  // position; d_cell[c] = bisect_right(bins, c << cshift), d_cell[ncell] =
+  // nbins, so a position's bisect runs over [d_cell[c], d_cell[c + 1]) only
+  uint32_t *d_cell = nullptr;
+  uint32_t ncell = 0, cshift = 0;
   uint64_t *d_match = nullptr;    // the current search set's (below)
   uint32_t *d_nmatch = nullptr;
   // two search sets: the k_mam_sm launch of batch b + 1 runs on its own
@@ -736,7 +741,8 @@ __global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
                                             const int64_t *__restrict__ absp,
                                             const uint32_t *npos_p, const int64_t *prev_p,
                                             const int64_t *__restrict__ bins, uint32_t nbins,
-                                            unsigned long long *counts,
+                                            const uint32_t *__restrict__ cell, uint32_t ncell,
+                                            uint32_t cshift, unsigned long long *counts,
                                             unsigned long long *stats) {
   const uint64_t n = *npos_p;
   const int64_t prev0 = *prev_p;
@@ -749,6 +755,12 @@ __global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
     if (pr >= 0 && pr == p) { ++d; continue; }
     const int64_t a = absp[i];
     uint32_t lo = 0, hi = nbins;
+    if (cell) {   // the cell's bin range (bisect_right is monotone in a)
+      uint64_t c = a < 0 ? 0 : uint64_t(a) >> cshift;
+      c = c < ncell ? c : ncell - 1;
+      lo = cell[c];
+      hi = cell[c + 1];
+    }
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       if (a < bins[mid]) hi = mid; else lo = mid + 1;
@@ -851,6 +863,28 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     SMASH_HIPX(hipMemcpy(p->d_small, cfg->h_small_chr, p->n_contig, hipMemcpyHostToDevice));
     SMASH_HIPX(hipMemcpy(p->d_chrom_off, cfg->h_chrom_off, 8 * p->n_contig, hipMemcpyHostToDevice));
     SMASH_HIPX(hipMemcpy(p->d_bins, cfg->h_bin_starts, 8 * p->nbins, hipMemcpyHostToDevice));
+    {   // bin directory (k_bin): at most 2^18 cells; only for ascending, non-negative starts
+      const int64_t *b = cfg->h_bin_starts;
+      bool ok = b[0] >= 0;
+      for (uint32_t k = 1; k < p->nbins && ok; ++k) ok = b[k] >= b[k - 1];
+      if (ok) {
+        const uint64_t top = uint64_t(b[p->nbins - 1]);
+        uint32_t sh = 10;
+        while ((top >> sh) + 2 > (1u << 18)) ++sh;
+        p->cshift = sh;
+        p->ncell = uint32_t((top >> sh) + 2);
+        std::vector<uint32_t> cell(p->ncell + 1);
+        uint32_t r = 0;
+        for (uint32_t c = 0; c < p->ncell; ++c) {
+          const int64_t x = int64_t(uint64_t(c) << sh);
+          while (r < p->nbins && b[r] <= x) ++r;   // bisect_right(bins, x)
+          cell[c] = r;
+        }
+        cell[p->ncell] = p->nbins;
+        p->d_cell = dalloc<uint32_t>(p->ncell + 1);
+        SMASH_HIPX(hipMemcpy(p->d_cell, cell.data(), 4 * (p->ncell + 1), hipMemcpyHostToDevice));
+      }
+    }
     p->rec_bytes = search_rec_bytes(2 * P, p->read_len);
     for (int k = 0; k < 2; ++k) {
       p->d_match_s[k] = dalloc<uint64_t>(2 * P * p->slots);
@@ -961,7 +995,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
   }
   if (p->ev_in) (void)hipEventDestroy(p->ev_in);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
-                  (void *)p->d_bins,
+                  (void *)p->d_bins, (void *)p->d_cell,
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
                   (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_first,
                   (void *)p->d_k[0], (void *)p->d_k[1], (void *)p->d_v[0],
@@ -1134,7 +1168,8 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
   const uint64_t n = p->n_pairs;
   const int64_t *prev = d_prev ? d_prev : p->d_prev;
   k_bin<<<2048, kB, 0, s>>>(p->d_pos0, p->d_abs, p->d_posoff + n, prev, p->d_bins,
-                            p->nbins, reinterpret_cast<unsigned long long *>(d_counts),
+                            p->nbins, p->d_cell, p->ncell, p->cshift,
+                            reinterpret_cast<unsigned long long *>(d_counts),
                             p->d_stats);
   // carry the adjacent-dup state across batches (single-GPU use)
   k_tail<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_pos0, p->d_prev, nullptr);
@@ -1548,6 +1583,7 @@ extern "C" int smash_bin_positions(const int64_t *d_pos0, const int64_t *d_abspo
     }
     k_bin<<<2048, kB, 0, s>>>(d_pos0 + b, d_abspos + b, reinterpret_cast<const uint32_t *>(scratch),
                               reinterpret_cast<const int64_t *>(scratch + 1), d_bin_starts, nbins,
+                              nullptr, 0, 0,
                               reinterpret_cast<unsigned long long *>(d_counts),
                               reinterpret_cast<unsigned long long *>(scratch + 2));
     if (hipGetLastError() != hipSuccess) rc = SMASH_ERR_HIP;

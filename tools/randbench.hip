@@ -88,14 +88,15 @@ __global__ __launch_bounds__(256) void k_chase_ua(const uint8_t *buf, uint64_t n
 // SAME line (requests that hit): the cost of a miss and of a hit request,
 // the two kinds the MAM search issues (new lines; re-probes of a line it
 // just touched, second blocks, prefetch elements)
-template <int W>
+template <int W, bool OFF = false>
 __global__ __launch_bounds__(256) void k_req(const uint4 *buf, uint64_t mask16, int steps,
                                              uint64_t *sink, uint64_t seed) {
   const uint64_t t = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
   uint64_t h = mix(t + seed);
   uint32_t acc = 0;
   for (int s = 0; s < steps; ++s) {
-    const uint64_t i = ((h >> 17) & mask16) & ~uint64_t(3);
+    // OFF: the 16-byte block at a random offset in its 64-byte line (W = 1)
+    const uint64_t i = ((h >> 17) & mask16) & (OFF ? ~uint64_t(0) : ~uint64_t(3));
     uint32_t x = 0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
@@ -131,17 +132,20 @@ int main(int argc, char **argv) {
   if (argc > 1 && std::string(argv[1]) == "req") {
     uint64_t *sink;
     CK(hipMalloc(&sink, 8));
-    for (int lg : {-5, -2, 2, 6, 7}) {   // 32 MiB (L2-sized), 256 MiB (Infinity Cache), 4-128 GiB
+    std::vector<int> lgs = {-5, -2, 2, 6, 7};   // 32 MiB (L2-sized), 256 MiB (Infinity Cache), 4-128 GiB
+    if (argc > 2) { lgs.clear(); for (int i = 2; i < argc; ++i) lgs.push_back(std::atoi(argv[i])); }
+    for (int lg : lgs) {
       const uint64_t bytes = lg < 0 ? (1ull << 30) >> -lg : (1ull << 30) << lg;
       void *buf = nullptr;
       CK(hipMalloc(&buf, bytes));
       CK(hipMemset(buf, 0, bytes));
       for (int wps : {4, 8}) {
-        for (int w : {1, 2, 3}) {
+        for (int w : {1, 2, 3, 0}) {   // 0: one block at a random 16-byte offset
           const uint64_t threads = uint64_t(wps) * 4 * cus * 64;
           const int steps = 64;
           auto launch = [&](uint64_t seed) {
-            if (w == 1) k_req<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
+            if (w == 0) k_req<1, true><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
+            else if (w == 1) k_req<1><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
             else if (w == 2) k_req<2><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
             else k_req<3><<<unsigned(threads / 256), 256>>>((const uint4 *)buf, bytes / 16 - 1, steps, sink, seed);
           };
@@ -156,9 +160,11 @@ int main(int argc, char **argv) {
           float ms = 0;
           CK(hipEventElapsedTime(&ms, a, b));
           const double lines = 3.0 * threads * steps;
-          std::printf("req footprint %9.4f GiB  waves/SIMD %d  %d x 16 B per random line : %7.3f G lines/s  %7.3f G requests/s  %.3f ns per line\n",
-                      double(bytes) / (1ull << 30), wps, w, lines / (ms * 1e-3) * 1e-9,
-                      w * lines / (ms * 1e-3) * 1e-9, ms * 1e6 / lines);
+          std::printf("req footprint %9.4f GiB  waves/SIMD %d  %s : %7.3f G lines/s  %7.3f G requests/s  %.3f ns per line\n",
+                      double(bytes) / (1ull << 30), wps,
+                      w == 0 ? "1 x 16 B, random offset  " : w == 1 ? "1 x 16 B per random line " :
+                      w == 2 ? "2 x 16 B per random line " : "3 x 16 B per random line ",
+                      lines / (ms * 1e-3) * 1e-9, (w ? w : 1) * lines / (ms * 1e-3) * 1e-9, ms * 1e6 / lines);
           std::fflush(stdout);
           CK(hipEventDestroy(a)); CK(hipEventDestroy(b));
         }
