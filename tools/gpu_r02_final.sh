@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-2 measurement at the session's build: the whole -m gpu suite, smoke(),
+# the default bench line, then the C3 step with 4 M-pair batches for comparison
+set -uo pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-r02f}
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu $R/tests > $O/tests.log 2>&1
+rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 -u -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+tail -1 $O/smoke.log
+timeout -k 10 600 python3 -u $R/bench.py > $O/bench.json 2> $O/bench.log || exit 1
+grep -E "timed|roofline" $O/bench.log | head -3
+timeout -k 10 400 python3 -u $R/bench.py --steps 3 --no-cpu-baseline --no-feed --no-c5 --batch 4000000 > $O/bench_b4m.json 2> $O/bench_b4m.log || exit 1
+grep timed $O/bench_b4m.log

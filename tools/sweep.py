@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=2_000_000,
+                    help="one batch of this many pairs (the A/B logs of round 2 use 2 M)")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     import tempfile
@@ -39,7 +41,7 @@ def main():
     dix = S.Index.create(T, sp, sz, names, device=0)
     starts = bench.bin_starts_for(cfg, contigs, tempfile.mkdtemp())
     cs = bench.chrom_sizes_for(cfg, contigs)
-    P, L = cfg["batch"], cfg["read_len"]      # one batch of the config
+    P, L = a.pairs, cfg["read_len"]           # one batch of the config's reads
     import readgen
     d_reads = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000).generate(P)
     pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P)
