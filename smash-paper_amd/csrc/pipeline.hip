@@ -84,6 +84,11 @@ struct smash_pipeline {
   uint32_t *d_cnt = nullptr;      // [max_pairs]
   int64_t *d_pos0 = nullptr, *d_abs = nullptr;
   int64_t *d_prev = nullptr;      // [2] carried {last pos0 or -1, -}
+  // fused positions + varbin (k_emit_bin): per pair the pos0 of its last
+  // emitted position (-1: none), and its inclusive "last valid" scan
+  int64_t *d_lp = nullptr, *d_lps = nullptr;
+  bool fused_bin = true;
+  bool pos_dirty = false;         // the positions arrays are not materialised yet
   unsigned long long *d_stats = nullptr;
   uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast<16> -> k_post pair list
   uint32_t *d_l16 = nullptr;      // [1 + max_pairs]: k_post_fast<8> -> k_post_fast<16>
@@ -736,6 +741,31 @@ __global__ void k_emit(const uint8_t *keep, const int32_t *nk,
   }
 }
 
+// the bin of absolute position a (varbin: bisect_right over the starts,
+// wrapping to the last bin below the first start), the cell directory
+// narrowing the bisect when present
+__device__ __forceinline__ uint32_t bin_of(int64_t a, const int64_t *__restrict__ bins,
+                                           uint32_t nbins, const uint32_t *__restrict__ cell,
+                                           uint32_t ncell, uint32_t cshift) {
+  uint32_t lo = 0, hi = nbins;
+  if (cell) {
+    uint64_t c = a < 0 ? 0 : uint64_t(a) >> cshift;
+    c = c < ncell ? c : ncell - 1;
+    lo = cell[c];
+    hi = cell[c + 1];
+  }
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a < bins[mid]) hi = mid; else lo = mid + 1;
+  }
+  return lo == 0 ? nbins - 1 : lo - 1;
+}
+
+// "last valid" scan operator (associative): the right operand unless it is -1
+struct LastValid {
+  __host__ __device__ int64_t operator()(int64_t a, int64_t b) const { return b >= 0 ? b : a; }
+};
+
 // varbin: adjacent de-dup on the pos string (== pos0), bisect_right, count.
 __global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
                                             const int64_t *__restrict__ absp,
@@ -753,19 +783,7 @@ __global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
     const int64_t pr = i ? pos0[i - 1] : prev0;
     ++t;
     if (pr >= 0 && pr == p) { ++d; continue; }
-    const int64_t a = absp[i];
-    uint32_t lo = 0, hi = nbins;
-    if (cell) {   // the cell's bin range (bisect_right is monotone in a)
-      uint64_t c = a < 0 ? 0 : uint64_t(a) >> cshift;
-      c = c < ncell ? c : ncell - 1;
-      lo = cell[c];
-      hi = cell[c + 1];
-    }
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a < bins[mid]) hi = mid; else lo = mid + 1;
-    }
-    atomicAdd(&counts[lo == 0 ? nbins - 1 : lo - 1], 1ull);
+    atomicAdd(&counts[bin_of(absp[i], bins, nbins, cell, ncell, cshift)], 1ull);
     ++k;
   }
   __shared__ unsigned long long sd, sk, st;
@@ -778,6 +796,86 @@ __global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
     atomicAdd(&stats[S_DUPS], sd);
     atomicAdd(&stats[S_KEPT], sk);
   }
+}
+
+// per pair: the count of positions it emits (kept pairs: their major hits)
+// and the pos0 of the last one (-1: none), read from the end of its hit row
+__global__ void k_count_last(const uint8_t *keep, const uint32_t *nmajor, const int32_t *nk,
+                             const uint64_t *hits, uint32_t slots, const int64_t *chrom_off,
+                             uint64_t n, uint32_t *cnt, int64_t *lp) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t c = keep[q] ? nmajor[q] : 0;
+  cnt[q] = c;
+  int64_t last = -1;
+  if (c) {
+    const uint64_t *h = hits + q * 2 * uint64_t(slots);
+    for (int32_t i = nk[q] - 1; i >= 0; --i)
+      if (chrom_off[uint32_t(h[i] >> 48)] >= 0) {
+        last = int64_t(h[i] & 0xFFFFFFFFFFFFull);
+        break;
+      }
+  }
+  lp[q] = last;
+}
+
+// positions + varbin in one pass (smash_mapping.sh:29 then varbin.py:52-92):
+// one thread per pair walks its kept major hits in emission order; the line
+// before its first is the last position of the nearest earlier pair that
+// emitted any (the "last valid" scan lps), else the carried one.  Same
+// adjacent de-dup, bins and statistics as k_emit followed by k_bin, without
+// writing and re-reading the positions.
+__global__ __launch_bounds__(kB) void k_emit_bin(
+    const uint8_t *__restrict__ keep, const int32_t *__restrict__ nk,
+    const uint64_t *__restrict__ hits, uint32_t slots, const int64_t *__restrict__ chrom_off,
+    const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
+    const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
+    uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats) {
+  const int64_t prev0 = *prev_p;
+  unsigned long long d = 0, k = 0, t = 0;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += stride) {
+    if (!keep[q]) continue;
+    const int32_t m = nk[q];
+    if (m <= 0) continue;
+    int64_t prev = q ? lps[q - 1] : -1;
+    if (prev < 0) prev = prev0;
+    const uint64_t *h = hits + q * 2 * uint64_t(slots);
+    for (int32_t i = 0; i < m; ++i) {
+      const uint64_t w = h[i];
+      const int64_t co = chrom_off[uint32_t(w >> 48)];
+      if (co < 0) continue;
+      const int64_t p = int64_t(w & 0xFFFFFFFFFFFFull);
+      ++t;
+      if (prev >= 0 && prev == p) {
+        ++d;
+      } else {
+        atomicAdd(&counts[bin_of(p + co, bins, nbins, cell, ncell, cshift)], 1ull);
+        ++k;
+      }
+      prev = p;
+    }
+  }
+  __shared__ unsigned long long sd, sk, st;
+  if (threadIdx.x == 0) { sd = 0; sk = 0; st = 0; }
+  __syncthreads();
+  if (t) { atomicAdd(&st, t); atomicAdd(&sd, d); atomicAdd(&sk, k); }
+  __syncthreads();
+  if (threadIdx.x == 0 && st) {
+    atomicAdd(&stats[S_POS], st);
+    atomicAdd(&stats[S_DUPS], sd);
+    atomicAdd(&stats[S_KEPT], sk);
+  }
+}
+
+// the batch's tail {count, last position} (lps_last: lps[n - 1]; count 0:
+// -1) and the carried line for the next batch
+__global__ void k_tail_lps(const uint32_t *npos_p, const int64_t *lps_last, int64_t *prev,
+                           int64_t *tail) {
+  const uint32_t c = *npos_p;
+  const int64_t last = c ? *lps_last : -1;
+  if (tail) { tail[0] = int64_t(c); tail[1] = last; }
+  if (prev && c) prev[0] = last;
 }
 
 __global__ void k_tail(const uint32_t *npos_p, const int64_t *pos0, int64_t *prev,
@@ -919,7 +1017,10 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_posoff = dalloc<uint32_t>(P + 1);
     p->d_cnt = dalloc<uint32_t>(P);
     SMASH_HIPX(hipcub::DeviceScan::InclusiveSum(nullptr, b, p->d_cnt, p->d_posoff + 1, P));
-    p->temp_bytes = std::max(a, b);
+    size_t c3 = 0;
+    SMASH_HIPX(hipcub::DeviceScan::InclusiveScan(nullptr, c3, static_cast<const int64_t *>(nullptr),
+                                                 static_cast<int64_t *>(nullptr), LastValid(), P));
+    p->temp_bytes = std::max({a, b, c3});
     p->d_temp = dalloc<uint8_t>(p->temp_bytes);
     uint64_t cap = 2 * std::max<uint64_t>(cfg->dedup_capacity, P);
     uint64_t pw = 1;
@@ -937,6 +1038,12 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_pos0 = dalloc<int64_t>(P * 2 * p->slots);
     p->d_abs = dalloc<int64_t>(P * 2 * p->slots);
     p->d_prev = dalloc<int64_t>(2);
+    p->d_lp = dalloc<int64_t>(P);
+    p->d_lps = dalloc<int64_t>(P);
+    {
+      const char *e = getenv("SMASH_FUSED_BIN");   // 0: k_emit + k_bin (A/B)
+      p->fused_bin = !(e && e[0] == '0');
+    }
     int64_t init[2] = {-1, -1};
     SMASH_HIPX(hipMemcpy(p->d_prev, init, 16, hipMemcpyHostToDevice));
     p->d_stats = dalloc<unsigned long long>(S_N);
@@ -1002,6 +1109,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
+                  (void *)p->d_lp, (void *)p->d_lps,
                   (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb, (void *)p->d_l16,
                   (void *)p->d_post_ws, (void *)p->d_arena, (void *)p->d_arena_top,
                   (void *)p->d_send_hdr, (void *)p->d_send_words, (void *)p->d_recv_base})
@@ -1147,6 +1255,23 @@ extern "C" int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *s
   hipStream_t s = static_cast<hipStream_t>(stream);
   p->last = s;
   const uint64_t n = p->n_pairs;
+  if (p->fused_bin) {
+    // counts, offsets and each pair's preceding line; the positions
+    // themselves are only written if someone asks (smash_pipeline_positions)
+    if (n) {
+      k_count_last<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, p->d_nk,
+                                                           p->d_hits, p->slots, p->d_chrom_off, n,
+                                                           p->d_cnt, p->d_lp);
+      size_t tb = p->temp_bytes;
+      SMASH_HIP(hipcub::DeviceScan::InclusiveSum(p->d_temp, tb, p->d_cnt, p->d_posoff + 1, n, s));
+      tb = p->temp_bytes;
+      SMASH_HIP(hipcub::DeviceScan::InclusiveScan(p->d_temp, tb, p->d_lp, p->d_lps, LastValid(), n, s));
+      p->pos_dirty = true;
+    }
+    k_tail_lps<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_lps + (n ? n - 1 : 0), nullptr, d_tail);
+    SMASH_HIP(hipGetLastError());
+    return SMASH_OK;
+  }
   if (n) {
     k_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, n, p->d_cnt);
     size_t tb = p->temp_bytes;
@@ -1155,6 +1280,7 @@ extern "C" int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *s
                                                     p->d_posoff, n, p->slots,
                                                     p->d_chrom_off, p->d_pos0, p->d_abs);
   }
+  p->pos_dirty = false;
   k_tail<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_pos0, nullptr, d_tail);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
@@ -1167,6 +1293,17 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
   p->last = s;
   const uint64_t n = p->n_pairs;
   const int64_t *prev = d_prev ? d_prev : p->d_prev;
+  if (p->fused_bin) {
+    if (n)
+      k_emit_bin<<<grid_for(n, kB, 8192), kB, 0, s>>>(
+          p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
+          p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
+          p->d_stats);
+    // carry the adjacent-dup state across batches (single-GPU use)
+    k_tail_lps<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_lps + (n ? n - 1 : 0), p->d_prev, nullptr);
+    SMASH_HIP(hipGetLastError());
+    return SMASH_OK;
+  }
   k_bin<<<2048, kB, 0, s>>>(p->d_pos0, p->d_abs, p->d_posoff + n, prev, p->d_bins,
                             p->nbins, p->d_cell, p->ncell, p->cshift,
                             reinterpret_cast<unsigned long long *>(d_counts),
@@ -1541,6 +1678,13 @@ extern "C" int smash_pipeline_positions(smash_pipeline *p, int64_t *h_pos0, int6
                                         uint64_t cap, uint64_t *n_out) {
   if (!p || !n_out) return SMASH_ERR_ARG;
   SMASH_HIP(hipSetDevice(p->device));
+  if (p->pos_dirty && p->n_pairs) {   // fused path: write the last batch's positions now
+    k_emit<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, p->last>>>(
+        p->d_keep, p->d_nk, p->d_hits, p->d_posoff, p->n_pairs, p->slots, p->d_chrom_off,
+        p->d_pos0, p->d_abs);
+    SMASH_HIP(hipGetLastError());
+    p->pos_dirty = false;
+  }
   if (p->last) SMASH_HIP(hipStreamSynchronize(p->last));
   uint32_t n = 0;
   if (p->n_pairs)

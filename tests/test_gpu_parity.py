@@ -309,3 +309,31 @@ def test_key_set_exact_under_hash_collisions(gix, tiny_ix, bits, monkeypatch):
     assert counts.tolist() == op.counts.tolist()
     assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
     assert st.dupe_pairs == op.n_dupe.value
+
+
+@pytest.mark.parametrize("batch", [7, 1000])
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_fused_positions_bins_agree(gix, s, batch, monkeypatch):
+    """k_count_last + k_emit_bin (positions and varbin in one pass) and the
+    two-kernel path (k_emit, then k_bin over the written positions) give the
+    same counts, statistics and, read back after every batch, positions
+    (the adjacent de-dup line carried across batches both ways)."""
+    reads = interleaved_reads(s)
+    n = reads.shape[0] // 2
+
+    def run():
+        pipe, starts = make_pipe(gix, reads.shape[1], n)
+        counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+        pos = []
+        for b0 in range(0, n, batch):
+            b1 = min(n, b0 + batch)
+            pipe.count_batch(_device_reads(reads[2 * b0:2 * b1]), b1 - b0, counts)
+            p0, pa = pipe.positions()
+            pos.append((p0.tolist(), pa.tolist()))
+        return counts.cpu().tolist(), pipe.stats().as_dict(), pos
+
+    a = run()
+    monkeypatch.setenv("SMASH_FUSED_BIN", "0")
+    b = run()
+    assert a[1]["error"] == 0
+    assert a == b

@@ -122,7 +122,7 @@ static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
 
 thread_local dim3 threadIdx, blockIdx, blockDim;
-namespace smash { namespace sm { uint32_t ldsw[1 << 12]; uint32_t prep_lds[1 << 16]; } }
+namespace smash { namespace sm { alignas(16) uint32_t ldsw[1 << 12]; alignas(16) uint32_t prep_lds[1 << 16]; } }
 
 using namespace smash;
 

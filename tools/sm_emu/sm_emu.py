@@ -17,9 +17,11 @@ def build():
         for f in ("mam_sm.hpp", "mam_device.hpp", "common.hpp")]
     if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs):
         return LIB
+    tmp = "%s.%d.tmp" % (LIB, os.getpid())   # atomic: parallel test workers may build at once
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-I", HERE,
                            "-I", os.path.join(HERE, "..", "..", "include"),
-                           "-o", LIB, os.path.join(HERE, "sm_emu.cpp")])
+                           "-o", tmp, os.path.join(HERE, "sm_emu.cpp")])
+    os.replace(tmp, LIB)
     return LIB
 
 
