@@ -49,9 +49,9 @@ METRIC = ("reads/sec mapped+binned (hg19, 150 bp) at 1/2/4/8 MI355X; "
 CONFIGS = {
     # BASELINE.json configs[2]: hg19, 50 M x 150 bp, sample_bins/50000 (the
     # metric's config); configs[3] (C4) is this at N = 8: 400 M reads
-    "c3": dict(genome="hg19", read_len=150, pairs=25_000_000, batch=4_000_000, bins="50000",
+    "c3": dict(genome="hg19", read_len=150, pairs=25_000_000, batch=6_250_000, bins="50000",
                seed=3, workload="C3 hg19-shaped, 50 M x 150 bp SMASH reads per rank "
-                                "(25 M pairs, 7 batches, one run), sample_bins/50000"),
+                                "(25 M pairs, 4 batches, one run), sample_bins/50000"),
     # configs[1]: hg19 1M x 100 bp, sample_bins/100000 (synthesized 2-way split)
     "c2": dict(genome="hg19", read_len=100, pairs=500_000, batch=500_000, bins="100000", seed=2,
                workload="C2 hg19-shaped 1M x 100 bp SMASH reads, sample_bins/100000"),

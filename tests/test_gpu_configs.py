@@ -235,8 +235,8 @@ def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, tmp_path):
 
 
 def test_c3_full_run_properties(hg19):
-    """The C3 run as stated, 25 M pairs (50 M mates) in 7 batches of 4 M (the
-    bench's split) with one key set and the adjacent-dup state carried: the
+    """The C3 run as stated, 25 M pairs (50 M mates) in 4 batches of 6.25 M
+    (the bench's split) with one key set and the adjacent-dup state carried: the
     counts sum to ReadsKept, every pair is accounted for, and the same reads
     in another batch split give the same counts (the oracle cannot run 50 M
     reads here)."""
@@ -249,7 +249,7 @@ def test_c3_full_run_properties(hg19):
     g = readgen.Generator(dix, contigs, 150, seed=3)
     d_reads = g.generate(P)
     outs = []
-    for batch in (4_000_000, 1_700_000):
+    for batch in (6_250_000, 1_700_000):
         pipe = S.Pipeline(dix, cs, starts, 150, batch, dedup_capacity=P)
         counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
         pipe.reset()
