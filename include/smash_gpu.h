@@ -26,7 +26,8 @@ extern "C" {
 #define SMASH_ERR_ARG (-1)       /* bad argument / shape */
 #define SMASH_ERR_HIP (-2)       /* HIP runtime error (message: smash_last_error) */
 #define SMASH_ERR_IO (-3)        /* file missing / unreadable / inconsistent */
-#define SMASH_ERR_NOMEM (-4)     /* device allocation failed */
+#define SMASH_ERR_NOMEM (-4)     /* device allocation failed; as a pipeline data
+                                    error: the de-dup key set is full */
 #define SMASH_ERR_UNSUPPORTED (-5)
 /* pipeline data errors (positive), reported by smash_pipeline_stats:        */
 #define SMASH_ERR_TAG_LEFT 1     /* "left mappability too big"  mappability_tag.cpp:107-111 */
@@ -238,7 +239,10 @@ int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
 /* smash_phase_map, then the search of the NEXT batch (d_next, n_next pairs,
  * its reads ready by the work already on `stream`) issued at once on the
  * pipeline's other search stream: it runs while the caller exchanges this
- * batch's keys; the next smash_phase_map[_ahead] with the same reads uses it. */
+ * batch's keys; the next smash_phase_map[_ahead] with the same reads uses it.
+ * d_next must stay allocated and UNMODIFIED until that call: the search reads
+ * it asynchronously and its result is matched by (pointer, n_next) only.
+ * smash_pipeline_reset drops a look-ahead that was not consumed. */
 int smash_phase_map_ahead(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                           const uint8_t *d_next, uint64_t n_next, void *stream);
 int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
@@ -326,7 +330,12 @@ int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_keep,
 /* (query.cpp:153-156).  *out_text is malloc'ed (smash_sam_free) and holds    */
 /* the SAM lines without the header; *tag_error gets the first                */
 /* SMASH_ERR_TAG_* that mappability_tag would throw (0 = none).               */
-/* cap_per_read 0: h_rec is packed (smash_sam_records_packed).               */
+/* cap_per_read: the search's slots per read; h_rec holds read i's records  */
+/* at i * cap_per_read.  SMASH_SAM_PACKED | cap: h_rec is packed read after   */
+/* read (smash_sam_records_packed with the same cap); either way a count     */
+/* h_n[i] > cap (a cut match list) is SMASH_ERR_ARG.  0: packed, unchecked    */
+/* (the caller guarantees every h_n[i] <= the records' cap).                  */
+#define SMASH_SAM_PACKED 0x80000000u
 /* ========================================================================== */
 typedef struct {
   int64_t pos;             /* 0-based on the forward contig (< 0: erased)   */

@@ -480,7 +480,8 @@ void run_batch(const Args &a, const Index &ix, Device &d, Sorter &out,
   char *text = nullptr;
   uint64_t len = 0;
   int32_t terr = 0;
-  ck(smash_sam_format(contigs.data(), uint32_t(contigs.size()), rec.data(), cnt.data(), 0, n,
+  ck(smash_sam_format(contigs.data(), uint32_t(contigs.size()), rec.data(), cnt.data(),
+                      SMASH_SAM_PACKED | cap, n,
                       names.data(), seqs.data(), quals.data(), opts.data(), a.nomap ? 1 : 0, 0,
                       nullptr, &text, &len, &terr),
      "smash_sam_format");

@@ -135,7 +135,9 @@ inline uint32_t prep_per_block(const Geom &g, uint64_t stride) {
   return uint32_t(per < 1 ? 1 : per > 64 ? 64 : per);
 }
 __host__ __device__ inline uint32_t prep_in_words(uint64_t stride, uint32_t per) {
-  return uint32_t((per * stride + 8 + 3) / 4 + 10);   // + the 9-word over-read of (2)
+  // + the 9-word over-read of (2); a multiple of 4 words (the records' LDS
+  // image after it takes 16-byte accesses)
+  return (uint32_t((per * stride + 8 + 3) / 4 + 10) + 3) & ~3u;
 }
 inline size_t prep_lds_bytes(const Geom &g, uint64_t stride, uint32_t per) {
   return size_t(prep_in_words(stride, per)) * 4 + size_t(per) * (g.chunks * 4) * 4;
@@ -159,9 +161,21 @@ __global__ __launch_bounds__(256) void k_prep(const uint8_t *__restrict__ seqs, 
   const uint32_t nw = uint32_t(((a1 + 3) & ~uint64_t(3)) - w0) / 4;
   uint32_t *in = prep_lds;
   uint32_t *out = prep_lds + prep_in_words(stride, per);
-  for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x)
+  // 16-byte loads when the span starts on a 16-byte boundary (the usual
+  // case: per * stride is a multiple of 16 for 150 bp and 100 bp reads),
+  // else words; the records (rw words per read, a multiple of 4) and the
+  // LDS images are always 16-byte aligned
+  uint32_t k0 = 0;
+  if ((w0 & 15) == 0) {
+    const uint32_t n4 = nw / 4;
+    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x)
+      reinterpret_cast<uint4 *>(in)[k] = reinterpret_cast<const uint4 *>(w0)[k];
+    k0 = 4 * n4;
+  }
+  for (uint32_t k = k0 + threadIdx.x; k < nw; k += blockDim.x)
     in[k] = reinterpret_cast<const uint32_t *>(w0)[k];
-  for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) out[k] = 0;
+  for (uint32_t k = threadIdx.x; k < nr * rw / 4; k += blockDim.x)
+    reinterpret_cast<uint4 *>(out)[k] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   // a/c/g/t occur in the text (anything else is always bad)
   auto itx = [&](uint32_t b) {
@@ -198,8 +212,9 @@ __global__ __launch_bounds__(256) void k_prep(const uint8_t *__restrict__ seqs, 
   }
   __syncthreads();
   // (3) contiguous stores of the block's records
-  uint32_t *dst = rec + r0 * rw;
-  for (uint32_t k = threadIdx.x; k < nr * rw; k += blockDim.x) dst[k] = out[k];
+  uint4 *dst = reinterpret_cast<uint4 *>(rec + r0 * rw);
+  for (uint32_t k = threadIdx.x; k < nr * rw / 4; k += blockDim.x)
+    dst[k] = reinterpret_cast<const uint4 *>(out)[k];
 }
 
 // lane states: S_COPY and above own a pending 16-byte probe at `addr`.

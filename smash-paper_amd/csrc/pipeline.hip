@@ -1613,6 +1613,13 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * S_N, s));
   k_reset_prev<<<1, 1, 0, s>>>(p->d_prev);   // no host source: stays asynchronous
   SMASH_HIP(hipGetLastError());
+  // a look-ahead search not consumed before the reset is dropped: the next
+  // phase_map searches its reads again (its set stays busy until ev_found)
+  for (int k = 0; k < 2; ++k) {
+    p->searched[k] = false;
+    p->pref_reads[k] = nullptr;
+    p->pref_n[k] = 0;
+  }
   return SMASH_OK;
 }
 

@@ -321,18 +321,23 @@ extern "C" int smash_sam_format(const char *const *contigs, uint32_t n_contig,
     set_error("smash_sam_format: bad arguments");
     return SMASH_ERR_ARG;
   }
-  // cap_per_read 0: packed records (smash_sam_records_packed), read r's
-  // h_n[r] records follow read r-1's; else read r's start at r * cap_per_read
+  // packed records (smash_sam_records_packed): read r's h_n[r] records
+  // follow read r-1's; else read r's start at r * cap_per_read.  The cap is
+  // the search's slots per read in both layouts (0: packed, unchecked): a
+  // count above it means the read's match list was cut, which no layout can
+  // format (and packed offsets would run past the records written)
+  const bool packed = cap_per_read == 0 || (cap_per_read & SMASH_SAM_PACKED);
+  const uint32_t cap = cap_per_read & ~uint32_t(SMASH_SAM_PACKED);
   std::vector<uint64_t> roff(n_reads);
   for (uint64_t r = 0, acc = 0; r < n_reads; ++r) {
-    roff[r] = cap_per_read ? r * cap_per_read : acc;
+    roff[r] = packed ? acc : r * cap;
     acc += h_n[r];
   }
   if (tag_error) *tag_error = 0;
   std::string o;
   o.reserve(n_reads * 256);
   for (uint64_t r = 0; r < n_reads; ++r) {   // every record's contig must be named
-    if (cap_per_read && h_n[r] > cap_per_read) {
+    if (cap && h_n[r] > cap) {
       set_error("smash_sam_format: a read has more matches than cap_per_read");
       return SMASH_ERR_ARG;
     }

@@ -272,9 +272,9 @@ class _Run:
             d = torch.from_numpy(np.ascontiguousarray(self.reads[2 * b0:2 * b1])).to(self.dev)
             pipe.count_batch(d, b1 - b0, counts)
             on_batch(pipe)
-        st = pipe.stats()
+        st = pipe.stats(raise_on_error=False)
         if st.error:
-            raise SystemExit("mappability_tag: %s" % S.ERRORS.get(st.error, st.error))
+            raise SystemExit("%s: %s" % (_err_label(st.error), S.ERRORS.get(st.error, st.error)))
         return counts.cpu().numpy(), st
 
 
@@ -291,6 +291,24 @@ def cmd_map(args):
         o.write("%d dupes\t%d non-dupes\n" % (st.dupe_pairs, st.key_pairs - st.dupe_pairs))
 
 
+def fastq_pairs_bound(paths, L):
+    """An upper bound on the pairs in the read-1 FASTQ list, for the key-set
+    capacity: a record is at least 2 L + 6 bytes ("@x", seq, "+", qual);
+    gzip is taken at <= 8x compression (FASTQ runs 3-5x).  A bound that is
+    still too small fails the run (SMASH_ERR_NOMEM), never cuts the set."""
+    n = 0
+    for p in paths:
+        z = os.path.getsize(p)
+        n += (8 * z if p.endswith(".gz") else z) // (2 * L + 6) + 1
+    return max(n, 1)
+
+
+def _err_label(code):
+    """the stage a pipeline data error belongs to: the tag throws are
+    mappability_tag's (mappability_tag.cpp:107-113), the rest the count's"""
+    return "mappability_tag" if code in (1, 2) else "count"
+
+
 def _count_files(args, bins):
     """count from the FASTQ lists through the file-fed pipeline
     (smash_count_fastq: parse / H2D / compute overlapped, pairs ordered by
@@ -302,13 +320,14 @@ def _count_files(args, bins):
     rows, starts = S.read_bins(bins)
     r1, r2 = args.reads1.split(), args.reads2.split()
     L = S.first_read_length(r1)
-    pipe = S.Pipeline(ix, cs, starts, L, args.batch, dedup_capacity=args.dedup_capacity)
+    cap = args.dedup_capacity or fastq_pairs_bound(r1, L)
+    pipe = S.Pipeline(ix, cs, starts, L, args.batch, dedup_capacity=cap)
     counts = torch.zeros(len(starts), dtype=torch.int64, device=torch.device("cuda", args.device))
     pipe.reset()
     pipe.count_fastq(r1, r2, counts, sort_names=not args.presorted)
-    st = pipe.stats()
+    st = pipe.stats(raise_on_error=False)
     if st.error:
-        raise SystemExit("mappability_tag: %s" % S.ERRORS.get(st.error, st.error))
+        raise SystemExit("%s: %s" % (_err_label(st.error), S.ERRORS.get(st.error, st.error)))
     return rows, counts.cpu().numpy(), st
 
 
@@ -506,8 +525,9 @@ def main(argv=None):
         if name == "count":
             p.add_argument("--presorted", action="store_true",
                            help="FASTQ pairs already in samtools sort -n order: stream them")
-            p.add_argument("--dedup-capacity", type=int, default=1 << 24,
-                           help="distinct pair keys the de-dup set holds")
+            p.add_argument("--dedup-capacity", type=int, default=0,
+                           help="distinct pair keys the de-dup set holds (0: sized from "
+                                "the input files)")
         p.set_defaults(fn=fn)
     p = sub.add_parser("varbin")
     for a in ("positions", "bins", "out", "stats", "chrom_sizes"):

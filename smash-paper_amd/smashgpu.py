@@ -32,6 +32,8 @@ SMASH_MODE_MAM_PLAIN = 2
 SMASH_MODE_MUM = 3
 SMASH_MODE_MEM = 4
 MODES = {"MAM": SMASH_MODE_MAM, "MUM": SMASH_MODE_MUM, "MEM": SMASH_MODE_MEM}
+SAM_PACKED = 0x80000000   # smash_sam_format: records packed read after read (| cap)
+
 ERRORS = {1: "left mappability too big (mappability_tag.cpp:110)",
           2: "right mappability too big (mappability_tag.cpp:113)",
           -4: "out of device memory / key set full",
@@ -457,9 +459,14 @@ class Pipeline:
     def reset(self, stream=None):
         check(lib().smash_pipeline_reset(self.h, vp(_stream(stream))), "smash_pipeline_reset")
 
-    def stats(self):
+    def stats(self, raise_on_error=True):
+        """Counters of the run so far.  A data error the device recorded (the
+        mappability_tag throw, a full key set) raises SmashError unless
+        raise_on_error=False, so no caller can read counts of a failed run."""
         s = Stats()
         check(lib().smash_pipeline_stats(self.h, C.byref(s)), "smash_pipeline_stats")
+        if s.error and raise_on_error:
+            raise SmashError("pipeline data error %d: %s" % (s.error, ERRORS.get(s.error, "?")))
         return s
 
     def profile(self, enable=True):
@@ -626,7 +633,8 @@ def sam_format(contigs, h_rec, h_n, cap, names, seqs, quals=None, optionals=None
     (bytes, tag_error)."""
     h_rec = np.ascontiguousarray(h_rec)
     h_n = np.ascontiguousarray(h_n, np.uint32)
-    need = len(names) * cap if cap else int(h_n.astype(np.int64).sum())
+    packed = cap == 0 or bool(cap & SAM_PACKED)
+    need = int(h_n.astype(np.int64).sum()) if packed else len(names) * cap
     assert h_rec.nbytes >= need * SAM_REC.itemsize and len(h_n) == len(names)
     sm = None if small_chr is None else np.ascontiguousarray(small_chr, np.uint8)
     out = C.c_void_p()
@@ -685,8 +693,8 @@ def sam_lines(index: Index, d_reads, read_len, names, seqs, quals=None, optional
     if cap is None:
         cap = read_len - min_len + 1
     h_rec, h_n = sam_records(index, d_reads, n, read_len, cap, tag_offsets, min_len, stream)
-    return sam_format(index.contigs, h_rec, h_n, 0, names, seqs, quals, optionals, nomap,
-                      tag_offsets is not None, small_chr)
+    return sam_format(index.contigs, h_rec, h_n, SAM_PACKED | cap, names, seqs, quals, optionals,
+                      nomap, tag_offsets is not None, small_chr)
 
 
 def read_fastq_pairs(r1_paths, r2_paths, batch_pairs=1 << 20, name_stride=64):

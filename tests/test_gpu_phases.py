@@ -24,9 +24,15 @@ def _prev(tails, carried):
     return ShardedCounter._prev(tails, carried)
 
 
-def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False):
+def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False, capacity=None):
+    """capacity: each rank's key-set capacity.  An owner holds every key whose
+    hash it owns over the whole run: ~n/W of the n pairs, but ALL of them
+    when the hash is cut to a few bits (SMASH_KEY_HASH_BITS; with 2 bits
+    every hash is odd, so owner 1 of 2 gets every key).  Default: n."""
     dev = torch.device("cuda")
-    pipes = [S.Pipeline(ix, cs, starts, reads.shape[1], per_rank) for _ in range(W)]
+    n_all = W * per_rank * steps
+    pipes = [S.Pipeline(ix, cs, starts, reads.shape[1], per_rank,
+                        dedup_capacity=capacity or n_all) for _ in range(W)]
     for p in pipes:
         p.reset()
     counts = [torch.zeros(len(starts), dtype=torch.int64, device=dev) for _ in range(W)]
@@ -140,3 +146,19 @@ def test_count_batches_equals_batch_by_batch(gix, batch):
         st = pipe.stats()
         out.append((c.cpu().numpy().tolist(), st.positions, st.dups, st.kept, st.dupe_pairs))
     assert out[0] == out[1]
+
+
+def test_full_key_set_fails_loudly(gix, monkeypatch):
+    """The round-2 over-count of [2-300-3-2-True]: with the key set sized for
+    one batch (per_rank), owner 1 receives all ~1 770 distinct keys of the run
+    (2-bit hashes are all odd) into 1 024 slots.  Once the table is full a key
+    cannot be inserted, so a later duplicate of it is not found and its pair
+    is counted again; which keys miss the table depends on the race for the
+    last slots, hence the intermittent failure.  The library records
+    SMASH_ERR_NOMEM; the run must fail, never return those counts."""
+    monkeypatch.setenv("SMASH_KEY_HASH_BITS", "2")
+    reads = interleaved_reads("s100")
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    with pytest.raises(S.SmashError, match="key set full"):
+        run_emulated(gix, reads, 2, 300, 3, starts, cs, True, capacity=300)
