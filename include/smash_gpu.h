@@ -214,7 +214,7 @@ int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pa
 /* Multi-GPU phases (one rank per GPU; the caller runs the collectives):
  *  1. smash_phase_map      -- map/resolve/tag/filter/hash + in-batch first-wins
  *  2. smash_phase_export   -- the in-batch-first keys grouped by owner rank
- *                             (hash % world): per key a 5-word header {hash hi,
+ *                             ((hash >> 1) % world): per key a 5-word header {hash hi,
  *                             hash lo, global pair index, nk, word offset in
  *                             its owner segment} in *d_send and the key's nk
  *                             canonical hit words (tid << 48 | pos0) in

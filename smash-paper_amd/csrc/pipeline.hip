@@ -70,7 +70,7 @@ struct smash_pipeline {
   uint64_t *d_hash = nullptr;   // [2*max_pairs] hi, lo
   uint8_t *d_keep = nullptr;
   uint8_t *d_first = nullptr;
-  uint64_t *d_k[2] = {nullptr, nullptr};
+  uint32_t *d_k[2] = {nullptr, nullptr};   // sort keys (sort_key32)
   uint32_t *d_v[2] = {nullptr, nullptr};
   void *d_temp = nullptr;
   size_t temp_bytes = 0;
@@ -555,11 +555,20 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
   post_stats(nm, np, err, stats);
 }
 
+// In-batch order for the de-dup: a stable radix sort of a 32-bit key = the
+// low half of the hash hi (4 passes instead of 8 for the whole hash).  Equal
+// keys stay adjacent and in pair order; keys sharing only the low half share
+// a group, which the word comparison tells apart.  Pairs without a key sort
+// last (0xFFFFFFFF, never a keyed pair's value), so no group reaches them.
+__device__ __forceinline__ uint32_t sort_key32(uint64_t hi) {
+  const uint32_t k = uint32_t(hi);
+  return k == 0xFFFFFFFFu ? 0xFFFFFFFEu : k;
+}
 __global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n,
-                             uint64_t *key, uint32_t *val) {
+                             uint32_t *key, uint32_t *val) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= n) return;
-  key[q] = nk[q] >= 0 ? hash[2 * q] : ~0ull;
+  key[q] = nk[q] >= 0 ? sort_key32(hash[2 * q]) : 0xFFFFFFFFu;
   val[q] = uint32_t(q);
 }
 
@@ -666,9 +675,9 @@ __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, con
 
 // mode 0: single GPU (test+insert the persistent set); mode 1: mark
 // in-batch first occurrences only (multi-GPU export).  key/val: the batch's
-// pairs sorted (stably) by hash hi; a pair is first unless an earlier pair
-// of its hi group has the same key.
-__global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
+// pairs sorted (stably) by sort_key32; a pair is first unless an earlier pair
+// of its group has the same key.
+__global__ void k_dedup_first(const uint32_t *__restrict__ key, const uint32_t *__restrict__ val,
                               uint64_t n, const int32_t *nk, const uint64_t *hash,
                               const uint64_t *hits, uint32_t slots, uint64_t *table,
                               uint64_t mask, uint64_t *arena, uint64_t arena_cap,
@@ -695,7 +704,8 @@ __global__ void k_dedup_first(const uint64_t *__restrict__ key, const uint32_t *
       }
       first[q] = f ? 1 : 0;
       if (mode == 0) {
-        bool k = f && !set_test_insert(table, mask, key[s], me, arena, arena_cap, off, epoch, &full);
+        bool k = f && !set_test_insert(table, mask, hash[2 * q], me, arena, arena_cap, off, epoch,
+                                       &full);
         keep[q] = k ? 1 : 0;
         dp = k ? 0 : 1;
       }
@@ -1005,14 +1015,14 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     // sort buffers also serve the owner side of the multi-GPU de-dup,
     // which may receive more keys than one batch holds
     for (int i = 0; i < 2; ++i) {
-      p->d_k[i] = dalloc<uint64_t>(2 * P);
+      p->d_k[i] = dalloc<uint32_t>(2 * P);
       p->d_v[i] = dalloc<uint32_t>(2 * P);
     }
     size_t a = 0, b = 0;
     {
-      hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
+      hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
       hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
-      SMASH_HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, a, kb, vb, 2 * P));
+      SMASH_HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, a, kb, vb, 2 * P, 0, 32));
     }
     p->d_posoff = dalloc<uint32_t>(P + 1);
     p->d_cnt = dalloc<uint32_t>(P);
@@ -1210,10 +1220,10 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
   // in-batch ordering for de-dup: stable radix sort of key hi, value = pair
   k_dedup_keys<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_nk, p->d_hash, n_pairs,
                                                              p->d_k[0], p->d_v[0]);
-  hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
+  hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
   hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
   size_t tb = p->temp_bytes;
-  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_pairs, 0, 64, s));
+  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_pairs, 0, 32, s));
   if (kb.Current() != p->d_k[0]) {   // keep sorted data in slot 0
     std::swap(p->d_k[0], p->d_k[1]);
     std::swap(p->d_v[0], p->d_v[1]);
@@ -1357,19 +1367,25 @@ extern "C" int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, ui
 }
 
 // ---- multi-GPU de-dup exchange ------------------------------------------------
-// Each rank exports its in-batch-first keys to owner = hash hi % world: a
+// Each rank exports its in-batch-first keys to owner = (hash hi >> 1) % world: a
 // 5-word header {hi, lo, global pair index, nk, word offset} per key and the
 // key's nk hit words (hash + canonical key bytes + index).
 // The owner decides first-wins over the exact keys and answers one byte per
 // header.
 namespace smash {
 namespace {
+// the owner rank of a key: its hash hi without bit 0, which is always set
+// (0 marks an empty slot of the key set), so hi % world would leave every
+// even rank of an even world without keys and double the odd ranks' share
+__device__ __forceinline__ uint64_t key_owner(uint64_t hi, int world) {
+  return (hi >> 1) % uint64_t(world);
+}
 __global__ void k_export_count(const uint8_t *first, const int32_t *nk,
                                const uint64_t *hash, uint64_t n, int world,
                                unsigned long long *cnt) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q < n && nk[q] >= 0 && first[q]) {
-    const uint64_t o = hash[2 * q] % uint64_t(world);
+    const uint64_t o = key_owner(hash[2 * q], world);
     atomicAdd(&cnt[o], 1ull);
     atomicAdd(&cnt[128 + o], (unsigned long long)nk[q]);
   }
@@ -1380,7 +1396,7 @@ __global__ void k_export_fill(const uint8_t *first, const int32_t *nk,
                               uint64_t *hdr, uint64_t *words, uint32_t *send_q) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= n || nk[q] < 0 || !first[q]) return;
-  const uint64_t ow = hash[2 * q] % uint64_t(world);
+  const uint64_t ow = key_owner(hash[2 * q], world);
   const uint64_t o = atomicAdd(&cnt[64 + ow], 1ull);             // entry slot
   const uint64_t k = uint64_t(nk[q]);
   const uint64_t w = atomicAdd(&cnt[192 + ow], (unsigned long long)k);   // word slot
@@ -1393,9 +1409,9 @@ __global__ void k_export_fill(const uint8_t *first, const int32_t *nk,
   for (uint64_t i = 0; i < k; ++i) words[w + i] = src[i];
   send_q[o] = uint32_t(q);
 }
-__global__ void k_owner_keys(const uint64_t *recv, uint64_t n, uint64_t *key, uint32_t *val) {
+__global__ void k_owner_keys(const uint64_t *recv, uint64_t n, uint32_t *key, uint32_t *val) {
   const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j < n) { key[j] = recv[5 * j]; val[j] = uint32_t(j); }
+  if (j < n) { key[j] = sort_key32(recv[5 * j]); val[j] = uint32_t(j); }
 }
 // base[0..world]: header prefix per source rank; base[65..65+world]: word
 // prefix per source rank
@@ -1406,7 +1422,7 @@ __device__ __forceinline__ KeyRef recv_key(const uint64_t *recv, const uint64_t 
   return KeyRef{words + base[65 + r] + recv[5 * j + 4], uint32_t(recv[5 * j + 3]),
                 recv[5 * j + 1]};
 }
-__global__ void k_owner_decide(const uint64_t *key, const uint32_t *val, const uint64_t *recv,
+__global__ void k_owner_decide(const uint32_t *key, const uint32_t *val, const uint64_t *recv,
                                const uint64_t *words, const uint64_t *base, int world,
                                uint64_t n, uint64_t *table, uint64_t mask, uint64_t *arena,
                                uint64_t arena_cap, unsigned long long *arena_top,
@@ -1432,7 +1448,7 @@ __global__ void k_owner_decide(const uint64_t *key, const uint32_t *val, const u
   }
   bool full = false;
   const bool keep =
-      win && !set_test_insert(table, mask, key[s], me, arena, arena_cap, off, epoch, &full);
+      win && !set_test_insert(table, mask, recv[5 * j], me, arena, arena_cap, off, epoch, &full);
   flags[j] = keep ? 1 : 0;
   if (full) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
 }
@@ -1543,10 +1559,10 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   SMASH_HIP(hipMemcpyAsync(p->d_recv_base, base, sizeof(base), hipMemcpyHostToDevice, s));
   // reuse the sort buffers (phase_map's sorted keys are no longer needed)
   k_owner_keys<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(d_recv, n_recv, p->d_k[0], p->d_v[0]);
-  hipcub::DoubleBuffer<uint64_t> kb(p->d_k[0], p->d_k[1]);
+  hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
   hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
   size_t tb = p->temp_bytes;
-  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_recv, 0, 64, s));
+  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_recv, 0, 32, s));
   k_owner_decide<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(
       kb.Current(), vb.Current(), d_recv, d_recv_words, p->d_recv_base, world, n_recv,
       p->d_table, p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, next_epoch(p), d_flags,

@@ -7,7 +7,7 @@ the two dependencies the reference's sequential scripts carry:
 
 * smashMEM.py's global first-wins pair de-dup (smashMEM.py:149,217-228): the
   in-batch-first keys -- a header {hash, global pair index, length} plus the
-  key's canonical hit words -- are sent to owner rank = hash % world
+  key's canonical hit words -- are sent to owner rank = (hash >> 1) % world
   (all_to_all of the counts, the headers and the words), the owner decides
   first-wins by global pair index over the exact keys against its persistent
   key set and returns one flag per key (all_to_all back);

@@ -73,7 +73,7 @@ class OraclePhasePipeline:
                 first[tuple(k)] = q
         groups = [[] for _ in range(world)]
         for k, q in first.items():
-            groups[self.hashes[q][0] % world].append((k, q))
+            groups[(self.hashes[q][0] >> 1) % world].append((k, q))   # key_owner
         self.order = []
         rows, words, counts, wcounts = [], [], [], []
         for w in range(world):

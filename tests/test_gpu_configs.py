@@ -16,6 +16,9 @@ hg19 (C2, C3, C5) no CPU suffix sort finishes here, so the device index is
     C2  hg19, 1 M x 100 bp (all 500 k pairs), sample_bins/100000
     C3  hg19, 150 bp, sample_bins/50000: a 100 k-pair sample of the bench's
         workload through the oracle; the full 25 M-pair run by properties
+    C4  240 k pairs of the 8-GPU workload (seed 4) over W = 8 and W = 3
+        emulated ranks with look-ahead (tests/phase_emu.py) == one pipeline
+        == the oracle over all of them
     C5  the map.bin self-scan of every forward base == the index build's
         map.bin, and windows of it == the oracle's longSA::show restatement
 idx8 the whole count pipeline with 64-bit SA/ISA (the hg19 element width) on
@@ -263,6 +266,56 @@ def test_c3_full_run_properties(hg19):
         outs.append((counts.cpu().numpy(), st.as_dict()))
         del pipe
     assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+
+
+# ---------------------------------------------------------------------------
+# C4's logic at C4's shape on one device: hg19, 150 bp SMASH reads (seed 4),
+# sample_bins/50000, ranks emulated in-process (tests/phase_emu.py)
+# ---------------------------------------------------------------------------
+C4_PAIRS = 240_000
+
+
+@pytest.fixture(scope="module")
+def c4_run(hg19, hg19_oracle):
+    """240 k pairs of C4's workload, their single-pipeline counts and the
+    oracle's counts over all of them."""
+    import readgen
+    contigs, _, dix = hg19
+    oix, mp = hg19_oracle
+    cs = _chrom_sizes(contigs)
+    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    starts = np.array([int(l.split("\t")[2]) for l in open(src)], np.int64)
+    d_reads = readgen.Generator(dix, contigs, 150, seed=4).generate(C4_PAIRS)
+    one = S.Pipeline(dix, cs, starts, 150, C4_PAIRS, dedup_capacity=C4_PAIRS)
+    one.reset()
+    c1 = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    one.count_batch(d_reads, C4_PAIRS, c1)
+    s1 = one.stats()
+    op, err = _oracle_counts(oix, mp, cs, starts, d_reads.cpu().numpy())
+    assert err == 0
+    single = (c1.cpu().numpy().astype(np.uint64), (s1.positions, s1.dups, s1.kept, s1.dupe_pairs))
+    orc = (op.counts.copy(), (op.state.total, op.state.dups, op.state.kept, op.n_dupe.value))
+    return dix, cs, starts, d_reads, single, orc
+
+
+@pytest.mark.parametrize("W,per_rank,steps,bits", [(8, 10_000, 3, 0), (3, 20_000, 4, 0),
+                                                   (8, 10_000, 3, 18)])
+def test_c4_sharded_equals_single_and_oracle(c4_run, W, per_rank, steps, bits, monkeypatch):
+    """W ranks (look-ahead search on, as dist.ShardedCounter runs it) over
+    the same 240 k pairs dealt in (step, rank, pair) order: counts and
+    stats equal one pipeline's and the oracle's (smashMEM.py:217-228
+    first-wins across ranks, varbin.py:56-58 across shard boundaries).
+    bits: the key hash cut to 18 bits, so ~100 k keys collide in it and
+    the owners must compare the exchanged key words."""
+    from phase_emu import run_emulated
+    dix, cs, starts, d_reads, single, orc = c4_run
+    assert W * per_rank * steps == C4_PAIRS
+    if bits:
+        monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
+    total, st = run_emulated(dix, d_reads, W, per_rank, steps, starts, cs, ahead=True)
+    assert orc[1][3] > 100          # duplicate pairs across ranks and steps occur
+    assert np.array_equal(total, orc[0]) and st == orc[1]
+    assert np.array_equal(single[0], orc[0]) and single[1] == orc[1]
 
 
 def test_c5_mappability_scan_full_genome(hg19, hg19_oracle):
