@@ -155,6 +155,14 @@ def test_pipeline_matches_reference_varbin(gix, s):
     g = open(gold("%s_varbin_stats_partial.txt" % s)).read().split("\n")[1].split("\t")
     assert (st.positions, st.dups, st.kept) == (int(g[0]), int(g[1]), int(g[2]))
     assert st.pairs == reads.shape[0] // 2
+    # smashMEM.py's own summary and positions (the reference script run on the
+    # reference's tagged mapout, tools/make_golden_smashmem.sh)
+    summ = read_gz_lines("%s_smashmem.txt.gz" % s)[-1]
+    assert summ == "%d dupes\t%d non-dupes" % (st.dupe_pairs, st.key_pairs - st.dupe_pairs)
+    pos0, absp = pipe.positions()
+    name_at = {v: k for k, v in load_chrom_sizes(gold("tiny_chrom_sizes.txt")).items()}
+    got = ["%s %d" % (name_at[a - p], p) for p, a in zip(pos0.tolist(), absp.tolist())]
+    assert got == open(gold("%s_positions.txt" % s)).read().splitlines()
 
 
 @pytest.mark.parametrize("batch", [1, 7, 137, 1000])

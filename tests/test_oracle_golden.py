@@ -3,7 +3,8 @@ made by tools/make_golden.sh from the compiled reference + varbin.py).
 
 Every stage of the chain is checked: text layout, SA/ISA/LCP/map.bin bytes,
 per-read MAM/MUM/MEM triples, prepare_matches + mappability_tag SAM fields,
-and varbin counts.  CPU only.
+smashMEM (the REFERENCE's smashMEM.py run over tools/pysam_shim,
+tools/make_golden_smashmem.sh) and varbin counts.  CPU only.
 """
 import hashlib
 import re
@@ -202,3 +203,88 @@ def test_varbin_before_first_bin_goes_to_last_bin():
     counts, st = O.varbin([5, 6, 1000], [5, 6, 1000], [10, 20, 30])
     assert counts.tolist() == [0, 0, 3 - 0]
     assert (st.total, st.dups, st.kept) == (3, 0, 3)
+
+
+# ---------------------------------------------------------------------------
+# smashMEM.py: the reference script's own output (tools/make_golden_smashmem.sh
+# ran it unmodified over tools/pysam_shim) against the oracle's restatement
+# ---------------------------------------------------------------------------
+_CIG = re.compile(r"(\d+)([MIDNSHP=X])")
+
+
+def tagged_sam(s):
+    """(@SQ names, body lines in samtools sort -n order) of the SAM the
+    reference script ran on"""
+    if s == "edge":
+        lines = open(gold("smashmem_edge.sam")).read().splitlines()
+        head = [l for l in lines if l.startswith("@")]
+        body = [l for l in lines if l and not l.startswith("@")]
+    else:
+        head = open(gold("tiny_mapout_header.txt")).read().splitlines()
+        body = read_gz_lines("%s_mapout_tagged_full.txt.gz" % s)
+        body.sort(key=lambda l: (l.split("\t", 1)[0], 0 if int(l.split("\t")[1]) & 64 else 1))
+    names = [x.split("SN:")[1].split("\t")[0] for x in head if x.startswith("@SQ")]
+    return names, body
+
+
+def orc_hit(f, tid_of):
+    """pysam 0.8 fields of one mapped full SAM line"""
+    h = O.OrcHit()
+    h.tid = tid_of[f[2]]
+    h.rc = 1 if int(f[1]) & 16 else 0
+    h.pos = int(f[3]) - 1
+    ops = _CIG.findall(f[5])
+    rlen = len(f[9])
+    lead = int(ops[0][0]) if ops[0][1] == "S" else 0
+    trail = int(ops[-1][0]) if len(ops) > 1 and ops[-1][1] == "S" else 0
+    h.qstart, h.qend = lead, rlen - trail
+    tags = {t.split(":")[0]: t.split(":")[2] for t in f[11:]}
+    h.hi, h.L0, h.R0 = int(tags["HI"]), int(tags["L0"]), int(tags["R0"])
+    return h
+
+
+@pytest.mark.parametrize("s", ["s100", "s150", "edge"])
+def test_smashmem_restatement_equals_reference_script(s):
+    """orc_smash_pair + the first-wins key set (smashMEM.py:154-228 restated)
+    over the same name-sorted tagged SAM reproduce the script's output: the
+    emitting pairs, each one's (chrom, pos) list in order (r1 by HI, then
+    r2 by HI), and the dupe / non-dupe counts (smashMEM.py:230)."""
+    names, body = tagged_sam(s)
+    tid_of = {n: i for i, n in enumerate(names)}
+    groups, order = {}, []
+    for line in body:
+        f = line.split("\t")
+        if f[0] not in groups:
+            groups[f[0]] = ([], [])
+            order.append(f[0])
+        if int(f[1]) & 4:
+            continue
+        groups[f[0]][0 if int(f[1]) & 64 else 1].append(orc_hit(f, tid_of))
+    got, seen, dup = [], set(), 0
+    for name in order:
+        h1, h2 = groups[name]
+        h1.sort(key=lambda h: h.hi)
+        h2.sort(key=lambda h: h.hi)
+        kept = O.smash_pair(h1, h2)
+        if kept is None:
+            continue
+        if tuple(kept) in seen:
+            dup += 1
+            continue
+        seen.add(tuple(kept))
+        got += [(name, names[t], p) for t, p in kept]
+    ref = read_gz_lines("%s_smashmem.txt.gz" % s)
+    assert ref[0].startswith("read_id\t")
+    exp = [(f[0], f[3], int(f[4])) for f in (l.split("\t") for l in ref[1:-1])]
+    assert got == exp
+    assert ref[-1] == "%d dupes\t%d non-dupes" % (dup, len(seen))
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_smashmem_reference_positions_are_the_golden_positions(s):
+    """The awk/perl extraction (smash_mapping.sh:29) of the reference script's
+    output is the positions file the varbin goldens were made from."""
+    rx = re.compile(r"^chr(\d+|[XY]) \d+$")
+    ref = read_gz_lines("%s_smashmem.txt.gz" % s)[1:-1]
+    pos = [l for l in ("%s %s" % tuple(x.split("\t")[3:5]) for x in ref) if rx.match(l)]
+    assert pos == open(gold("%s_positions.txt" % s)).read().splitlines()
