@@ -482,6 +482,7 @@ def main():
     el = time.perf_counter() - t1
     mam_ms, launches, mam_reads = pipe.profile_read()
     active_ms = pipe.profile_active()
+    launch_iv = pipe.profile_intervals()
     pipe.profile(False)
     st = pipe.stats()
     if st.error:
@@ -558,6 +559,10 @@ def main():
                           "of the time at least one ran (active_ms_per_launch)" % (
                               100.0 * (mam_ms - active_ms) / max(active_ms, 1e-9)),
                 "reads_per_launch": int(reads_per_launch),
+                # every timed launch's [start, end] (ms from the first start;
+                # HIP events on its stream): avg_kernel_ms is their mean
+                # duration, so frac can be recomputed from this line alone
+                "launch_intervals_ms": [[round(a, 3), round(b, 3)] for a, b in launch_iv],
                 "launches": int(launches),
                 "lines_per_read": {k: round(v[1] / ns, 3) for k, v in emu.counters.items()},
                 "probes_per_read": {k: round(v[0] / ns, 3) for k, v in emu.counters.items()},

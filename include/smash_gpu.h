@@ -283,6 +283,11 @@ int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
  * the launches' event intervals; launches on the two search streams of
  * smash_count_batches overlap).  Synchronises. */
 int smash_pipeline_profile_active(smash_pipeline *p, double *active_ms);
+/* Every profiled launch's [start, end] in milliseconds from the first one's
+ * start (h_ms[2i], h_ms[2i + 1]), for up to cap launches; *n = launches.
+ * Synchronises. */
+int smash_pipeline_profile_intervals(smash_pipeline *p, double *h_ms, uint64_t cap,
+                                     uint64_t *n);
 
 /* Start a new run: clears the pair-key set, the carried adjacent-dup state
  * and the stats (a fresh smashMEM.py + varbin.py invocation). */

@@ -1664,6 +1664,22 @@ extern "C" int smash_pipeline_profile_read(smash_pipeline *p, double *search_ms,
   return SMASH_OK;
 }
 
+extern "C" int smash_pipeline_profile_intervals(smash_pipeline *p, double *h_ms, uint64_t cap,
+                                                uint64_t *n) {
+  if (!p || !n || (cap && !h_ms)) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  *n = p->n_ev;
+  for (uint64_t i = 0; i < p->n_ev && i < cap; ++i) {
+    SMASH_HIP(hipEventSynchronize(p->ev[2 * i + 1]));
+    float a = 0, b = 0;
+    SMASH_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[2 * i]));
+    SMASH_HIP(hipEventElapsedTime(&b, p->ev[0], p->ev[2 * i + 1]));
+    h_ms[2 * i] = a;
+    h_ms[2 * i + 1] = b;
+  }
+  return SMASH_OK;
+}
+
 // The time at least one profiled k_mam_sm launch was running: the union of
 // the launches' [start, end] event intervals (launches on the two search
 // streams overlap, so their summed durations count the overlap twice).

@@ -52,6 +52,7 @@ EXPORTS = [
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
     "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
+    "smash_pipeline_profile_intervals",
     "smash_phase_map_ahead", "smash_sam_records_packed",
 ]
 
@@ -133,6 +134,7 @@ def lib():
     L.smash_count_batches.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp]
     L.smash_phase_map_ahead.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp]
     L.smash_pipeline_profile_active.argtypes = [vp, C.POINTER(C.c_double)]
+    L.smash_pipeline_profile_intervals.argtypes = [vp, C.POINTER(C.c_double), C.c_uint64, u64p]
     L.smash_phase_map.argtypes = [vp, vp, C.c_uint64, vp]
     L.smash_phase_export.argtypes = [vp, C.c_int, C.c_uint64, i64p, i64p, C.POINTER(vp),
                                      C.POINTER(vp), vp]
@@ -487,6 +489,16 @@ class Pipeline:
         check(lib().smash_pipeline_profile_active(self.h, C.byref(ms)),
               "smash_pipeline_profile_active")
         return ms.value
+
+    def profile_intervals(self):
+        """[(start, end)] ms of every profiled search launch, from the first start"""
+        n = C.c_uint64()
+        check(lib().smash_pipeline_profile_intervals(self.h, None, 0, C.byref(n)),
+              "smash_pipeline_profile_intervals")
+        out = (C.c_double * (2 * max(n.value, 1)))()
+        check(lib().smash_pipeline_profile_intervals(self.h, out, n.value, C.byref(n)),
+              "smash_pipeline_profile_intervals")
+        return [(out[2 * i], out[2 * i + 1]) for i in range(n.value)]
 
     def positions(self):
         """(pos0, abspos) int64 arrays of the positions the last batch emitted

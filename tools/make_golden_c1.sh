@@ -11,8 +11,10 @@
 #              LCP, map.bin: the device build must match byte for byte)
 #   mapping    fastqs_to_sam | mummer -verbose -rcref -qthreads 12 -nomap
 #              -samin -samout | mappability_tag  (smash_mapping.sh:19-23)
-#   smashMEM   tools/oracle_positions.py (the oracle's restatement; pysam is
-#              absent, so this link is parity-unpinned, as in make_golden.sh)
+#   smashMEM   the REFERENCE's smashMEM.py, unmodified, over tools/pysam_shim
+#              (a SAM-text stand-in for its pysam 0.8 calls; round 3), on the
+#              tagged SAM in samtools sort -n order, then the awk/perl
+#              extraction of smash_mapping.sh:29
 #   varbin     the REAL varbin.py (python3) -> c1_varbin_nonzero.txt
 #              (bin index, count of every non-empty bin) + c1_varbin_stats.txt
 set -eu
@@ -57,7 +59,21 @@ rm -rf mapout
   | grep -v '^@' \
   | awk -F'\t' 'BEGIN{OFS="\t"} {t=""; for(i=12;i<=NF;i++){ if($i ~ /^(XM|XU|XE|XS|NH|HI|L0|R0|cc|cp|xo|xc|CC|CP|XO|XC):/) t=t"\t"$i } print $1,$2,$3,$4,$5,$6,$7,$8,$9 t}' \
   | LC_ALL=C sort > tagged.txt
-python3 "$ROOT/tools/oracle_positions.py" chr21.fa tagged.txt chrom_sizes.txt > positions.txt
+"$R/mappability_tag" chr21.fa <(cat mapout/*.txt | head -n 100 | grep ^@ ;
+                                cat mapout/*.txt | grep -v ^@ | perl -pe 's/^(\S+?)\/\S+\/\d+/\1/') \
+  > tagged_full.sam
+python3 - <<'PY'
+lines = open("tagged_full.sam").read().splitlines()
+head = [l for l in lines if l.startswith("@")]
+body = [l for l in lines if l and not l.startswith("@")]
+# samtools sort -n: fixed-width names r%09d (plain order), read 1 first
+body.sort(key=lambda l: (l.split("\t", 1)[0], 0 if int(l.split("\t")[1]) & 64 else 1))
+open("namesort.sam", "w").write("\n".join(head + body) + "\n")
+PY
+PYTHONPATH="$ROOT/tools/pysam_shim" python3 "$REF/smashMEM.py" namesort.sam 0 0 10000 4 > smash.txt
+cat smash.txt | awk '{print $4, $5}' | perl -ne 'print if /^chr(\d+|[XY]) \d+$/' > positions.txt
+python3 "$ROOT/tools/oracle_positions.py" chr21.fa tagged.txt chrom_sizes.txt > positions_oracle.txt
+cmp positions.txt positions_oracle.txt   # the restatement agrees at C1 scale
 python3 "$REF/varbin.py" positions.txt bins500k.txt varbin.txt stats.txt chrom_sizes.txt \
     > /dev/null 2>&1 || true
 awk -F'\t' '$4 != 0 {print NR - 1 "\t" $4}' varbin.txt > "$OUT/c1_varbin_nonzero.txt"
