@@ -172,9 +172,10 @@ def host_index(S, O, dix, T, sp, sz, names, sample_reads=None):
             idx = torch.from_numpy(codes.astype(np.int64)).to(kt_dev.device)
             got = kt_dev.index_select(0, idx).cpu().numpy().view(np.uint64)
             KT.reshape(-1, 2)[codes.astype(np.int64)] = got
-    BM = S.download(i.d_bitmap, 8 * ((1 << (2 * i.bitmap_b)) // 64 + 1), np.uint64)
+    # (the window filter's presence bits ride in the k-mer entries: KT is
+    # the device layout, which the emulation reads as is; no bitmap)
     it = np.array([(i.in_text[c >> 6] >> (c & 63)) & 1 for c in range(256)], np.uint8)
-    oix.accel(U, KT, i.kmer_k, BM, i.bitmap_b, it)
+    oix.accel(U, KT, i.kmer_k, np.zeros(1, np.uint64), i.bitmap_b, it, KTF=KT)
     return oix, mp
 
 

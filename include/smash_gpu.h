@@ -107,9 +107,14 @@ typedef struct {
   /* search accelerators (results-preserving):           */
   uint32_t kmer_k;         /* k of the k-mer -> SA-interval table */
   const uint8_t *d_uniq;   /* U[x] = min(255, max(LCP[ISA[x]], LCP[ISA[x]+1])) */
-  const uint64_t *d_kmer;  /* 4^k x {lo, hi}; lo > hi = absent */
-  uint32_t bitmap_b;       /* B of the B-mer presence bitmap */
-  const uint64_t *d_bitmap;/* 4^B bits: ACGT B-mer occurs in the text */
+  const uint64_t *d_kmer;  /* 4^k x 16 B: words {lo, hi} in their low 40 bits
+                              (lo > hi = absent), and in their high 24 bits
+                              48 presence bits of the (k+2)-mers holding the
+                              k-mer: bit r1*4+r2 "w r1 r2", 16+l*4+r "l w r",
+                              32+l1*4+l2 "l1 l2 w" (bit f at 40 + f % 24 of
+                              word f / 24) */
+  uint32_t bitmap_b;       /* B = k + 2: the window filter's B-mer length */
+  const uint64_t *d_bitmap;/* NULL (round 3: the presence bits are in d_kmer) */
   uint64_t in_text[4];     /* 256-bit set of bytes occurring in the text */
 } smash_index_info;
 int smash_index_query(const smash_index *ix, smash_index_info *out);

@@ -126,6 +126,7 @@ def lib():
         L.orc_accel_k.argtypes = [C.c_uint64]
         L.orc_accel_k.restype = C.c_uint32
         L.orc_build_accel.argtypes = [C.POINTER(OrcIndex), C.c_uint32, u8p, u64p]
+        L.orc_build_ktf.argtypes = [C.POINTER(OrcIndex), C.c_uint32, u64p, u64p]
         L.orc_mam_fast.argtypes = [C.POINTER(OrcIndex), C.POINTER(OrcAccel), u8p,
                                    C.c_uint32, C.c_uint32, C.POINTER(OrcMatch),
                                    C.c_uint32, C.POINTER(OrcCounters)]
@@ -267,13 +268,21 @@ class Index:
             cap = n
         return [(out[i].ref, out[i].query, out[i].len) for i in range(n)]
 
-    def accel(self, U=None, KT=None, K=None, BM=None, B=None, in_text=None):
-        """Search accelerators (built here, or given, e.g. from the device)."""
+    def accel(self, U=None, KT=None, K=None, BM=None, B=None, in_text=None, KTF=None):
+        """Search accelerators (built here, or given, e.g. from the device).
+        KT: {lo, hi} per K-mer (the oracle's own accelerated searches); KTF:
+        the device layout with the (K+2)-mer presence bits (orc_build_ktf;
+        tools/sm_emu runs the device kernel over it)."""
         if U is None:
             K = lib().orc_accel_k(self.N)
             U = np.zeros(self.N + 64, np.uint8)
             KT = np.zeros(2 << (2 * K), np.uint64)
             lib().orc_build_accel(C.byref(self.c), K, _p(U, u8p), _p(KT, u64p))
+        if KTF is None:
+            KTF = np.zeros(2 << (2 * K), np.uint64)
+            lib().orc_build_ktf(C.byref(self.c), K, _p(np.ascontiguousarray(KT, np.uint64), u64p),
+                                _p(KTF, u64p))
+        self._KTF = np.ascontiguousarray(KTF, np.uint64)
         if BM is None:
             B = lib().orc_accel_b(self.N)
             BM = np.zeros((1 << (2 * B)) // 64 + 1, np.uint64)

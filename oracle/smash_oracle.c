@@ -1108,6 +1108,35 @@ void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT) 
   }
 }
 
+/* k-mer table with the (K+2)-mer presence bits (aux_build.hip k_kfilter
+ * restated): every ACGT (K+2)-mer b0 .. b(K+1) of the text sets bit
+ * b(K)*4+b(K+1) of the entry of b0..b(K-1), bit 16+b0*4+b(K+1) of b1..b(K)'s
+ * and bit 32+b0*4+b1 of b2..b(K+1)'s; filter bit f is bit 40 + f % 24 of word
+ * f / 24. */
+static void ktf_set(uint64_t *E, uint64_t w, uint32_t f) {
+  E[2 * w + (f >= 24)] |= 1ull << (40 + (f >= 24 ? f - 24 : f));
+}
+
+void orc_build_ktf(const orc_index *ix, uint32_t K, const uint64_t *KT, uint64_t *KTF) {
+  const uint64_t nk = 1ull << (2 * K), mask = nk - 1;
+  memcpy(KTF, KT, 16 * nk);
+  const uint64_t N = ix->N;
+  uint64_t c = 0;
+  uint32_t run = 0;   /* consecutive ACGT bytes ending at x */
+  for (uint64_t x = 0; x < N; ++x) {
+    const int v = acgt(ix->T[x]);
+    if (v < 0) { run = 0; c = 0; continue; }
+    c = (c << 2) | (uint64_t)v;          /* (only the low 2K + 4 bits are used) */
+    if (++run < K + 2) continue;
+    const uint64_t b = c & ((1ull << (2 * K + 4)) - 1);   /* the (K+2)-mer ending at x */
+    const uint32_t b0 = (uint32_t)(b >> (2 * K + 2)) & 3, b1 = (uint32_t)(b >> (2 * K)) & 3;
+    const uint32_t r1 = (uint32_t)(b >> 2) & 3, r2 = (uint32_t)b & 3;
+    ktf_set(KTF, b >> 4, r1 * 4 + r2);
+    ktf_set(KTF, (b >> 2) & mask, 16 + b0 * 4 + r2);
+    ktf_set(KTF, b & mask, 32 + b0 * 4 + b1);
+  }
+}
+
 int orc_mam_fast(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
                  uint32_t L, uint32_t min_len, orc_match *out, uint32_t cap,
                  orc_counters *ctr) {

@@ -112,6 +112,10 @@ uint64_t orc_map_only_v3(const orc_index *ix, const orc_accel *acc,
                          orc_counters *ctr);
 uint32_t orc_accel_k(uint64_t N);
 void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT);
+/* the device's k-mer table layout (smash-paper_amd/csrc/common.hpp,
+ * aux_build.hip k_kfilter): KTF[2w + i] = KT[2w + i] (low 40 bits) | presence
+ * bits of the (K+2)-mers holding w (high 24 bits); KTF: 2 * 4^K words */
+void orc_build_ktf(const orc_index *ix, uint32_t K, const uint64_t *KT, uint64_t *KTF);
 int orc_mam_fast(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
                  uint32_t L, uint32_t min_len, orc_match *out, uint32_t cap,
                  orc_counters *ctr);

@@ -8,10 +8,15 @@
 //        at a time with two random LCP loads; the device scans U[pos+1..]
 //        sequentially instead.  Same quantity as map.bin's `right` before the
 //        edge rules (longSA.cpp:628-641, 666).
-//  KT[w] ({lo, hi} u64 pair per ACGT k-mer w, 2 bits/char, first char most
-//        significant) = the SA interval of the suffixes starting with w, or
-//        lo > hi when w does not occur.  It replaces the first k narrowing
-//        steps of top_down_faster from the root (longSA.cpp:322-380).
+//  KT[w] (16 bytes per ACGT k-mer w, 2 bits/char, first char most
+//        significant; layout in common.hpp) = the SA interval of the
+//        suffixes starting with w, or lo > hi when w does not occur.  It
+//        replaces the first k narrowing steps of top_down_faster from the
+//        root (longSA.cpp:322-380).  The same entry carries the presence of
+//        the 48 (k+2)-mers that contain w (k_kfilter), which the (F) window
+//        filter of mam_sm.hpp reads: a window of min_len = k + 4 bases holds
+//        3 such B-mers, all contained in the k-mer two bases into it, so one
+//        entry decides the window.
 #include "common.hpp"
 
 namespace smash {
@@ -74,20 +79,33 @@ __global__ void k_kbounds(const uint32_t *__restrict__ code, uint64_t N, uint64_
   }
 }
 
-// presence bitmap of every ACGT B-mer of the text (bit = 2-bit code)
-__global__ void k_bitmap(const uint8_t *__restrict__ T, uint64_t N, int B,
-                         unsigned long long *bm) {
+// the (k+2)-mer presence bits of the table (common.hpp): every ACGT
+// (k+2)-mer b0 b1 .. b(k+1) of the text sets one bit in each of the entries
+// of the three k-mers it contains: b0..b(k-1) (bit b(k)*4 + b(k+1)),
+// b1..b(k) (bit 16 + b0*4 + b(k+1)) and b2..b(k+1) (bit 32 + b0*4 + b1);
+// filter bit f lives at bit 40 + f % 24 of word f / 24 of the entry
+__device__ inline void kt_set(unsigned long long *kt, uint64_t w, uint32_t f) {
+  atomicOr(&kt[2 * w + (f >= 24 ? 1 : 0)], 1ull << (40 + (f >= 24 ? f - 24 : f)));
+}
+__global__ void k_kfilter(const uint8_t *__restrict__ T, uint64_t N, int K,
+                          unsigned long long *kt) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  const uint64_t mask = (1ull << (2 * B)) - 1;
-  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x + B <= N; x += stride) {
-    uint64_t c = 0;
+  const uint64_t mask = (1ull << (2 * K)) - 1;
+  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x + K + 2 <= N;
+       x += stride) {
+    uint64_t c = 0;   // the (k+2)-mer, 2k + 4 bits
     bool ok = true;
-    for (int k = 0; k < B; ++k) {
+    for (int k = 0; k < K + 2; ++k) {
       const int v = acgt2(T[x + k]);
       ok = ok && v >= 0;
-      c = ((c << 2) | uint64_t(v & 3)) & mask;
+      c = (c << 2) | uint64_t(v & 3);
     }
-    if (ok) atomicOr(&bm[c >> 6], 1ull << (c & 63));
+    if (!ok) continue;
+    const uint32_t b0 = uint32_t(c >> (2 * K + 2)) & 3, b1 = uint32_t(c >> (2 * K)) & 3;
+    const uint32_t r1 = uint32_t(c >> 2) & 3, r2 = uint32_t(c) & 3;
+    kt_set(kt, c >> 4, r1 * 4 + r2);                       // w = b0..b(k-1)
+    kt_set(kt, (c >> 2) & mask, 16 + b0 * 4 + r2);          // w = b1..b(k)
+    kt_set(kt, c & mask, 32 + b0 * 4 + b1);                 // w = b2..b(k+1)
   }
 }
 
@@ -124,15 +142,11 @@ void build_aux_t(smash_index *ix, hipStream_t s) {
   k_kbounds<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(code, N, ix->d_kmer);
   SMASH_HIPX(hipStreamSynchronize(s));
   dfree(code);
-  // B-mer presence bitmap: about log4(N)+1 characters (sparse: 1-10 % set)
-  int B = 8;
-  while (B < 18 && (1ull << (2 * (B - 1))) <= N) ++B;
-  ix->bitmap_b = uint32_t(B);
-  const uint64_t words = ((1ull << (2 * B)) >> 6) + 1;
-  if (!ix->d_bitmap) ix->d_bitmap = dalloc<uint64_t>(words);
-  SMASH_HIPX(hipMemsetAsync(ix->d_bitmap, 0, 8 * words, s));
-  k_bitmap<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
-      ix->d_text, N, B, reinterpret_cast<unsigned long long *>(ix->d_bitmap));
+  // the (k+2)-mer presence bits, in the same entries (after k_kbounds, which
+  // writes whole words)
+  ix->bitmap_b = uint32_t(K + 2);
+  k_kfilter<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
+      ix->d_text, N, K, reinterpret_cast<unsigned long long *>(ix->d_kmer));
   unsigned int *pres = dalloc<unsigned int>(256);
   SMASH_HIPX(hipMemsetAsync(pres, 0, 1024, s));
   k_present<<<grid_for(N, 256, 4096), 256, 0, s>>>(ix->d_text, N, pres);

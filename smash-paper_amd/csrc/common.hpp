@@ -13,6 +13,24 @@ namespace smash {
 
 void set_error(const std::string &msg);
 
+// The k-mer table (aux_build.hip), one 16-byte entry per ACGT k-mer w (2 bits
+// per base, first base most significant): two u64 words whose low 40 bits
+// hold the SA interval {lo, hi} of the suffixes starting with w (lo > hi: w
+// does not occur) and whose high 24 bits hold, together, 48 presence bits of
+// the (k+2)-mers that contain w (the (F) window filter of mam_sm.hpp):
+//   bit r1*4 + r2          w r1 r2   occurs (the (k+2)-mer starting AT w)
+//   bit 16 + l*4 + r       l w r     occurs (starting one base before w)
+//   bit 32 + l1*4 + l2     l1 l2 w   occurs (starting two bases before w)
+constexpr uint64_t kKtMask = (1ull << 40) - 1;
+__host__ __device__ inline uint64_t kt_filter(uint64_t w0, uint64_t w1) {
+  return (w0 >> 40) | ((w1 >> 40) << 24);
+}
+// is the (k+2)-mer with code c (2k + 4 bits) in the text: bit c & 15 of its
+// first k-mer's entry (the "w r1 r2" bits live in the first word)
+__host__ __device__ inline bool kt_bmer_present(const uint64_t *KT, uint64_t c) {
+  return (KT[2 * (c >> 4)] >> (40 + (c & 15))) & 1ull;
+}
+
 #define SMASH_HIP(call)                                                      \
   do {                                                                       \
     hipError_t e_ = (call);                                                  \
@@ -89,10 +107,10 @@ struct smash_index {
   uint64_t map_bytes = 0;
   uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
   mutable uint64_t *d_nsdir = nullptr;   // first U < 255 per 4096 positions (mappability.hip)
-  uint64_t *d_kmer = nullptr;    // {lo,hi} per k-mer
+  uint64_t *d_kmer = nullptr;    // per k-mer: {lo,hi} + (k+2)-mer presence bits (kt_filter)
   uint32_t kmer_k = 0;
-  uint64_t *d_bitmap = nullptr;  // B-mer presence bits (aux_build.hip)
-  uint32_t bitmap_b = 0;
+  uint64_t *d_bitmap = nullptr;  // (none since round 3: the presence bits live in d_kmer)
+  uint32_t bitmap_b = 0;         // B = k + 2, the filter's B-mer length
   uint64_t in_text[4] = {0, 0, 0, 0};   // bytes occurring in the text
   uint64_t *d_work = nullptr;    // k_mam work counter (stream-ordered use)
   // k_mam_sm read records (mam_sm.hpp k_prep), grown on demand by

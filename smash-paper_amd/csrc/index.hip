@@ -67,7 +67,7 @@ void account(smash_index *ix) {
   ix->device_bytes = (N + 64) + 2 * N * ix->idx_bytes + (N + 64) + 16 * ix->n_ovf +
                      ix->map_bytes + 16 * ix->n_seq + (N + 64) +
                      (ix->kmer_k ? 16ull << (2 * ix->kmer_k) : 0) +
-                     (ix->bitmap_b ? (1ull << (2 * ix->bitmap_b)) / 8 : 0);
+                     (ix->d_bitmap ? (1ull << (2 * ix->bitmap_b)) / 8 : 0);
 }
 
 // u32 exact LCP from lcp8 + overflow (used when map.bin must be computed

@@ -147,7 +147,7 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
         "consume", "S_ALU", "S_COPY", "S_BM", "S_KT", "S_IDX", "S_BYTE", "S_CMP", "S_USCAN",
         "S_EX", "A_BS", "A_BS_DONE", "A_XL_DONE", "A_RUN_DONE", "A_CHAIN_DONE", "A_EXPAND",
         "A_AFTER", "A_TOP", "A_TRAV", "A_DONE", "TOP.!clean", "TOP.codes1", "TOP.codes2",
-        "TOP.kt", "TOP.filter", "-", "dma"};
+        "TOP.kt", "TOP.filter", "TOP.kcache", "dma"};
     std::fprintf(stderr, "[k_mam_sm] wave iterations running each region (%%):");
     for (int k = 0; k < 27; ++k)
       if (ws[64 + k])
@@ -191,7 +191,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   }
   sm::Ctx<IdxT> c;
   const DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
-  c.T = x.T; c.SA = x.SA; c.ISA = x.ISA; c.L8 = x.L8; c.U = x.U; c.KT = x.KT; c.BM = x.BM;
+  c.T = x.T; c.SA = x.SA; c.ISA = x.ISA; c.L8 = x.L8; c.U = x.U; c.KT = x.KT;
   c.N = x.N; c.logN = uint32_t(x.logN); c.K = uint32_t(x.K); c.B = uint32_t(x.B);
   c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(rec);
@@ -199,7 +199,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.lin_blocks = 8;
   c.pad = 0;
   c.grab = 16;
-  c.bm_dual = 2;
+  c.bm_dual = 3;
   c.pf = 1;
   c.u32 = 1;
   if (const char *e = std::getenv("SMASH_SM_PF")) c.pf = uint32_t(std::atoi(e));
@@ -216,17 +216,16 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.wave_stats = nullptr;
   {
     const uint64_t N = ix->N, isz = ix->idx_bytes;
-    const uint64_t spans[8][2] = {
+    const uint64_t spans[7][2] = {
         {reinterpret_cast<uint64_t>(ix->d_text), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_sa), N * isz},
         {reinterpret_cast<uint64_t>(ix->d_isa), N * isz},
         {reinterpret_cast<uint64_t>(ix->d_lcp8), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_uniq), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_kmer), 16ull << (2 * ix->kmer_k)},
-        {reinterpret_cast<uint64_t>(ix->d_bitmap), 8 * (((1ull << (2 * ix->bitmap_b)) >> 6) + 1)},
         {reinterpret_cast<uint64_t>(rec), n_reads * g.chunks * 16}};
     c.lo = ~0ull; c.hi = 0;
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 7; ++k) {
       c.lo = std::min<uint64_t>(c.lo, spans[k][0]);
       c.hi = std::max<uint64_t>(c.hi, spans[k][0] + spans[k][1]);
     }
@@ -313,7 +312,7 @@ int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint
     set_error("smash_map_batch: unknown mode");
     return SMASH_ERR_ARG;
   }
-  if (mode != SMASH_MODE_MAM_PLAIN && (!ix->d_uniq || !ix->d_kmer || !ix->d_bitmap)) {
+  if (mode != SMASH_MODE_MAM_PLAIN && (!ix->d_uniq || !ix->d_kmer)) {
     set_error("smash_map_batch: index lacks the search accelerators");
     return SMASH_ERR_ARG;
   }

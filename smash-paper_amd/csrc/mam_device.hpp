@@ -16,8 +16,7 @@ struct DevIndex {
   const IdxT *ISA;
   const uint8_t *L8;    // min(LCP,255)
   const uint8_t *U;     // per-position unique-length bytes (aux_build.hip)
-  const uint64_t *KT;   // k-mer -> {lo, hi}
-  const uint64_t *BM;   // B-mer presence bitmap
+  const uint64_t *KT;   // k-mer -> {lo, hi} + (k+2)-mer presence bits (common.hpp)
   uint64_t N, logN;
   int K, B;
   uint64_t in_text[4];  // bytes that occur in the text
@@ -35,7 +34,6 @@ inline DevIndex<IdxT> make_dev_index(const smash_index *ix) {
   x.N = ix->N;
   x.logN = ix->logN;
   x.K = int(ix->kmer_k);
-  x.BM = ix->d_bitmap;
   x.B = int(ix->bitmap_b);
   for (int k = 0; k < 4; ++k) x.in_text[k] = ix->in_text[k];
   return x;
@@ -219,7 +217,7 @@ __device__ void mam_read(const DevIndex<IdxT> &x, const uint8_t *P, uint32_t L,
         w = (w << 2) | uint32_t(v & 3);
       }
       if (ok) {
-        const uint64_t lo = x.KT[2 * uint64_t(w)], hi = x.KT[2 * uint64_t(w) + 1];
+        const uint64_t lo = x.KT[2 * uint64_t(w)] & kKtMask, hi = x.KT[2 * uint64_t(w) + 1] & kKtMask;
         if (lo <= hi) {
           depth = uint64_t(x.K);
           start = lo;
@@ -377,8 +375,7 @@ __device__ bool window_ok(const DevIndex<IdxT> &x, const uint8_t *P, uint64_t p,
     c0 = ((c0 << 2) | uint64_t(v0)) & mask;
     c1 = ((c1 << 2) | uint64_t(v1)) & mask;
   }
-  const uint64_t w0 = x.BM[c0 >> 6], w1 = x.BM[c1 >> 6];
-  return ((w0 >> (c0 & 63)) & (w1 >> (c1 & 63)) & 1ull) != 0;
+  return kt_bmer_present(x.KT, c0) && kt_bmer_present(x.KT, c1);
 }
 
 // (S): final traverse state over a small interval
@@ -439,7 +436,7 @@ __device__ void mam_read_v3(const DevIndex<IdxT> &x, const uint8_t *P, uint32_t 
         w = (w << 2) | uint32_t(v & 3);
       }
       if (ok) {
-        const uint64_t lo = x.KT[2 * uint64_t(w)], hi = x.KT[2 * uint64_t(w) + 1];
+        const uint64_t lo = x.KT[2 * uint64_t(w)] & kKtMask, hi = x.KT[2 * uint64_t(w) + 1] & kKtMask;
         if (lo <= hi) { depth = uint64_t(x.K); start = lo; end = hi; have_pos = false; }
       }
     }

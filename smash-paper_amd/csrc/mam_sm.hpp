@@ -32,13 +32,21 @@
 #define PAD_KEEP(x) asm volatile("" : "+v"(x))
 #endif
 #ifndef SM_HOOK_BM
-#define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes
+#define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes (policies 0-2)
+#endif
+#ifndef SM_HOOK_F
+#define SM_HOOK_F(j, bits)         // host emulation: filter outcomes (policy 3)
 #endif
 #ifndef SM_HOOK_BS
 #define SM_HOOK_BS(size, depth)   // host emulation: interval statistics
 #endif
 #ifndef SM_LOAD16
 #define SM_LOAD16(a) ::smash::sm::load16u(a)
+#endif
+// the same load, told the lane state that issues it (the host emulation files
+// the window filter's k-mer-table probes apart from the (C) descents')
+#ifndef SM_LOAD16ST
+#define SM_LOAD16ST(a, st) SM_LOAD16(a)
 #endif
 // speculative loads of a binary search's next SA elements (both children of
 // the probe being compared; one of them is used): the emulation does not
@@ -382,7 +390,7 @@ struct Ctx {
   const uint8_t *T;
   const IdxT *SA, *ISA;
   const uint8_t *L8, *U;
-  const uint64_t *KT, *BM;
+  const uint64_t *KT;     // k-mer table: {lo, hi} + (k+2)-mer presence bits (common.hpp)
   uint64_t N;
   uint32_t logN, K, B, min_len;
   // k_prep records and the LDS row geometry
@@ -391,8 +399,9 @@ struct Ctx {
   uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
   uint32_t pad;           // experiment: dependent ALU ops added per iteration (0 = none)
   uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
-  uint32_t bm_dual;       // (F): 0 one B-mer word per iteration, 1 last + first in one,
-                          // 2 the cover policy (two words per iteration chosen by mode)
+  uint32_t bm_dual;       // (F) policy: 0 one B-mer per iteration, 1 last + first in one,
+                          // 2 the cover policy (two B-mers per iteration chosen by mode),
+                          // 3 (default) one k-mer entry = the window's B + 2 B-mers
   uint32_t pf;            // binary-search compares also load the children's SA elements
   uint32_t u32;           // (B) U scans load 32 bytes per iteration (else 16)
   const uint16_t *lens;
@@ -478,6 +487,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   FlagRef hit{fl, 2}, bm2{fl, 3}, skip_f{fl, 4}, xrun{fl, 5};
   FlagRef rdone{fl, 6};   // a run's right side was finished by S_EXB
   uint32_t fm = 0;        // (F) probe mode (bm_dual 2)
+  // (F) policy 3: what the k-mer entries told about the read's B-mers, as
+  // offsets from read position kp: fk bit i = the B-mer at kp + i is known,
+  // bit 16 + i = it occurs; fj = the offset (from prefix) of the in-flight
+  // probe's window; the last entry's interval {klo, khi} of the k-mer at kx
+  // (its (C) descent needs no second probe)
+  uint32_t fk = 0, kp = 0, fj = 0, kx = 0xFFFFFFFFu;
+  uint64_t klo = 1, khi = 0;
+  FlagRef fdead{fl, 11};    // the last entry showed an absent B-mer
   FlagRef ktr_set{fl, 7};   // a passed window's k-mer code is in m
   FlagRef clean{fl, 8};     // the read has no bad base (bad mask all zero)
   // binary-search prefetch: the S_CMP O_BS probe in flight also loads the SA
@@ -552,10 +569,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
     uint64_t v3 = 0;
     const uint64_t amask = st >= S_BYTE ? ~uint64_t(0) : ~uint64_t(15);
-    if (st >= S_COPY) v = SM_LOAD16(addr & amask);
+    if (st >= S_COPY) v = SM_LOAD16ST(addr & amask, st);
     if (need2) {
       if (pf) v2 = SM_LOADPF16(addr2 & ~uint64_t(15));
-      else v2 = SM_LOAD16(addr2 & amask);
+      else v2 = SM_LOAD16ST(addr2 & amask, st);
     }
     if (pfr) v3 = SM_LOADIDX(c.SA, (m + 1 + hi) >> 1);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
@@ -632,20 +649,42 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         need2 = false;
         prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
         skip_f = false; fm = 0; ktr_set = false;
+        fk = 0; kp = 0; kx = 0xFFFFFFFFu; fdead = false;
         clean = (bad.w0 | bad.w1 | bad.w2 | bad.w3 | bad.w4 | bad.w5 | bad.w6 | bad.w7) == 0;
         a = A_TOP;
         break;
       }
-      case S_BM: {                                   // (F) last, then first B-mer present?
+      case S_BM: {                                   // (F) a k-mer table entry arrived
         SM_REGION(3);
+        need2 = false;
+        if (c.bm_dual == 3) {
+          // the entry of the k-mer at x = kp + fj + 2; c0 = the 2-bit codes of
+          // the k + 4 read bases [x - 2, x + k + 2), first most significant:
+          // its presence bits give the B-mers at x - 2, x - 1, x (common.hpp)
+          const uint64_t f48 = kt_filter(lo64(v), hi64(v));
+          const uint32_t nb = 2 * (c.K + 4);
+          const uint32_t l1 = uint32_t(c0 >> (nb - 2)) & 3, l0 = uint32_t(c0 >> (nb - 4)) & 3;
+          const uint32_t r1 = uint32_t(c0 >> 2) & 3, r2 = uint32_t(c0) & 3;
+          const uint32_t bits = (uint32_t(f48 >> (32 + 4 * l1 + l0)) & 1u) |
+                                ((uint32_t(f48 >> (16 + 4 * l0 + r1)) & 1u) << 1) |
+                                ((uint32_t(f48 >> (4 * r1 + r2)) & 1u) << 2);
+          SM_HOOK_F(fj, bits);
+          fk |= (7u << fj) | (bits << (16 + fj));
+          fdead = bits != 7u;
+          kx = kp + fj + 2;
+          klo = lo64(v) & kKtMask;
+          khi = hi64(v) & kKtMask;
+          a = A_TOP;
+          break;
+        }
         // The last B-mer [q1, q1+B) (q1 = prefix+min_len-B) is probed first:
         // absent, it lies inside every window starting in [prefix, q1], so
         // all of them are skipped at once; an absent first B-mer rules out
-        // this window only.  (bm_dual: v2 holds the first B-mer's word.)
+        // this window only.  (bm_dual: v2 holds the first B-mer's entry.)
+        // A B-mer's presence is bit (code & 15) of its first k-mer's entry.
         const uint64_t cc = bm2 ? c0 : c1;
-        const bool pa = (((ao & 8) ? hi64(v) : lo64(v)) >> (cc & 63)) & 1ull;
-        const bool pb = !c.bm_dual || ((((addr2 & 8) ? hi64(v2) : lo64(v2)) >> (c0 & 63)) & 1ull);
-        need2 = false;
+        const bool pa = (lo64(v) >> (40 + (cc & 15))) & 1ull;
+        const bool pb = !c.bm_dual || ((lo64(v2) >> (40 + (c0 & 15))) & 1ull);
         if (c.bm_dual == 2) {
           // cover policy (bm_dual 2): the pair probed depends on the mode fm
           // (A_TOP); an absent B-mer at s rules out the windows [s-D, s]
@@ -687,7 +726,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
         } else if (!bm2 && !c.bm_dual) {
           bm2 = true;
-          addr = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6));
+          addr = reinterpret_cast<uint64_t>(c.KT + 2 * (c0 >> 4));
         } else {
           skip_f = true;                              // window passed: go on at (C)
           a = A_TOP;
@@ -696,7 +735,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_KT: {                                   // (C)
         SM_REGION(4);
-        const uint64_t l0 = lo64(v), h0 = hi64(v);
+        const uint64_t l0 = lo64(v) & kKtMask, h0 = hi64(v) & kKtMask;
         if (l0 <= h0) { depth = c.K; start = l0; end = h0; have_pos = false; }
         a = A_TRAV;
         break;
@@ -997,66 +1036,135 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         int32_t kb = -1;
         const uint32_t B = c.B;
         const uint32_t D = c.min_len - B;
-        const uint32_t sM = prefix + 2 * D + 1;     // mode 1's second B-mer
-        bool okP = true, okQ = true;                // [p, p+B), [p+D, p+D+B): inside the read
-        bool okP1 = prefix + 1 + B <= L, okM = sM + B <= L;
         if (!clean) {
           SM_REGION(20);
           kb = bad.last(prefix, c.min_len);
           while (kb >= 0 && in_text(P[kb]))
             kb = bad.last(prefix, uint32_t(kb) - prefix);
-          okP = bad.bits(prefix, B) == 0;
-          okQ = bad.bits(prefix + D, B) == 0;
-          okP1 = okP1 && bad.bits(prefix + 1, B) == 0;
-          okM = okM && bad.bits(sM, B) == 0;
-        }
-        // probes: c1 <- B-mer at s1 (v), c0 <- B-mer at s2 (v2); mode 0 is
-        // {last, first} of this window, 1 and 2 (bm_dual 2) see S_BM
-        uint32_t s1 = prefix + D, s2 = prefix;
-        bool ok = okQ && okP;
-        if (c.bm_dual == 2 && fm == 1 && okQ && okM) {
-          s2 = sM; ok = true;
-        } else if (c.bm_dual == 2 && fm == 2 && okP && okP1) {
-          s1 = prefix; s2 = prefix + 1; ok = true;
-        } else {
-          fm = 0;
         }
         if (kb >= 0) {                                // absent byte: next window
           depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
           fm = 0;
-        } else if (B > 0 && B <= c.min_len && ok) {
-          // both codes from one pass over the row when the span allows
-          const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;
-          const uint32_t span = hi_s + B - lo_s;
-          if (span <= 21) {
-            SM_REGION(21);
-            const uint64_t X = codes_raw(row, c.w_row, lo_s, span);
-            const uint64_t mk = (1ull << (2 * B)) - 1;
-            c1 = (X >> (2 * (lo_s + span - s1 - B))) & mk;
-            c0 = (X >> (2 * (lo_s + span - s2 - B))) & mk;
+        } else if (c.bm_dual == 3) {
+          // (F) policy 3.  Window [p, p + min_len) can start a match only if
+          // its D + 1 B-mers (offsets 0..D from p) all occur; an absent
+          // B-mer at offset s rules out the windows s - D .. s.  One k-mer
+          // entry tells three consecutive B-mers (k_kfilter), so the window's
+          // D + 1 = 3 (B = k + 2 = min_len - 2) take one probe, and inside a
+          // run of absent B-mers the entry D + 2 bases in rules out D + 3
+          // windows at once.  What is known is kept per read position (fk).
+          if (B != c.K + 2 || B > c.min_len || D + 3 > 16) {
+            proceed = true;                           // no filter for this geometry
           } else {
-            SM_REGION(22);
-            c0 = codes_raw(row, c.w_row, s2, B);
-            c1 = codes_raw(row, c.w_row, s1, B);
+            const uint32_t sh = prefix - kp;         // (prefix never decreases)
+            uint32_t kn = sh < 16 ? (fk & 0xFFFFu) >> sh : 0u;
+            uint32_t pr = sh < 16 ? (fk >> 16) >> sh : 0u;
+            kp = prefix;
+            const uint32_t A = kn & ~pr;              // known absent B-mers
+            uint32_t kill = A;                        // windows they rule out
+            for (uint32_t i = 1; i <= D; ++i) kill |= A >> i;
+            const uint32_t adv = uint32_t(__builtin_ctz(~kill));
+            if (adv) {
+              prefix += adv; kp = prefix;
+              kn >>= adv; pr >>= adv;
+              depth = 0; start = 0; end = N - 1; have_pos = false;
+            }
+            fk = kn | (pr << 16);
+            const uint32_t need = (2u << D) - 1;     // offsets 0..D
+            if (prefix + c.min_len > L) {
+              a = A_DONE;
+            } else if ((kn & pr & need) == need) {
+              proceed = true;                         // the window passes: (C)
+            } else {
+              const uint32_t W = c.K + 4;             // read bases one entry needs
+              const uint32_t u = uint32_t(__builtin_ctz(~kn & need));   // lowest unknown
+              auto ok_at = [&](uint32_t jj) {
+                return prefix + jj + W <= L && (clean || bad.bits(prefix + jj, W) == 0);
+              };
+              // after an absent B-mer, bet on a run of them: offsets D..D+2;
+              // else the entry whose three B-mers start at the lowest
+              // unknown u (or end there: near the read end the entry's
+              // context must stay inside the read) -- every probe learns u
+              uint32_t jq = (fdead && ((kn & need) >> u) == 0) ? D : u;
+              if (!ok_at(jq)) jq = u;
+              if (!ok_at(jq) && u >= 1) jq = u - 1;
+              if (!ok_at(jq) && u >= 2) jq = u - 2;
+              if (!ok_at(jq)) {
+                proceed = true;                       // a non-ACGT text byte: no verdict
+              } else {
+                SM_REGION(21);
+                fj = jq;
+                c0 = codes_raw(row, c.w_row, prefix + jq, W);
+                addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((c0 >> 4) & ((1ull << (2 * c.K)) - 1)));
+                st = S_BM;
+                a = A_NONE;
+              }
+            }
           }
-          addr = reinterpret_cast<uint64_t>(c.BM + (c1 >> 6));
-          st = S_BM; bm2 = false;
-          if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.BM + (c0 >> 6)); need2 = true; }
-          a = A_NONE;
         } else {
-          proceed = true;                             // no bitmap verdict
-          fm = 1;
+          // policies 0-2: two B-mers per probe pair
+          const uint32_t sM = prefix + 2 * D + 1;   // mode 1's second B-mer
+          bool okP = true, okQ = true;              // [p, p+B), [p+D, p+D+B): inside the read
+          bool okP1 = prefix + 1 + B <= L, okM = sM + B <= L;
+          if (!clean) {
+            okP = bad.bits(prefix, B) == 0;
+            okQ = bad.bits(prefix + D, B) == 0;
+            okP1 = okP1 && bad.bits(prefix + 1, B) == 0;
+            okM = okM && bad.bits(sM, B) == 0;
+          }
+          // probes: c1 <- B-mer at s1 (v), c0 <- B-mer at s2 (v2); mode 0 is
+          // {last, first} of this window, 1 and 2 (bm_dual 2) see S_BM
+          uint32_t s1 = prefix + D, s2 = prefix;
+          bool ok = okQ && okP;
+          if (c.bm_dual == 2 && fm == 1 && okQ && okM) {
+            s2 = sM; ok = true;
+          } else if (c.bm_dual == 2 && fm == 2 && okP && okP1) {
+            s1 = prefix; s2 = prefix + 1; ok = true;
+          } else {
+            fm = 0;
+          }
+          if (B > 0 && B <= c.min_len && ok) {
+            // both codes from one pass over the row when the span allows
+            const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;
+            const uint32_t span = hi_s + B - lo_s;
+            if (span <= 21) {
+              SM_REGION(21);
+              const uint64_t X = codes_raw(row, c.w_row, lo_s, span);
+              const uint64_t mk = (1ull << (2 * B)) - 1;
+              c1 = (X >> (2 * (lo_s + span - s1 - B))) & mk;
+              c0 = (X >> (2 * (lo_s + span - s2 - B))) & mk;
+            } else {
+              SM_REGION(22);
+              c0 = codes_raw(row, c.w_row, s2, B);
+              c1 = codes_raw(row, c.w_row, s1, B);
+            }
+            // a B-mer's presence: its first k-mer's entry (B = k + 2)
+            addr = reinterpret_cast<uint64_t>(c.KT + 2 * (c1 >> 4));
+            st = S_BM; bm2 = false;
+            if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.KT + 2 * (c0 >> 4)); need2 = true; }
+            a = A_NONE;
+          } else {
+            proceed = true;                             // no bitmap verdict
+            fm = 1;
+          }
         }
       }
       if (a == A_TOP && proceed) {                     // (C) from the root
         if (depth == 0 && prefix + c.K <= L && (clean || bad.bits(prefix, c.K) == 0)) {
-          // the window's first B-mer code (c.B >= c.K) from the filter pass
-          SM_REGION(23);
-          const uint64_t kc = ktr ? m : codes_raw(row, c.w_row, prefix, c.K);
-          addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
-          st = S_KT;
-          a = A_NONE;
+          if (kx == prefix) {
+            // the filter loaded this k-mer's entry already (policy 3)
+            SM_REGION(25);
+            if (klo <= khi) { depth = c.K; start = klo; end = khi; have_pos = false; }
+            a = A_TRAV;
+          } else {
+            // the window's first B-mer code (c.B >= c.K) from the filter pass
+            SM_REGION(23);
+            const uint64_t kc = ktr ? m : codes_raw(row, c.w_row, prefix, c.K);
+            addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
+            st = S_KT;
+            a = A_NONE;
+          }
         } else {
           a = A_TRAV;
         }

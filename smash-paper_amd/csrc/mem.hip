@@ -98,7 +98,7 @@ __device__ void traverse_x(const MemIx<IdxT> &m, const uint8_t *P, uint64_t L, u
       w = (w << 2) | uint32_t(v & 3);
     }
     if (ok) {
-      const uint64_t lo = x.KT[2 * uint64_t(w)], hi = x.KT[2 * uint64_t(w) + 1];
+      const uint64_t lo = x.KT[2 * uint64_t(w)] & kKtMask, hi = x.KT[2 * uint64_t(w) + 1] & kKtMask;
       if (lo <= hi) {
         cur.depth = uint64_t(x.K);
         cur.start = lo;

@@ -99,16 +99,25 @@ def run_map(ix, reads, min_len=20, mode=S.SMASH_MODE_MAM):
 
 
 def test_device_accelerators_equal_oracle(gix, tiny_ix):
+    """U, and the k-mer table with the (k+2)-mer presence bits of the window
+    filter (aux_build.hip k_kfilter) == the oracle's orc_build_ktf; every
+    B-mer's presence bit == the oracle's B-mer bitmap (B = k + 2)."""
     i = gix.info
     U = S.download(i.d_uniq, i.N + 64)
     KT = S.download(i.d_kmer, 16 << (2 * i.kmer_k), np.uint64)
     U2, KT2, K2 = tiny_ix.accel()
     assert i.kmer_k == K2
     assert np.array_equal(U[:i.N], U2[:i.N])
-    assert np.array_equal(KT, KT2)
-    assert i.bitmap_b == tiny_ix.acc.B
-    BM = S.download(i.d_bitmap, 8 * ((1 << (2 * i.bitmap_b)) // 64 + 1), np.uint64)
-    assert np.array_equal(BM, tiny_ix._BM)
+    assert np.array_equal(KT, tiny_ix._KTF)
+    m40 = np.uint64((1 << 40) - 1)
+    assert np.array_equal(KT & m40, KT2)
+    assert i.bitmap_b == tiny_ix.acc.B == i.kmer_k + 2 and not i.d_bitmap
+    B = i.bitmap_b
+    codes = np.arange(1 << (2 * B), dtype=np.uint64)
+    bm = (tiny_ix._BM[codes >> np.uint64(6)] >> (codes & np.uint64(63))) & np.uint64(1)
+    w0 = KT.reshape(-1, 2)[:, 0]
+    kt_bits = (w0[codes >> np.uint64(4)] >> (np.uint64(40) + (codes & np.uint64(15)))) & np.uint64(1)
+    assert np.array_equal(bm, kt_bits)
     it = [(i.in_text[c >> 6] >> (c & 63)) & 1 for c in range(256)]
     assert it == list(tiny_ix.acc.in_text)
 

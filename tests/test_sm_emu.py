@@ -25,7 +25,7 @@ def emu(tiny_ix):
 @pytest.mark.parametrize("s", ["s100", "s150"])
 @pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("lin", [2, 1])
-@pytest.mark.parametrize("bm_dual", ["0", "1", "2"])
+@pytest.mark.parametrize("bm_dual", ["0", "1", "2", "3"])
 def test_state_machine_matches_reference_goldens(emu, s, wide, lin, bm_dual, monkeypatch):
     """lin: L8 blocks scanned per side of a run before bisecting (1 forces
     the bisection path on every run longer than one block); bm_dual: the (F)

@@ -61,6 +61,17 @@ static uint4 emu_load16(uint64_t a, bool count = true) {
   return r;
 }
 #define SM_LOAD16(a) emu_load16(a)
+// the window filter's k-mer-table probes (lane state S_BM) are filed under
+// array 6 ("bitmap": the filter), the (C) descents' under 5 ("kmer")
+static uint4 emu_load16st(uint64_t a, bool filter) {
+  if (!filter || emu_array(a) != 5) return emu_load16(a);
+  emu_reqs(a, 16, false);
+  emu_count(6, a, 16);
+  uint4 r;
+  std::memcpy(&r, reinterpret_cast<const void *>(a), 16);
+  return r;
+}
+#define SM_LOAD16ST(a, st) emu_load16st(a, (st) == 4u /* S_BM */)
 // speculative SA prefetches: checked, not counted; the element the search
 // goes on with is counted (one 8- or 4-byte probe) by SM_HOOK_PF
 #define SM_LOADPF16(a) emu_load16(a, false)
@@ -115,8 +126,10 @@ static uint32_t emu_pk_sub16(uint32_t a, uint32_t b) {
 }
 #define SM_PK_SUB16(a, b) emu_pk_sub16(a, b)
 // traverse binary searches by interval size (1..63, 64 = larger) and start depth
-static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16];
+static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16], emu_f[16 * 8];
 #define SM_HOOK_BM(mode, a1, a2) (++emu_bm[4 * (mode) + 2 * (a1) + (a2)])
+// policy 3: probes by (offset j of the entry's first B-mer, 3 presence bits)
+#define SM_HOOK_F(j, bits) (++emu_f[8 * ((j) < 16 ? (j) : 15) + (bits)])
 #define SM_HOOK_BS(size, depth) \
   do { ++emu_bs_size[(size) < 64 ? (size) : 64]; ++emu_bs_depth[(depth) < 255 ? (depth) : 255]; } while (0)
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
@@ -154,13 +167,14 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   threadIdx.x = 0;
   sm::Ctx<IdxT> c;
   c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);
-  c.L8 = L8; c.U = U; c.KT = KT; c.BM = BM;
+  c.L8 = L8; c.U = U; c.KT = KT;
+  (void)BM;   // (round 3: the filter's presence bits live in KT)
   c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
   c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
   c.lin_blocks = lin_blocks;
   c.pad = 0;
   c.grab = 1;
-  c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 2;   // = the device default (mam.hip)
+  c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 3;   // = the device default (mam.hip)
   c.pf = std::getenv("SMASH_SM_PF") ? uint32_t(std::atoi(std::getenv("SMASH_SM_PF"))) : 1;
   c.u32 = std::getenv("SMASH_SM_U32") ? uint32_t(std::atoi(std::getenv("SMASH_SM_U32"))) : 1;
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
@@ -198,6 +212,11 @@ extern "C" void sm_emu_ws(uint64_t *out) {
 
 // device requests of the last sm_emu_map: [0] all, [1] speculative
 extern "C" void sm_emu_requests(uint64_t *out) { out[0] = emu_req[0]; out[1] = emu_req[1]; }
+
+// (F) policy-3 probe outcomes since the last reset: [8 * j + bits]
+extern "C" void sm_emu_filter_hist(uint64_t *out, int reset) {
+  for (int k = 0; k < 128; ++k) { out[k] = emu_f[k]; if (reset) emu_f[k] = 0; }
+}
 
 // binary-search start histograms since the last reset (size[65], depth[256])
 extern "C" void sm_emu_bs_hist(uint64_t *size, uint64_t *depth, int reset) {

@@ -52,6 +52,7 @@ def in_text_words(in_text):
     return w
 
 
+# "bitmap": the window filter's probes (k-mer table entries since round 3)
 ARRAYS = ("text", "sa", "isa", "lcp", "uniq", "kmer", "bitmap", "records")
 # k_mam_sm lane states and ops (mam_sm.hpp enums), for the STATS counters
 STATES = ("EXIT", "NEW", "ALU", "COPY", "BM", "KT", "IDX", "BYTE", "CMP", "USCAN", "EXL", "EXR", "EXB")
@@ -84,8 +85,8 @@ class Emu:
         self.ISA = P(ix.ISA, it)
         self.L8 = P(ix.L8, np.uint8)
         self.U = P(ix._U, np.uint8)
-        self.KT = P(ix._KT, np.uint64)
-        self.BM = P(ix._BM, np.uint64)
+        self.KT = P(ix._KTF, np.uint64)          # the device layout (orc_build_ktf)
+        self.BM = P(np.zeros(1, np.uint64), np.uint64)   # (unused since round 3)
         self.K = ix.acc.K
         self.B = ix.acc.B
         self.it = in_text_words(list(ix.acc.in_text))

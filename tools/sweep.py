@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=2_000_000,
                     help="one batch of this many pairs (the A/B logs of round 2 use 2 M)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="run the --pairs as count_batches of this many pairs (the bench's "
+                         "C3 step: --pairs 25000000 --batch 6250000)")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     import tempfile
@@ -44,7 +47,8 @@ def main():
     P, L = a.pairs, cfg["read_len"]           # one batch of the config's reads
     import readgen
     d_reads = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000).generate(P)
-    pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P)
+    B = a.batch or P
+    pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
     counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
     ref = None
     print("[sweep] ready: %d pairs x %d bp" % (P, L), flush=True)
@@ -54,13 +58,20 @@ def main():
         os.environ.update(env)
         if any(k.startswith("SMASH_POST") for k in env) or pipe is None:
             pipe = None                      # read at create: a fresh pipeline
-            pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P)
-        pipe.reset(); counts.zero_(); pipe.count_batch(d_reads, P, counts)   # warm-up
+            pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
+
+        def run():
+            pipe.reset(); counts.zero_()
+            if a.batch:
+                pipe.count_batches(d_reads, P, B, counts)
+            else:
+                pipe.count_batch(d_reads, P, counts)
+        run()   # warm-up
         torch.cuda.synchronize()
         pipe.profile(True)
         t = time.perf_counter()
         for _ in range(a.steps):
-            pipe.reset(); counts.zero_(); pipe.count_batch(d_reads, P, counts)
+            run()
         torch.cuda.synchronize()
         el = (time.perf_counter() - t) / a.steps
         ms, launches, _ = pipe.profile_read()
