@@ -312,54 +312,63 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
-def feed_bench(S, dix, cs, starts, L, d_reads, P, dev, tmpdir, n_plain=1000000,
-               n_gz=250000, batch=250000):
-    """The file-fed rate (smash_count_fastq, csrc/feed.hip): the first pairs
-    of the same reads written as FASTQ (names in sort -n order) to local disk,
-    then counted from the files with parse / H2D / compute overlapped, plain
-    and gzip; the counts must equal the device-resident path's on the same
+def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_gz=4000000,
+               gz_lanes=8):
+    """The file-fed rate (smash_count_fastq, csrc/feed.hip): the same reads
+    written as FASTQ (names in sort -n order) to local disk, then counted from
+    the files through the bench's own pipeline (its batches of B pairs) with
+    parse / H2D / compute overlapped: plain as ONE file pair of all P pairs
+    (the C3 run; the parallel reader indexes it by byte range), gzip as
+    `gz_lanes` lane files per mate (SMASH passes lane lists; gzip inflates one
+    thread per file).  Counts must equal the device-resident run's on the same
     pairs.  Also the pinned H2D copy rate."""
+    import shutil
     import torch
     import readgen
     res = {}
-    n_plain = min(P, n_plain)
+    n_plain = min(P, n_plain or P)
+    rec = 2 * (2 * L + 21)                 # bytes per pair on disk
+    free = shutil.disk_usage(tmpdir).free
+    if n_plain * rec * 1.2 > free:         # (a box with little scratch space: fewer pairs)
+        n_plain = int(free / 1.2 / rec)
     n_gz = min(n_plain, n_gz)
-    h = d_reads[:2 * n_plain].cpu().numpy()
-    # resident reference counts on the same pairs and batches
-    pipe = S.Pipeline(dix, cs, starts, L, batch, dedup_capacity=n_plain + (1 << 16))
 
     def resident(n):
         pipe.reset()
         c = torch.zeros(len(starts), dtype=torch.int64, device=dev)
-        pipe.count_batches(d_reads, n, batch, c)
+        pipe.count_batches(d_reads, n, B, c)
         return c.cpu().numpy()
 
-    for kind, n in (("plain", n_plain), ("gz", n_gz)):
-        ext = ".fq.gz" if kind == "gz" else ".fq"
-        p1, p2 = os.path.join(tmpdir, "r1" + ext), os.path.join(tmpdir, "r2" + ext)
+    for kind, n, lanes in (("plain", n_plain, 1), ("gz", n_gz, gz_lanes)):
         t0 = time.perf_counter()
-        readgen.write_fastq(h[:2 * n], p1, p2, gz=kind == "gz")
+        h = d_reads[:2 * n].cpu().numpy()
+        p1, p2 = readgen.write_fastq_lanes(h, os.path.join(tmpdir, kind), lanes, gz=kind == "gz")
+        del h
         wr = time.perf_counter() - t0
-        nbytes = os.path.getsize(p1) + os.path.getsize(p2)
+        nbytes = sum(os.path.getsize(q) for q in p1 + p2)
         exp = resident(n)
         pipe.reset()
         c = torch.zeros(len(starts), dtype=torch.int64, device=dev)
         torch.cuda.synchronize()
-        fs = pipe.count_fastq([p1], [p2], c, sort_names=False)
+        fs = pipe.count_fastq(p1, p2, c, sort_names=False)
         same = bool(np.array_equal(c.cpu().numpy(), exp))
         res[kind] = {"reads_per_s": round(2 * fs["pairs"] / fs["wall_s"], 1),
                      "pairs": int(fs["pairs"]), "batches": int(fs["batches"]),
-                     "wall_s": round(fs["wall_s"], 3), "ingest_s": round(fs["ingest_s"], 3),
+                     "files_per_mate": lanes, "parallel_reader": bool(fs["parallel"]),
+                     "wall_s": round(fs["wall_s"], 3), "index_s": round(fs["index_s"], 3),
+                     "ingest_s": round(fs["ingest_s"], 3),
                      "device_waited_s": round(fs["wait_s"], 3), "file_bytes": int(nbytes),
                      "counts_identical_to_resident": same}
-        log("file-fed %s: %d pairs, %.3f s -> %.3e reads/s (ingest %.3f s, device waited %.3f s, "
-            "%.1f MB, written in %.1f s); counts == resident: %s"
-            % (kind, fs["pairs"], fs["wall_s"], 2 * fs["pairs"] / fs["wall_s"], fs["ingest_s"],
-               fs["wait_s"], nbytes / 1e6, wr, same))
-        for q in (p1, p2):
+        log("file-fed %s: %d pairs in %d file(s) per mate, %.3f s -> %.3e reads/s (index %.3f s, "
+            "ingest %.3f s, device waited %.3f s, %.1f GB, written in %.1f s, parallel reader %s); "
+            "counts == resident: %s"
+            % (kind, fs["pairs"], lanes, fs["wall_s"], 2 * fs["pairs"] / fs["wall_s"],
+               fs["index_s"], fs["ingest_s"], fs["wait_s"], nbytes / 1e9, wr,
+               bool(fs["parallel"]), same))
+        for q in p1 + p2:
             os.remove(q)
     # the pinned host -> device copy rate of one batch of reads
-    hp = torch.from_numpy(h[:2 * min(n_plain, batch)]).pin_memory()
+    hp = torch.from_numpy(d_reads[:2 * min(P, 1000000)].cpu().numpy()).pin_memory()
     dd = torch.empty_like(hp, device=dev)
     dd.copy_(hp, non_blocking=True)
     torch.cuda.synchronize()
@@ -370,10 +379,11 @@ def feed_bench(S, dix, cs, starts, L, d_reads, P, dev, tmpdir, n_plain=1000000,
     gbs = 5 * hp.numel() / (time.perf_counter() - t0) / 1e9
     res["h2d_pinned_GBps"] = round(gbs, 2)
     res["h2d_reads_per_s"] = round(gbs * 1e9 / L, 1)
-    res["method"] = ("smash_count_fastq (csrc/feed.hip): 2 parse threads (one per mate list), "
-                     "3 pinned slots, 2 device buffers, H2D on its own stream; batches of %d "
-                     "pairs; FASTQ on local disk, names in sort -n order (streamed)" % batch)
-    del pipe
+    res["method"] = ("smash_count_fastq (csrc/feed.hip) through the bench's pipeline: strict "
+                     "4-line FASTQ read by the parallel reader (csrc/fastq_par.hpp: files mapped "
+                     "or inflated, records indexed by byte range, checked and packed on all "
+                     "host threads), 3 pinned slots, 2 device buffers, H2D on its own stream; "
+                     "batches of %d pairs; FASTQ on local disk, names in sort -n order" % B)
     return res
 
 
@@ -389,7 +399,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 scan on the same index")
     ap.add_argument("--no-feed", action="store_true", help="skip the file-fed measurement")
-    ap.add_argument("--feed-pairs", type=int, default=1000000)
+    ap.add_argument("--feed-pairs", type=int, default=0,
+                    help="pairs of the file-fed run (0: all the rank's pairs, the C3 run)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.pairs:
@@ -630,7 +641,7 @@ def main():
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
     if rank == 0 and world == 1 and not args.no_feed:
-        out["host_boundary"] = feed_bench(S, dix, cs, starts, L, d_reads, P, dev, tmpdir,
+        out["host_boundary"] = feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir,
                                           n_plain=args.feed_pairs)
     if cfg["genome"] == "hg19" and not args.no_c5:
         out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)

@@ -412,9 +412,12 @@ int smash_strnum_order(const char *names, uint32_t stride, uint64_t n, uint64_t 
 /* stream into two device buffers, and counted with smash_count_batch on      */
 /* `stream`: parse, copy and compute of consecutive batches overlap.          */
 /*  sort_names = 0: the input is in samtools sort -n order already (checked   */
-/*                  on the read-1 names; SMASH_ERR_ARG if not, counts then    */
-/*                  partial); 1: all pairs are read, ordered by strnum_cmp    */
-/*                  (stable), then streamed.                                  */
+/*                  on the read-1 names; SMASH_ERR_ARG if not: before any     */
+/*                  count with strict 4-line FASTQ, else counts partial);     */
+/*                  1: all pairs are read, ordered by strnum_cmp (stable),    */
+/*                  then streamed.                                            */
+/*  Strict 4-line FASTQ (plain or gzip) is read by the parallel reader        */
+/*  (smash_fastq_read_parallel); anything else by the streaming reader.       */
 /* Adds into d_counts like smash_count_batch (the caller resets the pipeline  */
 /* when a new run starts).  Synchronises `stream` before returning.           */
 /* ========================================================================== */
@@ -425,7 +428,21 @@ typedef struct {
   double ingest_s;    /* host time parsing / converting / ordering */
   double wait_s;      /* time the device side waited for a parsed batch */
   uint32_t read_len;
+  uint32_t parallel;  /* 1: the parallel reader ran (strict 4-line FASTQ), 0: streaming */
+  double index_s;     /* parallel reader: map / inflate, index, checks before batch 0 */
 } smash_feed_stats;
+/* The parallel reader of smash_count_fastq, on its own (host only): every
+ * pair of the two lists (strict 4-line FASTQ, plain or gzip; plain files are
+ * mapped and indexed by byte range, gzip files inflated one thread per file)
+ * as smash_fastq_read returns them, in file order, on `threads` threads.
+ * *len: in, the required read length (0: the first pair's); out, the length.
+ * h_reads NULL: *n_pairs = the pairs only.  h_names: read-1 names, NUL
+ * padded, name_stride bytes each.  SMASH_ERR_UNSUPPORTED: the input is not
+ * strict 4-line FASTQ (FASTA records, blank lines, ...): use smash_fastq_read. */
+int smash_fastq_read_parallel(const char *const *r1, uint32_t n1, const char *const *r2,
+                              uint32_t n2, uint32_t threads, uint32_t *len, uint64_t cap_pairs,
+                              uint8_t *h_reads, char *h_names, uint32_t name_stride,
+                              uint64_t *n_pairs);
 int smash_count_fastq(smash_pipeline *p, const char *const *r1_paths, uint32_t n1,
                       const char *const *r2_paths, uint32_t n2, int sort_names,
                       uint32_t threads, uint64_t *d_counts, smash_feed_stats *stats,

@@ -27,6 +27,7 @@
 #include <thread>
 
 #include "common.hpp"
+#include "fastq_par.hpp"
 #include "ingest.hpp"
 
 using smash::ingest::Chunk;
@@ -83,6 +84,8 @@ struct Feed {
   int err = 0;
   std::string msg;
   double ingest_s = 0;
+  double index_s = 0;      // parallel path: map / inflate + index + checks, before batch 0
+  bool parallel = false;   // the parallel producer ran
 
   void fail(int e, const std::string &m) {
     std::lock_guard<std::mutex> g(mu);
@@ -226,6 +229,60 @@ struct Feed {
     }
   }
 
+  // parallel producer (fastq_par.hpp): every file mapped / inflated and
+  // indexed by byte range, the pairs checked, ordered (sort_names) or checked
+  // for order, all on T threads; then batches packed on T threads.  false:
+  // the input is not strict 4-line FASTQ (nothing consumed: the streaming
+  // producers take it from the start)
+  bool produce_parallel(bool sort_names) {
+    namespace I = smash::ingest;
+    const auto t0 = Clock::now();
+    I::PairIndex px;
+    std::string m;
+    int rc = px.build(r1.paths, r2.paths, T, m);
+    if (rc == SMASH_ERR_UNSUPPORTED) return false;
+    I::Plan pl;
+    if (rc == SMASH_OK) rc = I::plan_pairs(px, T, L, !sort_names, sort_names, pl, m);
+    if (rc != SMASH_OK) {
+      fail(rc, "smash_count_fastq: " + m);
+      return true;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu);
+      ingest_s += secs(t0, Clock::now());
+      index_s = secs(t0, Clock::now());
+      parallel = true;
+    }
+    for (uint64_t b = 0, k0 = 0;; ++b) {
+      Slot &s = slot[b % 3];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return s.state == 0 || err; });
+        if (err) return true;
+      }
+      const auto t1 = Clock::now();
+      const uint64_t k = std::min(B, pl.n_out - k0);
+      I::pack_pairs(px, pl, k0, k0 + k, s.h, nullptr, 0, T);
+      k0 += k;
+      const bool end = k0 >= pl.n_out;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        ingest_s += secs(t1, Clock::now());
+        s.n = k;
+        s.last = end;
+        s.state = 1;
+      }
+      cv.notify_all();
+      if (end) return true;
+    }
+  }
+
+  void produce(bool sort_names) {
+    if (produce_parallel(sort_names)) return;
+    if (sort_names) produce_sorted();
+    else produce_stream();
+  }
+
   // buffered producer: read all, order by name, stream batches
   void produce_sorted() {
     const uint8_t *lut = smash::ingest::lut();
@@ -350,10 +407,7 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
       rc = SMASH_ERR_NOMEM;
       break;
     }
-    prod = std::thread([&] {
-      if (sort_names) f->produce_sorted();
-      else f->produce_stream();
-    });
+    prod = std::thread([&] { f->produce(sort_names != 0); });
     for (uint64_t b = 0;; ++b) {
       Slot &s = f->slot[b % 3];
       const auto w0 = Clock::now();
@@ -409,6 +463,8 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
     st->ingest_s = f->ingest_s;
     st->wait_s = wait_s;
     st->read_len = f->L;
+    st->parallel = f->parallel ? 1u : 0u;
+    st->index_s = f->index_s;
   }
   return rc;
 }

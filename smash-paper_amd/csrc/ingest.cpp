@@ -20,6 +20,7 @@
 #include <thread>
 #include <vector>
 
+#include "fastq_par.hpp"
 #include "ingest.hpp"
 
 namespace smash {
@@ -131,5 +132,45 @@ extern "C" int smash_strnum_order(const char *names, uint32_t stride, uint64_t n
   std::stable_sort(perm, perm + n, [&](uint64_t x, uint64_t y) {
     return strnum_cmp(names + x * stride, len[x], names + y * stride, len[y]) < 0;
   });
+  return SMASH_OK;
+}
+
+// The parallel reader (fastq_par.hpp) over the same lists, all pairs at once:
+// the pairs smash_fastq_read would return, in file order, on `threads`
+// threads.  h_reads NULL: count only (*n_pairs = the kept pairs, *len their
+// length).  SMASH_ERR_UNSUPPORTED: not strict 4-line FASTQ (the streaming
+// reader handles those).  Host only.
+extern "C" int smash_fastq_read_parallel(const char *const *r1, uint32_t n1,
+                                         const char *const *r2, uint32_t n2, uint32_t threads,
+                                         uint32_t *len, uint64_t cap_pairs, uint8_t *h_reads,
+                                         char *h_names, uint32_t name_stride,
+                                         uint64_t *n_pairs) {
+  if (!r1 || !r2 || n1 == 0 || n2 == 0 || !len || !n_pairs || (h_names && name_stride < 2)) {
+    set_error("smash_fastq_read_parallel: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  std::vector<std::string> p1(r1, r1 + n1), p2(r2, r2 + n2);
+  smash::ingest::PairIndex px;
+  std::string msg;
+  const uint32_t T = threads ? threads : 1;
+  int rc = px.build(p1, p2, T, msg);
+  if (rc == SMASH_ERR_UNSUPPORTED) msg = "not strict 4-line FASTQ";
+  smash::ingest::Plan pl;
+  if (rc == SMASH_OK) rc = smash::ingest::plan_pairs(px, T, *len, false, false, pl, msg);
+  if (rc != SMASH_OK) {
+    set_error("smash_fastq_read_parallel: " + msg);
+    return rc;
+  }
+  *len = pl.L;
+  *n_pairs = pl.n_out;
+  if (!h_reads) return SMASH_OK;
+  if (pl.n_out > cap_pairs) {
+    set_error("smash_fastq_read_parallel: more pairs than cap_pairs");
+    return SMASH_ERR_ARG;
+  }
+  if (!smash::ingest::pack_pairs(px, pl, 0, pl.n_out, h_reads, h_names, name_stride, T)) {
+    set_error("smash_fastq_read_parallel: read name longer than name_stride - 1");
+    return SMASH_ERR_ARG;
+  }
   return SMASH_OK;
 }

@@ -52,7 +52,7 @@ EXPORTS = [
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
     "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
-    "smash_pipeline_profile_intervals",
+    "smash_pipeline_profile_intervals", "smash_fastq_read_parallel",
     "smash_phase_map_ahead", "smash_sam_records_packed",
 ]
 
@@ -78,7 +78,8 @@ class PipelineCfg(C.Structure):
 
 class FeedStats(C.Structure):
     _fields_ = [("pairs", C.c_uint64), ("batches", C.c_uint64), ("wall_s", C.c_double),
-                ("ingest_s", C.c_double), ("wait_s", C.c_double), ("read_len", C.c_uint32)]
+                ("ingest_s", C.c_double), ("wait_s", C.c_double), ("read_len", C.c_uint32),
+                ("parallel", C.c_uint32), ("index_s", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -168,6 +169,9 @@ def lib():
     L.smash_fastq_close.argtypes = [vp]
     L.smash_fastq_close.restype = None
     L.smash_strnum_order.argtypes = [vp, C.c_uint32, C.c_uint64, u64p]
+    L.smash_fastq_read_parallel.argtypes = [C.POINTER(C.c_char_p), C.c_uint32,
+                                            C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
+                                            u32p, C.c_uint64, vp, vp, C.c_uint32, u64p]
     L.smash_count_fastq.argtypes = [vp, C.POINTER(C.c_char_p), C.c_uint32,
                                     C.POINTER(C.c_char_p), C.c_uint32, C.c_int, C.c_uint32, vp,
                                     C.POINTER(FeedStats), vp]
@@ -739,6 +743,28 @@ def read_fastq_pairs(r1_paths, r2_paths, batch_pairs=1 << 20, name_stride=64):
     if not reads:
         return np.zeros(0, "S%d" % name_stride), np.zeros((0, 0), np.uint8)
     return np.concatenate(names), np.concatenate(reads)
+
+
+def read_fastq_pairs_parallel(r1_paths, r2_paths, threads=0, name_stride=64, read_len=0):
+    """read_fastq_pairs through the parallel reader (smash_fastq_read_parallel):
+    strict 4-line FASTQ only (SmashError SMASH_ERR_UNSUPPORTED otherwise)."""
+    arr1 = _cstrs([os.fsencode(p) for p in r1_paths])
+    arr2 = _cstrs([os.fsencode(p) for p in r2_paths])
+    T = threads or min(16, os.cpu_count() or 1)
+    L = C.c_uint32(read_len)
+    n = C.c_uint64()
+    check(lib().smash_fastq_read_parallel(arr1, len(r1_paths), arr2, len(r2_paths), T, C.byref(L),
+                                          0, None, None, name_stride, C.byref(n)),
+          "smash_fastq_read_parallel")
+    k = n.value
+    rb = np.empty((2 * max(k, 1), max(L.value, 1)), np.uint8)
+    nb = np.zeros(max(k, 1), "S%d" % name_stride)
+    check(lib().smash_fastq_read_parallel(arr1, len(r1_paths), arr2, len(r2_paths), T, C.byref(L),
+                                          k, _p(rb, vp), _p(nb, vp), name_stride, C.byref(n)),
+          "smash_fastq_read_parallel")
+    if not k:
+        return np.zeros(0, "S%d" % name_stride), np.zeros((0, 0), np.uint8)
+    return nb[:k], rb[:2 * k, :L.value]
 
 
 def first_read_length(paths):

@@ -244,6 +244,98 @@ def test_one_empty_mate_is_an_error(tmp_path):
         S.read_fastq_pairs([str(a)], [str(b)])
 
 
+def _strict_fq(path, recs, gz=False, crlf=False, final_nl=True):
+    """write 4-line FASTQ records [(name_line, bases, plus_line, quals)]"""
+    nl = b"\r\n" if crlf else b"\n"
+    body = nl.join(b"\n".join([a, b, c, d]) if not crlf else nl.join([a, b, c, d])
+                   for a, b, c, d in recs) + (nl if final_nl else b"")
+    if gz:
+        with gzip.open(path, "wb") as f:
+            f.write(body)
+    else:
+        path.write_bytes(body)
+    return str(path)
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+@pytest.mark.parametrize("threads", [1, 3, 16])
+def test_parallel_reader_equals_streaming_reader(tmp_path, s, threads):
+    """smash_fastq_read_parallel (csrc/fastq_par.hpp: files mapped / inflated,
+    records found per byte range) == smash_fastq_read on the golden reads:
+    gzip and plain, the read-1 list split over two files."""
+    lines = open(_fq(tmp_path, s, 1), "rb").read().split(b"\n")
+    cut = 4 * 37
+    a, b = tmp_path / "a.fq.gz", tmp_path / "b.fq"
+    with gzip.open(a, "wb") as f:
+        f.write(b"\n".join(lines[:cut]) + b"\n")
+    b.write_bytes(b"\n".join(lines[cut:]))
+    l1, l2 = [str(a), str(b)], [gold("%s_r2.fq.gz" % s)]
+    n0, r0 = S.read_fastq_pairs(l1, l2, batch_pairs=50)
+    n1, r1 = S.read_fastq_pairs_parallel(l1, l2, threads=threads)
+    assert n1.tolist() == n0.tolist() and np.array_equal(r1, r0)
+
+
+def test_parallel_reader_record_boundaries(tmp_path):
+    """Byte ranges that start inside any line: quality lines beginning with
+    '@' (and '+'), '+name' lines, CRLF endings, Illumina comments, N -> z,
+    a pair with both mates empty (dropped), a last line without '\\n', the
+    two lists of different lengths (zip: the shorter ends the pairs);
+    thousands of records so the 32 MB ranges of the index cut records."""
+    rng = np.random.default_rng(7)
+    recs1, recs2 = [], []
+    for i in range(40000):
+        L = 150
+        pick = lambda al, **k: np.array(rng.choice(list(al), L, **k), np.uint8).tobytes()
+        q1, q2 = pick(b"@+!#IJ"), pick(b"@+IJ")
+        b1 = pick(b"ACGTN", p=[.24, .24, .24, .24, .04])
+        b2 = pick(b"ACGTacgtN")
+        if i == 777:
+            b1, b2, q1, q2 = b"", b"", b"", b""
+        recs1.append((b"@r%08d 1:N:0:AC" % i, b1, b"+" if i % 3 else b"+r%08d" % i, q1))
+        recs2.append((b"@r%08d 2:N:0:AC" % i, b2, b"+", q2))
+    recs2.append((b"@extra", b"A" * 150, b"+", b"I" * 150))
+    a = _strict_fq(tmp_path / "a.fq", recs1, final_nl=False)
+    b = _strict_fq(tmp_path / "b.fq.gz", recs2, gz=True)
+    c = _strict_fq(tmp_path / "c.fq", recs1[:5], crlf=True)
+    d = _strict_fq(tmp_path / "d.fq", recs2[:5], crlf=True)
+    for l1, l2 in (([a], [b]), ([c], [d]), ([c, a], [d, b])):
+        n0, r0 = S.read_fastq_pairs(l1, l2, batch_pairs=4096)
+        for T in (1, 7):
+            n1, r1 = S.read_fastq_pairs_parallel(l1, l2, threads=T)
+            assert n1.tolist() == n0.tolist() and np.array_equal(r1, r0)
+    assert len(n1) == 40000 + 4    # (c: 5, a: 40000) - the empty pair; zip drops "extra"
+
+
+def test_parallel_reader_refuses_what_it_cannot_index(tmp_path):
+    """Not strict 4-line FASTQ (blank lines, FASTA records, a '+' line with
+    leading blanks, a truncated last record): SMASH_ERR_UNSUPPORTED, and the
+    streaming reader reads them; errors are the streaming reader's."""
+    bad = [b"@a\nACGT\n+\nIIII\n\n@b\nACGT\n+\nIIII\n",
+           b">a\nACGT\n>b\nACGT\n",
+           b"@a\nACGT\n +\nIIII\n",
+           b"@a\nACGT\n+\nIIII\n@b\nACGT\n"]
+    ok = tmp_path / "ok.fq"
+    ok.write_bytes(b"@a\nACGT\n+\nIIII\n@b\nACGT\n+\nIIII\n")
+    for k, body in enumerate(bad):
+        f = tmp_path / ("bad%d.fq" % k)
+        f.write_bytes(body)
+        with pytest.raises(S.SmashError, match="not strict"):
+            S.read_fastq_pairs_parallel([str(f)], [str(ok)])
+    a, b = tmp_path / "a.fq", tmp_path / "b.fq"
+    a.write_bytes(b"@p1\nACGT\n+\nIIII\n@p2\n\n+\n\n")
+    b.write_bytes(b"@p1\nTTTT\n+\nIIII\n@p2\nCCCC\n+\nJJJJ\n")
+    with pytest.raises(S.SmashError, match="no bases"):
+        S.read_fastq_pairs_parallel([str(a)], [str(b)])
+    b.write_bytes(b"@p1\nTTTT\n+\nIIII\n@p2\nCCCCC\n+\nJJJJJ\n")
+    a.write_bytes(b"@p1\nACGT\n+\nIIII\n@p2\nACGT\n+\nIIII\n")
+    with pytest.raises(S.SmashError, match="same length"):
+        S.read_fastq_pairs_parallel([str(a)], [str(b)])
+    with pytest.raises(S.SmashError, match="same length"):
+        S.read_fastq_pairs([str(a)], [str(b)])
+    with pytest.raises(S.SmashError, match="cannot open"):
+        S.read_fastq_pairs_parallel(["/nonexistent.fq"], [str(ok)])
+
+
 def test_native_strnum_order_equals_samtools_key():
     rng = np.random.default_rng(5)
     alpha = list("ab:_-./ ") + [str(d) for d in range(10)]

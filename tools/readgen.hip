@@ -16,7 +16,9 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -98,41 +100,75 @@ extern "C" uint32_t rg_iv_bytes(void) { return sizeof(Iv); }
 // zero-padded to 12 digits (already in samtools sort -n order), bases upper
 // case with 'z' -> 'N' (what ingest's replaceN + lowercasing turns back into
 // the same bytes), qualities 'I'.  gz: gzip level 1, else plain.  0 = ok.
+// one mate's records of pairs [i0, i1) (names r%012llu/<mate>, fixed width:
+// every record is 2L + 21 bytes) formatted into out
+static void rg_format(const uint8_t *h_reads, uint64_t i0, uint64_t i1, uint32_t L, uint64_t q0,
+                      int mate, char *out) {
+  char *o = out;
+  for (uint64_t i = i0; i < i1; ++i) {
+    o += snprintf(o, 20, "@r%012llu/%d\n", (unsigned long long)(q0 + i), mate + 1);
+    const uint8_t *r = h_reads + (2 * i + mate) * L;
+    for (uint32_t j = 0; j < L; ++j) o[j] = r[j] == 'z' ? 'N' : char(r[j] - 32);
+    o += L;
+    *o++ = '\n';
+    *o++ = '+';
+    *o++ = '\n';
+    memset(o, 'I', L);
+    o += L;
+    *o++ = '\n';
+  }
+}
+
+// pairs [0, n) split into `lanes` consecutive lane files per mate
+// (path1[k] / path2[k]), gzip (level 1) or plain; every file on its own
+// thread, plain files formatted in parallel slices
+extern "C" int rg_write_fastq_lanes(const uint8_t *h_reads, uint64_t n_pairs, uint32_t L,
+                                    uint64_t q0, uint32_t lanes, const char *const *path1,
+                                    const char *const *path2, int gz) {
+  const uint64_t rec = 2ull * L + 21;
+  std::vector<int> rc(2 * lanes, 0);
+  std::vector<std::thread> th;
+  for (uint32_t k = 0; k < lanes; ++k)
+    for (int mate = 0; mate < 2; ++mate)
+      th.emplace_back([&, k, mate] {
+        const uint64_t i0 = n_pairs * k / lanes, i1 = n_pairs * (k + 1) / lanes;
+        const char *path = mate ? path2[k] : path1[k];
+        std::vector<char> out(size_t((i1 - i0) * rec) + 32);
+        // format in 8 slices (plain files of one lane are large)
+        std::vector<std::thread> fs;
+        const uint32_t S = 8;
+        for (uint32_t t = 0; t < S; ++t)
+          fs.emplace_back([&, t] {
+            const uint64_t a = i0 + (i1 - i0) * t / S, b = i0 + (i1 - i0) * (t + 1) / S;
+            rg_format(h_reads, a, b, L, q0, mate, out.data() + (a - i0) * rec);
+          });
+        for (auto &x : fs) x.join();
+        const size_t bytes = size_t((i1 - i0) * rec);
+        int &r = rc[2 * k + mate];
+        if (gz) {
+          gzFile f = gzopen(path, "wb1");
+          if (!f) { r = 1; return; }
+          size_t o = 0;
+          while (o < bytes) {
+            const unsigned c = unsigned(std::min<size_t>(bytes - o, size_t(1) << 30));
+            if (gzwrite(f, out.data() + o, c) != int(c)) { r = 2; break; }
+            o += c;
+          }
+          if (gzclose(f) != Z_OK) r = 3;
+        } else {
+          FILE *f = fopen(path, "wb");
+          if (!f) { r = 1; return; }
+          const bool ok = fwrite(out.data(), 1, bytes, f) == bytes;
+          if (fclose(f) != 0 || !ok) r = 2;
+        }
+      });
+  for (auto &x : th) x.join();
+  for (int r : rc)
+    if (r) return r;
+  return 0;
+}
+
 extern "C" int rg_write_fastq(const uint8_t *h_reads, uint64_t n_pairs, uint32_t L, uint64_t q0,
                               const char *path1, const char *path2, int gz) {
-  const char *paths[2] = {path1, path2};
-  for (int mate = 0; mate < 2; ++mate) {
-    std::vector<char> out;
-    out.reserve(size_t(n_pairs) * (2 * L + 24));
-    char head[40];
-    for (uint64_t i = 0; i < n_pairs; ++i) {
-      const int h = snprintf(head, sizeof(head), "@r%012llu/%d\n", (unsigned long long)(q0 + i),
-                             mate + 1);
-      out.insert(out.end(), head, head + h);
-      const uint8_t *r = h_reads + (2 * i + mate) * L;
-      for (uint32_t j = 0; j < L; ++j) out.push_back(r[j] == 'z' ? 'N' : char(r[j] - 32));
-      out.push_back('\n');
-      out.push_back('+');
-      out.push_back('\n');
-      out.insert(out.end(), L, 'I');
-      out.push_back('\n');
-    }
-    if (gz) {
-      gzFile f = gzopen(paths[mate], "wb1");
-      if (!f) return 1;
-      size_t o = 0;
-      while (o < out.size()) {
-        const unsigned k = unsigned(std::min<size_t>(out.size() - o, size_t(1) << 30));
-        if (gzwrite(f, out.data() + o, k) != int(k)) { gzclose(f); return 2; }
-        o += k;
-      }
-      if (gzclose(f) != Z_OK) return 3;
-    } else {
-      FILE *f = fopen(paths[mate], "wb");
-      if (!f) return 1;
-      const bool ok = fwrite(out.data(), 1, out.size(), f) == out.size();
-      if (fclose(f) != 0 || !ok) return 2;
-    }
-  }
-  return 0;
+  return rg_write_fastq_lanes(h_reads, n_pairs, L, q0, 1, &path1, &path2, gz);
 }

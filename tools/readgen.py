@@ -28,6 +28,8 @@ def lib():
         L.rg_iv_bytes.restype = C.c_uint32
         L.rg_write_fastq.argtypes = [vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_char_p,
                                      C.c_char_p, C.c_int]
+        L.rg_write_fastq_lanes.argtypes = [vp, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
+                                           C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_int]
         _LIB = L
     return _LIB
 
@@ -78,6 +80,23 @@ def write_fastq(h_reads, path1, path2, gz=False, q0=0):
                               int(gz))
     if rc:
         raise RuntimeError("rg_write_fastq failed (%d)" % rc)
+
+
+def write_fastq_lanes(h_reads, prefix, lanes, gz=False, q0=0):
+    """pairs of h_reads as `lanes` consecutive lane files per mate
+    (prefix_L<k>_R<1|2>.fq[.gz], names in order; rg_write_fastq_lanes, one
+    thread per file); returns (read-1 paths, read-2 paths)."""
+    h = np.ascontiguousarray(h_reads)
+    n, L = h.shape[0] // 2, h.shape[1]
+    ext = ".fq.gz" if gz else ".fq"
+    p1 = ["%s_L%03d_R1%s" % (prefix, k, ext) for k in range(lanes)]
+    p2 = ["%s_L%03d_R2%s" % (prefix, k, ext) for k in range(lanes)]
+    a1 = (C.c_char_p * lanes)(*[os.fsencode(x) for x in p1])
+    a2 = (C.c_char_p * lanes)(*[os.fsencode(x) for x in p2])
+    rc = lib().rg_write_fastq_lanes(h.ctypes.data, n, L, q0, lanes, a1, a2, int(gz))
+    if rc:
+        raise RuntimeError("rg_write_fastq_lanes failed (%d)" % rc)
+    return p1, p2
 
 
 def S_startpos(index):
