@@ -453,7 +453,9 @@ def main():
 
     if world > 1:
         from dist import ShardedCounter
-        sc = ShardedCounter(pipe, rank, world, dev)
+        # the per-batch key counts are host integers: exchanged over gloo
+        # they need no device synchronisation
+        sc = ShardedCounter(pipe, rank, world, dev, count_group=dist.new_group(backend="gloo"))
 
     def step(i):
         """one run over the rank's P pairs: a fresh key set / adjacent-dup

@@ -443,6 +443,21 @@ int smash_fastq_read_parallel(const char *const *r1, uint32_t n1, const char *co
                               uint32_t n2, uint32_t threads, uint32_t *len, uint64_t cap_pairs,
                               uint8_t *h_reads, char *h_names, uint32_t name_stride,
                               uint64_t *n_pairs);
+/* The same reader as an object (host only): both lists mapped / inflated and
+ * indexed once, the pairs checked and put in samtools sort -n order
+ * (sort_names 1: stable sort by read-1 name; 0: the order is checked,
+ * SMASH_ERR_ARG if violated); *n_pairs planned pairs, *len their length
+ * (in: 0 or the required length).  _pack writes planned pairs [k0, k1) like
+ * smash_fastq_read (2 (k1 - k0) len bytes; names optional), on the index's
+ * threads -- the multi-GPU driver deals batches to ranks from one index
+ * (smash-paper_amd/dist.py count_fastq). */
+typedef struct smash_fastq_index smash_fastq_index;
+int smash_fastq_index_open(const char *const *r1, uint32_t n1, const char *const *r2,
+                           uint32_t n2, uint32_t threads, uint32_t *len, int sort_names,
+                           smash_fastq_index **out, uint64_t *n_pairs);
+int smash_fastq_index_pack(smash_fastq_index *ix, uint64_t k0, uint64_t k1, uint8_t *h_reads,
+                           char *h_names, uint32_t name_stride);
+void smash_fastq_index_close(smash_fastq_index *ix);
 int smash_count_fastq(smash_pipeline *p, const char *const *r1_paths, uint32_t n1,
                       const char *const *r2_paths, uint32_t n2, int sort_names,
                       uint32_t threads, uint64_t *d_counts, smash_feed_stats *stats,

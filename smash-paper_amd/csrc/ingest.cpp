@@ -135,11 +135,61 @@ extern "C" int smash_strnum_order(const char *names, uint32_t stride, uint64_t n
   return SMASH_OK;
 }
 
-// The parallel reader (fastq_par.hpp) over the same lists, all pairs at once:
-// the pairs smash_fastq_read would return, in file order, on `threads`
-// threads.  h_reads NULL: count only (*n_pairs = the kept pairs, *len their
-// length).  SMASH_ERR_UNSUPPORTED: not strict 4-line FASTQ (the streaming
-// reader handles those).  Host only.
+// The parallel reader (fastq_par.hpp) as an object: the two lists mapped /
+// inflated and indexed once, the pairs checked and ordered (plan_pairs);
+// any range of the planned pairs is packed on demand (the multi-GPU driver
+// deals batches to ranks from one index).  Host only.
+struct smash_fastq_index {
+  smash::ingest::PairIndex px;
+  smash::ingest::Plan pl;
+  uint32_t T = 1;
+};
+
+extern "C" int smash_fastq_index_open(const char *const *r1, uint32_t n1, const char *const *r2,
+                                      uint32_t n2, uint32_t threads, uint32_t *len,
+                                      int sort_names, smash_fastq_index **out,
+                                      uint64_t *n_pairs) {
+  if (!r1 || !r2 || n1 == 0 || n2 == 0 || !len || !out || !n_pairs) {
+    set_error("smash_fastq_index_open: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  auto *f = new smash_fastq_index;
+  f->T = threads ? threads : 1;
+  std::vector<std::string> p1(r1, r1 + n1), p2(r2, r2 + n2);
+  std::string msg;
+  int rc = f->px.build(p1, p2, f->T, msg);
+  if (rc == SMASH_ERR_UNSUPPORTED) msg = "not strict 4-line FASTQ";
+  // sort_names 0: the input must be in samtools sort -n order (checked)
+  if (rc == SMASH_OK)
+    rc = smash::ingest::plan_pairs(f->px, f->T, *len, sort_names == 0, sort_names != 0, f->pl, msg);
+  if (rc != SMASH_OK) {
+    set_error("smash_fastq_index_open: " + msg);
+    delete f;
+    return rc;
+  }
+  *len = f->pl.L;
+  *n_pairs = f->pl.n_out;
+  *out = f;
+  return SMASH_OK;
+}
+
+extern "C" int smash_fastq_index_pack(smash_fastq_index *f, uint64_t k0, uint64_t k1,
+                                      uint8_t *h_reads, char *h_names, uint32_t name_stride) {
+  if (!f || k1 < k0 || k1 > f->pl.n_out || (k1 > k0 && !h_reads) ||
+      (h_names && name_stride < 2)) {
+    set_error("smash_fastq_index_pack: bad arguments");
+    return SMASH_ERR_ARG;
+  }
+  if (!smash::ingest::pack_pairs(f->px, f->pl, k0, k1, h_reads, h_names, name_stride, f->T)) {
+    set_error("smash_fastq_index_pack: read name longer than name_stride - 1");
+    return SMASH_ERR_ARG;
+  }
+  return SMASH_OK;
+}
+
+extern "C" void smash_fastq_index_close(smash_fastq_index *f) { delete f; }
+
+// all pairs at once, in file order (the order check off)
 extern "C" int smash_fastq_read_parallel(const char *const *r1, uint32_t n1,
                                          const char *const *r2, uint32_t n2, uint32_t threads,
                                          uint32_t *len, uint64_t cap_pairs, uint8_t *h_reads,
@@ -149,26 +199,25 @@ extern "C" int smash_fastq_read_parallel(const char *const *r1, uint32_t n1,
     set_error("smash_fastq_read_parallel: bad arguments");
     return SMASH_ERR_ARG;
   }
+  smash_fastq_index f;
+  f.T = threads ? threads : 1;
   std::vector<std::string> p1(r1, r1 + n1), p2(r2, r2 + n2);
-  smash::ingest::PairIndex px;
   std::string msg;
-  const uint32_t T = threads ? threads : 1;
-  int rc = px.build(p1, p2, T, msg);
+  int rc = f.px.build(p1, p2, f.T, msg);
   if (rc == SMASH_ERR_UNSUPPORTED) msg = "not strict 4-line FASTQ";
-  smash::ingest::Plan pl;
-  if (rc == SMASH_OK) rc = smash::ingest::plan_pairs(px, T, *len, false, false, pl, msg);
+  if (rc == SMASH_OK) rc = smash::ingest::plan_pairs(f.px, f.T, *len, false, false, f.pl, msg);
   if (rc != SMASH_OK) {
     set_error("smash_fastq_read_parallel: " + msg);
     return rc;
   }
-  *len = pl.L;
-  *n_pairs = pl.n_out;
+  *len = f.pl.L;
+  *n_pairs = f.pl.n_out;
   if (!h_reads) return SMASH_OK;
-  if (pl.n_out > cap_pairs) {
+  if (f.pl.n_out > cap_pairs) {
     set_error("smash_fastq_read_parallel: more pairs than cap_pairs");
     return SMASH_ERR_ARG;
   }
-  if (!smash::ingest::pack_pairs(px, pl, 0, pl.n_out, h_reads, h_names, name_stride, T)) {
+  if (!smash::ingest::pack_pairs(f.px, f.pl, 0, f.pl.n_out, h_reads, h_names, name_stride, f.T)) {
     set_error("smash_fastq_read_parallel: read name longer than name_stride - 1");
     return SMASH_ERR_ARG;
   }

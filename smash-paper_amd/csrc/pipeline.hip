@@ -104,6 +104,12 @@ struct smash_pipeline {
   uint64_t *d_send_words = nullptr;   // the exported keys' hit words, grouped by owner
   uint64_t send_words_cap = 0;
   uint64_t *d_recv_base = nullptr;    // [2 * 65] owner side: header / word prefix per source
+  // pinned host images of d_owner and d_recv_base: their host-to-device
+  // copies stay asynchronous (the host rewrites an image only after the
+  // event of its previous copy)
+  unsigned long long *h_owner = nullptr;
+  uint64_t *h_recv_base = nullptr;
+  hipEvent_t ev_owner = nullptr, ev_base = nullptr;
   uint64_t n_pairs = 0, n_export = 0;
   hipStream_t last = nullptr;
   // profiling (smash_pipeline_profile)
@@ -1079,6 +1085,11 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_owner = dalloc<unsigned long long>(4 * 64);
     p->d_send_hdr = dalloc<uint64_t>(5 * P);
     p->d_recv_base = dalloc<uint64_t>(2 * 65);
+    SMASH_HIPX(hipHostMalloc(reinterpret_cast<void **>(&p->h_owner), 8 * 256, hipHostMallocDefault));
+    SMASH_HIPX(hipHostMalloc(reinterpret_cast<void **>(&p->h_recv_base), 8 * 2 * 65,
+                             hipHostMallocDefault));
+    SMASH_HIPX(hipEventCreateWithFlags(&p->ev_owner, hipEventDisableTiming));
+    SMASH_HIPX(hipEventCreateWithFlags(&p->ev_base, hipEventDisableTiming));
     SMASH_HIPX(hipMemset(p->d_posoff, 0, 4));
   } catch (hip_failure &f) {
     set_error(f.what);
@@ -1111,6 +1122,10 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
       dfree(q);
   }
   if (p->ev_in) (void)hipEventDestroy(p->ev_in);
+  if (p->ev_owner) (void)hipEventDestroy(p->ev_owner);
+  if (p->ev_base) (void)hipEventDestroy(p->ev_base);
+  if (p->h_owner) (void)hipHostFree(p->h_owner);
+  if (p->h_recv_base) (void)hipHostFree(p->h_recv_base);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
                   (void *)p->d_bins, (void *)p->d_cell,
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
@@ -1492,7 +1507,10 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
   if (n)
     k_export_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_first, p->d_nk, p->d_hash, n,
                                                            world, p->d_owner);
-  unsigned long long cnt[256];
+  // the per-owner counts come to the host (the collectives' split sizes):
+  // the one synchronisation of the exchange
+  unsigned long long *cnt = p->h_owner;
+  SMASH_HIP(hipEventSynchronize(p->ev_owner));   // (the last cursor upload read h_owner)
   SMASH_HIP(hipMemcpyAsync(cnt, p->d_owner, 8 * 256, hipMemcpyDeviceToHost, s));
   SMASH_HIP(hipStreamSynchronize(s));
   uint64_t tot = 0, wtot = 0;
@@ -1515,12 +1533,12 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
   // start, for the offsets relative to it (the cursors at [192 + r] move)
   for (int r = 0; r < world; ++r) cnt[128 + r] = cnt[192 + r];
   SMASH_HIP(hipMemcpyAsync(p->d_owner, cnt, 8 * 256, hipMemcpyHostToDevice, s));
+  SMASH_HIP(hipEventRecord(p->ev_owner, s));
   if (n)
     k_export_fill<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
         p->d_first, p->d_nk, p->d_hash, p->d_hits, p->slots, n, world, global_base, p->d_owner,
         p->d_send_hdr, p->d_send_words, p->d_send_q);
   SMASH_HIP(hipGetLastError());
-  SMASH_HIP(hipStreamSynchronize(s));   // cnt is a host local read by the copy above
   *d_send = p->d_send_hdr;
   *d_send_words = p->d_send_words;
   return SMASH_OK;
@@ -1539,7 +1557,10 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
     set_error("smash_dedup_owner: more keys than 2 * cfg.max_pairs");
     return SMASH_ERR_ARG;
   }
-  uint64_t base[2 * 65] = {0};
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SMASH_HIP(hipEventSynchronize(p->ev_base));   // (the last upload of the image read it)
+  uint64_t *base = p->h_recv_base;
+  std::fill(base, base + 2 * 65, uint64_t(0));
   uint64_t hs = 0, ws = 0;
   for (int r = 0; r < world; ++r) {
     base[r] = hs;
@@ -1553,10 +1574,10 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   }
   base[world] = hs;
   base[65 + world] = ws;
-  hipStream_t s = static_cast<hipStream_t>(stream);
   p->last = s;
   if (!n_recv) return SMASH_OK;
-  SMASH_HIP(hipMemcpyAsync(p->d_recv_base, base, sizeof(base), hipMemcpyHostToDevice, s));
+  SMASH_HIP(hipMemcpyAsync(p->d_recv_base, base, 8 * 2 * 65, hipMemcpyHostToDevice, s));
+  SMASH_HIP(hipEventRecord(p->ev_base, s));
   // reuse the sort buffers (phase_map's sorted keys are no longer needed)
   k_owner_keys<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(d_recv, n_recv, p->d_k[0], p->d_v[0]);
   hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
@@ -1568,7 +1589,6 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
       p->d_table, p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, next_epoch(p), d_flags,
       p->d_stats);
   SMASH_HIP(hipGetLastError());
-  SMASH_HIP(hipStreamSynchronize(s));   // `base` is a host local read by the copy above
   return SMASH_OK;
 }
 

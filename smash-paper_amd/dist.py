@@ -27,12 +27,16 @@ import torch.distributed as dist
 
 
 class ShardedCounter:
-    def __init__(self, pipe, rank, world, device, group=None):
+    def __init__(self, pipe, rank, world, device, group=None, count_group=None):
+        """count_group: a CPU (gloo) process group for the per-batch key
+        counts, which are host integers after smash_phase_export: exchanged
+        there they cost no device synchronisation (None: over `group`)."""
         self.pipe = pipe
         self.rank = rank
         self.world = world
         self.device = device
         self.group = group
+        self.count_group = count_group
         self.carried = torch.full((1,), -1, dtype=torch.int64, device=device)
         self.max_pairs = pipe.max_pairs
 
@@ -40,24 +44,37 @@ class ShardedCounter:
         self.pipe.reset()
         self.carried.fill_(-1)
 
-    def step(self, d_reads, n_pairs, step_base, d_counts, next_reads=None, next_pairs=0):
+    def _recv_counts(self, cnt, wcnt):
+        """what every rank sends me: [keys], [words] per source rank"""
+        rows = [[int(a), int(b)] for a, b in zip(cnt, wcnt)]
+        if self.count_group is not None:   # host integers over gloo: no device sync
+            sc = torch.as_tensor(rows, dtype=torch.int64)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=self.count_group)
+        else:
+            sc = torch.as_tensor(rows, dtype=torch.int64).to(self.device)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=self.group)   # row s: what rank s sends me
+        rcl = rc.cpu().tolist()
+        return [x[0] for x in rcl], [x[1] for x in rcl]
+
+    def step(self, d_reads, n_pairs, step_base, d_counts, next_reads=None, next_pairs=0,
+             stride=None):
         """One batch: this rank's n_pairs pairs start at global index
-        step_base + rank * n_pairs (every rank passes the same n_pairs).
-        next_reads / next_pairs: the rank's next batch, whose search the
-        pipeline starts now, so it runs under this batch's exchanges."""
+        step_base + rank * stride (stride: the nominal batch of every rank,
+        default n_pairs; a short last step keeps the (step, rank, pair)
+        order with the nominal stride).  next_reads / next_pairs: the rank's
+        next batch, whose search the pipeline starts now, so it runs under
+        this batch's exchanges."""
         dev, W, r = self.device, self.world, self.rank
         p = self.pipe
         if next_pairs:
             p.phase_map_ahead(d_reads, n_pairs, next_reads, next_pairs)
         else:
             p.phase_map(d_reads, n_pairs)
-        hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * n_pairs)
-        sc = torch.as_tensor([[int(a), int(b)] for a, b in zip(cnt, wcnt)],
-                             dtype=torch.int64).to(dev)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)   # row s: what rank s sends me
-        rcl = rc.cpu().tolist()
-        rcv, rcw = [x[0] for x in rcl], [x[1] for x in rcl]
+        hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * (n_pairs if stride is None
+                                                                     else stride))
+        rcv, rcw = self._recv_counts(cnt, wcnt)
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
         n_recv, n_words = sum(rcv), sum(rcw)
         recv = torch.empty((max(n_recv, 1), 5), dtype=torch.int64, device=dev)
@@ -92,3 +109,52 @@ class ShardedCounter:
         last = torch.where(nonempty, idx, torch.full_like(idx, -1)).max()
         pick = tails[last.clamp(min=0), 1].reshape(1)
         return torch.where(last >= 0, pick, carried)
+
+
+def count_fastq(sc, index, batch, d_counts, look_ahead=True, pin=True):
+    """File-fed multi-GPU run (smash_mapping.sh:19-29 over `world` ranks):
+    every rank holds the same smashgpu.FastqIndex (both FASTQ lists indexed
+    once, pairs in samtools sort -n order) and takes, in step s, planned pairs
+    [s W batch + rank batch, + batch): the global name order stays (step,
+    rank, pair), which is what ShardedCounter's first-wins de-dup and
+    adjacent-dup boundary assume.  Every rank runs the same number of steps
+    (an empty share in the last one still joins the collectives).  With
+    look_ahead the next batch is packed and copied before this one's
+    exchange and its search issued with it.  Returns the pairs this rank
+    counted."""
+    W, r = sc.world, sc.rank
+    n, L = index.n, index.L
+    steps = (n + W * batch - 1) // (W * batch)
+    dev = sc.device
+    on_dev = dev.type != "cpu"
+    host = [torch.empty((2 * batch, L), dtype=torch.uint8, pin_memory=pin and on_dev)
+            for _ in range(2)]
+    devb = [torch.empty((2 * batch, L), dtype=torch.uint8, device=dev) for _ in range(2)]
+
+    def share(s):
+        lo = min(n, s * W * batch + r * batch)
+        return lo, min(n, lo + batch)
+
+    def load(s, k):   # step s's share into device buffer k (host buffer k reused)
+        lo, hi = share(s)
+        if hi > lo:
+            index.pack(lo, hi, host[k])
+            devb[k][:2 * (hi - lo)].copy_(host[k][:2 * (hi - lo)], non_blocking=on_dev)
+        return hi - lo
+
+    done = 0
+    cur = load(0, 0) if steps else 0
+    for s in range(steps):
+        k = s % 2
+        nxt = 0
+        if look_ahead and s + 1 < steps:
+            if on_dev:
+                torch.cuda.current_stream(dev).synchronize()   # host buffer k ^ 1 is free again
+            nxt = load(s + 1, k ^ 1)
+        sc.step(devb[k][:2 * cur], cur, s * W * batch, d_counts,
+                devb[k ^ 1][:2 * nxt] if nxt else None, nxt, stride=batch)
+        done += cur
+        if not (look_ahead and s + 1 < steps) and s + 1 < steps:
+            nxt = load(s + 1, k ^ 1)
+        cur = nxt
+    return done

@@ -331,8 +331,57 @@ def _count_files(args, bins):
     return rows, counts.cpu().numpy(), st
 
 
+def _count_files_dist(args, bins, world):
+    """count over `world` ranks (one process per GPU, torch.distributed over
+    RCCL: torchrun sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*): every rank
+    indexes the FASTQ lists (smashgpu.FastqIndex, strict 4-line FASTQ) and
+    counts its (step, rank) batches (dist.count_fastq); counts and statistics
+    are summed over the ranks; rank 0 writes the output."""
+    import torch
+    import torch.distributed as tdist
+    from dist import ShardedCounter, count_fastq
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    tdist.init_process_group("nccl", device_id=dev)
+    cpu = tdist.new_group(backend="gloo")
+    ref = _ref(args)
+    ix = load_index(ref, local)
+    cs = S.read_chrom_sizes(args.chrom_sizes or ref + ".bin/chrom_sizes.txt")
+    rows, starts = S.read_bins(bins)
+    r1, r2 = args.reads1.split(), args.reads2.split()
+    fq = S.FastqIndex(r1, r2, sort_names=not args.presorted)
+    # an owner keeps the keys it owns for the whole run: ~pairs / world
+    cap = args.dedup_capacity or (fq.n // world + fq.n // (8 * world) + (1 << 20))
+    pipe = S.Pipeline(ix, cs, starts, fq.L, args.batch, dedup_capacity=cap)
+    counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+    sc = ShardedCounter(pipe, rank, world, dev, count_group=cpu)
+    sc.reset()
+    count_fastq(sc, fq, args.batch, counts)
+    st = pipe.stats(raise_on_error=False)
+    v = torch.tensor([st.positions, st.dups, st.kept, st.key_pairs, st.dupe_pairs,
+                      1 if st.error else 0], dtype=torch.int64, device=dev)
+    tdist.all_reduce(counts)
+    tdist.all_reduce(v)
+    tdist.barrier()
+    tdist.destroy_process_group()
+    if int(v[5]):
+        raise SystemExit("count: a rank recorded a pipeline data error (%s)"
+                         % S.ERRORS.get(st.error, st.error))
+    pos, dups, kept, kp, dp, _ = [int(x) for x in v.tolist()]
+    return rank, rows, counts.cpu().numpy(), (pos, dups, kept, kp, dp)
+
+
 def cmd_count(args):
     bins = os.path.join(args.bindir, "bins.txt")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if not args.sam and args.reads1 and world > 1:
+        rank, rows, counts, (pos, dups, kept, _, _) = _count_files_dist(args, bins, world)
+        if rank == 0:
+            write_varbin(rows, counts, pos, dups, kept, args.out or args.id + ".varbin.txt",
+                         args.id + ".stats.txt")
+        return
     if not args.sam and args.reads1:
         rows, counts, st = _count_files(args, bins)
         write_varbin(rows, counts, st.positions, st.dups, st.kept,

@@ -53,6 +53,7 @@ EXPORTS = [
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
     "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
     "smash_pipeline_profile_intervals", "smash_fastq_read_parallel",
+    "smash_fastq_index_open", "smash_fastq_index_pack", "smash_fastq_index_close",
     "smash_phase_map_ahead", "smash_sam_records_packed",
 ]
 
@@ -169,6 +170,12 @@ def lib():
     L.smash_fastq_close.argtypes = [vp]
     L.smash_fastq_close.restype = None
     L.smash_strnum_order.argtypes = [vp, C.c_uint32, C.c_uint64, u64p]
+    L.smash_fastq_index_open.argtypes = [C.POINTER(C.c_char_p), C.c_uint32,
+                                         C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32, u32p,
+                                         C.c_int, C.POINTER(vp), u64p]
+    L.smash_fastq_index_pack.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, C.c_uint32]
+    L.smash_fastq_index_close.argtypes = [vp]
+    L.smash_fastq_index_close.restype = None
     L.smash_fastq_read_parallel.argtypes = [C.POINTER(C.c_char_p), C.c_uint32,
                                             C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
                                             u32p, C.c_uint64, vp, vp, C.c_uint32, u64p]
@@ -765,6 +772,42 @@ def read_fastq_pairs_parallel(r1_paths, r2_paths, threads=0, name_stride=64, rea
     if not k:
         return np.zeros(0, "S%d" % name_stride), np.zeros((0, 0), np.uint8)
     return nb[:k], rb[:2 * k, :L.value]
+
+
+class FastqIndex:
+    """Both FASTQ lists indexed once by the parallel reader
+    (smash_fastq_index_*): .n pairs of .L bases in samtools sort -n order;
+    pack(k0, k1, out) fills a [2 (k1 - k0), L] uint8 array (or a pinned CPU
+    tensor) with planned pairs [k0, k1).  Strict 4-line FASTQ only."""
+
+    def __init__(self, r1_paths, r2_paths, threads=0, read_len=0, sort_names=False):
+        a1 = _cstrs([os.fsencode(p) for p in r1_paths])
+        a2 = _cstrs([os.fsencode(p) for p in r2_paths])
+        T = threads or min(16, os.cpu_count() or 1)
+        L = C.c_uint32(read_len)
+        n = C.c_uint64()
+        h = vp()
+        check(lib().smash_fastq_index_open(a1, len(r1_paths), a2, len(r2_paths), T, C.byref(L),
+                                           int(bool(sort_names)), C.byref(h), C.byref(n)),
+              "smash_fastq_index_open")
+        self.h, self.n, self.L = h, n.value, L.value
+
+    def pack(self, k0, k1, out):
+        ptr = out.data_ptr() if hasattr(out, "data_ptr") else out.ctypes.data
+        check(lib().smash_fastq_index_pack(self.h, k0, k1, vp(ptr), None, 0),
+              "smash_fastq_index_pack")
+        return out
+
+    def close(self):
+        if self.h:
+            lib().smash_fastq_index_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def first_read_length(paths):

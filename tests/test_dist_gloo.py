@@ -98,3 +98,91 @@ def test_two_rank_exchange_matches_single_process(world, per_rank, steps, tiny_i
     assert op.run(reads, threads=4) == 0
     assert got_counts == op.counts.tolist()
     assert got_stats == [op.state.total, op.state.dups, op.state.kept]
+
+
+def _worker_files(rank, world, port, batch, paths, out_q):
+    """the file-fed form: every rank indexes the same FASTQ lists
+    (smashgpu.FastqIndex) and counts its (step, rank) batches through
+    dist.count_fastq, the key counts exchanged on a gloo count group"""
+    import sys
+    for p in ("oracle", "tools", "tests", "smash-paper_amd"):
+        sys.path.insert(0, os.path.join(ROOT, p))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gzip, tempfile
+    import oracle as O
+    import smashgpu as S
+    from mock_pipeline import OraclePhasePipeline
+    from dist import ShardedCounter, count_fastq
+    d = tempfile.mkdtemp()
+    fa = os.path.join(d, "tiny.fa")
+    with gzip.open(gold("tiny.fa.gz"), "rb") as f, open(fa, "wb") as g:
+        g.write(f.read())
+    oix = O.Index.from_fasta(fa)
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    pipe = OraclePhasePipeline(oix, oix.mappability(), cs, starts, batch)
+    cg = dist.new_group(backend="gloo")
+    sc = ShardedCounter(pipe, rank, world, torch.device("cpu"), count_group=cg)
+    fq = S.FastqIndex(*paths, threads=2)
+    counts = torch.zeros(len(starts), dtype=torch.int64)
+    sc.reset()
+    done = count_fastq(sc, fq, batch, counts)
+    dist.all_reduce(counts)
+    st = torch.tensor([pipe.total, pipe.dups, pipe.kept, done], dtype=torch.int64)
+    dist.all_reduce(st)
+    if rank == 0:
+        out_q.put((counts.numpy().tolist(), st.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch", [(2, 300), (2, 173), (3, 256)])
+def test_file_fed_ranks_match_single_process(world, batch, tiny_ix, tmp_path):
+    """dist.count_fastq over world ranks (gloo, CPU) on the s100 FASTQ pair,
+    split over lane files, == the single-process oracle chain on the same
+    pairs read by the streaming reader; the last step's shares are short or
+    empty."""
+    import gzip
+    import oracle as O
+    import smashgpu as S
+    lanes = []
+    for m in (1, 2):
+        lines = gzip.open(gold("s100_r%d.fq.gz" % m), "rb").read().split(b"\n")
+        cut = 4 * 733
+        a, b = tmp_path / ("m%d_L1.fq" % m), tmp_path / ("m%d_L2.fq.gz" % m)
+        a.write_bytes(b"\n".join(lines[:cut]) + b"\n")
+        with gzip.open(b, "wb") as f:
+            f.write(b"\n".join(lines[cut:]))
+        lanes.append([str(a), str(b)])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker_files, args=(r, world, port, batch, lanes, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue as _queue
+    res = None
+    for _ in range(900):
+        try:
+            res = q.get(timeout=1)
+            break
+        except _queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        if res is None:
+            p.terminate()
+    assert res is not None, [p.exitcode for p in procs]
+    got_counts, got_stats = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, reads = S.read_fastq_pairs(*lanes)
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    op = O.Pipeline(tiny_ix, tiny_ix.mappability(), cs, starts)
+    assert op.run(reads, threads=4) == 0
+    assert got_counts == op.counts.tolist()
+    assert got_stats == [op.state.total, op.state.dups, op.state.kept, reads.shape[0] // 2]
