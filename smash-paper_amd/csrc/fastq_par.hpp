@@ -333,6 +333,7 @@ inline int plan_pairs(const PairIndex &px, uint32_t T, uint32_t L, bool check_or
                       Plan &pl, std::string &msg) {
   const uint64_t n = px.n;
   pl = Plan();
+  const bool given = L != 0;   // (the messages of the streaming readers)
   if (!L) {   // the first kept pair's length
     for (uint64_t i = 0; i < n; ++i) {
       const Rec a = parse(px.r1[i]), b = parse(px.r2[i]);
@@ -396,8 +397,9 @@ inline int plan_pairs(const PairIndex &px, uint32_t T, uint32_t L, bool check_or
   for (uint32_t r = 0; r < R; ++r)
     if (first_bad[r] != ~0ull) {
       msg = kind[r] == 1 ? "one mate of a pair has no bases (" + name_of(first_bad[r]) + ")"
-                         : "every mate must have the same length, " + std::to_string(L) + " (" +
-                               name_of(first_bad[r]) + ")";
+            : given ? "every mate must have the pipeline's read length, " + std::to_string(L) +
+                          " (" + name_of(first_bad[r]) + ")"
+                    : "all mates must have the same length (" + name_of(first_bad[r]) + ")";
       return SMASH_ERR_ARG;
     }
   uint64_t tot = 0, prev = ~0ull;

@@ -907,6 +907,14 @@ __global__ void k_reset_prev(int64_t *prev) {
   prev[1] = -1;
 }
 
+hipError_t ensure_positions(smash_pipeline *p) {
+  if (p->d_pos0) return hipSuccess;
+  const uint64_t n = p->max_pairs * 2 * p->slots;
+  hipError_t e = hipMalloc(reinterpret_cast<void **>(&p->d_pos0), 8 * n);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&p->d_abs), 8 * n);
+  return e;
+}
+
 int check_pipe(smash_pipeline *p, uint64_t n_pairs) {
   if (!p) { set_error("null pipeline"); return SMASH_ERR_ARG; }
   if (n_pairs > p->max_pairs) {
@@ -1051,8 +1059,6 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_arena = dalloc<uint64_t>(p->arena_cap);
     p->d_arena_top = dalloc<unsigned long long>(1);
     SMASH_HIPX(hipMemset(p->d_arena_top, 0, 8));
-    p->d_pos0 = dalloc<int64_t>(P * 2 * p->slots);
-    p->d_abs = dalloc<int64_t>(P * 2 * p->slots);
     p->d_prev = dalloc<int64_t>(2);
     p->d_lp = dalloc<int64_t>(P);
     p->d_lps = dalloc<int64_t>(P);
@@ -1060,6 +1066,10 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       const char *e = getenv("SMASH_FUSED_BIN");   // 0: k_emit + k_bin (A/B)
       p->fused_bin = !(e && e[0] == '0');
     }
+    // the positions arrays (2 x 8 B x every hit slot: 26 GB at 6.25 M
+    // pairs) only for the two-kernel path; the fused path writes them when
+    // smash_pipeline_positions asks (ensure_positions)
+    if (!p->fused_bin) SMASH_HIPX(ensure_positions(p));
     int64_t init[2] = {-1, -1};
     SMASH_HIPX(hipMemcpy(p->d_prev, init, 16, hipMemcpyHostToDevice));
     p->d_stats = dalloc<unsigned long long>(S_N);
@@ -1738,6 +1748,7 @@ extern "C" int smash_pipeline_positions(smash_pipeline *p, int64_t *h_pos0, int6
   if (!p || !n_out) return SMASH_ERR_ARG;
   SMASH_HIP(hipSetDevice(p->device));
   if (p->pos_dirty && p->n_pairs) {   // fused path: write the last batch's positions now
+    SMASH_HIP(ensure_positions(p));
     k_emit<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, p->last>>>(
         p->d_keep, p->d_nk, p->d_hits, p->d_posoff, p->n_pairs, p->slots, p->d_chrom_off,
         p->d_pos0, p->d_abs);
