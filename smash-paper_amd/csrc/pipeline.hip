@@ -88,6 +88,7 @@ struct smash_pipeline {
   // emitted position (-1: none), and its inclusive "last valid" scan
   int64_t *d_lp = nullptr, *d_lps = nullptr;
   bool fused_bin = true;
+  bool bin_lds = true;            // k_emit_bin_lds when the bins fit (SMASH_BIN_LDS=0: k_emit_bin)
   bool pos_dirty = false;         // the positions arrays are not materialised yet
   unsigned long long *d_stats = nullptr;
   uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast<16> -> k_post pair list
@@ -884,6 +885,67 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
   }
 }
 
+// k_emit_bin with the counts summed on chip: a global atomic per position
+// (one lane per random bin, executed at the memory side) is the slow shape
+// of an atomic (MI355X_MICROARCH.md, Global float atomics).  The bins are
+// cut in parts of kBinPart u32 LDS counters; block (x, part) walks the pairs
+// of its x slice, bins every emitted position as k_emit_bin does, counts the
+// ones in its part in LDS and adds the part to the global counts once, lane
+// i -> bin i (whole contiguous rows).  Every part re-walks the pairs (hit
+// words and bisects: cheap next to the atomics); part 0 keeps the stats.
+constexpr uint32_t kBinPart = 24576;   // 96 KB of counters: one 1024-thread block per CU
+constexpr uint32_t kBinPartsMax = 4;   // above: k_emit_bin
+__global__ __launch_bounds__(1024) void k_emit_bin_lds(
+    const uint8_t *__restrict__ keep, const int32_t *__restrict__ nk,
+    const uint64_t *__restrict__ hits, uint32_t slots, const int64_t *__restrict__ chrom_off,
+    const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
+    const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
+    uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats) {
+  __shared__ uint32_t hc[kBinPart];
+  const uint32_t b0 = blockIdx.y * kBinPart;
+  const uint32_t b1 = b0 + kBinPart < nbins ? b0 + kBinPart : nbins;
+  for (uint32_t i = threadIdx.x; i < kBinPart; i += blockDim.x) hc[i] = 0;
+  __syncthreads();
+  const int64_t prev0 = *prev_p;
+  unsigned long long d = 0, k = 0, t = 0;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += stride) {
+    if (!keep[q]) continue;
+    const int32_t m = nk[q];
+    if (m <= 0) continue;
+    int64_t prev = q ? lps[q - 1] : -1;
+    if (prev < 0) prev = prev0;
+    const uint64_t *h = hits + q * 2 * uint64_t(slots);
+    for (int32_t i = 0; i < m; ++i) {
+      const uint64_t w = h[i];
+      const int64_t co = chrom_off[uint32_t(w >> 48)];
+      if (co < 0) continue;
+      const int64_t p = int64_t(w & 0xFFFFFFFFFFFFull);
+      ++t;
+      if (prev >= 0 && prev == p) {
+        ++d;
+      } else {
+        const uint32_t b = bin_of(p + co, bins, nbins, cell, ncell, cshift);
+        if (b >= b0 && b < b1) atomicAdd(&hc[b - b0], 1u);
+        ++k;
+      }
+      prev = p;
+    }
+  }
+  __shared__ unsigned long long sd, sk, st;
+  if (threadIdx.x == 0) { sd = 0; sk = 0; st = 0; }
+  __syncthreads();
+  if (blockIdx.y == 0 && t) { atomicAdd(&st, t); atomicAdd(&sd, d); atomicAdd(&sk, k); }
+  __syncthreads();
+  if (threadIdx.x == 0 && st) {
+    atomicAdd(&stats[S_POS], st);
+    atomicAdd(&stats[S_DUPS], sd);
+    atomicAdd(&stats[S_KEPT], sk);
+  }
+  for (uint32_t i = threadIdx.x; b0 + i < b1; i += blockDim.x)
+    if (hc[i]) atomicAdd(&counts[b0 + i], (unsigned long long)hc[i]);
+}
+
 // the batch's tail {count, last position} (lps_last: lps[n - 1]; count 0:
 // -1) and the carried line for the next batch
 __global__ void k_tail_lps(const uint32_t *npos_p, const int64_t *lps_last, int64_t *prev,
@@ -1065,6 +1127,8 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     {
       const char *e = getenv("SMASH_FUSED_BIN");   // 0: k_emit + k_bin (A/B)
       p->fused_bin = !(e && e[0] == '0');
+      const char *l = getenv("SMASH_BIN_LDS");
+      p->bin_lds = !(l && l[0] == '0');
     }
     // the positions arrays (2 x 8 B x every hit slot: 26 GB at 6.25 M
     // pairs) only for the two-kernel path; the fused path writes them when
@@ -1329,11 +1393,19 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
   const uint64_t n = p->n_pairs;
   const int64_t *prev = d_prev ? d_prev : p->d_prev;
   if (p->fused_bin) {
-    if (n)
+    const uint32_t parts = (p->nbins + kBinPart - 1) / kBinPart;
+    if (n && p->bin_lds && parts <= kBinPartsMax) {
+      const dim3 grid(unsigned(std::min<uint64_t>(256, (n + 1023) / 1024)), parts);
+      k_emit_bin_lds<<<grid, 1024, 0, s>>>(
+          p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
+          p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
+          p->d_stats);
+    } else if (n) {
       k_emit_bin<<<grid_for(n, kB, 8192), kB, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
           p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
           p->d_stats);
+    }
     // carry the adjacent-dup state across batches (single-GPU use)
     k_tail_lps<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_lps + (n ? n - 1 : 0), p->d_prev, nullptr);
     SMASH_HIP(hipGetLastError());

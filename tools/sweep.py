@@ -56,7 +56,8 @@ def main():
         env = {} if setting == "base" else dict(kv.split("=", 1) for kv in setting.split(","))
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        if any(k.startswith("SMASH_POST") for k in env) or pipe is None:
+        fresh = ("SMASH_POST", "SMASH_BIN", "SMASH_FUSED", "SMASH_KEY")   # read at create
+        if any(k.startswith(fresh) for k in env) or pipe is None:
             pipe = None                      # read at create: a fresh pipeline
             pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
 
@@ -88,7 +89,7 @@ def main():
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-        if any(k.startswith("SMASH_POST") for k in env):
+        if any(k.startswith(fresh) for k in env):
             pipe = None
 
 
