@@ -1,13 +1,14 @@
 #!/bin/bash
-# tools/gpu_round.sh TAG [TESTS] -- one GPU call of a round: the named -m gpu
-# tests (pytest -k expression, "" = none, "all" = the whole suite), then
-# tools/measure_round.sh TAG (bench line, kernel trace + stats, FETCH_SIZE pass,
-# randbench calibration) and the SMASH_SM_CHECK=0 A/B of the search (two runs
-# each, alternating).  Every GPU step has its own time limit; the chain stops
-# at the first failure.
+# tools/gpu_round.sh TAG [TESTS] [CHECK_AB] -- one GPU call of a round: the
+# named -m gpu tests (pytest -k expression, "" = none, "all" = the whole
+# suite), then tools/measure_round.sh TAG (bench line, kernel trace + stats,
+# FETCH_SIZE pass, randbench calibration) and, with CHECK_AB = 1, the
+# SMASH_SM_CHECK=0 A/B of the search (two runs each, alternating).  Every GPU
+# step has its own time limit; the chain stops at the first failure.
 set -euo pipefail
 TAG=${1:?tag}
 TESTS=${2:-}
+CHECK_AB=${3:-0}
 R=$(cd "$(dirname "$0")/.." && pwd)
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
@@ -20,6 +21,7 @@ elif [ -n "$TESTS" ]; then
       -k "$TESTS" > "$O/tests.log" 2>&1
 fi
 "$R/tools/measure_round.sh" "$TAG"
+[ "$CHECK_AB" = "1" ] || exit 0
 cd /tmp
 for i in 1 2; do
   for ck in 1 0; do
