@@ -38,6 +38,7 @@ namespace smash {
 uint32_t pipe_read_len(const smash_pipeline *p);
 uint64_t pipe_max_pairs(const smash_pipeline *p);
 int pipe_device(const smash_pipeline *p);
+void *&pipe_feed(smash_pipeline *p, void (*freer)(void *));
 }  // namespace smash
 
 namespace {
@@ -63,11 +64,44 @@ void par_for(uint64_t n, uint32_t T, F f) {
 }
 
 struct Slot {
-  uint8_t *h = nullptr;   // pinned [2 * max_pairs * L]
+  uint8_t *h = nullptr;   // pinned [2 * max_pairs * L] (FeedBufs)
   uint64_t n = 0;
   bool last = false;
   int state = 0;          // 0 free, 1 filled
 };
+
+// the pinned slots, device buffers, events and copy stream of the feed,
+// owned by the pipeline between calls (pipe_feed)
+struct FeedBufs {
+  uint64_t bytes = 0;
+  uint8_t *h[3] = {nullptr, nullptr, nullptr};
+  uint8_t *d[2] = {nullptr, nullptr};
+  hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+  hipStream_t xs = nullptr;
+  ~FeedBufs() {
+    if (xs) (void)hipStreamSynchronize(xs);
+    for (int k = 0; k < 2; ++k) {
+      if (d[k]) (void)hipFree(d[k]);
+      if (copied[k]) (void)hipEventDestroy(copied[k]);
+      if (done[k]) (void)hipEventDestroy(done[k]);
+    }
+    for (auto *x : h)
+      if (x) (void)hipHostFree(x);
+    if (xs) (void)hipStreamDestroy(xs);
+  }
+  bool alloc(uint64_t b) {
+    bytes = b;
+    bool ok = hipStreamCreateWithFlags(&xs, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; k < 2 && ok; ++k)
+      ok = hipMalloc(&d[k], b) == hipSuccess &&
+           hipEventCreateWithFlags(&copied[k], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+    for (auto *&x : h)
+      ok = ok && hipHostMalloc(reinterpret_cast<void **>(&x), b, hipHostMallocDefault) == hipSuccess;
+    return ok;
+  }
+};
+void free_feed(void *f) { delete static_cast<FeedBufs *>(f); }
 
 struct Feed {
   smash_pipeline *p;
@@ -367,9 +401,26 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
   for (uint32_t i = 0; i < n2; ++i) f->r2.paths.emplace_back(r2[i]);
   const uint64_t bytes = 2 * f->B * f->L;
   SMASH_HIP(hipSetDevice(smash::pipe_device(p)));
-  hipStream_t cs = static_cast<hipStream_t>(stream), xs = nullptr;
-  uint8_t *dbuf[2] = {nullptr, nullptr};
-  hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+  hipStream_t cs = static_cast<hipStream_t>(stream);
+  void *&fb_slot = smash::pipe_feed(p, free_feed);
+  if (fb_slot && static_cast<FeedBufs *>(fb_slot)->bytes != bytes) {
+    free_feed(fb_slot);
+    fb_slot = nullptr;
+  }
+  if (!fb_slot) {
+    auto *nb = new FeedBufs;
+    if (!nb->alloc(bytes)) {
+      delete nb;
+      smash::set_error("smash_count_fastq: cannot allocate the batch buffers");
+      return SMASH_ERR_NOMEM;
+    }
+    fb_slot = nb;
+  }
+  FeedBufs &fb = *static_cast<FeedBufs *>(fb_slot);
+  hipStream_t xs = fb.xs;
+  uint8_t **dbuf = fb.d;
+  hipEvent_t *copied = fb.copied, *done = fb.done;
+  for (int k = 0; k < 3; ++k) f->slot[k].h = fb.h[k];
   int rc = SMASH_OK;
   uint64_t pairs = 0, batches = 0;
   double wait_s = 0;
@@ -381,32 +432,8 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
     }
     if (xs) (void)hipStreamSynchronize(xs);
     if (cs) (void)hipStreamSynchronize(cs);
-    for (int k = 0; k < 2; ++k) {
-      if (dbuf[k]) (void)hipFree(dbuf[k]);
-      if (copied[k]) (void)hipEventDestroy(copied[k]);
-      if (done[k]) (void)hipEventDestroy(done[k]);
-    }
-    for (Slot &s : f->slot)
-      if (s.h) (void)hipHostFree(s.h);
-    if (xs) (void)hipStreamDestroy(xs);
   };
   do {
-    if (hipStreamCreateWithFlags(&xs, hipStreamNonBlocking) != hipSuccess) {
-      rc = SMASH_ERR_HIP;
-      break;
-    }
-    bool ok = true;
-    for (int k = 0; k < 2 && ok; ++k)
-      ok = hipMalloc(&dbuf[k], bytes) == hipSuccess &&
-           hipEventCreateWithFlags(&copied[k], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
-    for (Slot &s : f->slot)
-      ok = ok && hipHostMalloc(reinterpret_cast<void **>(&s.h), bytes, hipHostMallocDefault) == hipSuccess;
-    if (!ok) {
-      smash::set_error("smash_count_fastq: cannot allocate the batch buffers");
-      rc = SMASH_ERR_NOMEM;
-      break;
-    }
     prod = std::thread([&] { f->produce(sort_names != 0); });
     for (uint64_t b = 0;; ++b) {
       Slot &s = f->slot[b % 3];

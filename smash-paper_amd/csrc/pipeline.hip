@@ -113,6 +113,10 @@ struct smash_pipeline {
   hipEvent_t ev_owner = nullptr, ev_base = nullptr;
   uint64_t n_pairs = 0, n_export = 0;
   hipStream_t last = nullptr;
+  // smash_count_fastq's pinned slots, device buffers and copy stream, kept
+  // across calls (pinning GBs of host memory costs more than a batch)
+  void *feed = nullptr;
+  void (*feed_free)(void *) = nullptr;
   // profiling (smash_pipeline_profile)
   bool prof = false;
   std::vector<hipEvent_t> ev;     // pairs: [2i] before, [2i+1] after k_mam
@@ -1178,11 +1182,16 @@ namespace smash {
 uint32_t pipe_read_len(const smash_pipeline *p) { return p->read_len; }
 uint64_t pipe_max_pairs(const smash_pipeline *p) { return p->max_pairs; }
 int pipe_device(const smash_pipeline *p) { return p->device; }
+void *&pipe_feed(smash_pipeline *p, void (*freer)(void *)) {
+  p->feed_free = freer;
+  return p->feed;
+}
 }  // namespace smash
 
 extern "C" void smash_pipeline_free(smash_pipeline *p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
+  if (p->feed && p->feed_free) p->feed_free(p->feed);
   for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
   for (int k = 0; k < 2; ++k) {
     if (p->xs[k]) {
