@@ -470,6 +470,8 @@ def main():
         # they need no device synchronisation
         sc = ShardedCounter(pipe, rank, world, dev, count_group=dist.new_group(backend="gloo"))
 
+    resident = os.environ.get("SMASH_BENCH_RESIDENT", "1") != "0"   # (A/B)
+
     def step(i):
         """one run over the rank's P pairs: a fresh key set / adjacent-dup
         state (a new smashMEM.py + varbin.py invocation), carried across
@@ -478,8 +480,10 @@ def main():
         if world == 1:
             pipe.reset()
             # the batches in order; each batch's search starts under the
-            # previous one's tail (smash_count_batches)
-            pipe.count_batches(d_reads, P, B, counts)
+            # previous one's tail, and (the reads are resident: no input
+            # event, smash_count_batches_ready) this run's first searches
+            # under the previous run's post stage
+            pipe.count_batches(d_reads, P, B, counts, resident=resident)
         else:
             sc.reset()
             for b in range(nb):

@@ -215,6 +215,16 @@ int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
  * reads must be ready by the work already on `stream`). */
 int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                         uint64_t batch_pairs, uint64_t *d_counts, void *stream);
+/* smash_count_batches with the reads' readiness stated by the caller rather
+ * than by the work on `stream`: `ready` is an event (hipEvent_t) after which
+ * every batch's reads are complete, or NULL: they are complete already (no
+ * pending writes on any stream).  The searches then wait for nothing queued on
+ * `stream` -- a run's first searches start under the post stage of the run
+ * queued before it (the de-dup set reset, the counts and every post-stage
+ * kernel stay ordered on `stream`). */
+int smash_count_batches_ready(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                              uint64_t batch_pairs, uint64_t *d_counts, void *stream,
+                              void *ready);
 
 /* Multi-GPU phases (one rank per GPU; the caller runs the collectives):
  *  1. smash_phase_map      -- map/resolve/tag/filter/hash + in-batch first-wins

@@ -142,6 +142,10 @@ struct SearchWs {
   uint8_t *rec = nullptr;
   uint64_t rec_bytes = 0;
   unsigned long long *work = nullptr;
+  // waited on between the read records (k_prep) and the search: the match
+  // buffers' previous reader, so the records of the next batch are built
+  // while that reader still runs
+  hipEvent_t gate = nullptr;
 };
 int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
                    uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,

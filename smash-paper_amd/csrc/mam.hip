@@ -181,14 +181,24 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
     ix->rec_bytes = bytes;
   }
   if (!ws) rec = ix->d_rec;
-  {
+  const uint32_t ga = sm::prep_groups(lens ? 255 : len);
+  const char *pl = std::getenv("SMASH_PREP_LDS");
+  if ((pl && pl[0] == '1') || n_reads * ga >= (1ull << 32)) {   // (A/B; huge launches)
     const uint32_t per = sm::prep_per_block(g, stride);
     const size_t plds = sm::prep_lds_bytes(g, stride, per);
     sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
         seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
         ix->in_text[3], g, per, rec);
     SMASH_HIP(hipGetLastError());
+  } else if (n_reads) {
+    // no LDS: runs beside the search of the previous batch (k_prep_direct)
+    const uint64_t items = n_reads * ga;
+    sm::k_prep_direct<<<unsigned((items + 255) / 256), 256, 0, s>>>(
+        seqs, stride, lens, len, uint32_t(n_reads), ga, ix->in_text[0], ix->in_text[1],
+        ix->in_text[2], ix->in_text[3], g, rec);
+    SMASH_HIP(hipGetLastError());
   }
+  if (ws && ws->gate) SMASH_HIP(hipStreamWaitEvent(s, ws->gate, 0));
   sm::Ctx<IdxT> c;
   const DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
   c.T = x.T; c.SA = x.SA; c.ISA = x.ISA; c.L8 = x.L8; c.U = x.U; c.KT = x.KT;
@@ -331,11 +341,13 @@ int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint
   if (n_reads == 0) return SMASH_OK;
   SMASH_HIP(hipSetDevice(ix->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool plain = mode == SMASH_MODE_MAM_PLAIN;
+  const bool sm_path = !plain && mode != SMASH_MODE_MUM && !use_direct();
+  if (ws && ws->gate && !sm_path) SMASH_HIP(hipStreamWaitEvent(s, ws->gate, 0));   // (launch_sm: after k_prep)
   if (mode == SMASH_MODE_MUM)
     return map_batch_mum(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out, cap_per_read,
                          d_n_out, s);
-  const bool plain = mode == SMASH_MODE_MAM_PLAIN;
-  if (!plain && !use_direct()) {
+  if (sm_path) {
     if (ix->idx_bytes == 4)
       return launch_sm<uint32_t>(ix, min_len, d_seqs, stride, d_lens, len, n_reads, d_out,
                                  cap_per_read, d_n_out, s, sync_check, ws);

@@ -225,6 +225,91 @@ __global__ __launch_bounds__(256) void k_prep(const uint8_t *__restrict__ seqs, 
     dst[k] = reinterpret_cast<const uint4 *>(out)[k];
 }
 
+// The same records without LDS: one thread per (read, 32-base group), ga =
+// ceil(max_len / 32) groups per read, reads the group's bytes straight from
+// HBM (the three aligned 16-byte blocks holding them) and writes the group's
+// bad-mask word and its 8 raw words (two 16-byte stores); the read's last
+// group also zeroes the bad-mask words and raw words past the groups.  Every
+// record word is written, so the records equal k_prep's.  A kernel without
+// LDS can share a CU with a running k_mam_sm (whose blocks hold all of it):
+// the pipeline builds the next batch's records under the current batch's
+// search instead of between the two searches.  Blocks are loaded only where
+// they start before the end of the input (never past its last aligned
+// block).  items = n * ga < 2^32 (host check).
+__global__ __launch_bounds__(256) void k_prep_direct(const uint8_t *__restrict__ seqs,
+                                                     uint64_t stride,
+                                                     const uint16_t *__restrict__ lens,
+                                                     uint32_t len0, uint32_t n, uint32_t ga,
+                                                     uint64_t it0, uint64_t it1, uint64_t it2,
+                                                     uint64_t it3, Geom g,
+                                                     uint32_t *__restrict__ rec) {
+#ifndef SM_DMA_ROW_HOST
+  __builtin_amdgcn_s_setprio(2);   // beside the search (pipeline.hip SMASH_BESIDE_SEARCH)
+#endif
+  const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= n * ga) return;
+  const uint32_t r = item / ga;
+  const uint32_t gi = item - r * ga;
+  const uint32_t L = lens ? lens[r] : len0;
+  uint32_t *o = rec + uint64_t(r) * (g.chunks * 4);
+  uint32_t w8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t bw = 0;
+  if (32 * gi < L) {
+    auto itx = [&](uint32_t b) {
+      const uint64_t w = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
+      return uint32_t((w >> (b & 63)) & 1ull);
+    };
+    const uint32_t ia = itx('a'), ic = itx('c'), ig = itx('g'), iu = itx('t');
+    const uint64_t end = reinterpret_cast<uint64_t>(seqs) + uint64_t(n) * stride;
+    const uint64_t b0 = reinterpret_cast<uint64_t>(seqs) + uint64_t(r) * stride + 32 * gi;
+    const uint64_t a16 = b0 & ~uint64_t(15);
+    const uint32_t off = uint32_t(b0 & 15);
+    uint32_t d[12];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint4 v = a16 + 16 * k < end && (k < 2 || off) ? reinterpret_cast<const uint4 *>(a16)[k]
+                                                          : make_uint4(0, 0, 0, 0);
+      d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+    }
+    const uint32_t q = off >> 2, sh = (off & 3) * 8;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      // dwords k + q and k + q + 1 of the blocks, q in 0..3
+      const uint32_t lo = q == 0 ? d[k] : q == 1 ? d[k + 1] : q == 2 ? d[k + 2] : d[k + 3];
+      const uint32_t hi = q == 0 ? d[k + 1] : q == 1 ? d[k + 2] : q == 2 ? d[k + 3] : d[k + 4];
+      uint32_t w = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+      const uint32_t i0 = 32 * gi + 4 * k;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t b = (w >> (8 * j)) & 0xFF;
+        const bool live = i0 + j < L;
+        if (!live) w &= ~(0xFFu << (8 * j));
+        const uint32_t good = (b == 'a' ? ia : 0u) | (b == 'c' ? ic : 0u) |
+                              (b == 'g' ? ig : 0u) | (b == 't' ? iu : 0u);
+        bw |= uint32_t(live && !good) << (4 * k + j);
+      }
+      w8[k] = 8 * gi + k < g.w_raw ? w : 0u;
+    }
+  }
+  o[gi] = bw;
+  uint32_t *raw = o + 4 * g.c_bad;
+  if (8 * gi + 8 <= g.w_row) {   // 16-byte aligned: records and their raw part are whole chunks
+    reinterpret_cast<uint4 *>(raw + 8 * gi)[0] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
+    reinterpret_cast<uint4 *>(raw + 8 * gi)[1] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k)
+      if (8 * gi + k < g.w_row) raw[8 * gi + k] = w8[k];
+  }
+  if (gi == ga - 1) {
+    for (uint32_t k = ga; k < 4 * g.c_bad; ++k) o[k] = 0;
+    for (uint32_t k = 8 * ga; k < g.w_row; ++k) raw[k] = 0;
+  }
+}
+
+// groups per read of k_prep_direct
+inline uint32_t prep_groups(uint32_t max_len) { return (max_len + 31) / 32; }
+
 // lane states: S_COPY and above own a pending 16-byte probe at `addr`.
 // S_BYTE and above probe byte arrays (text, U, L8) at the exact byte
 // address (the block holds bytes [addr, addr + 16)); the states below

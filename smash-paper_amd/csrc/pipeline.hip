@@ -27,7 +27,20 @@ constexpr int kB = 256;
 constexpr unsigned kPostBlocks = 64;
 constexpr unsigned kPostThreads = kPostBlocks * kB;
 enum Stat { S_PAIRS, S_KEYPAIRS, S_DUPEPAIRS, S_POS, S_DUPS, S_KEPT, S_MATCHES, S_ERR, S_N };
+// d_stats: kStatStripes rows of kStatStride words.  The post-stage kernels
+// add their counters wave by wave into row (wave id % kStatStripes), so no
+// single word takes every wave's atomic, and need no LDS for a block
+// reduction (a kernel with LDS cannot share a CU with the search, whose
+// blocks hold all of it); the host sums the rows.  S_ERR lives in row 0.
+constexpr uint32_t kStatStride = 16, kStatStripes = 16, kStatWords = kStatStride * kStatStripes;
 }  // namespace
+
+// The post-stage kernels run beside the next batch's k_mam_sm (no LDS, so
+// they fit next to its blocks), whose waves are older and always ready: at
+// equal priority the SIMD's oldest-first issue leaves them a trickle and
+// they finish only when the search drains.  Raised priority lets them
+// through; the search absorbs their (small) share of the memory system.
+#define SMASH_BESIDE_SEARCH() __builtin_amdgcn_s_setprio(2)
 
 struct smash_pipeline {
   const smash_index *ix = nullptr;
@@ -45,6 +58,8 @@ struct smash_pipeline {
   // nbins, so a position's bisect runs over [d_cell[c], d_cell[c + 1]) only
   uint32_t *d_cell = nullptr;
   uint32_t ncell = 0, cshift = 0;
+  uint32_t *d_sp_cell = nullptr;  // contig directory (PostCfg::sp_cell)
+  uint32_t sp_ncell = 0, sp_shift = 0;
   uint64_t *d_match = nullptr;    // the current search set's (below)
   uint32_t *d_nmatch = nullptr;
   // two search sets: the k_mam_sm launch of batch b + 1 runs on its own
@@ -58,6 +73,7 @@ struct smash_pipeline {
   uint64_t rec_bytes = 0;
   hipStream_t xs[2] = {nullptr, nullptr};
   hipEvent_t ev_in = nullptr, ev_found[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+  hipEvent_t ev_done = nullptr;   // recorded once at creation: "inputs already complete"
   bool set_used[2] = {false, false};
   // a search already issued into a set (smash_phase_map_ahead): its reads
   const uint8_t *pref_reads[2] = {nullptr, nullptr};
@@ -70,6 +86,10 @@ struct smash_pipeline {
   uint64_t *d_hash = nullptr;   // [2*max_pairs] hi, lo
   uint8_t *d_keep = nullptr;
   uint8_t *d_first = nullptr;
+  uint64_t *d_slot = nullptr;     // [max_pairs] k_dedup_claim -> k_dedup_decide
+  uint64_t *d_tsum = nullptr;     // [tiles] the LDS-free scans' tile aggregates / prefixes
+  int64_t *d_tlast = nullptr;
+  bool cnt_ready = false;         // k_dedup_decide wrote d_cnt / d_lp for this batch
   uint32_t *d_k[2] = {nullptr, nullptr};   // sort keys (sort_key32)
   uint32_t *d_v[2] = {nullptr, nullptr};
   void *d_temp = nullptr;
@@ -88,7 +108,8 @@ struct smash_pipeline {
   // emitted position (-1: none), and its inclusive "last valid" scan
   int64_t *d_lp = nullptr, *d_lps = nullptr;
   bool fused_bin = true;
-  bool bin_lds = true;            // k_emit_bin_lds when the bins fit (SMASH_BIN_LDS=0: k_emit_bin)
+  bool bin_lds = false;           // SMASH_BIN_LDS=1: k_emit_bin_lds when the bins fit (A/B;
+                                  // it holds LDS, so it cannot run beside a search)
   bool pos_dirty = false;         // the positions arrays are not materialised yet
   unsigned long long *d_stats = nullptr;
   uint32_t *d_fb = nullptr;       // [1 + max_pairs]: k_post_fast<16> -> k_post pair list
@@ -139,6 +160,12 @@ struct PostCfg {
   uint32_t fast_cap;   // k_post_fast: mates with more matches go to k_post
   uint64_t hash_mask;  // ~0; tests shorten the key hash (SMASH_KEY_HASH_BITS) so
                        // that the exact key comparison meets real collisions
+  // contig directory (k_post_fast): cell c = text positions [c << sp_shift,
+  // (c + 1) << sp_shift); sp_cell[c] = upper_bound(startpos, c << sp_shift),
+  // sp_cell[sp_ncell] = n_seq, so a position's contig bisect runs over
+  // [sp_cell[c], sp_cell[c + 1]] only
+  const uint32_t *sp_cell;
+  uint32_t sp_shift, sp_ncell;
 };
 
 struct Aln {
@@ -326,26 +353,38 @@ __device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restr
   }
 }
 
-// block-aggregated stats of the pairs this thread handled
+// the wave's sum of v (every lane of the wave calls it)
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// the stats row of this wave (kStatStripes rows, see d_stats)
+__device__ __forceinline__ unsigned long long *stat_row(unsigned long long *stats) {
+  const uint32_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  return stats + kStatStride * (w % kStatStripes);
+}
+
+// the wave's sums of a and b added to counters ia and ib of its stats row
+// (every lane of the wave calls it); err: the first data error, row 0
+__device__ __forceinline__ void wave_stats(unsigned long long *stats, int ia,
+                                           unsigned long long a, int ib, unsigned long long b,
+                                           int32_t err) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  unsigned long long *row = stat_row(stats);
+  if ((threadIdx.x & 63) == 0) {
+    if (a) atomicAdd(&row[ia], a);
+    if (b) atomicAdd(&row[ib], b);
+  }
+  if (err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)err);
+}
+
+// stats of the pairs this thread handled (no LDS: see d_stats)
 __device__ __forceinline__ void post_stats(unsigned long long nm, unsigned long long np,
                                            int32_t err, unsigned long long *stats) {
-  __shared__ unsigned long long s_nm, s_pairs;
-  __shared__ int s_err;
-  if (threadIdx.x == 0) { s_nm = 0; s_pairs = 0; s_err = 0; }
-  __syncthreads();
-  if (np) {
-    atomicAdd(&s_nm, nm);
-    atomicAdd(&s_pairs, np);
-  }
-  if (err) atomicCAS(&s_err, 0, err);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (s_pairs) {
-      atomicAdd(&stats[S_MATCHES], s_nm);
-      atomicAdd(&stats[S_PAIRS], s_pairs);
-    }
-    if (s_err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)s_err);
-  }
+  wave_stats(stats, S_MATCHES, nm, S_PAIRS, np, err);
 }
 
 // general path: every pair (list == nullptr), or the pairs listed by
@@ -357,6 +396,7 @@ __global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restri
                                              uint32_t *nmajor_out, uint64_t *hits_out,
                                              uint64_t *hash_out, unsigned long long *stats,
                                              uint8_t *ws) {
+  SMASH_BESIDE_SEARCH();
   int32_t err = 0;
   unsigned long long nm = 0, np = 0;
   const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -381,11 +421,10 @@ __global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restri
 // sort last).  Mates with more than FCAP matches go to k_post.
 //   alignment: rc:1 | tid:15 | pos:32 | prefix:8 | len:8   (to_merge order)
 //   hit:       qmin:8 | rc:1 | pass:1 | - | tid:16 | pos:32 (to_print order)
-// Valid when the contig table fits in LDS (n_seq <= kSeqLds), every contig
-// is shorter than 2^31 and there are fewer than 2^15 contigs (host check).
+// Valid when every contig is shorter than 2^31 and there are fewer than 2^15
+// contigs (host check).
 // ---------------------------------------------------------------------------
 constexpr int FCAP = 16;
-constexpr uint32_t kSeqLds = 1024;
 
 __device__ __forceinline__ void cx(uint64_t &a, uint64_t &b) {
   const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
@@ -421,8 +460,9 @@ __device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
 }
 
 template <int CAP>
-__device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *sp, const uint64_t *m,
-                                          uint32_t n, uint64_t (&H)[CAP], int32_t &err) {
+__device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *__restrict__ sp,
+                                          const uint64_t *m, uint32_t n, uint64_t (&H)[CAP],
+                                          int32_t &err) {
   const uint32_t L = c.L;
   uint64_t A[CAP];
   uint64_t w[CAP];
@@ -432,7 +472,15 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *sp, 
   for (int k = 0; k < CAP; ++k) {
     const uint64_t ref = w[k] & 0xFFFFFFFFFFFFull;
     const uint32_t q = uint32_t((w[k] >> 48) & 0xFF), len = uint32_t(w[k] >> 56);
-    uint32_t lo = 0, hi = c.n_seq;          // upper_bound(startpos, ref), LDS copy
+    // upper_bound(startpos, ref) over the directory's cell range (global
+    // memory: no LDS, see d_stats); slots past n skip it (not ok below)
+    uint32_t lo = 0, hi = 0;
+    if (uint32_t(k) < n) {
+      uint64_t cl = ref >> c.sp_shift;
+      cl = cl < c.sp_ncell ? cl : c.sp_ncell - 1;
+      lo = c.sp_cell[cl];
+      hi = c.sp_cell[cl + 1];
+    }
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       if (sp[mid] <= ref) lo = mid + 1; else hi = mid;
@@ -498,9 +546,8 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
                                                   int32_t *nk_out, uint32_t *nmajor_out,
                                                   uint64_t *hits_out, uint64_t *hash_out,
                                                   unsigned long long *stats) {
-  __shared__ uint64_t sp[kSeqLds];
-  for (uint32_t i = threadIdx.x; i < c.n_seq; i += blockDim.x) sp[i] = c.startpos[i];
-  __syncthreads();
+  SMASH_BESIDE_SEARCH();
+  const uint64_t *sp = c.startpos;
   const uint64_t n = list ? *n_list : n_pairs;
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   const uint64_t t0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -600,6 +647,9 @@ __global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n
 // (agent-scope fences write back / invalidate the XCD's L2 on gfx950 and
 // made this kernel 5 ms per 2 M pairs).  Epochs wrap after 2^24 launches.
 constexpr int kRefShift = 40;
+// a published ref (the key's record is in the arena) carries kRefPub; the
+// in-batch claims of k_dedup_claim (pair index + 1, this epoch) do not
+constexpr uint64_t kRefPub = 1ull << 39;
 struct KeyRef {
   const uint64_t *w;   // the key's hit words
   uint32_t nk;
@@ -663,7 +713,7 @@ __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, con
         rec[1] = k.nk;
         for (uint32_t j = 0; j < k.nk; ++j) rec[2 + j] = k.w[j];
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * i + 1]),
-                           (unsigned long long)((epoch << kRefShift) | (off + 1)),
+                           (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
@@ -674,8 +724,8 @@ __device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, con
       const unsigned long long ref = __hip_atomic_load(
           reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_RELAXED,
           __HIP_MEMORY_SCOPE_AGENT);
-      if (ref && (ref >> kRefShift) != epoch &&
-          same_key(arena + ((ref & ((1ull << kRefShift) - 1)) - 1), k))
+      if (ref && (ref >> kRefShift) != epoch && (ref & kRefPub) &&
+          same_key(arena + ((ref & (kRefPub - 1)) - 1), k))
         return true;
     }
     i = (i + 1) & mask;
@@ -734,6 +784,288 @@ __global__ void k_dedup_first(const uint32_t *__restrict__ key, const uint32_t *
     if (a && mode == 0) atomicAdd(&stats[S_KEYPAIRS], a);
     if (b) atomicAdd(&stats[S_DUPEPAIRS], b);
     if (fl) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Single-GPU de-dup without a sort (the pair-key set of smashMEM.py:149,
+// 217-228, first occurrence in pair order wins): two kernels, no LDS, so they
+// run beside the next batch's search.
+//
+// k_dedup_claim: every keyed pair q walks the probe sequence of its hash hi.
+//   * an empty slot: CAS the hi in, then publish ref = epoch << 40 | (q + 1),
+//     a claim of this batch;
+//   * a slot holding hi whose ref is published (kRefPub, an earlier batch's
+//     key): same key (record words compared) -> q is a duplicate of an
+//     earlier batch; else go on probing (a hash collision);
+//   * a slot holding hi claimed in this batch (this epoch, no kRefPub) by pair
+//     q2: same key (q2's hit row compared) -> atomicMin the ref with
+//     epoch << 40 | (q + 1): the slot ends up naming the smallest pair of the
+//     batch with that key; else go on probing.
+//   A slot's key never changes once claimed (every pair that lowers its ref
+//   has the claimer's key), so a comparison against whichever pair the ref
+//   names is a comparison against the claimer.  A claim's ref is stored right
+//   after its CAS; a prober that sees the hi before the ref reads the slot
+//   again on its next trip.
+// k_dedup_decide: pair q is kept iff its slot's ref is still its own claim
+//   (the smallest pair of its key in the batch, and the key is new); the
+//   kept pair writes the key's record into the arena and publishes the ref
+//   (kRefPub: never equal to a claim, so the other pairs of the slot, reading
+//   it before or after, all lose).  Fused: k_count_last's per-pair count and
+//   last position.
+// slot_of[q]: the claimed slot, kSlotOld (a key of an earlier batch) or
+// kSlotNone (no key, or the set is full: the error is raised).
+// ---------------------------------------------------------------------------
+constexpr uint64_t kSlotOld = ~0ull, kSlotNone = ~0ull - 1;
+
+__device__ __forceinline__ KeyRef pair_key(const uint64_t *hits, uint32_t slots, const int32_t *nk,
+                                           const uint64_t *hash, uint64_t q) {
+  return KeyRef{hits + q * 2 * uint64_t(slots), uint32_t(nk[q]), hash[2 * q + 1]};
+}
+
+__global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__restrict__ hash,
+                              const uint64_t *__restrict__ hits, uint32_t slots, uint64_t n,
+                              uint64_t *table, uint64_t mask, const uint64_t *arena,
+                              uint64_t epoch, uint64_t *slot_of, unsigned long long *stats) {
+  SMASH_BESIDE_SEARCH();
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  int32_t err = 0;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += stride) {
+    if (nk[q] < 0) continue;
+    const KeyRef me = pair_key(hits, slots, nk, hash, q);
+    const uint64_t hi = hash[2 * q];
+    const unsigned long long mine = (epoch << kRefShift) | (q + 1);
+    uint64_t res = kSlotNone;
+    uint64_t i = (hi ^ (hi >> 31)) & mask;
+    uint32_t waits = 0;
+    for (uint64_t probe = 0; probe <= mask;) {
+      unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
+      unsigned long long *sr = sh + 1;
+      unsigned long long cur = __hip_atomic_load(sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == 0) {
+        const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
+        if (prev == 0) {
+          __hip_atomic_store(sr, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          res = i;
+          break;
+        }
+        cur = prev;
+      }
+      if (cur == hi) {
+        const unsigned long long ref =
+            __hip_atomic_load(sr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ref == 0) {
+          // the claimer is between its CAS and its ref store: read this slot
+          // again next trip (no wait inside the trip: a claimer in this wave
+          // may be laid out after this branch)
+          if (++waits > (1u << 22)) {   // (not a reachable state)
+            err = SMASH_ERR_UNSUPPORTED;
+            break;
+          }
+          continue;
+        }
+        if (ref & kRefPub) {
+          if ((ref >> kRefShift) != epoch &&
+              same_key(arena + ((ref & (kRefPub - 1)) - 1), me)) {
+            res = kSlotOld;
+            break;
+          }
+        } else if ((ref >> kRefShift) == epoch) {
+          const uint64_t q2 = (ref & (kRefPub - 1)) - 1;
+          if (same_key(me, pair_key(hits, slots, nk, hash, q2))) {
+            atomicMin(sr, mine);
+            res = i;
+            break;
+          }
+        }
+        // (an unpublished ref of an earlier epoch: its batch ran out of
+        // arena, an error already raised; no record to compare)
+      }
+      ++probe;
+      i = (i + 1) & mask;
+    }
+    if (res == kSlotNone && err == 0) err = SMASH_ERR_NOMEM;   // the set is full
+    slot_of[q] = res;
+  }
+  if (err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)err);
+}
+
+// one wave per 64 consecutive pairs per trip (wave_alloc is wave-wide)
+__global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *__restrict__ hash,
+                               const uint64_t *__restrict__ hits, uint32_t slots,
+                               const uint32_t *__restrict__ nmajor,
+                               const int64_t *__restrict__ chrom_off, uint64_t n,
+                               uint64_t *table, uint64_t *arena, uint64_t arena_cap,
+                               unsigned long long *arena_top, uint64_t epoch,
+                               const uint64_t *__restrict__ slot_of, uint8_t *keep,
+                               uint32_t *cnt, int64_t *lp, unsigned long long *stats) {
+  SMASH_BESIDE_SEARCH();
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  unsigned long long kp = 0, dp = 0;
+  bool full = false;
+  for (uint64_t base = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); base < n;
+       base += stride) {
+    const uint64_t q = base + (threadIdx.x & 63);
+    const bool in = q < n;
+    const int32_t m = in ? nk[q] : -1;
+    bool win = false;
+    if (m >= 0) {
+      const uint64_t sl = slot_of[q];
+      if (sl < kSlotNone) {
+        const unsigned long long ref = __hip_atomic_load(
+            reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        win = ref == ((epoch << kRefShift) | (q + 1));
+      }
+      ++kp;
+      dp += win ? 0 : 1;
+    }
+    const uint32_t need = win ? 2u + uint32_t(m) : 0u;
+    const uint64_t off = wave_alloc(arena_top, need);
+    if (win) {
+      if (off + need > arena_cap) {
+        full = true;   // the slot stays a claim: never matched (no kRefPub)
+      } else {
+        uint64_t *rec = arena + off;
+        const uint64_t *w = hits + q * 2 * uint64_t(slots);
+        rec[0] = hash[2 * q + 1];
+        rec[1] = uint64_t(m);
+        for (int32_t j = 0; j < m; ++j) rec[2 + j] = w[j];
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[q] + 1]),
+                           (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (in) {
+      keep[q] = win ? 1 : 0;
+      const uint32_t c = win ? nmajor[q] : 0;   // k_count_last
+      cnt[q] = c;
+      int64_t last = -1;
+      if (c) {
+        const uint64_t *h = hits + q * 2 * uint64_t(slots);
+        for (int32_t j = m - 1; j >= 0; --j)
+          if (chrom_off[uint32_t(h[j] >> 48)] >= 0) {
+            last = int64_t(h[j] & 0xFFFFFFFFFFFFull);
+            break;
+          }
+      }
+      lp[q] = last;
+    }
+  }
+  wave_stats(stats, S_KEYPAIRS, kp, S_DUPEPAIRS, dp, full ? SMASH_ERR_NOMEM : 0);
+}
+
+// ---------------------------------------------------------------------------
+// The two scans of the fused positions path without LDS (hipcub's use LDS and
+// a decoupled look-back): per pair cnt (u32, inclusive sum -> posoff[q + 1])
+// and lp (i64, inclusive "last valid" -> lps[q]).  A wave owns a tile of
+// kScanTile consecutive pairs, kScanPer per lane; (1) tile aggregates, (2)
+// one wave scans the aggregates into tile prefixes, (3) every tile re-scans
+// its pairs from its prefix.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kScanPer = 16, kScanTile = 64 * kScanPer;
+
+__device__ __forceinline__ int64_t last_valid(int64_t a, int64_t b) { return b >= 0 ? b : a; }
+
+// inclusive scans over the wave of (s, l) (sum, last valid)
+__device__ __forceinline__ void wave_scan(uint64_t &s, int64_t &l) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t ys = __shfl_up(s, d, 64);
+    const int64_t yl = __shfl_up(l, d, 64);
+    if (lane >= uint32_t(d)) {
+      s += ys;
+      l = last_valid(yl, l);
+    }
+  }
+}
+
+__global__ void k_scan_tiles(const uint32_t *__restrict__ cnt, const int64_t *__restrict__ lp,
+                             uint64_t n, uint64_t *tsum, int64_t *tlast) {
+  SMASH_BESIDE_SEARCH();
+  const uint64_t t = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+  const uint64_t q0 = t * kScanTile + uint64_t(threadIdx.x & 63) * kScanPer;
+  uint64_t s = 0;
+  int64_t l = -1;
+  if (t * kScanTile < n) {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k)
+      if (q0 + k < n) {
+        s += cnt[q0 + k];
+        l = last_valid(l, lp[q0 + k]);
+      }
+  }
+  wave_scan(s, l);
+  if ((threadIdx.x & 63) == 63 && t * kScanTile < n) {
+    tsum[t] = s;
+    tlast[t] = l;
+  }
+}
+
+// one wave: the exclusive prefixes of the ntile aggregates, in place
+__global__ void k_scan_top(uint64_t *tsum, int64_t *tlast, uint64_t ntile) {
+  SMASH_BESIDE_SEARCH();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t per = (ntile + 63) / 64;
+  const uint64_t a = lane * per, b = a + per < ntile ? a + per : ntile;
+  uint64_t s = 0;
+  int64_t l = -1;
+  for (uint64_t t = a; t < b; ++t) {
+    s += tsum[t];
+    l = last_valid(l, tlast[t]);
+  }
+  uint64_t is = s;
+  int64_t il = l;
+  wave_scan(is, il);
+  uint64_t es = __shfl_up(is, 1, 64);   // exclusive prefix of this lane's range
+  int64_t el = __shfl_up(il, 1, 64);
+  if (lane == 0) { es = 0; el = -1; }
+  for (uint64_t t = a; t < b; ++t) {
+    const uint64_t ts = tsum[t];
+    const int64_t tl = tlast[t];
+    tsum[t] = es;
+    tlast[t] = el;
+    es += ts;
+    el = last_valid(el, tl);
+  }
+}
+
+__global__ void k_scan_apply(const uint32_t *__restrict__ cnt, const int64_t *__restrict__ lp,
+                             uint64_t n, const uint64_t *__restrict__ tsum,
+                             const int64_t *__restrict__ tlast, uint32_t *posoff, int64_t *lps) {
+  SMASH_BESIDE_SEARCH();
+  const uint64_t t = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+  const uint64_t q0 = t * kScanTile + uint64_t(threadIdx.x & 63) * kScanPer;
+  const bool live = t * kScanTile < n;
+  uint32_t c[kScanPer];
+  int64_t v[kScanPer];
+  uint64_t s = 0;
+  int64_t l = -1;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    const bool ok = live && q0 + k < n;
+    c[k] = ok ? cnt[q0 + k] : 0;
+    v[k] = ok ? lp[q0 + k] : -1;
+    s += c[k];
+    l = last_valid(l, v[k]);
+  }
+  uint64_t is = s;
+  int64_t il = l;
+  wave_scan(is, il);
+  uint64_t es = __shfl_up(is, 1, 64);
+  int64_t el = __shfl_up(il, 1, 64);
+  if ((threadIdx.x & 63) == 0) { es = 0; el = -1; }
+  if (!live) return;
+  es += tsum[t];
+  el = last_valid(tlast[t], el);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    if (q0 + k >= n) break;
+    es += c[k];
+    el = last_valid(el, v[k]);
+    posoff[q0 + k + 1] = uint32_t(es);
+    lps[q0 + k] = el;
   }
 }
 
@@ -852,6 +1184,7 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
     const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
     const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
     uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats) {
+  SMASH_BESIDE_SEARCH();
   const int64_t prev0 = *prev_p;
   unsigned long long d = 0, k = 0, t = 0;
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
@@ -877,16 +1210,8 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
       prev = p;
     }
   }
-  __shared__ unsigned long long sd, sk, st;
-  if (threadIdx.x == 0) { sd = 0; sk = 0; st = 0; }
-  __syncthreads();
-  if (t) { atomicAdd(&st, t); atomicAdd(&sd, d); atomicAdd(&sk, k); }
-  __syncthreads();
-  if (threadIdx.x == 0 && st) {
-    atomicAdd(&stats[S_POS], st);
-    atomicAdd(&stats[S_DUPS], sd);
-    atomicAdd(&stats[S_KEPT], sk);
-  }
+  wave_stats(stats, S_POS, t, S_DUPS, d, 0);   // no LDS (d_stats)
+  wave_stats(stats, S_KEPT, k, S_KEPT, 0, 0);
 }
 
 // k_emit_bin with the counts summed on chip: a global atomic per position
@@ -1006,6 +1331,9 @@ PostCfg post_cfg(const smash_pipeline *p) {
   c.window = p->hit_window;
   c.fast_cap = p->post_cap;
   c.hash_mask = p->hash_mask;
+  c.sp_cell = p->d_sp_cell;
+  c.sp_shift = p->sp_shift;
+  c.sp_ncell = p->sp_ncell;
   return c;
 }
 
@@ -1073,6 +1401,24 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
         SMASH_HIPX(hipMemcpy(p->d_cell, cell.data(), 4 * (p->ncell + 1), hipMemcpyHostToDevice));
       }
     }
+    {   // contig directory (PostCfg::sp_cell): at most 2^16 cells over the text
+      const std::vector<uint64_t> &sp = ix->startpos;
+      const uint64_t top = ix->N;
+      uint32_t sh = 8;
+      while ((top >> sh) + 2 > (1u << 16)) ++sh;
+      p->sp_shift = sh;
+      p->sp_ncell = uint32_t((top >> sh) + 2);
+      std::vector<uint32_t> cell(p->sp_ncell + 1);
+      uint32_t r = 0;
+      for (uint32_t c = 0; c < p->sp_ncell; ++c) {
+        const uint64_t x = uint64_t(c) << sh;
+        while (r < sp.size() && sp[r] <= x) ++r;   // upper_bound(startpos, x)
+        cell[c] = r;
+      }
+      cell[p->sp_ncell] = uint32_t(sp.size());
+      p->d_sp_cell = dalloc<uint32_t>(p->sp_ncell + 1);
+      SMASH_HIPX(hipMemcpy(p->d_sp_cell, cell.data(), 4 * (p->sp_ncell + 1), hipMemcpyHostToDevice));
+    }
     p->rec_bytes = search_rec_bytes(2 * P, p->read_len);
     for (int k = 0; k < 2; ++k) {
       p->d_match_s[k] = dalloc<uint64_t>(2 * P * p->slots);
@@ -1084,6 +1430,9 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       SMASH_HIPX(hipEventCreateWithFlags(&p->ev_free[k], hipEventDisableTiming));
     }
     SMASH_HIPX(hipEventCreateWithFlags(&p->ev_in, hipEventDisableTiming));
+    SMASH_HIPX(hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming));
+    SMASH_HIPX(hipEventRecord(p->ev_done, nullptr));
+    SMASH_HIPX(hipEventSynchronize(p->ev_done));
     p->d_match = p->d_match_s[0];
     p->d_nmatch = p->d_nmatch_s[0];
     p->d_nk = dalloc<int32_t>(P);
@@ -1121,7 +1470,8 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     // key records: 2 + nk words each; SMASH reads keep ~7 hits per pair, the
     // arena holds 16 words per key of the capacity (an exhausted arena is a
     // reported error, SMASH_ERR_NOMEM, never a silent cut)
-    p->arena_cap = 16 * std::max<uint64_t>(cfg->dedup_capacity, P) + (1u << 20);
+    p->arena_cap = std::min<uint64_t>(16 * std::max<uint64_t>(cfg->dedup_capacity, P) + (1u << 20),
+                                      kRefPub - 2);   // (refs hold offset + 1 below kRefPub)
     p->d_arena = dalloc<uint64_t>(p->arena_cap);
     p->d_arena_top = dalloc<unsigned long long>(1);
     SMASH_HIPX(hipMemset(p->d_arena_top, 0, 8));
@@ -1132,7 +1482,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       const char *e = getenv("SMASH_FUSED_BIN");   // 0: k_emit + k_bin (A/B)
       p->fused_bin = !(e && e[0] == '0');
       const char *l = getenv("SMASH_BIN_LDS");
-      p->bin_lds = !(l && l[0] == '0');
+      p->bin_lds = l && l[0] == '1';
     }
     // the positions arrays (2 x 8 B x every hit slot: 26 GB at 6.25 M
     // pairs) only for the two-kernel path; the fused path writes them when
@@ -1140,14 +1490,17 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     if (!p->fused_bin) SMASH_HIPX(ensure_positions(p));
     int64_t init[2] = {-1, -1};
     SMASH_HIPX(hipMemcpy(p->d_prev, init, 16, hipMemcpyHostToDevice));
-    p->d_stats = dalloc<unsigned long long>(S_N);
-    SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * S_N));
+    p->d_stats = dalloc<unsigned long long>(kStatWords);
+    SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * kStatWords));
+    p->d_slot = dalloc<uint64_t>(P);
+    p->d_tsum = dalloc<uint64_t>(P / kScanTile + 1);
+    p->d_tlast = dalloc<int64_t>(P / kScanTile + 1);
     p->d_send_q = dalloc<uint32_t>(P);
     p->d_fb = dalloc<uint32_t>(P + 1);
     p->d_l16 = dalloc<uint32_t>(P + 1);
     p->d_post_ws = dalloc<uint8_t>(uint64_t(kPostThreads) * post_ws_bytes(p->slots));
     {
-      bool ok = ix->n_seq <= kSeqLds && p->n_contig < 0x7FFF;
+      bool ok = p->n_contig < 0x7FFF;
       for (uint64_t z : ix->sizes) ok = ok && z < (1ull << 31);
       const char *e = getenv("SMASH_POST_LEGACY");
       p->post_fast = ok && !(e && *e && *e != '0');
@@ -1205,14 +1558,16 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
       dfree(q);
   }
   if (p->ev_in) (void)hipEventDestroy(p->ev_in);
+  if (p->ev_done) (void)hipEventDestroy(p->ev_done);
   if (p->ev_owner) (void)hipEventDestroy(p->ev_owner);
   if (p->ev_base) (void)hipEventDestroy(p->ev_base);
   if (p->h_owner) (void)hipHostFree(p->h_owner);
   if (p->h_recv_base) (void)hipHostFree(p->h_recv_base);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
-                  (void *)p->d_bins, (void *)p->d_cell,
+                  (void *)p->d_bins, (void *)p->d_cell, (void *)p->d_sp_cell,
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
                   (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_first,
+                  (void *)p->d_slot, (void *)p->d_tsum, (void *)p->d_tlast,
                   (void *)p->d_k[0], (void *)p->d_k[1], (void *)p->d_v[0],
                   (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
@@ -1231,7 +1586,9 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
                        hipEvent_t in_ev) {
   hipStream_t xs = p->xs[k];
   SMASH_HIP(hipStreamWaitEvent(xs, in_ev, 0));
-  if (p->set_used[k]) SMASH_HIP(hipStreamWaitEvent(xs, p->ev_free[k], 0));
+  // the set's records were last read by its previous search, earlier on xs;
+  // its match buffers by that batch's post stage: k_prep runs now, the
+  // search after ev_free (SearchWs::gate)
   if (p->prof) {
     if (2 * p->n_ev + 2 > p->ev.size()) {
       for (int q = 0; q < 64; ++q) {
@@ -1243,7 +1600,8 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
     p->ix->kev[0] = p->ev[2 * p->n_ev];          // recorded around k_mam_sm itself
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
-  const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k]};
+  const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k],
+                    p->set_used[k] ? p->ev_free[k] : nullptr};
   const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
                                 p->read_len, 2 * n_pairs, p->d_match_s[k], p->slots,
                                 p->d_nmatch_s[k], xs, false, &ws);   // probe check at stats time
@@ -1315,7 +1673,14 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
   SMASH_HIP(hipGetLastError());
   SMASH_HIP(hipEventRecord(p->ev_free[k], s));   // the set's matches are read
   p->set_used[k] = true;
-  // in-batch ordering for de-dup: stable radix sort of key hi, value = pair
+  p->cnt_ready = false;
+  return SMASH_OK;
+}
+
+// the multi-GPU export's in-batch order: stable radix sort of sort_key32,
+// value = pair (the single-GPU de-dup needs no sort: k_dedup_claim)
+static int sort_batch_keys(smash_pipeline *p, hipStream_t s) {
+  const uint64_t n_pairs = p->n_pairs;
   k_dedup_keys<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_nk, p->d_hash, n_pairs,
                                                              p->d_k[0], p->d_v[0]);
   hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
@@ -1347,14 +1712,22 @@ static uint64_t next_epoch(smash_pipeline *p) {
   return p->epoch;
 }
 
+// single GPU: the persistent set, first occurrence in pair order
+// (k_dedup_claim, k_dedup_decide), and the positions' per-pair counts
 static int dedup_local(smash_pipeline *p, hipStream_t s) {
-  if (!p->n_pairs) return SMASH_OK;
-  k_dedup_first<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, s>>>(
-      p->d_k[0], p->d_v[0], p->n_pairs, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
-      p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, next_epoch(p), 0, p->d_keep,
-      p->d_first,
+  const uint64_t n = p->n_pairs;
+  if (!n) return SMASH_OK;
+  const uint64_t epoch = next_epoch(p);
+  k_dedup_claim<<<grid_for(n, kB, 8192), kB, 0, s>>>(p->d_nk, p->d_hash, p->d_hits, p->slots, n,
+                                                     p->d_table, p->table_mask, p->d_arena, epoch,
+                                                     p->d_slot, p->d_stats);
+  SMASH_HIP(hipGetLastError());
+  k_dedup_decide<<<grid_for(n, kB, 8192), kB, 0, s>>>(
+      p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_nmajor, p->d_chrom_off, n, p->d_table,
+      p->d_arena, p->arena_cap, p->d_arena_top, epoch, p->d_slot, p->d_keep, p->d_cnt, p->d_lp,
       p->d_stats);
   SMASH_HIP(hipGetLastError());
+  p->cnt_ready = true;
   return SMASH_OK;
 }
 
@@ -1367,13 +1740,18 @@ extern "C" int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *s
     // counts, offsets and each pair's preceding line; the positions
     // themselves are only written if someone asks (smash_pipeline_positions)
     if (n) {
-      k_count_last<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, p->d_nk,
-                                                           p->d_hits, p->slots, p->d_chrom_off, n,
-                                                           p->d_cnt, p->d_lp);
-      size_t tb = p->temp_bytes;
-      SMASH_HIP(hipcub::DeviceScan::InclusiveSum(p->d_temp, tb, p->d_cnt, p->d_posoff + 1, n, s));
-      tb = p->temp_bytes;
-      SMASH_HIP(hipcub::DeviceScan::InclusiveScan(p->d_temp, tb, p->d_lp, p->d_lps, LastValid(), n, s));
+      if (!p->cnt_ready)   // (the multi-GPU path: keep came from the owners)
+        k_count_last<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, p->d_nk,
+                                                             p->d_hits, p->slots, p->d_chrom_off,
+                                                             n, p->d_cnt, p->d_lp);
+      // posoff (offsets) and lps ("last valid" position), no LDS
+      const uint64_t ntile = (n + kScanTile - 1) / kScanTile;
+      const unsigned g = unsigned((ntile * 64 + kB - 1) / kB);
+      k_scan_tiles<<<g, kB, 0, s>>>(p->d_cnt, p->d_lp, n, p->d_tsum, p->d_tlast);
+      k_scan_top<<<1, 64, 0, s>>>(p->d_tsum, p->d_tlast, ntile);
+      k_scan_apply<<<g, kB, 0, s>>>(p->d_cnt, p->d_lp, n, p->d_tsum, p->d_tlast, p->d_posoff,
+                                    p->d_lps);
+      SMASH_HIP(hipGetLastError());
       p->pos_dirty = true;
     }
     k_tail_lps<<<1, 1, 0, s>>>(p->d_posoff + n, p->d_lps + (n ? n - 1 : 0), nullptr, d_tail);
@@ -1448,28 +1826,48 @@ extern "C" int smash_count_batch(smash_pipeline *p, const uint8_t *d_reads,
                                nullptr);
 }
 
-extern "C" int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
-                                   uint64_t batch_pairs, uint64_t *d_counts, void *stream) {
+// ready: the reads' input event (hipEvent_t); null with `resident`: none
+static int count_batches_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                              uint64_t batch_pairs, uint64_t *d_counts, hipStream_t s,
+                              hipEvent_t ready, bool resident) {
   if (!p || (n_pairs && !d_reads) || !d_counts || batch_pairs == 0 ||
       batch_pairs > p->max_pairs) {
     set_error("smash_count_batches: bad arguments");
     return SMASH_ERR_ARG;
   }
-  hipStream_t s = static_cast<hipStream_t>(stream);
   SMASH_HIP(hipSetDevice(p->device));
-  // every batch's reads are ready once the work before this call on s is:
-  // one input event for all, so batch b + 1's search can start under the
-  // tail of batch b's
-  hipEvent_t in_ev = nullptr;
-  SMASH_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
-  int rc = hipEventRecord(in_ev, s) == hipSuccess ? SMASH_OK : SMASH_ERR_HIP;
+  // one input event for all batches, so batch b + 1's search can start under
+  // the tail of batch b's: the caller's, an event already complete (resident
+  // reads), or every batch's reads are ready once the work before this call
+  // on s is
+  hipEvent_t in_ev = ready ? ready : resident ? p->ev_done : nullptr;
+  const bool own = !in_ev;
+  int rc = SMASH_OK;
+  if (own) {
+    SMASH_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
+    rc = hipEventRecord(in_ev, s) == hipSuccess ? SMASH_OK : SMASH_ERR_HIP;
+  }
   const uint64_t L2 = 2 * uint64_t(p->read_len);
   for (uint64_t b0 = 0; rc == SMASH_OK && b0 < n_pairs; b0 += batch_pairs) {
     const uint64_t n = std::min(batch_pairs, n_pairs - b0);
     rc = smash::count_batch_ev(p, d_reads + b0 * L2, n, d_counts, s, in_ev);
   }
-  (void)hipEventDestroy(in_ev);   // released once the waits on it have completed
+  if (own) (void)hipEventDestroy(in_ev);   // released once the waits on it have completed
   return rc;
+}
+
+extern "C" int smash_count_batches(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                                   uint64_t batch_pairs, uint64_t *d_counts, void *stream) {
+  return count_batches_impl(p, d_reads, n_pairs, batch_pairs, d_counts,
+                            static_cast<hipStream_t>(stream), nullptr, false);
+}
+
+extern "C" int smash_count_batches_ready(smash_pipeline *p, const uint8_t *d_reads,
+                                         uint64_t n_pairs, uint64_t batch_pairs,
+                                         uint64_t *d_counts, void *stream, void *ready) {
+  return count_batches_impl(p, d_reads, n_pairs, batch_pairs, d_counts,
+                            static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(ready),
+                            true);
 }
 
 // ---- multi-GPU de-dup exchange ------------------------------------------------
@@ -1589,6 +1987,7 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
   SMASH_HIP(hipMemsetAsync(p->d_keep, 0, n ? n : 1, s));
   if (n) {
     // in-batch first occurrences (mode 1: no persistent-set probe)
+    if (int rc = sort_batch_keys(p, s)) return rc;
     k_dedup_first<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
         p->d_k[0], p->d_v[0], n, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
         p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 0, 1, p->d_keep, p->d_first,
@@ -1704,8 +2103,12 @@ extern "C" int smash_pipeline_stats(smash_pipeline *p, smash_stats *o) {
   if (p->last) SMASH_HIP(hipStreamSynchronize(p->last));
   SMASH_HIP(hipDeviceSynchronize());
   if (int rc = probe_check(p->ix)) return rc;   // k_mam_sm's sticky probe check
-  unsigned long long st[S_N];
-  SMASH_HIP(hipMemcpy(st, p->d_stats, sizeof(st), hipMemcpyDeviceToHost));
+  unsigned long long rows[kStatWords], st[S_N] = {0};
+  SMASH_HIP(hipMemcpy(rows, p->d_stats, sizeof(rows), hipMemcpyDeviceToHost));
+  for (uint32_t r = 0; r < kStatStripes; ++r)
+    for (int k = 0; k < S_N; ++k)
+      if (k != S_ERR) st[k] += rows[r * kStatStride + k];
+  st[S_ERR] = rows[S_ERR];
   o->pairs = st[S_PAIRS];
   o->key_pairs = st[S_KEYPAIRS];
   o->dupe_pairs = st[S_DUPEPAIRS];
@@ -1737,7 +2140,7 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   SMASH_HIP(hipSetDevice(p->device));
   SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * (p->table_mask + 1), s));
   SMASH_HIP(hipMemsetAsync(p->d_arena_top, 0, 8, s));
-  SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * S_N, s));
+  SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * kStatWords, s));
   k_reset_prev<<<1, 1, 0, s>>>(p->d_prev);   // no host source: stays asynchronous
   SMASH_HIP(hipGetLastError());
   // a look-ahead search not consumed before the reset is dropped: the next

@@ -51,7 +51,8 @@ EXPORTS = [
     "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
     "smash_fastq_open", "smash_fastq_read", "smash_fastq_close", "smash_strnum_order",
-    "smash_count_fastq", "smash_count_batches", "smash_pipeline_profile_active",
+    "smash_count_fastq", "smash_count_batches", "smash_count_batches_ready",
+    "smash_pipeline_profile_active",
     "smash_pipeline_profile_intervals", "smash_fastq_read_parallel",
     "smash_fastq_index_open", "smash_fastq_index_pack", "smash_fastq_index_close",
     "smash_phase_map_ahead", "smash_sam_records_packed",
@@ -134,6 +135,7 @@ def lib():
     L.smash_pipeline_free.restype = None
     L.smash_count_batch.argtypes = [vp, vp, C.c_uint64, vp, vp]
     L.smash_count_batches.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp]
+    L.smash_count_batches_ready.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp, vp]
     L.smash_phase_map_ahead.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp]
     L.smash_pipeline_profile_active.argtypes = [vp, C.POINTER(C.c_double)]
     L.smash_pipeline_profile_intervals.argtypes = [vp, C.POINTER(C.c_double), C.c_uint64, u64p]
@@ -413,9 +415,18 @@ class Pipeline:
                                       vp(_stream(stream))), "smash_count_fastq")
         return st.as_dict()
 
-    def count_batches(self, d_reads, n_pairs, batch_pairs, d_counts, stream=None):
+    def count_batches(self, d_reads, n_pairs, batch_pairs, d_counts, stream=None,
+                      resident=False):
         """n_pairs resident pairs in batches (smash_count_batches): one batch's
-        search overlaps the previous one's tail."""
+        search overlaps the previous one's tail.  resident=True: the reads are
+        complete already (smash_count_batches_ready, no input event), so the
+        searches need not wait for the work queued on the stream before this
+        call -- consecutive runs over the same reads overlap."""
+        if resident:
+            check(lib().smash_count_batches_ready(self.h, _ptr(d_reads), n_pairs, batch_pairs,
+                                                  _ptr(d_counts), vp(_stream(stream)), None),
+                  "smash_count_batches_ready")
+            return
         check(lib().smash_count_batches(self.h, _ptr(d_reads), n_pairs, batch_pairs,
                                         _ptr(d_counts), vp(_stream(stream))),
               "smash_count_batches")

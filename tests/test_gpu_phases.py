@@ -72,6 +72,35 @@ def test_count_batches_equals_batch_by_batch(gix, batch):
     assert out[0] == out[1]
 
 
+@pytest.mark.parametrize("batch", [97, 2000])
+def test_resident_runs_back_to_back(gix, batch):
+    """smash_count_batches_ready (no input event: the searches of a run start
+    under the post stage of the run queued before it), three runs queued
+    with no synchronisation, each after a reset and a zeroing of its own
+    counts: every run's counts == one run of smash_count_batches."""
+    reads = interleaved_reads("s150")
+    n = reads.shape[0] // 2
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    d = torch.from_numpy(np.ascontiguousarray(reads)).cuda()
+    torch.cuda.synchronize()
+    ref = S.Pipeline(gix, cs, starts, reads.shape[1], batch, dedup_capacity=n)
+    ref.reset()
+    c0 = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    ref.count_batches(d, n, batch, c0)
+    st0 = ref.stats()
+    pipe = S.Pipeline(gix, cs, starts, reads.shape[1], batch, dedup_capacity=n)
+    cs_ = [torch.zeros(len(starts), dtype=torch.int64, device="cuda") for _ in range(3)]
+    for c in cs_:
+        pipe.reset()
+        pipe.count_batches(d, n, batch, c, resident=True)
+    st = pipe.stats()
+    for c in cs_:
+        assert c.cpu().numpy().tolist() == c0.cpu().numpy().tolist()
+    assert (st.positions, st.dups, st.kept, st.dupe_pairs) == (
+        st0.positions, st0.dups, st0.kept, st0.dupe_pairs)
+
+
 def test_full_key_set_fails_loudly(gix, monkeypatch):
     """The round-2 over-count of [2-300-3-2-True]: each emulated rank's key
     set was sized for one batch (1 024 slots), while an owner keeps the keys

@@ -101,3 +101,37 @@ def test_request_accounting(emu, pf, monkeypatch):
     assert allr <= probes + spec + len(got) * 4   # + the record lines per read
     print("requests/read %.1f (spec %.1f) probes/read %.1f lines/read %.1f" % (
         allr / len(got), spec / len(got), probes / len(got), lines / len(got)))
+
+
+@pytest.mark.parametrize("L,stride", [(15, 15), (32, 32), (33, 35), (100, 100), (128, 128),
+                                      (129, 131), (150, 150), (151, 153), (255, 255)])
+@pytest.mark.parametrize("var", [False, True])
+def test_prep_direct_equals_lds(L, stride, var):
+    """k_prep_direct (the pipeline's default record builder, no LDS) writes
+    every word of every record, equal to k_prep's: ACGT and other bytes,
+    'N' and case, odd strides (unaligned reads), per-read lengths, the input's
+    last read (no load past its last word)."""
+    import ctypes as C
+    rng = np.random.default_rng(L * 7 + stride + var)
+    n = 97
+    alphabet = np.frombuffer(b"acgtacgtacgtnNAZ$`", np.uint8)
+    buf = alphabet[rng.integers(0, len(alphabet), n * stride)].astype(np.uint8)
+    lens = rng.integers(1, L + 1, n).astype(np.uint16) if var else None
+    if var:
+        lens[:3] = (L, 1, 32 if L >= 32 else L)
+    in_text = np.zeros(256, bool)
+    for b in b"acgtn":
+        in_text[b] = True
+    it = sm_emu.in_text_words(in_text)
+    g_chunks_max = 4 * (2 + 68)   # words per record, generous
+    a = np.zeros(n * g_chunks_max, np.uint32)
+    b = np.zeros(n * g_chunks_max, np.uint32)
+    rc = sm_emu.lib().sm_emu_prep(
+        buf.ctypes.data_as(C.c_void_p), C.c_uint64(stride),
+        lens.ctypes.data_as(C.c_void_p) if var else None, C.c_uint32(L), C.c_uint64(n),
+        it.ctypes.data_as(C.c_void_p), a.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p))
+    assert rc > 0
+    w = n * rc
+    assert not (a[:w] == 0xDEADBEEF).any()
+    bad = np.nonzero(a[:w] != b[:w])[0]
+    assert bad.size == 0, (bad[:8] // rc, bad[:8] % rc, a[bad[:8]], b[bad[:8]])

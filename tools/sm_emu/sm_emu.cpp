@@ -139,6 +139,52 @@ namespace smash { namespace sm { alignas(16) uint32_t ldsw[1 << 12]; alignas(16)
 
 using namespace smash;
 
+// the records of n reads, by k_prep (one lane per block, LDS image) or by
+// k_prep_direct (every (read, group) item, 256-thread blocks), as the device
+// default (mam.hip) does
+static int prep_records(const uint8_t *reads, uint64_t stride, const uint16_t *lens, uint32_t L,
+                        uint64_t n, const uint64_t *in_text, const sm::Geom &g, uint32_t *rec,
+                        bool direct) {
+  if (direct) {
+    blockDim.x = 256;
+    const uint32_t ga = sm::prep_groups(lens ? 255 : L);
+    const uint64_t items = n * ga;
+    for (uint64_t i = 0; i < items; ++i) {
+      blockIdx.x = unsigned(i / 256);
+      threadIdx.x = unsigned(i % 256);
+      sm::k_prep_direct(reads, stride, lens, L, uint32_t(n), ga, in_text[0], in_text[1], in_text[2],
+                        in_text[3], g, rec);
+    }
+  } else {
+    const uint32_t per = sm::prep_per_block(g, stride);
+    if (sm::prep_lds_bytes(g, stride, per) > sizeof(sm::prep_lds)) return -1;
+    blockDim.x = 1;
+    threadIdx.x = 0;
+    for (uint64_t b = 0; b * per < n; ++b) {
+      blockIdx.x = unsigned(b);
+      sm::k_prep(reads, stride, lens, L, n, in_text[0], in_text[1], in_text[2], in_text[3], g, per,
+                 rec);
+    }
+  }
+  blockIdx.x = 0;
+  threadIdx.x = 0;
+  blockDim.x = 1;
+  return 0;
+}
+
+// both record builders over the same reads (tests: k_prep_direct == k_prep,
+// word for word); returns the record words per read, -1 on a geometry error
+extern "C" int sm_emu_prep(const uint8_t *reads, uint64_t stride, const uint16_t *lens, uint32_t L,
+                           uint64_t n, const uint64_t *in_text, uint32_t *out_lds,
+                           uint32_t *out_direct) {
+  const sm::Geom g = sm::make_geom(lens ? 255 : L);
+  const uint64_t words = n * g.chunks * 4;
+  for (uint64_t i = 0; i < words; ++i) out_lds[i] = out_direct[i] = 0xDEADBEEFu;   // all written?
+  if (prep_records(reads, stride, lens, L, n, in_text, g, out_lds, false)) return -1;
+  if (prep_records(reads, stride, lens, L, n, in_text, g, out_direct, true)) return -1;
+  return int(g.chunks * 4);
+}
+
 template <class IdxT>
 static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t *L8,
                const uint8_t *U, const uint64_t *KT, int K, const uint64_t *BM, int B,
@@ -154,16 +200,9 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   while (reinterpret_cast<uint64_t>(rec_p) & 63) ++rec_p;
   struct { uint4 *p; size_t n; uint4 *data() { return p; } size_t size() const { return n; } } rec{
       rec_p, size_t(n * g.chunks)};
-  const uint32_t per = sm::prep_per_block(g, stride);
-  if (sm::prep_lds_bytes(g, stride, per) > sizeof(sm::prep_lds)) return -1;
-  blockDim.x = 1;
-  threadIdx.x = 0;
-  for (uint64_t b = 0; b * per < n; ++b) {
-    blockIdx.x = unsigned(b);
-    sm::k_prep(reads, stride, nullptr, L, n, in_text[0], in_text[1], in_text[2], in_text[3], g, per,
-               reinterpret_cast<uint32_t *>(rec.data()));
-  }
-  blockIdx.x = 0;
+  if (prep_records(reads, stride, nullptr, L, n, in_text, g, reinterpret_cast<uint32_t *>(rec.data()),
+                   !(std::getenv("SMASH_PREP_LDS") && std::getenv("SMASH_PREP_LDS")[0] == '1')))
+    return -1;
   threadIdx.x = 0;
   sm::Ctx<IdxT> c;
   c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);

@@ -55,6 +55,46 @@ def main(trace, warm=4, per_step=4):
     u += ce - cs
     print("search union %.2f ms per step; not covered by a search: %.2f ms per step"
           % (u / 1e6 / steps, (t1 - t0 - u) / 1e6 / steps))
+    # what runs in the uncovered time: per kernel, its overlap with the gaps
+    # between search launches (kernels on other streams may overlap each other)
+    merged, (cs, ce) = [], iv[0]
+    for a, b in iv[1:]:
+        if a > ce:
+            merged.append((cs, ce))
+            cs, ce = a, b
+        else:
+            ce = max(ce, b)
+    merged.append((cs, ce))
+    gaps = [(merged[i][1], merged[i + 1][0]) for i in range(len(merged) - 1)]
+    gaps.append((merged[-1][1], t1))
+    gap_k = defaultdict(float)
+    busy = []
+    for r in rs:
+        if "k_mam_sm" in r["Kernel_Name"]:
+            continue
+        a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        for g0, g1 in gaps:
+            o0, o1 = max(a, g0), min(b, g1)
+            if o1 > o0:
+                gap_k[short(r["Kernel_Name"])] += o1 - o0
+                busy.append((o0, o1))
+    busy.sort()
+    bu = 0
+    if busy:
+        (cs, ce) = busy[0]
+        for a, b in busy[1:]:
+            if a > ce:
+                bu += ce - cs
+                cs, ce = a, b
+            else:
+                ce = max(ce, b)
+        bu += ce - cs
+    gap_total = sum(g1 - g0 for g0, g1 in gaps)
+    print("uncovered time: %.2f ms per step in kernels, %.2f ms per step idle"
+          % (bu / 1e6 / steps, (gap_total - bu) / 1e6 / steps))
+    for k, t in sorted(gap_k.items(), key=lambda x: -x[1]):
+        if t / 1e6 / steps >= 0.05:
+            print("  %-43s %10.2f ms/step uncovered" % (k, t / 1e6 / steps))
 
 
 if __name__ == "__main__":
