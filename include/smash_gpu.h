@@ -43,6 +43,12 @@ const char *smash_last_error(void);   /* thread-local text of the last error */
 int smash_text_from_fasta(const char *path, uint8_t **text, uint64_t *N,
                           uint32_t *n_seq, uint64_t **startpos,
                           uint64_t **sizes, char ***names);
+/* The same with the layout chosen: rcref = 1 as above; rcref = 0 the
+ * forward-only text of `mummer` without -rcref (fasta.cpp:160-169:
+ * c1 ` c2 ` ... cn $, one entry per contig). */
+int smash_text_from_fasta_layout(const char *path, int rcref, uint8_t **text, uint64_t *N,
+                                 uint32_t *n_seq, uint64_t **startpos, uint64_t **sizes,
+                                 char ***names);
 void smash_text_free(uint8_t *text, uint32_t n_seq, uint64_t *startpos,
                      uint64_t *sizes, char **names);
 
@@ -80,6 +86,19 @@ int smash_index_create(const uint8_t *h_text, uint64_t N, uint32_t n_seq,
  * util.cpp:100-125. */
 int smash_index_load(const char *fasta_path, int device, smash_index **out);
 
+/* Either text layout (Sequence/longSA with ref.rcref = rcref): rcref = 0
+ * takes the forward-only text (one entry per contig, any n_seq) and the
+ * rc0.* cache files (fasta.cpp:98, longSA.cpp:103).  Such an index has no
+ * map.bin (-mappability requires -rcref, mummer.cpp:145): it serves
+ * smash_map_batch / smash_match_batch / smash_sam_records* (mummer without
+ * -rcref) and is refused by smash_pipeline_create and
+ * smash_mappability_scan, whose SMASH chain always passes -rcref. */
+int smash_index_create_layout(const uint8_t *h_text, uint64_t N, uint32_t n_seq,
+                              const uint64_t *h_startpos, const uint64_t *h_sizes,
+                              const char *const *names, int rcref, int device,
+                              smash_index **out);
+int smash_index_load_layout(const char *fasta_path, int rcref, int device, smash_index **out);
+
 /* Write the reference's on-disk cache (rc1.i4 when N <= INT32_MAX-100000 as
  * `mummer` would, else rc1.i8, mummer.cpp:156-183) + map.bin
  * (index_setup.sh:19-22).  fasta_size is stored in the headers
@@ -116,6 +135,8 @@ typedef struct {
   uint32_t bitmap_b;       /* B = k + 2: the window filter's B-mer length */
   const uint64_t *d_bitmap;/* NULL (round 3: the presence bits are in d_kmer) */
   uint64_t in_text[4];     /* 256-bit set of bytes occurring in the text */
+  uint32_t rcref;          /* 1: c ` rc(c) layout; 0: forward only, no map.bin */
+  uint32_t reserved;
 } smash_index_info;
 int smash_index_query(const smash_index *ix, smash_index_info *out);
 

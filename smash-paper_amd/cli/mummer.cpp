@@ -46,6 +46,12 @@ namespace {
 struct Fail : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// raised where the reference's worker thread throws (memsam.h:148-150,
+// MemSam::chromosomes.at): Pair::runner_thread prints e.what() alone and
+// exits 1 (query.cpp:522-535), without main's "Error" line
+struct ThreadFail : Fail {
+  using Fail::Fail;
+};
 
 void ck(int rc, const char *what) {
   if (rc != SMASH_OK) throw Fail(std::string(what) + ": " + smash_last_error());
@@ -143,9 +149,6 @@ Args parse(int argc, char **argv) {
   if (a.fastq && a.sam_in) throw Fail("-fastq cannot be used with -samin");
   if (a.nomap && !a.sam_out) throw Fail("-nomap can only be used with -sam_out");
   if (a.mappability && !a.rcref) throw Fail("-mappability requires -rcref");
-  if (!a.rcref)
-    throw Fail("only the -rcref text layout is implemented (every SMASH script passes "
-               "-rcref, index_setup.sh:19-22, smash_mapping.sh:19)");
   a.ref = argv[optind];
   for (int i = optind + 1; i < argc; ++i) a.input.emplace_back(argv[i]);
   return a;
@@ -159,8 +162,9 @@ bool exists(const std::string &p) {
 // ---- the index: REF.fa.bin/ cache or a device build + save ------------------
 struct Index {
   smash_index *h = nullptr;
-  std::vector<std::string> names;   // 2 per contig
+  std::vector<std::string> names;   // 2 per contig with -rcref, else 1
   std::vector<uint64_t> sizes;
+  bool rcref = true;
   ~Index() {
     if (h) smash_index_free(h);
   }
@@ -168,12 +172,14 @@ struct Index {
 
 void load_or_build(const Args &a, Index &ix) {
   const std::string dir = a.ref + ".bin/";
+  const std::string rc = a.rcref ? "rc1" : "rc0";   // fasta.cpp:98, longSA.cpp:103
+  ix.rcref = a.rcref;
   const double t0 = now_s();
-  if (exists(dir + "rc1.i4.index.bin") || exists(dir + "rc1.i8.index.bin")) {
+  if (exists(dir + rc + ".i4.index.bin") || exists(dir + rc + ".i8.index.bin")) {
     if (a.verbose) std::fprintf(stderr, "# loading index binary\n");
-    ck(smash_index_load(a.ref.c_str(), 0, &ix.h), "smash_index_load");
-    // names and sizes from rc1.ref.bin (fasta.cpp:221-233)
-    std::ifstream f(dir + "rc1.ref.bin", std::ios::binary);
+    ck(smash_index_load_layout(a.ref.c_str(), a.rcref ? 1 : 0, 0, &ix.h), "smash_index_load");
+    // names and sizes from rc?.ref.bin (fasta.cpp:221-233)
+    std::ifstream f(dir + rc + ".ref.bin", std::ios::binary);
     auto rd = [&]() {
       uint64_t v = 0;
       f.read(reinterpret_cast<char *>(&v), 8);
@@ -190,7 +196,7 @@ void load_or_build(const Args &a, Index &ix) {
       f.read(&s[0], std::streamsize(L));
       ix.names.push_back(s);
     }
-    if (!f) throw Fail("cannot read " + dir + "rc1.ref.bin");
+    if (!f) throw Fail("cannot read " + dir + rc + ".ref.bin");
   } else {
     if (!exists(a.ref)) throw Fail("reference file not found: " + a.ref);
     if (a.verbose) std::fprintf(stderr, "# building the index on the device\n");
@@ -198,15 +204,16 @@ void load_or_build(const Args &a, Index &ix) {
     uint64_t N = 0, *sp = nullptr, *sz = nullptr;
     uint32_t ns = 0;
     char **nm = nullptr;
-    ck(smash_text_from_fasta(a.ref.c_str(), &text, &N, &ns, &sp, &sz, &nm),
+    ck(smash_text_from_fasta_layout(a.ref.c_str(), a.rcref ? 1 : 0, &text, &N, &ns, &sp, &sz,
+                                    &nm),
        "smash_text_from_fasta");
     for (uint32_t i = 0; i < ns; ++i) {
       ix.names.emplace_back(nm[i]);
       ix.sizes.push_back(sz[i]);
     }
-    const int rc = smash_index_create(text, N, ns, sp, sz, nm, 0, &ix.h);
+    const int rcode = smash_index_create_layout(text, N, ns, sp, sz, nm, a.rcref ? 1 : 0, 0, &ix.h);
     smash_text_free(text, ns, sp, sz, nm);
-    ck(rc, "smash_index_create");
+    ck(rcode, "smash_index_create");
     struct stat st;
     stat(a.ref.c_str(), &st);
     ck(smash_index_save(ix.h, a.ref.c_str(), uint64_t(st.st_size)), "smash_index_save");
@@ -297,14 +304,18 @@ struct Sorter {
   std::string tag;
   int seq = 0;
   explicit Sorter(const Index &ix) {
+    // the absolute-position map steps over descr by 2 with or without
+    // -rcref (query.cpp:547-551): without it every second contig is missing
+    // and a line on one of them ends the run with "map::at", as it does there
     uint64_t off = 0;
-    header = "@HD\tVN:1.0\tSO:unsorted\n";
     for (size_t i = 0; i < ix.names.size(); i += 2) {
       chrom[ix.names[i]] = off;
       off += ix.sizes[i];
-      header += "@SQ\tSN:" + ix.names[i] + "\tLN:" + std::to_string(ix.sizes[i]) + "\n";
     }
     chrom["*"] = off;
+    header = "@HD\tVN:1.0\tSO:unsorted\n";   // Sequence::sam_header (fasta.cpp:243-252)
+    for (size_t i = 0; i < ix.names.size(); i += ix.rcref ? 2 : 1)
+      header += "@SQ\tSN:" + ix.names[i] + "\tLN:" + std::to_string(ix.sizes[i]) + "\n";
     header += "@PG\tID:longMEM\tPN:longMEM\tVN:0.5\n";
     tag = std::to_string(uint64_t(getpid()));
   }
@@ -335,7 +346,7 @@ struct Sorter {
       const unsigned flag = unsigned(std::atoi(f1));
       k.mate = flag & (64u | 128u | 16u);
       const auto c = chrom.find(std::string(f2, size_t(f3 - 1 - f2)));
-      if (c == chrom.end()) throw Fail("map::at");   // MemSam::chromosomes.at
+      if (c == chrom.end()) throw ThreadFail("map::at");   // MemSam::chromosomes.at
       k.abspos = uint64_t(std::atol(f3)) + c->second;
       keys.push_back(std::move(k));
       p += len;
@@ -343,7 +354,7 @@ struct Sorter {
     std::sort(keys.begin(), keys.end(), [](const Key &a, const Key &b) {
       if (a.abspos != b.abspos) return a.abspos < b.abspos;
       if (a.name != b.name) return a.name < b.name;
-      if (a.mate == b.mate) throw Fail("flags equal");   // memsam.h:148-150
+      if (a.mate == b.mate) throw ThreadFail("flags equal");   // memsam.h:148-150
       return a.mate < b.mate;
     });
     const std::string path = "mapout/mapout" + tag + "." + std::to_string(++seq) + ".txt";
@@ -509,8 +520,9 @@ int run(int argc, char **argv) {
     std::fclose(o);
     return 0;
   }
-  std::vector<const char *> contigs;
-  for (size_t i = 0; i < ix.names.size(); i += 2) contigs.push_back(ix.names[i].c_str());
+  std::vector<const char *> contigs;   // per record tid (k_sam_recs)
+  for (size_t i = 0; i < ix.names.size(); i += a.rcref ? 2 : 1)
+    contigs.push_back(ix.names[i].c_str());
   Sorter out(ix);
   Device d;
   const size_t batch = 1u << 18;   // reads per device batch (even: mates stay together)
@@ -549,6 +561,9 @@ int run(int argc, char **argv) {
 int main(int argc, char **argv) {
   try {
     return run(argc, argv);
+  } catch (ThreadFail &e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return 1;
   } catch (std::exception &e) {
     std::fprintf(stderr, "Error\n%s\n", e.what());
     return 1;

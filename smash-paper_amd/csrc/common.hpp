@@ -95,6 +95,7 @@ struct smash_index {
   uint64_t N = 0, logN = 0;
   uint32_t idx_bytes = 4;
   uint32_t n_seq = 0;
+  bool rcref = true;             // text layout: -rcref (2 entries per contig) or forward only
   std::vector<uint64_t> startpos, sizes;
   std::vector<std::string> names;
   uint8_t *d_text = nullptr;     // N + 64 (zero pad)

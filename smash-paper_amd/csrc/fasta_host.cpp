@@ -1,8 +1,9 @@
 // smash-paper_amd/csrc/fasta_host.cpp -- host-side reference text builder.
 //
-// Sequence::Sequence with -rcref (fasta.cpp:133-285): per contig the
+// Sequence::Sequence (fasta.cpp:133-285).  With -rcref: per contig the
 // lowercased forward sequence, '`', its reverse complement (the IUPAC map of
 // reverse_complement, fasta.cpp:26-61), '`' between contigs, one final '$'.
+// Without it (fasta.cpp:165-168): c1 ` c2 ` ... cn $, one entry per contig.
 // Line handling follows std::getline + trim (fasta.cpp:107-124,195-246),
 // including the eof-without-newline behaviour.
 #include <cstdio>
@@ -29,9 +30,9 @@ unsigned char comp(unsigned char c) {
 }
 }  // namespace
 
-extern "C" int smash_text_from_fasta(const char *path, uint8_t **text, uint64_t *N,
-                                     uint32_t *n_seq, uint64_t **startpos,
-                                     uint64_t **sizes, char ***names) {
+extern "C" int smash_text_from_fasta_layout(const char *path, int rcref, uint8_t **text,
+                                            uint64_t *N, uint32_t *n_seq, uint64_t **startpos,
+                                            uint64_t **sizes, char ***names) {
   if (!path || !text || !N || !n_seq || !startpos || !sizes || !names) {
     smash::set_error("smash_text_from_fasta: bad arguments");
     return SMASH_ERR_ARG;
@@ -79,16 +80,20 @@ extern "C" int smash_text_from_fasta(const char *path, uint8_t **text, uint64_t 
       if (length > 0) {
         const uint64_t this_start = sp.back();
         descr.push_back(meta);
-        seq.push_back('`');
-        sp.push_back(seq.size());
-        sz.push_back(length);
-        descr.push_back(meta);
-        sz.push_back(length);
-        for (uint64_t k = 0; k < length; ++k)
-          seq.push_back(comp(seq[this_start + length - 1 - k]));
-        if (!eof) {
+        if (rcref || !eof) {
           seq.push_back('`');
           sp.push_back(seq.size());
+        }
+        sz.push_back(length);
+        if (rcref) {
+          descr.push_back(meta);
+          sz.push_back(length);
+          for (uint64_t k = 0; k < length; ++k)
+            seq.push_back(comp(seq[this_start + length - 1 - k]));
+          if (!eof) {
+            seq.push_back('`');
+            sp.push_back(seq.size());
+          }
         }
         if (eof) break;
       }
@@ -128,6 +133,12 @@ extern "C" int smash_text_from_fasta(const char *path, uint8_t **text, uint64_t 
     (*names)[i] = strdup(descr[i].c_str());
   }
   return SMASH_OK;
+}
+
+extern "C" int smash_text_from_fasta(const char *path, uint8_t **text, uint64_t *N,
+                                     uint32_t *n_seq, uint64_t **startpos,
+                                     uint64_t **sizes, char ***names) {
+  return smash_text_from_fasta_layout(path, 1, text, N, n_seq, startpos, sizes, names);
 }
 
 extern "C" void smash_text_free(uint8_t *text, uint32_t n_seq, uint64_t *startpos,

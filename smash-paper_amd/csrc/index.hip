@@ -118,13 +118,13 @@ bool write_file(const std::string &path, const void *data, uint64_t n) {
 
 }  // namespace
 
-extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N,
-                                  uint32_t n_seq, const uint64_t *h_startpos,
-                                  const uint64_t *h_sizes,
-                                  const char *const *names, int device,
-                                  smash_index **out) {
+extern "C" int smash_index_create_layout(const uint8_t *h_text, uint64_t N,
+                                         uint32_t n_seq, const uint64_t *h_startpos,
+                                         const uint64_t *h_sizes,
+                                         const char *const *names, int rcref, int device,
+                                         smash_index **out) {
   if (!h_text || N < 2 || !h_startpos || !h_sizes || !out || n_seq == 0 ||
-      (n_seq & 1)) {
+      (rcref && (n_seq & 1))) {
     set_error("smash_index_create: bad arguments");
     return SMASH_ERR_ARG;
   }
@@ -141,6 +141,7 @@ extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N,
     ix->logN = uint64_t(std::ceil(std::log(double(N)) / std::log(2.0)));
     ix->idx_bytes = (N <= 0xFFFFFFFFull && !force_wide_index()) ? 4 : 8;
     ix->n_seq = n_seq;
+    ix->rcref = rcref != 0;
     ix->startpos.assign(h_startpos, h_startpos + n_seq);
     ix->sizes.assign(h_sizes, h_sizes + n_seq);
     if (names)
@@ -154,7 +155,7 @@ extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N,
     build_sa_isa(ix.get(), s);
     uint32_t *lcp = build_lcp32(ix.get(), s);
     finish_lcp(ix.get(), lcp, s);
-    build_map(ix.get(), lcp, s);
+    if (ix->rcref) build_map(ix.get(), lcp, s);   // -mappability requires -rcref (mummer.cpp:145)
     SMASH_HIPX(hipStreamSynchronize(s));
     dfree(lcp);
     build_aux(ix.get(), s);
@@ -171,16 +172,23 @@ extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N,
   return SMASH_OK;
 }
 
-extern "C" int smash_index_load(const char *fasta_path, int device,
-                                smash_index **out) {
+extern "C" int smash_index_create(const uint8_t *h_text, uint64_t N, uint32_t n_seq,
+                                  const uint64_t *h_startpos, const uint64_t *h_sizes,
+                                  const char *const *names, int device, smash_index **out) {
+  return smash_index_create_layout(h_text, N, n_seq, h_startpos, h_sizes, names, 1, device, out);
+}
+
+extern "C" int smash_index_load_layout(const char *fasta_path, int rcref, int device,
+                                       smash_index **out) {
   if (!fasta_path || !out) {
     set_error("smash_index_load: bad arguments");
     return SMASH_ERR_ARG;
   }
   const std::string dir = std::string(fasta_path) + ".bin/";
+  const std::string rc = rcref ? "rc1" : "rc0";   // fasta.cpp:98, longSA.cpp:103
   std::vector<uint8_t> refhdr, idxhdr;
-  if (!read_file(dir + "rc1.ref.bin", refhdr) || refhdr.size() < 24) {
-    set_error("cannot read " + dir + "rc1.ref.bin");
+  if (!read_file(dir + rc + ".ref.bin", refhdr) || refhdr.size() < 24) {
+    set_error("cannot read " + dir + rc + ".ref.bin");
     return SMASH_ERR_IO;
   }
   std::unique_ptr<smash_index, void (*)(smash_index *)> ix(new smash_index, free_index);
@@ -193,23 +201,25 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
     const uint64_t N = rd64(p);
     const uint64_t nd = rd64(p);
     for (uint64_t i = 0; i < nd; ++i) {
-      if (p + 24 > end) throw hip_failure{"truncated rc1.ref.bin"};
+      if (p + 24 > end) throw hip_failure{"truncated " + rc + ".ref.bin"};
       ix->startpos.push_back(rd64(p));
       ix->sizes.push_back(rd64(p));
       const uint64_t L = rd64(p);
-      if (p + L > end) throw hip_failure{"truncated rc1.ref.bin"};
+      if (p + L > end) throw hip_failure{"truncated " + rc + ".ref.bin"};
       ix->names.emplace_back(reinterpret_cast<const char *>(p), L);
       p += L;
     }
     ix->N = N;
     ix->n_seq = uint32_t(nd);
+    ix->rcref = rcref != 0;
+    if (!nd || (rcref && (nd & 1))) throw hip_failure{"bad contig table in " + rc + ".ref.bin"};
     ix->logN = uint64_t(std::ceil(std::log(double(N)) / std::log(2.0)));
-    // index flavour: rc1.i4 or rc1.i8 (longSA.cpp:101-107)
+    // index flavour: rc?.i4 or rc?.i8 (longSA.cpp:101-107)
     int W = 0;
     for (int w : {4, 8})
-      if (!W && exists(dir + "rc1.i" + std::to_string(w) + ".index.bin")) W = w;
-    if (!W) throw hip_failure{"no rc1.i{4,8}.index.bin under " + dir};
-    const std::string base = dir + "rc1.i" + std::to_string(W) + ".index";
+      if (!W && exists(dir + rc + ".i" + std::to_string(w) + ".index.bin")) W = w;
+    if (!W) throw hip_failure{"no " + rc + ".i{4,8}.index.bin under " + dir};
+    const std::string base = dir + rc + ".i" + std::to_string(W) + ".index";
     if (!read_file(base + ".bin", idxhdr) || idxhdr.size() < 48)
       throw hip_failure{"cannot read " + base + ".bin"};
     p = idxhdr.data();
@@ -224,8 +234,8 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
     hipStream_t s;
     SMASH_HIPX(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::vector<uint8_t> buf;
-    if (!read_file(dir + "rc1.ref.seq.bin", buf) || buf.size() != N)
-      throw hip_failure{"cannot read rc1.ref.seq.bin"};
+    if (!read_file(dir + rc + ".ref.seq.bin", buf) || buf.size() != N)
+      throw hip_failure{"cannot read " + rc + ".ref.seq.bin"};
     ix->d_text = dalloc<uint8_t>(N + 64);
     SMASH_HIPX(hipMemset(ix->d_text + N, 0, 64));
     SMASH_HIPX(hipMemcpy(ix->d_text, buf.data(), N, hipMemcpyHostToDevice));
@@ -265,7 +275,9 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
     upload_tables(ix.get(), s);
     uint64_t total = 0;
     for (uint32_t c = 0; c < ix->n_seq; c += 2) total += ix->sizes[c];
-    if (read_file(dir + "map.bin", buf) && buf.size() == 2 + 2 * total) {
+    if (!ix->rcref) {
+      // no map.bin for the forward-only layout (-mappability requires -rcref)
+    } else if (read_file(dir + "map.bin", buf) && buf.size() == 2 + 2 * total) {
       ix->map_bytes = buf.size();
       ix->d_map = dalloc<uint8_t>(buf.size());
       SMASH_HIPX(hipMemcpy(ix->d_map, buf.data(), buf.size(), hipMemcpyHostToDevice));
@@ -292,6 +304,10 @@ extern "C" int smash_index_load(const char *fasta_path, int device,
   return SMASH_OK;
 }
 
+extern "C" int smash_index_load(const char *fasta_path, int device, smash_index **out) {
+  return smash_index_load_layout(fasta_path, 1, device, out);
+}
+
 extern "C" int smash_index_save(const smash_index *ix, const char *fasta_path,
                                 uint64_t fasta_size) {
   if (!ix || !fasta_path) {
@@ -304,8 +320,9 @@ extern "C" int smash_index_save(const smash_index *ix, const char *fasta_path,
     mkdir(dir.c_str(), 0777);
     const uint64_t N = ix->N;
     // flavour mummer would run for this fasta (mummer.cpp:156-183)
-    const int W = (fasta_size * 2 > 0xFFFFFFFFull - 100000) ? 8 : 4;
-    if (W == 4 && ix->idx_bytes == 8) throw hip_failure{"index too large for rc1.i4"};
+    const std::string rc = ix->rcref ? "rc1" : "rc0";
+    const int W = (fasta_size * (ix->rcref ? 2 : 1) > 0xFFFFFFFFull - 100000) ? 8 : 4;
+    if (W == 4 && ix->idx_bytes == 8) throw hip_failure{"index too large for " + rc + ".i4"};
     std::vector<uint8_t> hdr;
     auto put64 = [&](uint64_t v) {
       const uint8_t *b = reinterpret_cast<const uint8_t *>(&v);
@@ -317,7 +334,8 @@ extern "C" int smash_index_save(const smash_index *ix, const char *fasta_path,
     put64(ix->n_seq);
     uint64_t maxd = 0;
     for (uint32_t i = 0; i < ix->n_seq; ++i) {
-      const std::string nm = i < ix->names.size() ? ix->names[i] : ("seq" + std::to_string(i / 2));
+      const std::string nm = i < ix->names.size() ? ix->names[i]
+                                                   : ("seq" + std::to_string(ix->rcref ? i / 2 : i));
       put64(ix->startpos[i]);
       put64(ix->sizes[i]);
       put64(nm.size());
@@ -325,11 +343,12 @@ extern "C" int smash_index_save(const smash_index *ix, const char *fasta_path,
       maxd = std::max<uint64_t>(maxd, nm.size());
     }
     put64(maxd);
-    if (!write_file(dir + "rc1.ref.bin", hdr.data(), hdr.size())) throw hip_failure{"write rc1.ref.bin"};
+    if (!write_file(dir + rc + ".ref.bin", hdr.data(), hdr.size()))
+      throw hip_failure{"write " + rc + ".ref.bin"};
     std::vector<uint8_t> buf(N);
     SMASH_HIPX(hipMemcpy(buf.data(), ix->d_text, N, hipMemcpyDeviceToHost));
-    if (!write_file(dir + "rc1.ref.seq.bin", buf.data(), N)) throw hip_failure{"write seq"};
-    const std::string base = dir + "rc1.i" + std::to_string(W) + ".index";
+    if (!write_file(dir + rc + ".ref.seq.bin", buf.data(), N)) throw hip_failure{"write seq"};
+    const std::string base = dir + rc + ".i" + std::to_string(W) + ".index";
     // SA / ISA
     for (int which = 0; which < 2; ++which) {
       std::vector<uint8_t> a(N * ix->idx_bytes);
@@ -357,9 +376,11 @@ extern "C" int smash_index_save(const smash_index *ix, const char *fasta_path,
     put64(N);
     put64(ix->n_ovf);
     if (!write_file(base + ".bin", hdr.data(), hdr.size())) throw hip_failure{"write index.bin"};
-    std::vector<uint8_t> m(ix->map_bytes);
-    SMASH_HIPX(hipMemcpy(m.data(), ix->d_map, m.size(), hipMemcpyDeviceToHost));
-    if (!write_file(dir + "map.bin", m.data(), m.size())) throw hip_failure{"write map.bin"};
+    if (ix->d_map) {
+      std::vector<uint8_t> m(ix->map_bytes);
+      SMASH_HIPX(hipMemcpy(m.data(), ix->d_map, m.size(), hipMemcpyDeviceToHost));
+      if (!write_file(dir + "map.bin", m.data(), m.size())) throw hip_failure{"write map.bin"};
+    }
   } catch (hip_failure &f) {
     set_error(f.what);
     return SMASH_ERR_IO;
@@ -378,6 +399,7 @@ extern "C" int smash_index_query(const smash_index *ix, smash_index_info *o) {
   o->logN = ix->logN;
   o->idx_bytes = ix->idx_bytes;
   o->n_seq = ix->n_seq;
+  o->rcref = ix->rcref ? 1 : 0;
   o->n_lcp_overflow = ix->n_ovf;
   o->map_bytes = ix->map_bytes;
   o->d_text = ix->d_text;

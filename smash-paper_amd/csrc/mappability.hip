@@ -548,6 +548,10 @@ extern "C" int smash_mappability_scan(const smash_index *ix, uint64_t begin, uin
     set_error("smash_mappability_scan: bad arguments");
     return SMASH_ERR_ARG;
   }
+  if (!ix->rcref) {   // mummer.cpp:145-146
+    set_error("smash_mappability_scan: -mappability requires -rcref");
+    return SMASH_ERR_ARG;
+  }
   uint64_t total = 0;
   for (uint32_t q = 0; q < ix->n_seq; q += 2) total += ix->sizes[q];
   if (end > total) {

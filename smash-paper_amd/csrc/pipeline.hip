@@ -1353,6 +1353,10 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     set_error("smash_pipeline_create: bad configuration");
     return SMASH_ERR_ARG;
   }
+  if (!ix->rcref) {   // the SMASH chain maps with -rcref (smash_mapping.sh:19)
+    set_error("smash_pipeline_create: the count chain needs the -rcref text layout");
+    return SMASH_ERR_ARG;
+  }
   if (!ix->d_map) {
     set_error("smash_pipeline_create: index has no map.bin");
     return SMASH_ERR_ARG;

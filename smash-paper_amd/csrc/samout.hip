@@ -31,9 +31,9 @@ __global__ __launch_bounds__(kSB) void k_sam_recs(
     uint64_t n_reads, const uint8_t *__restrict__ reads, uint64_t stride,
     const uint16_t *__restrict__ lens, uint32_t L0,
     const uint8_t *__restrict__ text, uint64_t N, const uint64_t *__restrict__ startpos,
-    const uint64_t *__restrict__ sizes, uint32_t n_seq, const uint32_t *__restrict__ tag_off,
-    const uint8_t *__restrict__ map, uint64_t map_bytes, const uint64_t *__restrict__ off,
-    smash_sam_rec *__restrict__ out) {
+    const uint64_t *__restrict__ sizes, uint32_t n_seq, int rcref,
+    const uint32_t *__restrict__ tag_off, const uint8_t *__restrict__ map, uint64_t map_bytes,
+    const uint64_t *__restrict__ off, smash_sam_rec *__restrict__ out) {
   const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t r = t / cap;
   const uint32_t k = uint32_t(t % cap);
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kSB) void k_sam_recs(
   int64_t pos = rcpos - int64_t(startpos[si]);
   const uint32_t extra = L - len - q;
   smash_sam_rec o;
-  if (si & 1) {   // rcref: odd sequences are reverse complements
+  if (rcref && (si & 1)) {   // rcref: odd sequences are reverse complements (query.cpp:80)
     si -= 1;
     pos = int64_t(sizes[si]) - pos - int64_t(L);
     o.prefix = uint16_t(extra);
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kSB) void k_sam_recs(
     o.rc = 0;
   }
   o.pos = pos;
-  o.tid = si >> 1;
+  o.tid = rcref ? si >> 1 : si;
   o.qpos = uint16_t(q);
   o.len = uint16_t(len);
   // XE of the diagonal: ref_pos = rcpos + j in [0, N) and text == query
@@ -281,8 +281,8 @@ static int sam_records(const smash_index *ix, const uint8_t *d_reads, uint64_t s
   const hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_sam_recs, dim3(unsigned((slots + kSB - 1) / kSB)), dim3(kSB), 0, s,
                      d_match, d_n_match, cap_per_read, n_reads, d_reads, stride, d_lens, len,
-                     ix->d_text, ix->N, ix->d_startpos, ix->d_sizes, ix->n_seq, d_tag_offsets,
-                     ix->d_map, ix->map_bytes, d_rec_off, d_out);
+                     ix->d_text, ix->N, ix->d_startpos, ix->d_sizes, ix->n_seq,
+                     ix->rcref ? 1 : 0, d_tag_offsets, ix->d_map, ix->map_bytes, d_rec_off, d_out);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }

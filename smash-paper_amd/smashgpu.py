@@ -56,6 +56,7 @@ EXPORTS = [
     "smash_pipeline_profile_intervals", "smash_fastq_read_parallel",
     "smash_fastq_index_open", "smash_fastq_index_pack", "smash_fastq_index_close",
     "smash_phase_map_ahead", "smash_sam_records_packed",
+    "smash_text_from_fasta_layout", "smash_index_create_layout", "smash_index_load_layout",
 ]
 
 
@@ -66,7 +67,8 @@ class IndexInfo(C.Structure):
                 ("d_isa", vp), ("d_lcp8", vp), ("d_lcp_ovf", vp), ("d_map", vp),
                 ("device_bytes", C.c_uint64), ("build_seconds", C.c_double),
                 ("kmer_k", C.c_uint32), ("d_uniq", vp), ("d_kmer", vp),
-                ("bitmap_b", C.c_uint32), ("d_bitmap", vp), ("in_text", C.c_uint64 * 4)]
+                ("bitmap_b", C.c_uint32), ("d_bitmap", vp), ("in_text", C.c_uint64 * 4),
+                ("rcref", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class PipelineCfg(C.Structure):
@@ -117,11 +119,18 @@ def lib():
     L.smash_text_from_fasta.argtypes = [C.c_char_p, C.POINTER(u8p), u64p, u32p,
                                         C.POINTER(u64p), C.POINTER(u64p),
                                         C.POINTER(C.POINTER(C.c_char_p))]
+    L.smash_text_from_fasta_layout.argtypes = [C.c_char_p, C.c_int, C.POINTER(u8p), u64p, u32p,
+                                               C.POINTER(u64p), C.POINTER(u64p),
+                                               C.POINTER(C.POINTER(C.c_char_p))]
     L.smash_text_free.argtypes = [u8p, C.c_uint32, u64p, u64p, C.POINTER(C.c_char_p)]
     L.smash_text_free.restype = None
     L.smash_index_create.argtypes = [u8p, C.c_uint64, C.c_uint32, u64p, u64p,
                                      C.POINTER(C.c_char_p), C.c_int, C.POINTER(vp)]
+    L.smash_index_create_layout.argtypes = [u8p, C.c_uint64, C.c_uint32, u64p, u64p,
+                                            C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                            C.POINTER(vp)]
     L.smash_index_load.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+    L.smash_index_load_layout.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(vp)]
     L.smash_index_save.argtypes = [vp, C.c_char_p, C.c_uint64]
     L.smash_index_free.argtypes = [vp]
     L.smash_index_free.restype = None
@@ -215,8 +224,9 @@ for _a, _b in zip(b"acgtrymkbdhvACGTRYMKBDHV", b"tgcayrkmvhdbTGCAYRKMVHDB"):
     _COMP[_a] = _b
 
 
-def text_from_fasta(path):
-    """Sequence::Sequence with -rcref (fasta.cpp:133-285), in the library."""
+def text_from_fasta(path, rcref=True):
+    """Sequence::Sequence (fasta.cpp:133-285), in the library: with -rcref
+    (default) or the forward-only layout of `mummer` without it."""
     L = lib()
     t = u8p()
     N = C.c_uint64()
@@ -224,8 +234,9 @@ def text_from_fasta(path):
     sp = u64p()
     sz = u64p()
     nm = C.POINTER(C.c_char_p)()
-    check(L.smash_text_from_fasta(path.encode(), C.byref(t), C.byref(N), C.byref(ns),
-                                  C.byref(sp), C.byref(sz), C.byref(nm)),
+    check(L.smash_text_from_fasta_layout(path.encode(), 1 if rcref else 0, C.byref(t),
+                                         C.byref(N), C.byref(ns), C.byref(sp), C.byref(sz),
+                                         C.byref(nm)),
           "smash_text_from_fasta")
     T = np.ctypeslib.as_array(t, shape=(N.value,)).copy()
     startpos = np.ctypeslib.as_array(sp, shape=(ns.value,)).copy()
@@ -274,39 +285,43 @@ class Index:
         self.h = vp(handle)
         self.info = IndexInfo()
         check(lib().smash_index_query(self.h, C.byref(self.info)), "smash_index_query")
+        self.rcref = bool(self.info.rcref)
         self.names = list(names)
         self.sizes = [int(x) for x in sizes]
-        self.contigs = [self.names[i] for i in range(0, len(self.names), 2)]
-        self.contig_sizes = self.sizes[0::2]
+        step = 2 if self.rcref else 1
+        self.contigs = [self.names[i] for i in range(0, len(self.names), step)]
+        self.contig_sizes = self.sizes[0::step]
 
     @classmethod
-    def create(cls, T, startpos, sizes, names, device=0):
+    def create(cls, T, startpos, sizes, names, device=0, rcref=True):
         T = np.ascontiguousarray(T, np.uint8)
         sp = np.ascontiguousarray(startpos, np.uint64)
         sz = np.ascontiguousarray(sizes, np.uint64)
         arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
         h = vp()
-        check(lib().smash_index_create(_p(T, u8p), len(T), len(sp), _p(sp, u64p),
-                                       _p(sz, u64p), arr, device, C.byref(h)),
+        check(lib().smash_index_create_layout(_p(T, u8p), len(T), len(sp), _p(sp, u64p),
+                                              _p(sz, u64p), arr, 1 if rcref else 0, device,
+                                              C.byref(h)),
               "smash_index_create")
         return cls(h.value, names, sz)
 
     @classmethod
-    def from_fasta(cls, path, device=0):
-        return cls.create(*text_from_fasta(path), device=device)
+    def from_fasta(cls, path, device=0, rcref=True):
+        return cls.create(*text_from_fasta(path, rcref), device=device, rcref=rcref)
 
     @classmethod
     def from_contigs(cls, contigs, device=0):
         return cls.create(*text_from_contigs(contigs), device=device)
 
     @classmethod
-    def load(cls, fasta_path, device=0):
+    def load(cls, fasta_path, device=0, rcref=True):
         """Load the reference's <fasta>.bin/ cache (longSA.cpp:100-136)."""
         h = vp()
-        check(lib().smash_index_load(fasta_path.encode(), device, C.byref(h)),
+        check(lib().smash_index_load_layout(fasta_path.encode(), 1 if rcref else 0, device,
+                                            C.byref(h)),
               "smash_index_load")
         names, sizes = [], []
-        with open(fasta_path + ".bin/rc1.ref.bin", "rb") as f:
+        with open(fasta_path + ".bin/rc%d.ref.bin" % (1 if rcref else 0), "rb") as f:
             b = f.read()
         n = int.from_bytes(b[16:24], "little")
         off = 24

@@ -231,3 +231,99 @@ def test_binning_varbin_line_as_written(tmp_path, s):
     st = open(tmp_path / "id.stats.txt").read().splitlines()[1].split("\t")
     g = open(gold("%s_varbin_stats_partial.txt" % s)).read().splitlines()[1].split("\t")
     assert st[:3] == g[:3]
+
+
+# ---------------------------------------------------------------------------
+# GPU: mummer without -rcref (the forward-only text, fasta.cpp:160-169),
+# pinned to tools/make_golden_r03.sh's reference output
+# ---------------------------------------------------------------------------
+def _chr1_fa(tmp_path, tiny_fa):
+    """tiny.fa up to its second '>' line (awk '/^>/{n++} n<2')."""
+    out, n = [], 0
+    for l in open(tiny_fa):
+        if l.startswith(">"):
+            n += 1
+        if n < 2:
+            out.append(l)
+    fa = str(tmp_path / "chr1.fa")
+    open(fa, "w").write("".join(out))
+    return fa
+
+
+@pytest.mark.gpu
+def test_mummer_without_rcref_writes_the_reference_rc0_cache(tmp_path, tiny_fa):
+    """`mummer tiny.fa dummy`: the rc0.* cache (text, contig table, SA, ISA,
+    LCP) built on the device equals the reference's byte for byte (lcp.m.bin
+    with its uninitialised padding masked); no map.bin (-mappability requires
+    -rcref); the cache loads back through smash_index_load_layout."""
+    import hashlib
+    fa = str(tmp_path / "tiny.fa")
+    shutil.copy(tiny_fa, fa)
+    r = subprocess.run([_tool("mummer"), fa, "dummy"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 1 and "unable to open dummy" in r.stderr, r.stderr
+    sums = {l.split()[0]: (l.split()[1], int(l.split()[2]))
+            for l in open(gold("tiny_index_rc0.sha256"))}
+    for name, (h, size) in sums.items():
+        if name.endswith(":masked") or name == "rc0.i4.index.lcp.m.bin":
+            continue
+        b = open(fa + ".bin/" + name, "rb").read()
+        assert (hashlib.sha256(b).hexdigest(), len(b)) == (h, size), name
+    m = np.fromfile(fa + ".bin/rc0.i4.index.lcp.m.bin", np.uint64).reshape(-1, 2).copy()
+    m[:, 1] &= 0xFFFFFFFF
+    assert hashlib.sha256(m.tobytes()).hexdigest() == sums["rc0.i4.index.lcp.m.bin:masked"][0]
+    assert not os.path.exists(fa + ".bin/map.bin")
+    assert not os.path.exists(fa + ".bin/rc1.ref.bin")
+    import smashgpu as S
+    ix = S.Index.load(fa, rcref=False)
+    assert not ix.rcref and ix.info.map_bytes == 0 and ix.contigs == S.Index.from_fasta(
+        fa, rcref=False).contigs
+    with pytest.raises(S.SmashError, match="-mappability requires -rcref"):
+        S.check(S.lib().smash_mappability_scan(ix.h, 0, 10, 36, None, None, None, 0, None, None,
+                                               None), "smash_mappability_scan")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,args,golden,n", [
+    ("sam", ["-qthreads", "2", "-nomap", "-samin", "-samout"], "s150_chr1_mapout_fwd_full", None),
+    ("sam", ["-qthreads", "2", "-maxmatch", "-nomap", "-samin", "-samout"],
+     "s100_60_chr1_mapout_MEM_fwd_full", 60),
+    ("sam", ["-qthreads", "2", "-mum", "-samin", "-samout"],
+     "s100_300_chr1_mapout_MUM_fwd_full", 300),
+])
+def test_mummer_without_rcref_modes(tmp_path, tiny_fa, kind, args, golden, n):
+    """MAM / MEM / MUM on the forward-only text of one contig: the reference's
+    own -samout lines (forward hits only, every record's XS '+'), full lines,
+    and its header (one @SQ per contig, fasta.cpp:247)."""
+    import golden_queries
+    fa = _chr1_fa(tmp_path, tiny_fa)
+    src = gold(("s150" if golden.startswith("s150") else "s100") + "_fastqs_to_sam.sam.gz")
+    q = str(tmp_path / ("q." + kind))
+    golden_queries.write(src, kind, q, n)
+    r = subprocess.run([_tool("mummer")] + args + [fa, q], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert _body(str(tmp_path / "mapout")) == sorted(read_gz_lines(golden + ".txt.gz"))
+    hdr = sorted(open(gold("tiny_chr1_fwd_mapout_header.txt")).read().splitlines())
+    for f in os.listdir(tmp_path / "mapout"):
+        lines = open(tmp_path / "mapout" / f).read().splitlines()
+        assert sorted(l for l in lines if l.startswith("@")) == hdr
+
+
+@pytest.mark.gpu
+def test_mummer_without_rcref_samout_on_every_second_contig_fails_as_the_reference(
+        tmp_path, tiny_fa):
+    """The reference's absolute-position map steps over the contigs by 2
+    without -rcref too (query.cpp:547-551), so a -samout line on chr2 / chrM
+    ends its run: the worker thread prints "map::at" and exits 1
+    (query.cpp:522-535).  Recorded in tests/golden/tiny_fwd_samout_error.txt."""
+    fa = str(tmp_path / "tiny.fa")
+    shutil.copy(tiny_fa, fa)
+    q = str(tmp_path / "s150.sam")
+    with open(q, "wb") as f:
+        f.write(gzip.open(gold("s150_fastqs_to_sam.sam.gz")).read())
+    r = subprocess.run([_tool("mummer"), "-qthreads", "2", "-nomap", "-samin", "-samout", fa, q],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    want = open(gold("tiny_fwd_samout_error.txt")).read().splitlines()
+    assert want[0] == "exit 1"
+    assert r.returncode == 1 and r.stderr.splitlines() == want[1:], r.stderr

@@ -58,3 +58,58 @@ def test_fasta_edge_cases(tmp_path):
         b = O.text_from_fasta(str(p))
         assert a[0].tobytes() == b[0].tobytes(), c
         assert list(a[1]) == list(b[1]) and list(a[2]) == list(b[2]) and a[3] == b[3]
+
+
+def _ref_bin_image(fasta_size, T, sp, sz, names):
+    """rc?.ref.bin as Sequence::Sequence writes it (fasta.cpp:265-277)."""
+    b = bytearray()
+    for v in (fasta_size, len(T), len(sp)):
+        b += int(v).to_bytes(8, "little")
+    for s, z, n in zip(sp, sz, names):
+        b += int(s).to_bytes(8, "little") + int(z).to_bytes(8, "little")
+        b += len(n).to_bytes(8, "little") + n.encode()
+    b += max(len(n) for n in names).to_bytes(8, "little")
+    return bytes(b)
+
+
+def test_text_from_fasta_forward_layout_matches_reference(tiny_fa):
+    """`mummer` without -rcref (fasta.cpp:160-169): c1 ` c2 ` ... cn $, one
+    entry per contig; the text and the whole rc0.ref.bin (sizes, start
+    positions, names) equal the reference's own (tests/golden/
+    tiny_index_rc0.sha256, tools/make_golden_r03.sh)."""
+    sums = {l.split()[0]: l.split()[1] for l in open(gold("tiny_index_rc0.sha256"))}
+    T, sp, sz, names = S.text_from_fasta(tiny_fa, rcref=False)
+    assert hashlib.sha256(T.tobytes()).hexdigest() == sums["rc0.ref.seq.bin"]
+    img = _ref_bin_image(os.path.getsize(tiny_fa), T, sp, sz, names)
+    assert hashlib.sha256(img).hexdigest() == sums["rc0.ref.bin"]
+    # and the -rcref layout's image of rc1.ref.bin
+    T1, sp1, sz1, n1 = S.text_from_fasta(tiny_fa)
+    sums1 = {l.split()[0]: l.split()[1] for l in open(gold("tiny_index.sha256"))}
+    if "rc1.ref.bin" in sums1:
+        img1 = _ref_bin_image(os.path.getsize(tiny_fa), T1, sp1, sz1, n1)
+        assert hashlib.sha256(img1).hexdigest() == sums1["rc1.ref.bin"]
+
+
+def test_fasta_forward_layout_edge_cases(tmp_path):
+    """The forward-only text is the -rcref text's forward contigs joined by
+    '`' (no separator after the last one), on the edge-case files above; a
+    last line without a newline is read with eof set and its bytes after the
+    first land in the text with no contig entry (fasta.cpp:195-240), in
+    both layouts."""
+    cases = [b">a x\nACGT\n\nacgN\n>b\nTTTT\n",
+             b">a\n  AC GT  \n>b\nGG\n",
+             b">a\nACGT\n>b\nGG",
+             b">only\nRYKMBDHVN\n",
+             b">a\nAC\n>b\nGG\n>c\nT\n"]
+    for i, c in enumerate(cases):
+        p = tmp_path / ("f%d.fa" % i)
+        p.write_bytes(c)
+        T1, sp1, sz1, n1 = S.text_from_fasta(str(p))
+        T0, sp0, sz0, n0 = S.text_from_fasta(str(p), rcref=False)
+        fw = [T1[int(sp1[k]):int(sp1[k] + sz1[k])].tobytes() for k in range(0, len(sp1), 2)]
+        end = int(sp1[-1] + sz1[-1])
+        tail = T1[end + 1:-1].tobytes()
+        want = b"`".join(fw) + (b"`" + tail if tail else b"") + b"$"
+        assert T0.tobytes() == want, c
+        assert n0 == n1[0::2] and list(sz0) == list(sz1[0::2])
+        assert list(sp0) == [sum(len(f) + 1 for f in fw[:k]) for k in range(len(fw))]
