@@ -242,9 +242,9 @@ __global__ __launch_bounds__(256) void k_prep_direct(const uint8_t *__restrict__
                                                      uint32_t len0, uint32_t n, uint32_t ga,
                                                      uint64_t it0, uint64_t it1, uint64_t it2,
                                                      uint64_t it3, Geom g,
-                                                     uint32_t *__restrict__ rec) {
+                                                     uint32_t *__restrict__ rec, uint32_t prio) {
 #ifndef SM_DMA_ROW_HOST
-  __builtin_amdgcn_s_setprio(2);   // beside the search (pipeline.hip SMASH_BESIDE_SEARCH)
+  if (prio) __builtin_amdgcn_s_setprio(2);   // beside the search (pipeline.hip SMASH_BESIDE_SEARCH)
 #endif
   const uint32_t item = blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= n * ga) return;

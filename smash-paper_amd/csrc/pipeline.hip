@@ -40,7 +40,12 @@ constexpr uint32_t kStatStride = 16, kStatStripes = 16, kStatWords = kStatStride
 // equal priority the SIMD's oldest-first issue leaves them a trickle and
 // they finish only when the search drains.  Raised priority lets them
 // through; the search absorbs their (small) share of the memory system.
-#define SMASH_BESIDE_SEARCH() __builtin_amdgcn_s_setprio(2)
+// (SMASH_PRIO=0 at pipeline creation leaves them at the default priority: A/B)
+__constant__ uint32_t g_beside_prio = 1;
+#define SMASH_BESIDE_SEARCH()                          \
+  do {                                                 \
+    if (g_beside_prio) __builtin_amdgcn_s_setprio(2);  \
+  } while (0)
 
 struct smash_pipeline {
   const smash_index *ix = nullptr;
@@ -75,6 +80,14 @@ struct smash_pipeline {
   hipEvent_t ev_in = nullptr, ev_found[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
   hipEvent_t ev_done = nullptr;   // recorded once at creation: "inputs already complete"
   bool set_used[2] = {false, false};
+  // schedule (A/B, read at creation): SMASH_GATE_PREP=1 the next search's
+  // k_prep also waits for ev_free; SMASH_GATE_POST=1 ev_free is recorded
+  // after the batch's whole post stage (single-GPU count path), not after
+  // k_post; SMASH_ONE_SEARCH=1 a search waits for the other set's (never
+  // two k_mam_sm at once)
+  bool gate_prep = false, gate_post = false, one_search = false;
+  bool found_rec[2] = {false, false};
+  bool defer_free = false;        // count_batch_ev under gate_post
   // a search already issued into a set (smash_phase_map_ahead): its reads
   const uint8_t *pref_reads[2] = {nullptr, nullptr};
   uint64_t pref_n[2] = {0, 0};
@@ -1487,6 +1500,14 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       p->fused_bin = !(e && e[0] == '0');
       const char *l = getenv("SMASH_BIN_LDS");
       p->bin_lds = l && l[0] == '1';
+      auto on = [](const char *v) { const char *x = getenv(v); return x && x[0] == '1'; };
+      p->gate_prep = on("SMASH_GATE_PREP");
+      p->gate_post = on("SMASH_GATE_POST");
+      p->one_search = on("SMASH_ONE_SEARCH");
+      const char *pr = getenv("SMASH_PRIO");
+      const uint32_t prio = pr && pr[0] == '0' ? 0u : 1u;
+      SMASH_HIPX(hipMemcpyToSymbol(HIP_SYMBOL(g_beside_prio), &prio, 4));
+      smash::set_prep_prio(prio);
     }
     // the positions arrays (2 x 8 B x every hit slot: 26 GB at 6.25 M
     // pairs) only for the two-kernel path; the fused path writes them when
@@ -1590,6 +1611,8 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
                        hipEvent_t in_ev) {
   hipStream_t xs = p->xs[k];
   SMASH_HIP(hipStreamWaitEvent(xs, in_ev, 0));
+  if (p->one_search && p->found_rec[k ^ 1]) SMASH_HIP(hipStreamWaitEvent(xs, p->ev_found[k ^ 1], 0));
+  if (p->gate_prep && p->set_used[k]) SMASH_HIP(hipStreamWaitEvent(xs, p->ev_free[k], 0));
   // the set's records were last read by its previous search, earlier on xs;
   // its match buffers by that batch's post stage: k_prep runs now, the
   // search after ev_free (SearchWs::gate)
@@ -1605,7 +1628,7 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
   const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k],
-                    p->set_used[k] ? p->ev_free[k] : nullptr};
+                    p->set_used[k] && !p->gate_prep ? p->ev_free[k] : nullptr};
   const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
                                 p->read_len, 2 * n_pairs, p->d_match_s[k], p->slots,
                                 p->d_nmatch_s[k], xs, false, &ws);   // probe check at stats time
@@ -1616,6 +1639,7 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
     p->prof_reads += 2 * n_pairs;
   }
   SMASH_HIP(hipEventRecord(p->ev_found[k], xs));
+  p->found_rec[k] = true;
   p->pref_reads[k] = d_reads;
   p->pref_n[k] = n_pairs;
   p->searched[k] = true;
@@ -1675,7 +1699,8 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
                                       p->d_stats, p->d_post_ws);
   }
   SMASH_HIP(hipGetLastError());
-  SMASH_HIP(hipEventRecord(p->ev_free[k], s));   // the set's matches are read
+  if (!p->defer_free)
+    SMASH_HIP(hipEventRecord(p->ev_free[k], s));   // the set's matches are read
   p->set_used[k] = true;
   p->cnt_ready = false;
   return SMASH_OK;
@@ -1816,11 +1841,15 @@ namespace smash {
 // one batch, its search after in_ev (null: after everything on s so far)
 int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                    uint64_t *d_counts, hipStream_t s, hipEvent_t in_ev) {
+  p->defer_free = p->gate_post;
   int rc = phase_map_impl(p, d_reads, n_pairs, s, in_ev);
+  p->defer_free = false;
   if (rc) return rc;
   if ((rc = dedup_local(p, s))) return rc;
   if ((rc = smash_phase_positions(p, nullptr, s))) return rc;
-  return smash_phase_bin(p, nullptr, d_counts, s);
+  if ((rc = smash_phase_bin(p, nullptr, d_counts, s))) return rc;
+  if (p->gate_post && n_pairs) SMASH_HIP(hipEventRecord(p->ev_free[p->set], s));
+  return SMASH_OK;
 }
 }  // namespace smash
 

@@ -153,7 +153,7 @@ static int prep_records(const uint8_t *reads, uint64_t stride, const uint16_t *l
       blockIdx.x = unsigned(i / 256);
       threadIdx.x = unsigned(i % 256);
       sm::k_prep_direct(reads, stride, lens, L, uint32_t(n), ga, in_text[0], in_text[1], in_text[2],
-                        in_text[3], g, rec);
+                        in_text[3], g, rec, 0u);
     }
   } else {
     const uint32_t per = sm::prep_per_block(g, stride);

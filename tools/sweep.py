@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0,
                     help="run the --pairs as count_batches of this many pairs (the bench's "
                          "C3 step: --pairs 25000000 --batch 6250000)")
+    ap.add_argument("--resident", action="store_true",
+                    help="count_batches(resident=True) as bench.py's C3 step")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     import tempfile
@@ -56,7 +58,8 @@ def main():
         env = {} if setting == "base" else dict(kv.split("=", 1) for kv in setting.split(","))
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        fresh = ("SMASH_POST", "SMASH_BIN", "SMASH_FUSED", "SMASH_KEY")   # read at create
+        fresh = ("SMASH_POST", "SMASH_BIN", "SMASH_FUSED", "SMASH_KEY", "SMASH_GATE",
+                 "SMASH_ONE", "SMASH_PRIO")   # read at create
         if any(k.startswith(fresh) for k in env) or pipe is None:
             pipe = None                      # read at create: a fresh pipeline
             pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
@@ -64,7 +67,7 @@ def main():
         def run():
             pipe.reset(); counts.zero_()
             if a.batch:
-                pipe.count_batches(d_reads, P, B, counts)
+                pipe.count_batches(d_reads, P, B, counts, resident=a.resident)
             else:
                 pipe.count_batch(d_reads, P, counts)
         run()   # warm-up
