@@ -189,8 +189,11 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   }
   if (!ws) rec = ix->d_rec;
   const uint32_t ga = sm::prep_groups(lens ? 255 : len);
+  // k_prep (LDS-staged, the default: profiles/r03/sched) or, with
+  // SMASH_PREP_LDS=0, k_prep_direct (no LDS: it fits beside a running search
+  // but moves ~2x the bytes)
   const char *pl = std::getenv("SMASH_PREP_LDS");
-  if ((pl && pl[0] == '1') || n_reads * ga >= (1ull << 32)) {   // (A/B; huge launches)
+  if (!(pl && pl[0] == '0') || n_reads * ga >= (1ull << 32)) {
     const uint32_t per = sm::prep_per_block(g, stride);
     const size_t plds = sm::prep_lds_bytes(g, stride, per);
     sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
@@ -198,7 +201,6 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
         ix->in_text[3], g, per, rec);
     SMASH_HIP(hipGetLastError());
   } else if (n_reads) {
-    // no LDS: runs beside the search of the previous batch (k_prep_direct)
     const uint64_t items = n_reads * ga;
     sm::k_prep_direct<<<unsigned((items + 255) / 256), 256, 0, s>>>(
         seqs, stride, lens, len, uint32_t(n_reads), ga, ix->in_text[0], ix->in_text[1],

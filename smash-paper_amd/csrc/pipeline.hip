@@ -80,11 +80,14 @@ struct smash_pipeline {
   hipEvent_t ev_in = nullptr, ev_found[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
   hipEvent_t ev_done = nullptr;   // recorded once at creation: "inputs already complete"
   bool set_used[2] = {false, false};
-  // schedule (A/B, read at creation): SMASH_GATE_PREP=1 the next search's
-  // k_prep also waits for ev_free; SMASH_GATE_POST=1 ev_free is recorded
-  // after the batch's whole post stage (single-GPU count path), not after
-  // k_post; SMASH_ONE_SEARCH=1 a search waits for the other set's (never
-  // two k_mam_sm at once)
+  // schedule (read at creation; A/B): SMASH_GATE_POST (default 1) ev_free
+  // is recorded after the batch's whole post stage (single-GPU count path),
+  // so a set's next search starts once that batch is binned: the post stage
+  // of batch b shares the GPU with search b + 1 only, never with b + 2's
+  // (=0: after k_post, the set's match buffers' last reader);
+  // SMASH_GATE_PREP=1 the next search's k_prep also waits for ev_free;
+  // SMASH_ONE_SEARCH=1 a search waits for the other set's (never two
+  // k_mam_sm at once)
   bool gate_prep = false, gate_post = false, one_search = false;
   bool found_rec[2] = {false, false};
   bool defer_free = false;        // count_batch_ev under gate_post
@@ -1500,10 +1503,13 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       p->fused_bin = !(e && e[0] == '0');
       const char *l = getenv("SMASH_BIN_LDS");
       p->bin_lds = l && l[0] == '1';
-      auto on = [](const char *v) { const char *x = getenv(v); return x && x[0] == '1'; };
-      p->gate_prep = on("SMASH_GATE_PREP");
-      p->gate_post = on("SMASH_GATE_POST");
-      p->one_search = on("SMASH_ONE_SEARCH");
+      auto on = [](const char *v, bool dflt) {
+        const char *x = getenv(v);
+        return x && x[0] ? x[0] == '1' : dflt;
+      };
+      p->gate_prep = on("SMASH_GATE_PREP", false);
+      p->gate_post = on("SMASH_GATE_POST", true);   // profiles/r03/sched: 150.9 vs 160.1 ms
+      p->one_search = on("SMASH_ONE_SEARCH", false);
       const char *pr = getenv("SMASH_PRIO");
       const uint32_t prio = pr && pr[0] == '0' ? 0u : 1u;
       SMASH_HIPX(hipMemcpyToSymbol(HIP_SYMBOL(g_beside_prio), &prio, 4));

@@ -72,12 +72,24 @@ def test_count_batches_equals_batch_by_batch(gix, batch):
     assert out[0] == out[1]
 
 
+SCHEDULES = {"default": {},
+             # round 3's first form: ev_free after k_post, k_prep_direct
+             "post_gate_kpost": {"SMASH_GATE_POST": "0", "SMASH_PREP_LDS": "0"},
+             "one_search": {"SMASH_ONE_SEARCH": "1", "SMASH_PRIO": "0"},
+             "gate_prep": {"SMASH_GATE_PREP": "1"}}
+
+
+@pytest.mark.parametrize("sched", sorted(SCHEDULES))
 @pytest.mark.parametrize("batch", [97, 2000])
-def test_resident_runs_back_to_back(gix, batch):
+def test_resident_runs_back_to_back(gix, batch, sched, monkeypatch):
     """smash_count_batches_ready (no input event: the searches of a run start
     under the post stage of the run queued before it), three runs queued
     with no synchronisation, each after a reset and a zeroing of its own
-    counts: every run's counts == one run of smash_count_batches."""
+    counts: every run's counts == one run of smash_count_batches, under
+    each stream schedule (SMASH_GATE_POST / _PREP, SMASH_ONE_SEARCH,
+    SMASH_PREP_LDS, SMASH_PRIO: read at pipeline creation / per launch)."""
+    for k, v in SCHEDULES[sched].items():
+        monkeypatch.setenv(k, v)
     reads = interleaved_reads("s150")
     n = reads.shape[0] // 2
     _, starts = load_bins(gold("tiny_bins.txt"))

@@ -3,7 +3,8 @@
 # (tools/sweep.py, resident reads, 4 x 6.25 M-pair batches per run; every
 # setting must give the base's counts), then FETCH_SIZE / WRITE_SIZE and the
 # SQ issue counters of the post-stage kernels (rocprofv3 serialises the
-# dispatches of a --pmc pass: isolated per-kernel figures).
+# dispatches of a --pmc pass: isolated per-kernel figures; PMC=1).
+# SETTINGS overrides the sweep's settings.
 set -euo pipefail
 TAG=${1:?tag}
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -11,9 +12,9 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 python3 -u "$R/tools/sweep.py" --pairs 25000000 --batch 6250000 --steps 5 --resident \
-    base SMASH_PRIO=0 SMASH_GATE_PREP=1 SMASH_PREP_LDS=1 SMASH_GATE_PREP=1,SMASH_PREP_LDS=1 \
-    SMASH_ONE_SEARCH=1 SMASH_GATE_POST=1 SMASH_GATE_POST=1,SMASH_PREP_LDS=1 base \
+    ${SETTINGS:-base SMASH_GATE_POST=0,SMASH_PREP_LDS=0 SMASH_PRIO=0 SMASH_ONE_SEARCH=1 SMASH_BIN_LDS=1 SMASH_ONE_SEARCH=1,SMASH_PRIO=0 base} \
     > "$O/sweep.log" 2>&1
+[ "${PMC:-0}" = "1" ] || exit 0
 POST='k_post_fast|k_dedup|k_emit_bin|k_prep|k_scan|k_post'
 for C in FETCH_SIZE WRITE_SIZE; do   # one TCC counter per pass (3 + 2 > 4 TCC slots)
   timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex "$POST" \
