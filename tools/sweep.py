@@ -59,7 +59,7 @@ def main():
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         fresh = ("SMASH_POST", "SMASH_BIN", "SMASH_FUSED", "SMASH_KEY", "SMASH_GATE",
-                 "SMASH_ONE", "SMASH_PRIO")   # read at create
+                 "SMASH_ONE", "SMASH_PRIO", "SMASH_PREP_ALL")   # read at create
         if any(k.startswith(fresh) for k in env) or pipe is None:
             pipe = None                      # read at create: a fresh pipeline
             pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
