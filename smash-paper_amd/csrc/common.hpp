@@ -148,15 +148,7 @@ struct SearchWs {
   // buffers' previous reader, so the records of the next batch are built
   // while that reader still runs
   hipEvent_t gate = nullptr;
-  // the records are already in rec (built for the whole run by
-  // smash_count_batches' SMASH_PREP_ALL=1): no k_prep
-  bool prepared = false;
 };
-// the read records of n reads (k_prep16 / k_prep / k_prep_direct per
-// SMASH_PREP), into rec (n * record bytes), on s
-int prep_records(const smash_index *ix, const uint8_t *seqs, uint64_t stride,
-                 const uint16_t *lens, uint32_t len, uint64_t n_reads, void *rec, hipStream_t s);
-uint64_t record_bytes(uint32_t max_len);   // per read
 int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
                    uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,
                    uint64_t *d_out, uint32_t cap_per_read, uint32_t *d_n_out, void *stream,

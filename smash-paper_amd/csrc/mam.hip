@@ -164,51 +164,6 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   return SMASH_OK;
 }
 
-}  // namespace
-
-uint64_t record_bytes(uint32_t max_len) { return uint64_t(sm::make_geom(max_len).chunks) * 16; }
-
-// SMASH_PREP: "lds" k_prep (LDS-staged rows, the default), "direct"
-// k_prep_direct (one thread per 32-base group), "16" k_prep16 (one thread per
-// 16-byte record chunk, LDS-free, whole-line stores); SMASH_PREP_LDS=1 / 0
-// (round 3's first knob) = lds / direct
-int prep_records(const smash_index *ix, const uint8_t *seqs, uint64_t stride,
-                 const uint16_t *lens, uint32_t len, uint64_t n_reads, void *rec_v,
-                 hipStream_t s) {
-  if (!n_reads) return SMASH_OK;
-  const sm::Geom g = sm::make_geom(lens ? 255 : len);
-  uint32_t *rec = static_cast<uint32_t *>(rec_v);
-  const uint32_t ga = sm::prep_groups(lens ? 255 : len);
-  int kind = 0;
-  if (const char *e = std::getenv("SMASH_PREP"))
-    kind = std::strcmp(e, "direct") == 0 ? 1 : std::strcmp(e, "16") == 0 ? 2 : 0;
-  else if (const char *pl = std::getenv("SMASH_PREP_LDS"))
-    kind = pl[0] == '0' ? 1 : 0;
-  if (kind == 1 && n_reads * ga >= (1ull << 32)) kind = 0;
-  if (kind == 2 && (n_reads * g.chunks + 255) / 256 >= (1ull << 31)) kind = 0;
-  if (kind == 0) {
-    const uint32_t per = sm::prep_per_block(g, stride);
-    const size_t plds = sm::prep_lds_bytes(g, stride, per);
-    sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
-        seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
-        ix->in_text[3], g, per, rec);
-  } else if (kind == 1) {
-    const uint64_t items = n_reads * ga;
-    sm::k_prep_direct<<<unsigned((items + 255) / 256), 256, 0, s>>>(
-        seqs, stride, lens, len, uint32_t(n_reads), ga, ix->in_text[0], ix->in_text[1],
-        ix->in_text[2], ix->in_text[3], g, rec, g_prep_prio);
-  } else {
-    const uint64_t items = n_reads * g.chunks;
-    sm::k_prep16<<<unsigned((items + 255) / 256), 256, 0, s>>>(
-        seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
-        ix->in_text[3], g, reinterpret_cast<uint4 *>(rec), g_prep_prio);
-  }
-  SMASH_HIP(hipGetLastError());
-  return SMASH_OK;
-}
-
-namespace {
-
 template <class IdxT>
 int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
               uint64_t stride, const uint16_t *lens, uint32_t len,
@@ -233,9 +188,24 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
     ix->rec_bytes = bytes;
   }
   if (!ws) rec = ix->d_rec;
-  if (!(ws && ws->prepared)) {
-    const int rc = prep_records(ix, seqs, stride, lens, len, n_reads, rec, s);
-    if (rc) return rc;
+  const uint32_t ga = sm::prep_groups(lens ? 255 : len);
+  // k_prep (LDS-staged, the default: profiles/r03/sched) or, with
+  // SMASH_PREP_LDS=0, k_prep_direct (no LDS: it fits beside a running search
+  // but moves ~2x the bytes)
+  const char *pl = std::getenv("SMASH_PREP_LDS");
+  if (!(pl && pl[0] == '0') || n_reads * ga >= (1ull << 32)) {
+    const uint32_t per = sm::prep_per_block(g, stride);
+    const size_t plds = sm::prep_lds_bytes(g, stride, per);
+    sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
+        seqs, stride, lens, len, n_reads, ix->in_text[0], ix->in_text[1], ix->in_text[2],
+        ix->in_text[3], g, per, rec);
+    SMASH_HIP(hipGetLastError());
+  } else if (n_reads) {
+    const uint64_t items = n_reads * ga;
+    sm::k_prep_direct<<<unsigned((items + 255) / 256), 256, 0, s>>>(
+        seqs, stride, lens, len, uint32_t(n_reads), ga, ix->in_text[0], ix->in_text[1],
+        ix->in_text[2], ix->in_text[3], g, rec, g_prep_prio);
+    SMASH_HIP(hipGetLastError());
   }
   if (ws && ws->gate) SMASH_HIP(hipStreamWaitEvent(s, ws->gate, 0));
   sm::Ctx<IdxT> c;

@@ -310,86 +310,6 @@ __global__ __launch_bounds__(256) void k_prep_direct(const uint8_t *__restrict__
 // groups per read of k_prep_direct
 inline uint32_t prep_groups(uint32_t max_len) { return (max_len + 31) / 32; }
 
-// The same records, one thread per 16-byte record chunk (no LDS, no
-// partial-line stores): chunk j < c_bad of read r is the bad-mask words of
-// bases [128 j, 128 j + 128), chunk j >= c_bad the read's bytes
-// [16 (j - c_bad), + 16) with the bytes at or past L zeroed; each thread
-// writes its chunk with one 16-byte store, so a wave writes 1 KB of
-// consecutive records.  Reads are loaded 16 bytes at a time at their exact
-// (unaligned) address; a load that would cross the input's end (the last
-// read's last chunk) is done byte by byte.  items = n * g.chunks.
-__device__ __forceinline__ uint4 prep_bytes16(const uint8_t *rd, uint32_t off, uint32_t L,
-                                              const uint8_t *end) {
-  if (off >= L) return make_uint4(0, 0, 0, 0);
-  const uint8_t *p = rd + off;
-  uint32_t w[4];
-  if (p + 16 <= end) {
-    const uint4 v = load16u(reinterpret_cast<uint64_t>(p));
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-  } else {
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      uint32_t x = 0;
-#pragma unroll
-      for (uint32_t b = 0; b < 4; ++b)
-        if (p + 4 * k + b < end) x |= uint32_t(p[4 * k + b]) << (8 * b);
-      w[k] = x;
-    }
-  }
-  const uint32_t live = L - off;   // bytes of this chunk inside the read (>= 1)
-#pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t lo = 4 * k;
-    const uint32_t keep = live >= lo + 4 ? 0xFFFFFFFFu : live <= lo ? 0u : (1u << (8 * (live - lo))) - 1u;
-    w[k] &= keep;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-__global__ __launch_bounds__(256) void k_prep16(const uint8_t *__restrict__ seqs, uint64_t stride,
-                                                const uint16_t *__restrict__ lens, uint32_t len0,
-                                                uint64_t n, uint64_t it0, uint64_t it1,
-                                                uint64_t it2, uint64_t it3, Geom g,
-                                                uint4 *__restrict__ rec, uint32_t prio) {
-#ifndef SM_DMA_ROW_HOST
-  if (prio) __builtin_amdgcn_s_setprio(2);   // beside the search (pipeline.hip SMASH_BESIDE_SEARCH)
-#endif
-  const uint64_t item = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (item >= n * g.chunks) return;
-  const uint64_t r = item / g.chunks;
-  const uint32_t j = uint32_t(item - r * g.chunks);
-  const uint32_t L = lens ? lens[r] : len0;
-  const uint8_t *rd = seqs + r * stride;
-  const uint8_t *end = seqs + n * stride;
-  if (j >= g.c_bad) {
-    rec[item] = prep_bytes16(rd, 16 * (j - g.c_bad), L, end);
-    return;
-  }
-  auto itx = [&](uint32_t b) {
-    const uint64_t w = b < 64 ? it0 : b < 128 ? it1 : b < 192 ? it2 : it3;
-    return uint32_t((w >> (b & 63)) & 1ull);
-  };
-  const uint32_t ia = itx('a'), ic = itx('c'), ig = itx('g'), iu = itx('t');
-  uint32_t m[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t off = 128 * j + 16 * k;
-    if (off >= L) break;
-    const uint4 v = prep_bytes16(rd, off, L, end);
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-    uint32_t bits = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) {
-      const uint32_t b = (wv[i >> 2] >> (8 * (i & 3))) & 0xFF;
-      const uint32_t good = (b == 'a' ? ia : 0u) | (b == 'c' ? ic : 0u) | (b == 'g' ? ig : 0u) |
-                            (b == 't' ? iu : 0u);
-      bits |= uint32_t(off + i < L && !good) << i;
-    }
-    m[k >> 1] |= bits << (16 * (k & 1));
-  }
-  rec[item] = make_uint4(m[0], m[1], m[2], m[3]);
-}
-
 // lane states: S_COPY and above own a pending 16-byte probe at `addr`.
 // S_BYTE and above probe byte arrays (text, U, L8) at the exact byte
 // address (the block holds bytes [addr, addr + 16)); the states below

@@ -89,14 +89,6 @@ struct smash_pipeline {
   // SMASH_ONE_SEARCH=1 a search waits for the other set's (never two
   // k_mam_sm at once)
   bool gate_prep = false, gate_post = false, one_search = false;
-  // SMASH_PREP_ALL=1: smash_count_batches builds every batch's read records
-  // with one launch at the start of the run (rec_all, grown on first use)
-  // instead of one k_prep per batch between the searches
-  bool prep_all = false;
-  uint8_t *d_rec_all = nullptr;
-  uint64_t rec_all_bytes = 0;
-  hipEvent_t ev_prep = nullptr;
-  const uint8_t *run_rec = nullptr;   // records of the current batch (prep_all)
   bool found_rec[2] = {false, false};
   bool defer_free = false;        // count_batch_ev under gate_post
   // a search already issued into a set (smash_phase_map_ahead): its reads
@@ -1518,7 +1510,6 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       p->gate_prep = on("SMASH_GATE_PREP", false);
       p->gate_post = on("SMASH_GATE_POST", true);   // profiles/r03/sched: 150.9 vs 160.1 ms
       p->one_search = on("SMASH_ONE_SEARCH", false);
-      p->prep_all = on("SMASH_PREP_ALL", false);
       const char *pr = getenv("SMASH_PRIO");
       const uint32_t prio = pr && pr[0] == '0' ? 0u : 1u;
       SMASH_HIPX(hipMemcpyToSymbol(HIP_SYMBOL(g_beside_prio), &prio, 4));
@@ -1591,8 +1582,6 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
       (void)hipStreamSynchronize(p->xs[k]);
       (void)hipStreamDestroy(p->xs[k]);
     }
-    if (k == 0 && p->ev_prep) (void)hipEventDestroy(p->ev_prep);
-    if (k == 0 && p->d_rec_all) (void)hipFree(p->d_rec_all);
     if (p->ev_found[k]) (void)hipEventDestroy(p->ev_found[k]);
     if (p->ev_free[k]) (void)hipEventDestroy(p->ev_free[k]);
     for (void *q : {(void *)p->d_match_s[k], (void *)p->d_nmatch_s[k], (void *)p->d_rec_s[k],
@@ -1644,14 +1633,8 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
     p->ix->kev[0] = p->ev[2 * p->n_ev];          // recorded around k_mam_sm itself
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
-  SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k],
-              p->set_used[k] && !p->gate_prep ? p->ev_free[k] : nullptr};
-  if (p->run_rec) {   // built for the whole run (count_batches_impl)
-    ws.rec = const_cast<uint8_t *>(p->run_rec);
-    ws.rec_bytes = 2 * n_pairs * record_bytes(p->read_len);
-    ws.prepared = true;
-    SMASH_HIP(hipStreamWaitEvent(xs, p->ev_prep, 0));
-  }
+  const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k],
+                    p->set_used[k] && !p->gate_prep ? p->ev_free[k] : nullptr};
   const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
                                 p->read_len, 2 * n_pairs, p->d_match_s[k], p->slots,
                                 p->d_nmatch_s[k], xs, false, &ws);   // probe check at stats time
@@ -1904,37 +1887,10 @@ static int count_batches_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_
     rc = hipEventRecord(in_ev, s) == hipSuccess ? SMASH_OK : SMASH_ERR_HIP;
   }
   const uint64_t L2 = 2 * uint64_t(p->read_len);
-  const uint64_t rb = record_bytes(p->read_len);
-  const bool all = p->prep_all && rc == SMASH_OK && n_pairs > batch_pairs;
-  if (all) {
-    // every batch's records in one launch, on the stream of the run's first
-    // search, after the reads' input event
-    const uint64_t need = 2 * n_pairs * rb;
-    if (need > p->rec_all_bytes) {
-      SMASH_HIP(hipDeviceSynchronize());
-      if (p->d_rec_all) (void)hipFree(p->d_rec_all);
-      p->d_rec_all = nullptr;
-      p->rec_all_bytes = 0;
-      SMASH_HIP(hipMalloc(&p->d_rec_all, need));
-      p->rec_all_bytes = need;
-    }
-    if (!p->ev_prep) SMASH_HIP(hipEventCreateWithFlags(&p->ev_prep, hipEventDisableTiming));
-    const int k0 = p->set ^ 1;
-    hipStream_t xs = p->xs[k0];
-    SMASH_HIP(hipStreamWaitEvent(xs, in_ev, 0));
-    // the previous run's searches read rec_all until their end: those on xs
-    // are ordered before this launch, the other stream's last one is waited
-    if (p->found_rec[k0 ^ 1]) SMASH_HIP(hipStreamWaitEvent(xs, p->ev_found[k0 ^ 1], 0));
-    rc = prep_records(p->ix, d_reads, p->read_len, nullptr, p->read_len, 2 * n_pairs,
-                      p->d_rec_all, xs);
-    if (rc == SMASH_OK) SMASH_HIP(hipEventRecord(p->ev_prep, xs));
-  }
   for (uint64_t b0 = 0; rc == SMASH_OK && b0 < n_pairs; b0 += batch_pairs) {
     const uint64_t n = std::min(batch_pairs, n_pairs - b0);
-    p->run_rec = all ? p->d_rec_all + 2 * b0 * rb : nullptr;
     rc = smash::count_batch_ev(p, d_reads + b0 * L2, n, d_counts, s, in_ev);
   }
-  p->run_rec = nullptr;
   if (own) (void)hipEventDestroy(in_ev);   // released once the waits on it have completed
   return rc;
 }

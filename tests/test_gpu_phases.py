@@ -76,13 +76,7 @@ SCHEDULES = {"default": {},
              # round 3's first form: ev_free after k_post, k_prep_direct
              "post_gate_kpost": {"SMASH_GATE_POST": "0", "SMASH_PREP_LDS": "0"},
              "one_search": {"SMASH_ONE_SEARCH": "1", "SMASH_PRIO": "0"},
-             "gate_prep": {"SMASH_GATE_PREP": "1"},
-             "prep16": {"SMASH_PREP": "16"},
-             # every batch's records in one launch per run, the runs queued
-             # back to back (a run's record build must wait for the previous
-             # run's last search)
-             "prep_all16": {"SMASH_PREP_ALL": "1", "SMASH_PREP": "16"},
-             "prep_all_lds": {"SMASH_PREP_ALL": "1", "SMASH_PREP": "lds"}}
+             "gate_prep": {"SMASH_GATE_PREP": "1"}}
 
 
 @pytest.mark.parametrize("sched", sorted(SCHEDULES))
@@ -92,9 +86,8 @@ def test_resident_runs_back_to_back(gix, batch, sched, monkeypatch):
     under the post stage of the run queued before it), three runs queued
     with no synchronisation, each after a reset and a zeroing of its own
     counts: every run's counts == one run of smash_count_batches, under
-    each stream schedule and record builder (SMASH_GATE_POST / _PREP,
-    SMASH_ONE_SEARCH, SMASH_PREP_ALL, SMASH_PRIO: read at pipeline creation;
-    SMASH_PREP / SMASH_PREP_LDS: per launch)."""
+    each stream schedule (SMASH_GATE_POST / _PREP, SMASH_ONE_SEARCH,
+    SMASH_PREP_LDS, SMASH_PRIO: read at pipeline creation / per launch)."""
     for k, v in SCHEDULES[sched].items():
         monkeypatch.setenv(k, v)
     reads = interleaved_reads("s150")

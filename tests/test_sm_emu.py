@@ -135,15 +135,3 @@ def test_prep_direct_equals_lds(L, stride, var):
     assert not (a[:w] == 0xDEADBEEF).any()
     bad = np.nonzero(a[:w] != b[:w])[0]
     assert bad.size == 0, (bad[:8] // rc, bad[:8] % rc, a[bad[:8]], b[bad[:8]])
-    # k_prep16 (one thread per 16-byte chunk, the pipeline's default): the
-    # input copied to an exact-size buffer, so a load past its end would
-    # read outside it
-    exact = np.ascontiguousarray(buf.copy())
-    c = np.zeros(n * g_chunks_max, np.uint32)
-    rc2 = sm_emu.lib().sm_emu_prep16(
-        exact.ctypes.data_as(C.c_void_p), C.c_uint64(stride),
-        lens.ctypes.data_as(C.c_void_p) if var else None, C.c_uint32(L), C.c_uint64(n),
-        it.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p))
-    assert rc2 == rc
-    bad = np.nonzero(a[:w] != c[:w])[0]
-    assert bad.size == 0, (bad[:8] // rc, bad[:8] % rc, a[bad[:8]], c[bad[:8]])

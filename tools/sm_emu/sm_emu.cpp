@@ -144,17 +144,8 @@ using namespace smash;
 // default (mam.hip) does
 static int prep_records(const uint8_t *reads, uint64_t stride, const uint16_t *lens, uint32_t L,
                         uint64_t n, const uint64_t *in_text, const sm::Geom &g, uint32_t *rec,
-                        int direct) {
-  if (direct == 2) {   // k_prep16
-    blockDim.x = 256;
-    const uint64_t items = n * g.chunks;
-    for (uint64_t i = 0; i < items; ++i) {
-      blockIdx.x = unsigned(i / 256);
-      threadIdx.x = unsigned(i % 256);
-      sm::k_prep16(reads, stride, lens, L, n, in_text[0], in_text[1], in_text[2], in_text[3], g,
-                   reinterpret_cast<uint4 *>(rec), 0u);
-    }
-  } else if (direct) {
+                        bool direct) {
+  if (direct) {
     blockDim.x = 256;
     const uint32_t ga = sm::prep_groups(lens ? 255 : L);
     const uint64_t items = n * ga;
@@ -189,18 +180,8 @@ extern "C" int sm_emu_prep(const uint8_t *reads, uint64_t stride, const uint16_t
   const sm::Geom g = sm::make_geom(lens ? 255 : L);
   const uint64_t words = n * g.chunks * 4;
   for (uint64_t i = 0; i < words; ++i) out_lds[i] = out_direct[i] = 0xDEADBEEFu;   // all written?
-  if (prep_records(reads, stride, lens, L, n, in_text, g, out_lds, 0)) return -1;
-  if (prep_records(reads, stride, lens, L, n, in_text, g, out_direct, 1)) return -1;
-  return int(g.chunks * 4);
-}
-
-// k_prep16's records of the same reads into out (every word poisoned first)
-extern "C" int sm_emu_prep16(const uint8_t *reads, uint64_t stride, const uint16_t *lens,
-                             uint32_t L, uint64_t n, const uint64_t *in_text, uint32_t *out) {
-  const sm::Geom g = sm::make_geom(lens ? 255 : L);
-  const uint64_t words = n * g.chunks * 4;
-  for (uint64_t i = 0; i < words; ++i) out[i] = 0xDEADBEEFu;
-  if (prep_records(reads, stride, lens, L, n, in_text, g, out, 2)) return -1;
+  if (prep_records(reads, stride, lens, L, n, in_text, g, out_lds, false)) return -1;
+  if (prep_records(reads, stride, lens, L, n, in_text, g, out_direct, true)) return -1;
   return int(g.chunks * 4);
 }
 
