@@ -429,7 +429,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # SMASH_BENCH_SHARDED=1 (under torchrun, any world size): the multi-GPU
+    # step (dist.ShardedCounter, collectives over RCCL) even at world 1 --
+    # the per-rank rate of the N > 1 path, measurable on one GPU
+    sharded = world > 1 or os.environ.get("SMASH_BENCH_SHARDED", "0") == "1"
+    if sharded:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -464,7 +468,7 @@ def main():
     counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
     nb = (P + B - 1) // B
 
-    if world > 1:
+    if sharded:
         from dist import ShardedCounter
         # the per-batch key counts are host integers: exchanged over gloo
         # they need no device synchronisation
@@ -477,7 +481,7 @@ def main():
         state (a new smashMEM.py + varbin.py invocation), carried across
         the batches"""
         counts.zero_()
-        if world == 1:
+        if not sharded:
             pipe.reset()
             # the batches in order; each batch's search starts under the
             # previous one's tail, and (the reads are resident: no input
@@ -544,7 +548,7 @@ def main():
                    "bins": int(len(starts)),
                    "parallelism": "dp%d: pair shards, all_to_all key de-dup, "
                                   "all_gather tails, all_reduce counts" % world
-                   if world > 1 else "single GPU",
+                   if sharded else "single GPU",
                    "index_build_s": round(dix.info.build_seconds, 2),
                    "index_hbm_gb": round(dix.info.device_bytes / 1e9, 2)},
     }
@@ -668,7 +672,7 @@ def main():
     out["stats_last_step"] = st.as_dict()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 
