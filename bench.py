@@ -475,6 +475,7 @@ def main():
         sc = ShardedCounter(pipe, rank, world, dev, count_group=dist.new_group(backend="gloo"))
 
     resident = os.environ.get("SMASH_BENCH_RESIDENT", "1") != "0"   # (A/B)
+    ahead2 = os.environ.get("SMASH_BENCH_AHEAD2", "1") != "0"       # (A/B, sharded step)
 
     def step(i):
         """one run over the rank's P pairs: a fresh key set / adjacent-dup
@@ -493,8 +494,13 @@ def main():
             for b in range(nb):
                 b0, b1 = b * B, min(P, (b + 1) * B)
                 n0, n1 = b1, min(P, b1 + B)   # the next batch, searched under this one's exchange
+                m0, m1 = n1, min(P, n1 + B)   # and the one after, once this one's export is done
+                if not ahead2:
+                    m1 = m0
                 sc.step(d_reads[2 * b0:2 * b1], b1 - b0, b0 * world, counts,
-                        d_reads[2 * n0:2 * n1] if n1 > n0 else None, n1 - n0)
+                        d_reads[2 * n0:2 * n1] if n1 > n0 else None, n1 - n0,
+                        next2_reads=d_reads[2 * m0:2 * m1] if m1 > m0 else None,
+                        next2_pairs=m1 - m0)
             dist.all_reduce(counts)
 
     for i in range(args.warmup):

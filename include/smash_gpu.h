@@ -281,6 +281,14 @@ int smash_phase_map(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
  * smash_pipeline_reset drops a look-ahead that was not consumed. */
 int smash_phase_map_ahead(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                           const uint8_t *d_next, uint64_t n_next, void *stream);
+/* After smash_phase_export of batch b: the search of batch b + 2 (d_reads,
+ * n_pairs) issued into the search set batch b used, whose matches b's post
+ * stage has read by then; with batch b + 1's search (smash_phase_map_ahead)
+ * already running, the device has two searches queued while the caller
+ * exchanges batch b's keys.  Batch b + 2's smash_phase_map[_ahead] with the
+ * same (pointer, n_pairs) uses it; same lifetime rule as d_next above. */
+int smash_phase_search_ahead(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
+                             void *stream);
 int smash_phase_export(smash_pipeline *p, int world, uint64_t global_base,
                        int64_t *h_send_counts, int64_t *h_send_words,
                        const uint64_t **d_send, const uint64_t **d_send_words,

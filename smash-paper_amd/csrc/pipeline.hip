@@ -1680,7 +1680,10 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
   }
   if (!have && (rc = search_into(p, k, d_reads, n_pairs, in_ev))) return rc;
   p->searched[k] = false;   // consumed by this batch
-  if (d_next && n_next && (rc = search_into(p, k ^ 1, d_next, n_next, in_ev))) return rc;
+  const bool next_have = p->searched[k ^ 1] && p->pref_reads[k ^ 1] == d_next &&
+                         p->pref_n[k ^ 1] == n_next;   // (smash_phase_search_ahead)
+  if (d_next && n_next && !next_have && (rc = search_into(p, k ^ 1, d_next, n_next, in_ev)))
+    return rc;
   SMASH_HIP(hipStreamWaitEvent(s, p->ev_found[k], 0));
   if (p->post_fast) {
     // mates of <= 8 matches (most pairs) in 8-word networks, <= 16 in
@@ -1739,6 +1742,27 @@ extern "C" int smash_phase_map_ahead(smash_pipeline *p, const uint8_t *d_reads,
                                      void *stream) {
   return phase_map_impl(p, d_reads, n_pairs, static_cast<hipStream_t>(stream), nullptr, d_next,
                         n_next);
+}
+
+// the search of the batch after the next one, into the set the current
+// batch used: its post stage has read that set's matches once
+// smash_phase_export has returned (the host synchronisation there), so the
+// search is gated on nothing the caller still waits for; the next-but-one
+// smash_phase_map[_ahead] with the same reads uses it
+extern "C" int smash_phase_search_ahead(smash_pipeline *p, const uint8_t *d_reads,
+                                        uint64_t n_pairs, void *stream) {
+  int rc = check_pipe(p, n_pairs);
+  if (rc) return rc;
+  if (!n_pairs) return SMASH_OK;
+  const int k = p->set;   // the set of the batch smash_phase_map last took
+  if (p->searched[k]) {
+    set_error("smash_phase_search_ahead: the set still holds an unconsumed search");
+    return SMASH_ERR_ARG;
+  }
+  SMASH_HIP(hipSetDevice(p->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SMASH_HIP(hipEventRecord(p->ev_in, s));   // the reads are ready after the caller's work
+  return search_into(p, k, d_reads, n_pairs, p->ev_in);
 }
 
 // 1 .. 2^24 - 1, never 0 (an unpublished slot)

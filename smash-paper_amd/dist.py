@@ -59,13 +59,17 @@ class ShardedCounter:
         return [x[0] for x in rcl], [x[1] for x in rcl]
 
     def step(self, d_reads, n_pairs, step_base, d_counts, next_reads=None, next_pairs=0,
-             stride=None):
+             stride=None, next2_reads=None, next2_pairs=0):
         """One batch: this rank's n_pairs pairs start at global index
         step_base + rank * stride (stride: the nominal batch of every rank,
         default n_pairs; a short last step keeps the (step, rank, pair)
         order with the nominal stride).  next_reads / next_pairs: the rank's
         next batch, whose search the pipeline starts now, so it runs under
-        this batch's exchanges."""
+        this batch's exchanges; next2_reads / next2_pairs (with next_*): the
+        batch after it, searched as soon as this batch's export has returned
+        (its set is free then), so the device holds a queued search while
+        the host exchanges this batch's keys.  Every batch must stay
+        allocated and unmodified until its own step."""
         dev, W, r = self.device, self.world, self.rank
         p = self.pipe
         if next_pairs:
@@ -74,6 +78,8 @@ class ShardedCounter:
             p.phase_map(d_reads, n_pairs)
         hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * (n_pairs if stride is None
                                                                      else stride))
+        if next_pairs and next2_pairs:
+            p.phase_search_ahead(next2_reads, next2_pairs)
         rcv, rcw = self._recv_counts(cnt, wcnt)
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
         n_recv, n_words = sum(rcv), sum(rcw)

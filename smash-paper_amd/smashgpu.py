@@ -57,6 +57,7 @@ EXPORTS = [
     "smash_fastq_index_open", "smash_fastq_index_pack", "smash_fastq_index_close",
     "smash_phase_map_ahead", "smash_sam_records_packed",
     "smash_text_from_fasta_layout", "smash_index_create_layout", "smash_index_load_layout",
+    "smash_phase_search_ahead",
 ]
 
 
@@ -146,6 +147,7 @@ def lib():
     L.smash_count_batches.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp]
     L.smash_count_batches_ready.argtypes = [vp, vp, C.c_uint64, C.c_uint64, vp, vp, vp]
     L.smash_phase_map_ahead.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp]
+    L.smash_phase_search_ahead.argtypes = [vp, vp, C.c_uint64, vp]
     L.smash_pipeline_profile_active.argtypes = [vp, C.POINTER(C.c_double)]
     L.smash_pipeline_profile_intervals.argtypes = [vp, C.POINTER(C.c_double), C.c_uint64, u64p]
     L.smash_phase_map.argtypes = [vp, vp, C.c_uint64, vp]
@@ -456,6 +458,12 @@ class Pipeline:
         check(lib().smash_phase_map_ahead(self.h, _ptr(d_reads), n_pairs,
                                           _ptr(d_next) if n_next else None, n_next,
                                           vp(_stream(stream))), "smash_phase_map_ahead")
+
+    def phase_search_ahead(self, d_reads, n_pairs, stream=None):
+        """after phase_export of batch b: batch b + 2's search into the set
+        b used (smash_phase_search_ahead)."""
+        check(lib().smash_phase_search_ahead(self.h, _ptr(d_reads), n_pairs,
+                                             vp(_stream(stream))), "smash_phase_search_ahead")
 
     def phase_export(self, world, global_base, stream=None):
         """(headers [n, 5] int64, words [w] int64, per-owner key counts,

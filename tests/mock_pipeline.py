@@ -63,6 +63,9 @@ class OraclePhasePipeline:
     def phase_map_ahead(self, d_reads, n_pairs, d_next, n_next):
         self.phase_map(d_reads, n_pairs)   # (no streams: the look-ahead is a no-op)
 
+    def phase_search_ahead(self, d_reads, n_pairs):
+        pass                               # (likewise)
+
     def phase_export(self, world, gbase):
         """smash_phase_export's layout: per owner, 5-word headers {hi, lo,
         global index, nk, word offset in the owner segment} and the keys'

@@ -21,10 +21,12 @@ def _prev(tails, carried):
     return ShardedCounter._prev(tails, carried)
 
 
-def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False, capacity=None):
+def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False, capacity=None,
+                 ahead2=False):
     """reads: [2n, L] mates (numpy or a device tensor), n = W * per_rank *
     steps pairs in global order.  ahead: each rank's next batch is searched
-    by smash_phase_map_ahead.  capacity: each rank's key-set capacity; an
+    by smash_phase_map_ahead; ahead2 (with ahead): and the batch after it by
+    smash_phase_search_ahead right after the export.  capacity: each rank's key-set capacity; an
     owner holds every key whose hash it owns over the whole run, ~n/W of the
     pairs, and up to all of them when SMASH_KEY_HASH_BITS cuts the hash to
     a few values.  Default: n.  Returns (summed counts, summed stats)."""
@@ -36,25 +38,28 @@ def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False, capacit
         p.reset()
     counts = [torch.zeros(len(starts), dtype=torch.int64, device=dev) for _ in range(W)]
     carried = torch.full((1,), -1, dtype=torch.int64, device=dev)
-    keep_alive, prev_next = [], [None] * W
+    batches = {}   # (rank, step) -> its reads on the device, kept alive for the run
+
+    def batch(r, s):
+        if (r, s) not in batches:
+            lo = s * W * per_rank + r * per_rank
+            batches[(r, s)] = _rows(reads, 2 * lo, 2 * (lo + per_rank), dev)
+        return batches[(r, s)]
+
     for s in range(steps):
         base = s * W * per_rank
         sends = []
         for r in range(W):
-            lo = base + r * per_rank
-            d = _rows(reads, 2 * lo, 2 * (lo + per_rank), dev)
             # ahead: this batch was searched by the previous step's look-ahead
-            cur = prev_next[r] if (ahead and s > 0) else d
+            cur = batch(r, s)
             if ahead and s + 1 < steps:
                 # the rank's next batch searched now, on the other search stream
-                nlo = lo + W * per_rank
-                nxt = _rows(reads, 2 * nlo, 2 * (nlo + per_rank), dev)
-                keep_alive.append(nxt)
-                pipes[r].phase_map_ahead(cur, per_rank, nxt, per_rank)
-                prev_next[r] = nxt
+                pipes[r].phase_map_ahead(cur, per_rank, batch(r, s + 1), per_rank)
             else:
                 pipes[r].phase_map(cur, per_rank)
             hdr, words, cnt, wcnt = pipes[r].phase_export(W, base + r * per_rank)
+            if ahead and ahead2 and s + 2 < steps:
+                pipes[r].phase_search_ahead(batch(r, s + 2), per_rank)
             # copies: the export buffers are the pipeline's own
             sends.append((hdr.clone(), words.clone(), [int(c) for c in cnt],
                           [int(c) for c in wcnt]))

@@ -52,7 +52,11 @@ def _worker(rank, world, port, per_rank, steps, out_q):
         if s + 1 < steps and s % 2 == 0:   # the look-ahead form (next batch's search issued now)
             nlo = lo + world * per_rank
             nxt = torch.from_numpy(reads[2 * nlo:2 * (nlo + per_rank)].copy())
-            sc.step(d_reads, per_rank, base, counts, nxt, per_rank)
+            n2lo = nlo + world * per_rank   # and the one after (smash_phase_search_ahead)
+            nxt2 = (torch.from_numpy(reads[2 * n2lo:2 * (n2lo + per_rank)].copy())
+                    if s + 2 < steps else None)
+            sc.step(d_reads, per_rank, base, counts, nxt, per_rank,
+                    next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
         else:
             sc.step(d_reads, per_rank, base, counts)
     dist.all_reduce(counts)

@@ -298,10 +298,14 @@ def c4_run(hg19, hg19_oracle):
     return dix, cs, starts, d_reads, single, orc
 
 
-@pytest.mark.parametrize("W,per_rank,steps,bits", [(8, 10_000, 3, 0), (3, 20_000, 4, 0),
-                                                   (8, 10_000, 3, 18)])
-def test_c4_sharded_equals_single_and_oracle(c4_run, W, per_rank, steps, bits, monkeypatch):
-    """W ranks (look-ahead search on, as dist.ShardedCounter runs it) over
+@pytest.mark.parametrize("W,per_rank,steps,bits,ahead2", [(8, 10_000, 3, 0, True),
+                                                          (3, 20_000, 4, 0, True),
+                                                          (3, 20_000, 4, 0, False),
+                                                          (8, 10_000, 3, 18, True)])
+def test_c4_sharded_equals_single_and_oracle(c4_run, W, per_rank, steps, bits, ahead2,
+                                             monkeypatch):
+    """W ranks (look-ahead search on, as dist.ShardedCounter runs it: the
+    next batch with this one, ahead2: the one after right after the export) over
     the same 240 k pairs dealt in (step, rank, pair) order: counts and
     stats equal one pipeline's and the oracle's (smashMEM.py:217-228
     first-wins across ranks, varbin.py:56-58 across shard boundaries).
@@ -312,7 +316,8 @@ def test_c4_sharded_equals_single_and_oracle(c4_run, W, per_rank, steps, bits, m
     assert W * per_rank * steps == C4_PAIRS
     if bits:
         monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
-    total, st = run_emulated(dix, d_reads, W, per_rank, steps, starts, cs, ahead=True)
+    total, st = run_emulated(dix, d_reads, W, per_rank, steps, starts, cs, ahead=True,
+                             ahead2=ahead2)
     assert orc[1][3] > 100          # duplicate pairs across ranks and steps occur
     assert np.array_equal(total, orc[0]) and st == orc[1]
     assert np.array_equal(single[0], orc[0]) and single[1] == orc[1]

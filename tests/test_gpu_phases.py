@@ -27,10 +27,14 @@ from phase_emu import run_emulated  # noqa: E402
                                                          (4, 250, 1, 0, False),
                                                          (3, 200, 2, 3, False),
                                                          (3, 111, 3, 0, True),
-                                                         (2, 300, 3, 2, True)])
+                                                         (2, 300, 3, 2, True),
+                                                         (3, 111, 4, 0, 2),
+                                                         (2, 300, 4, 2, 2)])
 def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, ahead, monkeypatch):
     """bits > 0: the key hash cut to `bits` bits, so owners see colliding
-    keys and must compare the exchanged key words."""
+    keys and must compare the exchanged key words.  ahead: the next batch's
+    search issued with this one's (smash_phase_map_ahead); 2: and the batch
+    after it right after this one's export (smash_phase_search_ahead)."""
     if bits:
         monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
     reads = interleaved_reads("s100")
@@ -42,7 +46,8 @@ def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, ahead, monk
     c1 = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
     one.count_batch(torch.from_numpy(np.ascontiguousarray(reads[:2 * n])).cuda(), n, c1)
     s1 = one.stats()
-    total, st = run_emulated(gix, reads, W, per_rank, steps, starts, cs, ahead)
+    total, st = run_emulated(gix, reads, W, per_rank, steps, starts, cs, bool(ahead),
+                             ahead2=ahead == 2)
     assert total.tolist() == c1.cpu().numpy().astype(np.uint64).tolist()
     assert st == (s1.positions, s1.dups, s1.kept, s1.dupe_pairs)
 
