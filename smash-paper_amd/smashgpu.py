@@ -414,7 +414,8 @@ class Pipeline:
 
     def count_batch(self, d_reads, n_pairs, d_counts, stream=None):
         """d_reads: device uint8 [2*n_pairs, read_len] (torch tensor or ptr)."""
-        check(lib().smash_count_batch(self.h, _ptr(d_reads), n_pairs, _ptr(d_counts),
+        check(lib().smash_count_batch(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+                                      _ptr(d_counts),
                                       vp(_stream(stream))), "smash_count_batch")
 
     def count_fastq(self, r1_paths, r2_paths, d_counts, sort_names=True, threads=0,
@@ -440,29 +441,33 @@ class Pipeline:
         searches need not wait for the work queued on the stream before this
         call -- consecutive runs over the same reads overlap."""
         if resident:
-            check(lib().smash_count_batches_ready(self.h, _ptr(d_reads), n_pairs, batch_pairs,
+            check(lib().smash_count_batches_ready(self.h, _reads(d_reads, n_pairs, self.read_len),
+                                                  n_pairs, batch_pairs,
                                                   _ptr(d_counts), vp(_stream(stream)), None),
                   "smash_count_batches_ready")
             return
-        check(lib().smash_count_batches(self.h, _ptr(d_reads), n_pairs, batch_pairs,
+        check(lib().smash_count_batches(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+                                        batch_pairs,
                                         _ptr(d_counts), vp(_stream(stream))),
               "smash_count_batches")
 
     def phase_map(self, d_reads, n_pairs, stream=None):
-        check(lib().smash_phase_map(self.h, _ptr(d_reads), n_pairs, vp(_stream(stream))),
+        check(lib().smash_phase_map(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+                                    vp(_stream(stream))),
               "smash_phase_map")
 
     def phase_map_ahead(self, d_reads, n_pairs, d_next, n_next, stream=None):
         """phase_map, and the next batch's search issued at once on the
         pipeline's other search stream (smash_phase_map_ahead)."""
-        check(lib().smash_phase_map_ahead(self.h, _ptr(d_reads), n_pairs,
-                                          _ptr(d_next) if n_next else None, n_next,
+        check(lib().smash_phase_map_ahead(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+                                          _reads(d_next, n_next, self.read_len) if n_next else None,
+                                          n_next,
                                           vp(_stream(stream))), "smash_phase_map_ahead")
 
     def phase_search_ahead(self, d_reads, n_pairs, stream=None):
         """after phase_export of batch b: batch b + 2's search into the set
         b used (smash_phase_search_ahead)."""
-        check(lib().smash_phase_search_ahead(self.h, _ptr(d_reads), n_pairs,
+        check(lib().smash_phase_search_ahead(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
                                              vp(_stream(stream))), "smash_phase_search_ahead")
 
     def phase_export(self, world, global_base, stream=None):
@@ -572,6 +577,19 @@ class Pipeline:
                 self.h = None
         except Exception:
             pass
+
+
+def _reads(x, n_pairs, read_len):
+    """the pointer of a batch of n_pairs pairs: a torch tensor must hold
+    2 * n_pairs * read_len bytes (the kernels read that many; a short tensor
+    would be an out-of-bounds device read), a raw pointer is the caller's
+    responsibility"""
+    if x is not None and not isinstance(x, int) and n_pairs:
+        have = x.numel() * x.element_size()
+        if have < 2 * n_pairs * read_len:
+            raise SmashError("reads tensor holds %d bytes, %d pairs x %d bp need %d"
+                             % (have, n_pairs, read_len, 2 * n_pairs * read_len))
+    return _ptr(x)
 
 
 def _ptr(x):

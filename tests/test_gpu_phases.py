@@ -29,7 +29,7 @@ from phase_emu import run_emulated  # noqa: E402
                                                          (3, 111, 3, 0, True),
                                                          (2, 300, 3, 2, True),
                                                          (3, 111, 4, 0, 2),
-                                                         (2, 300, 4, 2, 2)])
+                                                         (2, 250, 4, 2, 2)])
 def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, ahead, monkeypatch):
     """bits > 0: the key hash cut to `bits` bits, so owners see colliding
     keys and must compare the exchanged key words.  ahead: the next batch's
@@ -39,6 +39,7 @@ def test_phases_equal_single_pipeline(gix, W, per_rank, steps, bits, ahead, monk
         monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
     reads = interleaved_reads("s100")
     n = W * per_rank * steps
+    assert 2 * n <= reads.shape[0], "the case needs more pairs than s100 holds"
     _, starts = load_bins(gold("tiny_bins.txt"))
     cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
     one = S.Pipeline(gix, cs, starts, reads.shape[1], n)
