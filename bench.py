@@ -521,6 +521,9 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t1
+    if sharded and sc.timing:
+        log("sharded step phases (s, synchronised): %s"
+            % ", ".join("%s %.3f" % kv for kv in sc.timing.items()))
     mam_ms, launches, mam_reads = pipe.profile_read()
     active_ms = pipe.profile_active()
     launch_iv = pipe.profile_intervals()

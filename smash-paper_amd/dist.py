@@ -22,8 +22,16 @@ oracle-backed stand-in).
 """
 from __future__ import annotations
 
+import os
+import time
+
 import torch
 import torch.distributed as dist
+
+# SMASH_DIST_TIMING=1: wall time per phase of ShardedCounter.step, each phase
+# closed by a device synchronisation (diagnostic only: it removes the
+# overlap the step otherwise has); ShardedCounter.timing holds the sums
+_TIMING = os.environ.get("SMASH_DIST_TIMING", "0") == "1"
 
 
 class ShardedCounter:
@@ -39,6 +47,18 @@ class ShardedCounter:
         self.count_group = count_group
         self.carried = torch.full((1,), -1, dtype=torch.int64, device=device)
         self.max_pairs = pipe.max_pairs
+        self.timing = {}
+        self._t = None
+
+    def _mark(self, name):
+        if not _TIMING:
+            return
+        if self.device.type != "cpu":
+            torch.cuda.synchronize(self.device)
+        t = time.perf_counter()
+        if self._t is not None:
+            self.timing[name] = self.timing.get(name, 0.0) + (t - self._t)
+        self._t = t
 
     def reset(self):
         self.pipe.reset()
@@ -72,15 +92,20 @@ class ShardedCounter:
         allocated and unmodified until its own step."""
         dev, W, r = self.device, self.world, self.rank
         p = self.pipe
+        self._t = None
+        self._mark("start")
         if next_pairs:
             p.phase_map_ahead(d_reads, n_pairs, next_reads, next_pairs)
         else:
             p.phase_map(d_reads, n_pairs)
+        self._mark("map")
         hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * (n_pairs if stride is None
                                                                      else stride))
+        self._mark("export")
         if next_pairs and next2_pairs:
             p.phase_search_ahead(next2_reads, next2_pairs)
         rcv, rcw = self._recv_counts(cnt, wcnt)
+        self._mark("counts")
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
         n_recv, n_words = sum(rcv), sum(rcw)
         recv = torch.empty((max(n_recv, 1), 5), dtype=torch.int64, device=dev)
@@ -89,20 +114,25 @@ class ShardedCounter:
         recv_words = torch.empty(max(n_words, 1), dtype=torch.int64, device=dev)
         dist.all_to_all_single(recv_words[:n_words], words[:sum(sndw)], output_split_sizes=rcw,
                                input_split_sizes=sndw, group=self.group)
+        self._mark("all_to_all_keys")
         flags = torch.empty(max(n_recv, 1), dtype=torch.uint8, device=dev)
         p.dedup_owner(recv, n_recv, recv_words, rcv, rcw, flags)
+        self._mark("owner")
         back = torch.empty(max(sum(snd), 1), dtype=torch.uint8, device=dev)
         dist.all_to_all_single(back[:sum(snd)], flags[:n_recv], output_split_sizes=snd,
                                input_split_sizes=rcv, group=self.group)
+        self._mark("all_to_all_flags")
         p.phase_import(back)
         tail = torch.empty(2, dtype=torch.int64, device=dev)
         p.phase_positions(tail)
+        self._mark("import_positions")
         parts = [torch.empty(2, dtype=torch.int64, device=dev) for _ in range(W)]
         dist.all_gather(parts, tail, group=self.group)
         tails = torch.stack(parts)
         prev = self._prev(tails[:r], self.carried)
         p.phase_bin(prev, d_counts)
         self.carried = self._prev(tails, self.carried)
+        self._mark("tails_bin")
 
     @staticmethod
     def _prev(tails, carried):
