@@ -1949,8 +1949,8 @@ __device__ __forceinline__ uint64_t key_owner(uint64_t hi, int world) {
 }
 // The wave's exported keys grouped by owner: for each owner present in the
 // wave, one lane adds the group's key and word totals to the owner's
-// counters (k_export_count) or takes the group's entry and word slots with
-// one atomic each and hands every lane its own (k_export_fill).  One atomic
+// counters and hands every lane of the group its entry and word offsets from
+// the counters' old values (counters in LDS: the block's, below).  One atomic
 // per key on W addresses serialised ~6 M same-address atomics per batch on
 // one L2 channel: 76 ms per launch at W = 1 (profiles/r03/sharded).  Every
 // lane of the wave calls it; `act` marks the lanes with a key.
@@ -1992,25 +1992,50 @@ __device__ __forceinline__ OwnerSlot wave_owner_slots(bool act, uint32_t ow, uin
   }
   return mine;
 }
-__global__ void k_export_count(const uint8_t *first, const int32_t *nk,
-                               const uint64_t *hash, uint64_t n, int world,
-                               unsigned long long *cnt) {
+// k_export_count / k_export_fill: the wave groups above add into per-owner
+// counters in LDS, and the block adds its totals (count) or reserves its
+// slots (fill) with one global atomic per owner present: ~2 atomics per
+// owner per 256 pairs instead of 2 per wave (1.2 ms per 6.25 M-pair batch at
+// W = 1 with wave atomics alone, profiles/r03/sharded)
+__global__ __launch_bounds__(kB) void k_export_count(const uint8_t *first, const int32_t *nk,
+                                                     const uint64_t *hash, uint64_t n, int world,
+                                                     unsigned long long *cnt) {
+  __shared__ unsigned long long s_e[64], s_w[64];
+  for (uint32_t o = threadIdx.x; o < 64; o += blockDim.x) s_e[o] = s_w[o] = 0;
+  __syncthreads();
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const bool act = q < n && nk[q] >= 0 && first[q];
   const uint32_t ow = act ? uint32_t(key_owner(hash[2 * q], world)) : 0u;
-  (void)wave_owner_slots(act, ow, act ? uint32_t(nk[q]) : 0u, cnt, cnt + 128);
+  (void)wave_owner_slots(act, ow, act ? uint32_t(nk[q]) : 0u, s_e, s_w);
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < uint32_t(world); o += blockDim.x)
+    if (s_e[o]) {
+      atomicAdd(&cnt[o], s_e[o]);
+      atomicAdd(&cnt[128 + o], s_w[o]);
+    }
 }
-__global__ void k_export_fill(const uint8_t *first, const int32_t *nk,
-                              const uint64_t *hash, const uint64_t *hits, uint32_t slots,
-                              uint64_t n, int world, uint64_t gbase, unsigned long long *cnt,
-                              uint64_t *hdr, uint64_t *words, uint32_t *send_q) {
+__global__ __launch_bounds__(kB) void k_export_fill(const uint8_t *first, const int32_t *nk,
+                                                    const uint64_t *hash, const uint64_t *hits,
+                                                    uint32_t slots, uint64_t n, int world,
+                                                    uint64_t gbase, unsigned long long *cnt,
+                                                    uint64_t *hdr, uint64_t *words,
+                                                    uint32_t *send_q) {
+  __shared__ unsigned long long s_e[64], s_w[64], s_be[64], s_bw[64];
+  for (uint32_t o = threadIdx.x; o < 64; o += blockDim.x) s_e[o] = s_w[o] = 0;
+  __syncthreads();
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const bool act = q < n && nk[q] >= 0 && first[q];
   const uint32_t ow = act ? uint32_t(key_owner(hash[2 * q], world)) : 0u;
   const uint64_t k = act ? uint64_t(nk[q]) : 0;
-  const OwnerSlot sl = wave_owner_slots(act, ow, uint32_t(k), cnt + 64, cnt + 192);
+  const OwnerSlot sl = wave_owner_slots(act, ow, uint32_t(k), s_e, s_w);   // within the block
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < uint32_t(world); o += blockDim.x) {
+    s_be[o] = s_e[o] ? atomicAdd(&cnt[64 + o], s_e[o]) : 0;     // the block's entry slots
+    s_bw[o] = s_e[o] ? atomicAdd(&cnt[192 + o], s_w[o]) : 0;    // and word slots
+  }
+  __syncthreads();
   if (!act) return;
-  const uint64_t o = sl.entry, w = sl.word;   // entry slot, word slot
+  const uint64_t o = s_be[ow] + sl.entry, w = s_bw[ow] + sl.word;
   hdr[5 * o] = hash[2 * q];
   hdr[5 * o + 1] = hash[2 * q + 1];
   hdr[5 * o + 2] = gbase + q;

@@ -11,6 +11,9 @@ from collections import defaultdict
 def short(n):
     if "onesweep" in n:
         return "radix_sort_onesweep_" + ("iteration" if "iteration" in n else "global_offsets")
+    if "nccl" in n.lower() or "rccl" in n.lower():
+        return "rccl_" + (re.search(r"(AllToAll|SendRecv|AllGather|AllReduce|Send|Recv)", n) or
+                          re.search(r"(\w+)", n)).group(1)
     for k, v in (("scan_config", "rocprim_scan"), ("partition", "rocprim_partition"),
                  ("copyBuffer", "copyBuffer"), ("fillBuffer", "fillBuffer")):
         if k in n:
@@ -25,9 +28,13 @@ def main(trace, warm=4, per_step=4):
     first, last = mi[int(warm)], mi[-1]
     t0 = int(rows[first]["Start_Timestamp"])
     # the step ends with the last batch's k_emit_bin (or k_bin) after the last search
-    end_i = max(i for i in range(last, len(rows)) if short(rows[i]["Kernel_Name"]) in
-                ("k_emit_bin", "k_bin", "k_tail_lps", "k_tail") and
-                not any("copyBuffer" in rows[j]["Kernel_Name"] for j in range(last, i)))
+    ends = [i for i in range(last, len(rows)) if short(rows[i]["Kernel_Name"]) in
+            ("k_emit_bin", "k_emit_bin_lds", "k_bin", "k_tail_lps", "k_tail") and
+            not any("copyBuffer" in rows[j]["Kernel_Name"] for j in range(last, i))]
+    if not ends:   # (the sharded step: collectives' copies follow the last search)
+        ends = [i for i in range(last, len(rows)) if short(rows[i]["Kernel_Name"]) in
+                ("k_emit_bin", "k_emit_bin_lds", "k_bin")]
+    end_i = max(ends)
     rs = rows[first:end_i + 1]
     t1 = max(int(r["End_Timestamp"]) for r in rs)
     steps = (len(mi) - int(warm)) / int(per_step)
