@@ -597,6 +597,11 @@ def main():
                 "traffic": None, "bytes_per_read": round(b_read, 1),
                 "avg_kernel_ms": round(avg_ms, 3),
                 "active_ms_per_launch": round(act_ms, 3),
+                # the step's time split: the union of the search launches'
+                # intervals and the rest (the post stage and record builds
+                # the searches do not cover; DESIGN.md §3 schedule table)
+                "search_union_ms_per_step": round(active_ms / args.steps, 3),
+                "non_search_ms_per_step": round(1000.0 * el / args.steps - active_ms / args.steps, 3),
                 "frac_over_active_time": round(mam_reads * b_read / (active_ms / 1e3) / 1e9 / 8000.0, 5),
                 "timing": "achieved = reads_per_launch x bytes_per_read / avg_kernel_ms (HIP events "
                           "around each k_mam_sm launch on its stream); launches overlap by %.1f%% "
