@@ -1238,18 +1238,26 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
 // ones in its part in LDS and adds the part to the global counts once, lane
 // i -> bin i (whole contiguous rows).  Every part re-walks the pairs (hit
 // words and bisects: cheap next to the atomics); part 0 keeps the stats.
-constexpr uint32_t kBinPart = 24576;   // 96 KB of counters: one 1024-thread block per CU
+constexpr uint32_t kBinPart = 38912;   // <= 152 KB of counters: one 1024-thread block per CU
 constexpr uint32_t kBinPartsMax = 4;   // above: k_emit_bin
+// the parts balanced: ceil(nbins / parts) bins each (50 k bins: 2 x 25 000,
+// not 24 576 + 24 576 + 848 -- every part re-walks all the pairs)
+inline uint32_t bin_parts(uint32_t nbins) { return (nbins + kBinPart - 1) / kBinPart; }
+inline uint32_t bin_part_size(uint32_t nbins) {
+  const uint32_t np = bin_parts(nbins);
+  return np ? (nbins + np - 1) / np : 1;
+}
 __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     const uint8_t *__restrict__ keep, const int32_t *__restrict__ nk,
     const uint64_t *__restrict__ hits, uint32_t slots, const int64_t *__restrict__ chrom_off,
     const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
     const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
-    uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats) {
+    uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats,
+    uint32_t part) {
   __shared__ uint32_t hc[kBinPart];
-  const uint32_t b0 = blockIdx.y * kBinPart;
-  const uint32_t b1 = b0 + kBinPart < nbins ? b0 + kBinPart : nbins;
-  for (uint32_t i = threadIdx.x; i < kBinPart; i += blockDim.x) hc[i] = 0;
+  const uint32_t b0 = blockIdx.y * part;
+  const uint32_t b1 = b0 + part < nbins ? b0 + part : nbins;
+  for (uint32_t i = threadIdx.x; i < part; i += blockDim.x) hc[i] = 0;
   __syncthreads();
   const int64_t prev0 = *prev_p;
   unsigned long long d = 0, k = 0, t = 0;
@@ -1839,13 +1847,14 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
   const uint64_t n = p->n_pairs;
   const int64_t *prev = d_prev ? d_prev : p->d_prev;
   if (p->fused_bin) {
-    const uint32_t parts = (p->nbins + kBinPart - 1) / kBinPart;
+    const uint32_t parts = bin_parts(p->nbins);
     if (n && p->bin_lds && parts <= kBinPartsMax) {
+      const uint32_t part = bin_part_size(p->nbins);
       const dim3 grid(unsigned(std::min<uint64_t>(256, (n + 1023) / 1024)), parts);
       k_emit_bin_lds<<<grid, 1024, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
           p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
-          p->d_stats);
+          p->d_stats, part);
     } else if (n) {
       k_emit_bin<<<grid_for(n, kB, 8192), kB, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
