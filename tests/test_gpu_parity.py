@@ -350,8 +350,9 @@ def test_fused_positions_bins_agree(gix, s, batch, monkeypatch):
         return counts.cpu().tolist(), pipe.stats().as_dict(), pos
 
     a = run()
-    monkeypatch.setenv("SMASH_BIN_LDS", "1")   # the bin counts summed in LDS (k_emit_bin_lds)
+    monkeypatch.setenv("SMASH_BIN_LDS", "0")   # global bin atomics (k_emit_bin), not LDS
     c = run()
+    monkeypatch.setenv("SMASH_BIN_LDS", "1")
     monkeypatch.setenv("SMASH_FUSED_BIN", "0")
     b = run()
     assert a[1]["error"] == 0
