@@ -134,7 +134,6 @@ uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, satu
 void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
 void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
 void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
-void set_prep_prio(uint32_t on);   // mam.hip: k_prep_direct's priority (SMASH_PRIO)
 // mam.hip: smash_map_batch without the per-launch synchronisation of the
 // probe check (sync_check = false: the caller runs probe_check later)
 // caller-owned search workspace (the pipeline's double-buffered sets): the

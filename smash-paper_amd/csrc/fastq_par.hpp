@@ -174,14 +174,19 @@ inline const char *line_end(const char *p, const char *e) {
   return q ? static_cast<const char *>(q) : nullptr;
 }
 
+// the longest name or bases line the parallel reader takes (parse() finds
+// line ends within it); a longer one is "not strict": the streaming reader
+// takes the input and reports it by its own rules
+constexpr size_t kMaxLine = size_t(1) << 16;
+
 // one strict record at r (r[0] == '@'): the end of its fourth line (its
 // '\n'); nullptr = not strict
 inline const char *strict_record(const char *r, const char *e) {
   if (r >= e || r[0] != '@') return nullptr;
   const char *l1 = line_end(r, e);
-  if (!l1) return nullptr;
+  if (!l1 || size_t(l1 - r) >= kMaxLine) return nullptr;
   const char *l2 = line_end(l1 + 1, e);
-  if (!l2 || l2 + 1 >= e || l2[1] != '+') return nullptr;
+  if (!l2 || size_t(l2 - l1) > kMaxLine || l2 + 1 >= e || l2[1] != '+') return nullptr;
   const char *l3 = line_end(l2 + 1, e);
   return l3 ? line_end(l3 + 1, e) : nullptr;   // nullptr: no qualities line
 }
@@ -266,14 +271,14 @@ struct Rec {
   uint32_t sn;
 };
 inline Rec parse(const char *r) {
-  // (every line of an indexed record ends in '\n')
-  const char *l1 = static_cast<const char *>(memchr(r, '\n', size_t(1) << 20));
+  // (every line of an indexed record ends in '\n' within kMaxLine bytes)
+  const char *l1 = static_cast<const char *>(memchr(r, '\n', kMaxLine));
   const char *nb = r + 1;
   while (nb < l1 && isspace(uint8_t(*nb))) ++nb;
   const char *ne = nb;
   while (ne < l1 && !isspace(uint8_t(*ne))) ++ne;
   const char *b = l1 + 1;
-  const char *l2 = static_cast<const char *>(memchr(b, '\n', size_t(1) << 20));
+  const char *l2 = static_cast<const char *>(memchr(b, '\n', kMaxLine));
   const char *be = l2;
   while (be > b && be[-1] == '\r') --be;
   return Rec{nb, uint32_t(ne - nb), b, uint32_t(be - b)};

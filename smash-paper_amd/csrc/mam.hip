@@ -23,13 +23,6 @@
 #include <cstring>
 
 namespace smash {
-// k_prep_direct's raised priority beside a running search (SMASH_PRIO, set
-// by smash_pipeline_create; A/B)
-static uint32_t g_prep_prio = 1;
-void set_prep_prio(uint32_t on) { g_prep_prio = on; }
-}  // namespace smash
-
-namespace smash {
 namespace {
 
 // Persistent grid sized to the resident capacity; each lane pulls the next
@@ -204,7 +197,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
     const uint64_t items = n_reads * ga;
     sm::k_prep_direct<<<unsigned((items + 255) / 256), 256, 0, s>>>(
         seqs, stride, lens, len, uint32_t(n_reads), ga, ix->in_text[0], ix->in_text[1],
-        ix->in_text[2], ix->in_text[3], g, rec, g_prep_prio);
+        ix->in_text[2], ix->in_text[3], g, rec, 1u);   // raised priority beside a running search
     SMASH_HIP(hipGetLastError());
   }
   if (ws && ws->gate) SMASH_HIP(hipStreamWaitEvent(s, ws->gate, 0));

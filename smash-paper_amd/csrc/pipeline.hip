@@ -40,12 +40,9 @@ constexpr uint32_t kStatStride = 16, kStatStripes = 16, kStatWords = kStatStride
 // equal priority the SIMD's oldest-first issue leaves them a trickle and
 // they finish only when the search drains.  Raised priority lets them
 // through; the search absorbs their (small) share of the memory system.
-// (SMASH_PRIO=0 at pipeline creation leaves them at the default priority: A/B)
-__constant__ uint32_t g_beside_prio = 1;
-#define SMASH_BESIDE_SEARCH()                          \
-  do {                                                 \
-    if (g_beside_prio) __builtin_amdgcn_s_setprio(2);  \
-  } while (0)
+// (Round 3 A/B, profiles/r03/sched: default priority 150.7 vs 150.2-151.9 ms
+// per C3 step; the knob was a process-global symbol and is gone.)
+#define SMASH_BESIDE_SEARCH() __builtin_amdgcn_s_setprio(2)
 
 struct smash_pipeline {
   const smash_index *ix = nullptr;
@@ -1323,10 +1320,15 @@ __global__ void k_reset_prev(int64_t *prev) {
 }
 
 hipError_t ensure_positions(smash_pipeline *p) {
-  if (p->d_pos0) return hipSuccess;
+  if (p->d_pos0 && p->d_abs) return hipSuccess;
   const uint64_t n = p->max_pairs * 2 * p->slots;
-  hipError_t e = hipMalloc(reinterpret_cast<void **>(&p->d_pos0), 8 * n);
+  hipError_t e = p->d_pos0 ? hipSuccess : hipMalloc(reinterpret_cast<void **>(&p->d_pos0), 8 * n);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&p->d_abs), 8 * n);
+  if (e != hipSuccess) {   // all or nothing: a later call must not find half the arrays
+    (void)hipFree(p->d_pos0);
+    p->d_pos0 = nullptr;
+    p->d_abs = nullptr;
+  }
   return e;
 }
 
@@ -1518,10 +1520,6 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       p->gate_prep = on("SMASH_GATE_PREP", false);
       p->gate_post = on("SMASH_GATE_POST", true);   // profiles/r03/sched: 150.9 vs 160.1 ms
       p->one_search = on("SMASH_ONE_SEARCH", false);
-      const char *pr = getenv("SMASH_PRIO");
-      const uint32_t prio = pr && pr[0] == '0' ? 0u : 1u;
-      SMASH_HIPX(hipMemcpyToSymbol(HIP_SYMBOL(g_beside_prio), &prio, 4));
-      smash::set_prep_prio(prio);
     }
     // the positions arrays (2 x 8 B x every hit slot: 26 GB at 6.25 M
     // pairs) only for the two-kernel path; the fused path writes them when
@@ -1884,11 +1882,16 @@ int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
   int rc = phase_map_impl(p, d_reads, n_pairs, s, in_ev);
   p->defer_free = false;
   if (rc) return rc;
-  if ((rc = dedup_local(p, s))) return rc;
-  if ((rc = smash_phase_positions(p, nullptr, s))) return rc;
-  if ((rc = smash_phase_bin(p, nullptr, d_counts, s))) return rc;
-  if (p->gate_post && n_pairs) SMASH_HIP(hipEventRecord(p->ev_free[p->set], s));
-  return SMASH_OK;
+  rc = dedup_local(p, s);
+  if (!rc) rc = smash_phase_positions(p, nullptr, s);
+  if (!rc) rc = smash_phase_bin(p, nullptr, d_counts, s);
+  // on every exit once the search is queued: the set's next search must
+  // follow whatever of this batch's post stage was queued on s
+  if (p->gate_post && n_pairs && hipEventRecord(p->ev_free[p->set], s) != hipSuccess && !rc) {
+    set_error("hipEventRecord failed");
+    rc = SMASH_ERR_HIP;
+  }
+  return rc;
 }
 }  // namespace smash
 

@@ -34,17 +34,50 @@ import torch.distributed as dist
 _TIMING = os.environ.get("SMASH_DIST_TIMING", "0") == "1"
 
 
+class TorchComm:
+    """The step's collectives over torch.distributed: device tensors on
+    `group` (RCCL on MI355X), the per-batch key counts -- host integers --
+    on `count_group` (gloo: no device synchronisation) when one is given."""
+
+    def __init__(self, device, group=None, count_group=None):
+        self.device = device
+        self.group = group
+        self.count_group = count_group
+
+    def exchange_counts(self, rows):
+        """rows[o] = [keys, words] this rank sends owner o; returns what every
+        source rank sends this one, as rows in rank order"""
+        if self.count_group is not None:
+            sc = torch.as_tensor(rows, dtype=torch.int64)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=self.count_group)
+        else:
+            sc = torch.as_tensor(rows, dtype=torch.int64).to(self.device)
+            rc = torch.empty_like(sc)
+            dist.all_to_all_single(rc, sc, group=self.group)
+        return rc.cpu().tolist()
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                               input_split_sizes=in_splits, group=self.group)
+
+    def all_gather(self, parts, t):
+        dist.all_gather(parts, t, group=self.group)
+
+
 class ShardedCounter:
-    def __init__(self, pipe, rank, world, device, group=None, count_group=None):
+    def __init__(self, pipe, rank, world, device, group=None, count_group=None, comm=None):
         """count_group: a CPU (gloo) process group for the per-batch key
         counts, which are host integers after smash_phase_export: exchanged
-        there they cost no device synchronisation (None: over `group`)."""
+        there they cost no device synchronisation (None: over `group`).
+        comm: the collectives (default TorchComm(device, group, count_group));
+        tests pass an in-process transport to run W ranks of this exact step
+        on one device."""
         self.pipe = pipe
         self.rank = rank
         self.world = world
         self.device = device
-        self.group = group
-        self.count_group = count_group
+        self.comm = comm if comm is not None else TorchComm(device, group, count_group)
         self.carried = torch.full((1,), -1, dtype=torch.int64, device=device)
         self.max_pairs = pipe.max_pairs
         self.timing = {}
@@ -66,16 +99,7 @@ class ShardedCounter:
 
     def _recv_counts(self, cnt, wcnt):
         """what every rank sends me: [keys], [words] per source rank"""
-        rows = [[int(a), int(b)] for a, b in zip(cnt, wcnt)]
-        if self.count_group is not None:   # host integers over gloo: no device sync
-            sc = torch.as_tensor(rows, dtype=torch.int64)
-            rc = torch.empty_like(sc)
-            dist.all_to_all_single(rc, sc, group=self.count_group)
-        else:
-            sc = torch.as_tensor(rows, dtype=torch.int64).to(self.device)
-            rc = torch.empty_like(sc)
-            dist.all_to_all_single(rc, sc, group=self.group)   # row s: what rank s sends me
-        rcl = rc.cpu().tolist()
+        rcl = self.comm.exchange_counts([[int(a), int(b)] for a, b in zip(cnt, wcnt)])
         return [x[0] for x in rcl], [x[1] for x in rcl]
 
     def step(self, d_reads, n_pairs, step_base, d_counts, next_reads=None, next_pairs=0,
@@ -109,25 +133,22 @@ class ShardedCounter:
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
         n_recv, n_words = sum(rcv), sum(rcw)
         recv = torch.empty((max(n_recv, 1), 5), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(recv[:n_recv], hdr[:sum(snd)], output_split_sizes=rcv,
-                               input_split_sizes=snd, group=self.group)
+        self.comm.all_to_all(recv[:n_recv], hdr[:sum(snd)], rcv, snd)
         recv_words = torch.empty(max(n_words, 1), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(recv_words[:n_words], words[:sum(sndw)], output_split_sizes=rcw,
-                               input_split_sizes=sndw, group=self.group)
+        self.comm.all_to_all(recv_words[:n_words], words[:sum(sndw)], rcw, sndw)
         self._mark("all_to_all_keys")
         flags = torch.empty(max(n_recv, 1), dtype=torch.uint8, device=dev)
         p.dedup_owner(recv, n_recv, recv_words, rcv, rcw, flags)
         self._mark("owner")
         back = torch.empty(max(sum(snd), 1), dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(back[:sum(snd)], flags[:n_recv], output_split_sizes=snd,
-                               input_split_sizes=rcv, group=self.group)
+        self.comm.all_to_all(back[:sum(snd)], flags[:n_recv], snd, rcv)
         self._mark("all_to_all_flags")
         p.phase_import(back)
         tail = torch.empty(2, dtype=torch.int64, device=dev)
         p.phase_positions(tail)
         self._mark("import_positions")
         parts = [torch.empty(2, dtype=torch.int64, device=dev) for _ in range(W)]
-        dist.all_gather(parts, tail, group=self.group)
+        self.comm.all_gather(parts, tail)
         tails = torch.stack(parts)
         prev = self._prev(tails[:r], self.carried)
         p.phase_bin(prev, d_counts)

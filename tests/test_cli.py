@@ -313,7 +313,11 @@ def test_parallel_reader_refuses_what_it_cannot_index(tmp_path):
     bad = [b"@a\nACGT\n+\nIIII\n\n@b\nACGT\n+\nIIII\n",
            b">a\nACGT\n>b\nACGT\n",
            b"@a\nACGT\n +\nIIII\n",
-           b"@a\nACGT\n+\nIIII\n@b\nACGT\n"]
+           b"@a\nACGT\n+\nIIII\n@b\nACGT\n",
+           # a name line and a bases line longer than the reader's 64 KB
+           # line bound (fastq_par.hpp kMaxLine): refused, not parsed past
+           b"@" + b"x" * (2 << 20) + b"\nACGT\n+\nIIII\n",
+           b"@a\n" + b"A" * (1 << 17) + b"\n+\n" + b"I" * (1 << 17) + b"\n"]
     ok = tmp_path / "ok.fq"
     ok.write_bytes(b"@a\nACGT\n+\nIIII\n@b\nACGT\n+\nIIII\n")
     for k, body in enumerate(bad):

@@ -382,3 +382,146 @@ def test_idx8_pipeline_equals_independent_oracle(monkeypatch, tmp_path):
     assert np.array_equal(counts, op.counts)
     assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
     assert st.dupe_pairs == op.n_dupe.value
+
+
+# ---------------------------------------------------------------------------
+# The REAL multi-GPU driver (dist.ShardedCounter.step, dist.count_fastq) on
+# C4's workload: W ranks as threads of this process (tests/thread_ranks.py:
+# only the transport differs), and one rank over a real RCCL process group
+# (the collectives SCALE runs, to itself) -- against the oracle
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("W,per_rank,bits,ahead2", [(8, 10_000, 0, True),
+                                                    (3, 20_000, 0, True),
+                                                    (3, 20_000, 0, False),
+                                                    (8, 10_000, 18, True)])
+def test_c4_real_driver_threads_equal_oracle(c4_run, W, per_rank, bits, ahead2, monkeypatch):
+    """ShardedCounter.step itself, as bench.py's sharded loop calls it (next
+    batch searched with this one, the one after right after the export),
+    W ranks over the 240 k pairs == the oracle (smashMEM.py:217-228 first-wins
+    across ranks and steps, varbin.py:56-58 across shard boundaries)."""
+    from thread_ranks import run_resident
+    dix, cs, starts, d_reads, single, orc = c4_run
+    if bits:
+        monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
+    total, st = run_resident(dix, d_reads, W, per_rank, starts, cs, ahead2=ahead2)
+    assert orc[1][3] > 100
+    assert np.array_equal(total, orc[0]) and st == orc[1]
+
+
+@pytest.fixture(scope="module")
+def c4_fastq(c4_run, tmp_path_factory):
+    """C4's 240 k pairs as FASTQ lane files (names r%09d in order): 3 plain
+    lanes and 2 gzip lanes per mate."""
+    import readgen
+    _, _, _, d_reads, _, _ = c4_run
+    h = d_reads.cpu().numpy()
+    d = tmp_path_factory.mktemp("c4fq")
+    cut = 2 * 150_000
+    a1, a2 = readgen.write_fastq_lanes(h[:cut], str(d / "plain"), 3)
+    b1, b2 = readgen.write_fastq_lanes(h[cut:], str(d / "gz"), 2, gz=True, q0=cut // 2)
+    return a1 + b1, a2 + b2
+
+
+@pytest.mark.parametrize("W,batch", [(3, 30_000), (8, 7_000)])
+def test_c4_real_driver_files_threads_equal_oracle(c4_run, c4_fastq, W, batch):
+    """dist.count_fastq (every rank its own FastqIndex of the lane lists,
+    look-ahead packing, short and empty last shares) == the oracle."""
+    from thread_ranks import run_files
+    dix, cs, starts, _, _, orc = c4_run
+    total, st, done = run_files(dix, c4_fastq, W, batch, starts, cs, capacity=C4_PAIRS)
+    assert sum(done) == C4_PAIRS
+    assert np.array_equal(total, orc[0]) and st == orc[1]
+
+
+def _port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_c4_real_driver_rccl_world1_equals_oracle(c4_run, c4_fastq, monkeypatch):
+    """One rank over a real nccl (RCCL) process group plus the gloo count
+    group, exactly as bench.py --gpus N and smash_cli count set them up:
+    the bench's step loop (4 batches, next / next-two search), the same
+    with the key hash cut to 18 bits, and dist.count_fastq from the lane
+    files -- all == the oracle."""
+    import torch.distributed as tdist
+    from dist import ShardedCounter, count_fastq
+    dix, cs, starts, d_reads, _, orc = c4_run
+    dev = torch.device("cuda", 0)
+    tdist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0,
+                             world_size=1, device_id=dev)
+    try:
+        cg = tdist.new_group(backend="gloo")
+        B = 60_000
+        nb = C4_PAIRS // B
+        for bits in (0, 18):
+            if bits:
+                monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
+            pipe = S.Pipeline(dix, cs, starts, 150, B, dedup_capacity=C4_PAIRS)
+            counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+            sc = ShardedCounter(pipe, 0, 1, dev, count_group=cg)
+            sc.reset()
+            for b in range(nb):   # bench.py's sharded loop at world 1
+                b0, b1 = b * B, (b + 1) * B
+                n0, n1 = b1, min(C4_PAIRS, b1 + B)
+                m0, m1 = n1, min(C4_PAIRS, n1 + B)
+                sc.step(d_reads[2 * b0:2 * b1], B, b0, counts,
+                        d_reads[2 * n0:2 * n1] if n1 > n0 else None, n1 - n0,
+                        next2_reads=d_reads[2 * m0:2 * m1] if m1 > m0 else None,
+                        next2_pairs=m1 - m0)
+            tdist.all_reduce(counts)
+            s = pipe.stats()
+            assert np.array_equal(counts.cpu().numpy().astype(np.uint64), orc[0]), bits
+            assert (s.positions, s.dups, s.kept, s.dupe_pairs) == orc[1], bits
+            del pipe
+        monkeypatch.delenv("SMASH_KEY_HASH_BITS")
+        fq = S.FastqIndex(*c4_fastq)
+        assert fq.n == C4_PAIRS
+        pipe = S.Pipeline(dix, cs, starts, fq.L, 70_000, dedup_capacity=C4_PAIRS)
+        counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+        sc = ShardedCounter(pipe, 0, 1, dev, count_group=cg)
+        sc.reset()
+        assert count_fastq(sc, fq, 70_000, counts) == C4_PAIRS
+        tdist.all_reduce(counts)
+        s = pipe.stats()
+        assert np.array_equal(counts.cpu().numpy().astype(np.uint64), orc[0])
+        assert (s.positions, s.dups, s.kept, s.dupe_pairs) == orc[1]
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_c3_production_batch_equals_oracle(hg19, hg19_oracle):
+    """C3 at the bench's production batch size: 6.6 M pairs of the bench's
+    workload (seed 3, 150 bp, sample_bins/50000) counted as bench.py counts a
+    run -- smash_count_batches_ready over batches of 6.25 M pairs, one key set
+    and the adjacent-dup state carried into the second, short batch -- equal
+    the oracle's whole chain over the same 13.2 M reads (smashMEM.py:147-228,
+    varbin.py:52-92).  ~2 minutes of oracle time on 16 threads."""
+    import readgen
+    contigs, _, dix = hg19
+    oix, mp = hg19_oracle
+    cs = _chrom_sizes(contigs)
+    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+    starts = np.array([int(l.split("\t")[2]) for l in open(src)], np.int64)
+    P, B = 6_600_000, 6_250_000
+    d_reads = readgen.Generator(dix, contigs, 150, seed=3000).generate(P)
+    pipe = S.Pipeline(dix, cs, starts, 150, B, dedup_capacity=P + P // 8 + (1 << 20))
+    counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    pipe.reset()
+    pipe.count_batches(d_reads, P, B, counts, resident=True)
+    st = pipe.stats()
+    got = counts.cpu().numpy().astype(np.uint64)
+    h = d_reads.cpu().numpy()
+    del d_reads, pipe
+    op = O.Pipeline(oix, mp, cs, starts)
+    for a in range(0, P, 500_000):   # the oracle's state carries across calls
+        assert op.run(h[2 * a:2 * min(P, a + 500_000)], threads=THREADS) == 0
+        print("oracle: %d of %d pairs" % (min(P, a + 500_000), P), flush=True)
+    assert st.pairs == P
+    assert np.array_equal(got, op.counts)
+    assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
+    assert st.dupe_pairs == op.n_dupe.value and st.dupe_pairs > 1000

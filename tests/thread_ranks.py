@@ -1,0 +1,159 @@
+"""W ranks of the REAL multi-GPU step (smash-paper_amd/dist.py
+ShardedCounter.step / count_fastq) as W threads of one process on ONE
+device (test infrastructure).  Only the transport is replaced: ThreadComm
+implements the three collectives the step uses (the key-count exchange,
+all_to_all with split sizes, all_gather) with device copies between the
+threads' tensors.  Everything else -- the look-ahead search of the next
+batch, the two-ahead search after the export, the owner de-dup, the tail
+bookkeeping -- is the code `bench.py --gpus N` and `smash_cli count` run.
+
+Each collective synchronises the device before it publishes its input and
+after it has copied its output (the ranks' pipelines run on their own
+streams), then meets the other threads at a barrier: slow, but every byte
+a rank reads was complete when it was published."""
+import threading
+
+import numpy as np
+import torch
+
+import smashgpu as S
+from dist import ShardedCounter, count_fastq
+
+
+class ThreadWorld:
+    def __init__(self, world, timeout=600.0):
+        self.world = world
+        self.barrier = threading.Barrier(world, timeout=timeout)
+        self.slot = [None] * world
+
+    def comm(self, rank):
+        return ThreadComm(self, rank)
+
+
+class ThreadComm:
+    def __init__(self, tw, rank):
+        self.tw = tw
+        self.rank = rank
+
+    def _publish(self, x):
+        torch.cuda.synchronize()
+        self.tw.slot[self.rank] = x
+        self.tw.barrier.wait()
+
+    def _done(self):
+        torch.cuda.synchronize()
+        self.tw.barrier.wait()   # nobody republishes before every rank has read
+
+    def exchange_counts(self, rows):
+        self._publish([list(r) for r in rows])
+        got = [self.tw.slot[s][self.rank] for s in range(self.tw.world)]
+        self._done()
+        return got
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        self._publish((inp, [int(x) for x in in_splits]))
+        o = 0
+        for s in range(self.tw.world):
+            src, sp = self.tw.slot[s]
+            a, n = sum(sp[:self.rank]), sp[self.rank]
+            assert n == int(out_splits[s]), (s, n, out_splits)
+            if n:
+                out[o:o + n].copy_(src[a:a + n])
+            o += n
+        self._done()
+
+    def all_gather(self, parts, t):
+        self._publish(t)
+        for s in range(self.tw.world):
+            parts[s].copy_(self.tw.slot[s])
+        self._done()
+
+
+def _run_threads(world, body):
+    tw = ThreadWorld(world)
+    errs = [None] * world
+
+    def run(r):
+        try:
+            body(r, tw.comm(r))
+        except BaseException as e:   # noqa: BLE001 -- reported below
+            errs[r] = e
+            tw.barrier.abort()       # the other ranks leave their barrier too
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errs:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+def _summary(pipes, counts):
+    total = sum(c.cpu().numpy().astype(np.uint64) for c in counts)
+    st = [p.stats() for p in pipes]
+    return total, (sum(x.positions for x in st), sum(x.dups for x in st),
+                   sum(x.kept for x in st), sum(x.dupe_pairs for x in st))
+
+
+def make_pipes(ix, world, cs, starts, L, batch, capacity):
+    pipes = [S.Pipeline(ix, cs, starts, L, batch, dedup_capacity=capacity)
+             for _ in range(world)]
+    counts = [torch.zeros(len(starts), dtype=torch.int64, device="cuda") for _ in range(world)]
+    return pipes, counts
+
+
+def run_resident(ix, d_reads, world, per_rank, starts, cs, ahead2=True, capacity=None):
+    """bench.py's sharded step loop, one thread per rank: rank r's pairs are
+    d_reads' global pairs [b W B + r B, + B) of batch b (the bench's layout:
+    each rank holds its own P pairs, here dealt from one tensor), with the
+    next batch searched under this one's exchange and, with ahead2, the one
+    after that right after the export."""
+    n = d_reads.shape[0] // 2
+    nb = n // (world * per_rank)
+    assert nb * world * per_rank == n
+    pipes, counts = make_pipes(ix, world, cs, starts, d_reads.shape[1], per_rank,
+                               capacity or n)
+    dev = d_reads.device
+
+    def body(r, comm):
+        sc = ShardedCounter(pipes[r], r, world, dev, comm=comm)
+        sc.reset()
+
+        def mine(b):   # rank r's batch b, or None past the end
+            if b >= nb:
+                return None
+            lo = b * world * per_rank + r * per_rank
+            return d_reads[2 * lo:2 * (lo + per_rank)]
+
+        for b in range(nb):
+            nxt, nxt2 = mine(b + 1), mine(b + 2) if ahead2 else None
+            sc.step(mine(b), per_rank, b * world * per_rank, counts[r],
+                    nxt, per_rank if nxt is not None else 0,
+                    next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
+
+    _run_threads(world, body)
+    return _summary(pipes, counts)
+
+
+def run_files(ix, paths, world, batch, starts, cs, capacity):
+    """dist.count_fastq over `world` ranks, each with its own
+    smashgpu.FastqIndex of the same lists (as smash_cli count runs under
+    torchrun).  Returns (counts, stats, pairs counted per rank)."""
+    fqs = [S.FastqIndex(*paths) for _ in range(world)]
+    L = fqs[0].L
+    pipes, counts = make_pipes(ix, world, cs, starts, L, batch, capacity)
+    done = [0] * world
+
+    def body(r, comm):
+        sc = ShardedCounter(pipes[r], r, world, torch.device("cuda"), comm=comm)
+        sc.reset()
+        done[r] = count_fastq(sc, fqs[r], batch, counts[r])
+
+    _run_threads(world, body)
+    total, st = _summary(pipes, counts)
+    return total, st, done
