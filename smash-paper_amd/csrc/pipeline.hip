@@ -98,13 +98,17 @@ struct smash_pipeline {
   uint64_t *d_hits = nullptr;
   uint64_t *d_hash = nullptr;   // [2*max_pairs] hi, lo
   uint8_t *d_keep = nullptr;
-  uint8_t *d_first = nullptr;
   uint64_t *d_slot = nullptr;     // [max_pairs] k_dedup_claim -> k_dedup_decide
   uint64_t *d_tsum = nullptr;     // [tiles] the LDS-free scans' tile aggregates / prefixes
   int64_t *d_tlast = nullptr;
   bool cnt_ready = false;         // k_dedup_decide wrote d_cnt / d_lp for this batch
-  uint32_t *d_k[2] = {nullptr, nullptr};   // sort keys (sort_key32)
-  uint32_t *d_v[2] = {nullptr, nullptr};
+  // multi-GPU export: per (owner, block) keys << 32 | words and their
+  // exclusive scan (k_export_count / k_export_fill); the owner's claim slots
+  uint64_t *d_bcnt = nullptr, *d_boff = nullptr;
+  void *d_scan_temp = nullptr;
+  size_t scan_temp_bytes = 0;
+  uint64_t *d_oslot = nullptr;
+  uint64_t oslot_cap = 0;
   void *d_temp = nullptr;
   size_t temp_bytes = 0;
   uint64_t *d_table = nullptr;   // {hash hi, arena ref + 1} slots, 0 = empty
@@ -132,19 +136,17 @@ struct smash_pipeline {
   bool post_fast = false;
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
-  unsigned long long *d_owner = nullptr;  // per owner: [0,64) entries [64,128) entry cursors
-                                          // [128,192) words (for the fill: word-segment
-                                          // starts) [192,256) word cursors
+  unsigned long long *d_owner = nullptr;  // per owner: [0,64) keys [64,128) words (k_export_totals)
   uint64_t *d_send_hdr = nullptr; // [n_export][5] {hi, lo, global index, nk, word offset}
   uint64_t *d_send_words = nullptr;   // the exported keys' hit words, grouped by owner
   uint64_t send_words_cap = 0;
   uint64_t *d_recv_base = nullptr;    // [2 * 65] owner side: header / word prefix per source
-  // pinned host images of d_owner and d_recv_base: their host-to-device
-  // copies stay asynchronous (the host rewrites an image only after the
-  // event of its previous copy)
+  // pinned host images of d_owner (the per-owner totals) and d_recv_base
+  // (its host-to-device copy stays asynchronous: the host rewrites the image
+  // only after the event of its previous copy)
   unsigned long long *h_owner = nullptr;
   uint64_t *h_recv_base = nullptr;
-  hipEvent_t ev_owner = nullptr, ev_base = nullptr;
+  hipEvent_t ev_base = nullptr;
   uint64_t n_pairs = 0, n_export = 0;
   hipStream_t last = nullptr;
   // smash_count_fastq's pinned slots, device buffers and copy stream, kept
@@ -626,23 +628,6 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
   post_stats(nm, np, err, stats);
 }
 
-// In-batch order for the de-dup: a stable radix sort of a 32-bit key = the
-// low half of the hash hi (4 passes instead of 8 for the whole hash).  Equal
-// keys stay adjacent and in pair order; keys sharing only the low half share
-// a group, which the word comparison tells apart.  Pairs without a key sort
-// last (0xFFFFFFFF, never a keyed pair's value), so no group reaches them.
-__device__ __forceinline__ uint32_t sort_key32(uint64_t hi) {
-  const uint32_t k = uint32_t(hi);
-  return k == 0xFFFFFFFFu ? 0xFFFFFFFEu : k;
-}
-__global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n,
-                             uint32_t *key, uint32_t *val) {
-  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (q >= n) return;
-  key[q] = nk[q] >= 0 ? sort_key32(hash[2 * q]) : 0xFFFFFFFFu;
-  val[q] = uint32_t(q);
-}
-
 // The persistent pair-key set of smashMEM.py:149,217-228 (dupeSet), exact:
 // a key is the pair's kept hit list (tid << 48 | pos0 per hit, r1 then r2 in
 // HI order, smashMEM.py:122-131).  Open addressing on the 64-bit hash `hi`;
@@ -652,13 +637,12 @@ __global__ void k_dedup_keys(const int32_t *nk, const uint64_t *hash, uint64_t n
 // agree, so a hash collision is a different key (it goes on probing), never a
 // false duplicate.
 //
-// The threads of one insert launch hold distinct keys (the in-batch pass ran
-// first), so a slot published by this launch (ref 0 or tagged with this
-// launch's epoch) is never the probing thread's key, and its record need not
-// be read; records of earlier launches are visible across the kernel
-// boundary.  Hence relaxed slot accesses, no per-key release / acquire
-// (agent-scope fences write back / invalidate the XCD's L2 on gfx950 and
-// made this kernel 5 ms per 2 M pairs).  Epochs wrap after 2^24 launches.
+// Slot accesses are relaxed, with no per-key release / acquire (agent-scope
+// fences write back / invalidate the XCD's L2 on gfx950 and made the round-2
+// insert kernel 5 ms per 2 M pairs): a launch compares only against records
+// of earlier launches, which are visible across the kernel boundary, and
+// against this launch's claims through the claimers' own input rows (the
+// claim / decide kernels below).  Epochs wrap after 2^24 launches.
 constexpr int kRefShift = 40;
 // a published ref (the key's record is in the arena) carries kRefPub; the
 // in-batch claims of k_dedup_claim (pair index + 1, this epoch) do not
@@ -701,103 +685,6 @@ __device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need) {
   if (lane == 63 && total) base = atomicAdd(top, (unsigned long long)total);
   base = __shfl(base, 63, 64);
   return uint64_t(base) + x - need;
-}
-
-// true if the key was already present; inserts it otherwise, its record at
-// arena[off] (wave_alloc) (*full: the table or the arena ran out -- an error
-// the caller reports)
-__device__ bool set_test_insert(uint64_t *table, uint64_t mask, uint64_t hi, const KeyRef &k,
-                                uint64_t *arena, uint64_t arena_cap, uint64_t off,
-                                uint64_t epoch, bool *full) {
-  uint64_t i = (hi ^ (hi >> 31)) & mask;
-  for (uint64_t probe = 0; probe <= mask; ++probe) {
-    unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
-    unsigned long long cur = __hip_atomic_load(sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cur == 0) {
-      const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
-      if (prev == 0) {
-        const uint64_t need = 2 + uint64_t(k.nk);
-        if (off + need > arena_cap) {
-          *full = true;
-          return false;
-        }
-        uint64_t *rec = arena + off;
-        rec[0] = k.lo;
-        rec[1] = k.nk;
-        for (uint32_t j = 0; j < k.nk; ++j) rec[2 + j] = k.w[j];
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * i + 1]),
-                           (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-      cur = prev;
-    }
-    if (cur == hi) {
-      // ref 0 or this epoch: a key of this launch, not ours
-      const unsigned long long ref = __hip_atomic_load(
-          reinterpret_cast<unsigned long long *>(&table[2 * i + 1]), __ATOMIC_RELAXED,
-          __HIP_MEMORY_SCOPE_AGENT);
-      if (ref && (ref >> kRefShift) != epoch && (ref & kRefPub) &&
-          same_key(arena + ((ref & (kRefPub - 1)) - 1), k))
-        return true;
-    }
-    i = (i + 1) & mask;
-  }
-  *full = true;
-  return false;
-}
-
-// mode 0: single GPU (test+insert the persistent set); mode 1: mark
-// in-batch first occurrences only (multi-GPU export).  key/val: the batch's
-// pairs sorted (stably) by sort_key32; a pair is first unless an earlier pair
-// of its group has the same key.
-__global__ void k_dedup_first(const uint32_t *__restrict__ key, const uint32_t *__restrict__ val,
-                              uint64_t n, const int32_t *nk, const uint64_t *hash,
-                              const uint64_t *hits, uint32_t slots, uint64_t *table,
-                              uint64_t mask, uint64_t *arena, uint64_t arena_cap,
-                              unsigned long long *arena_top, uint64_t epoch, int mode,
-                              uint8_t *keep, uint8_t *first, unsigned long long *stats) {
-  const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  unsigned long long kp = 0, dp = 0;
-  bool full = false;
-  const bool act = mode == 0 && s < n && nk[val[s]] >= 0;
-  const uint64_t off = wave_alloc(arena_top, act ? 2u + uint32_t(nk[val[s]]) : 0u);
-  if (s < n) {
-    const uint32_t q = val[s];
-    if (nk[q] < 0) {
-      keep[q] = 0;
-      first[q] = 0;
-    } else {
-      kp = 1;
-      bool f = true;
-      const KeyRef me{hits + uint64_t(q) * 2 * slots, uint32_t(nk[q]), hash[2 * q + 1]};
-      for (uint64_t t = s; t-- > 0 && key[t] == key[s];) {
-        const uint32_t q2 = val[t];
-        const KeyRef other{hits + uint64_t(q2) * 2 * slots, uint32_t(nk[q2]), hash[2 * q2 + 1]};
-        if (same_key(me, other)) { f = false; break; }
-      }
-      first[q] = f ? 1 : 0;
-      if (mode == 0) {
-        bool k = f && !set_test_insert(table, mask, hash[2 * q], me, arena, arena_cap, off, epoch,
-                                       &full);
-        keep[q] = k ? 1 : 0;
-        dp = k ? 0 : 1;
-      }
-    }
-  }
-  __shared__ unsigned long long a, b;
-  __shared__ int fl;
-  if (threadIdx.x == 0) { a = 0; b = 0; fl = 0; }
-  __syncthreads();
-  if (kp) atomicAdd(&a, kp);
-  if (dp) atomicAdd(&b, dp);
-  if (full) fl = 1;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (a && mode == 0) atomicAdd(&stats[S_KEYPAIRS], a);
-    if (b) atomicAdd(&stats[S_DUPEPAIRS], b);
-    if (fl) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1470,26 +1357,22 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_hits = dalloc<uint64_t>(P * 2 * p->slots);
     p->d_hash = dalloc<uint64_t>(2 * P);
     p->d_keep = dalloc<uint8_t>(P);
-    p->d_first = dalloc<uint8_t>(P);
-    // sort buffers also serve the owner side of the multi-GPU de-dup,
-    // which may receive more keys than one batch holds
-    for (int i = 0; i < 2; ++i) {
-      p->d_k[i] = dalloc<uint32_t>(2 * P);
-      p->d_v[i] = dalloc<uint32_t>(2 * P);
+    {   // the multi-GPU export's per-(owner, block) counts, up to 64 owners
+      const uint64_t nb = 64 * ((P + kB - 1) / kB);
+      p->d_bcnt = dalloc<uint64_t>(nb);
+      p->d_boff = dalloc<uint64_t>(nb);
+      SMASH_HIPX(hipcub::DeviceScan::ExclusiveSum(nullptr, p->scan_temp_bytes, p->d_bcnt,
+                                                  p->d_boff, nb));
+      p->d_scan_temp = dalloc<uint8_t>(p->scan_temp_bytes);
     }
-    size_t a = 0, b = 0;
-    {
-      hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
-      hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
-      SMASH_HIPX(hipcub::DeviceRadixSort::SortPairs(nullptr, a, kb, vb, 2 * P, 0, 32));
-    }
+    size_t b = 0;
     p->d_posoff = dalloc<uint32_t>(P + 1);
     p->d_cnt = dalloc<uint32_t>(P);
     SMASH_HIPX(hipcub::DeviceScan::InclusiveSum(nullptr, b, p->d_cnt, p->d_posoff + 1, P));
     size_t c3 = 0;
     SMASH_HIPX(hipcub::DeviceScan::InclusiveScan(nullptr, c3, static_cast<const int64_t *>(nullptr),
                                                  static_cast<int64_t *>(nullptr), LastValid(), P));
-    p->temp_bytes = std::max({a, b, c3});
+    p->temp_bytes = std::max(b, c3);
     p->d_temp = dalloc<uint8_t>(p->temp_bytes);
     uint64_t cap = 2 * std::max<uint64_t>(cfg->dedup_capacity, P);
     uint64_t pw = 1;
@@ -1556,7 +1439,6 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     SMASH_HIPX(hipHostMalloc(reinterpret_cast<void **>(&p->h_owner), 8 * 256, hipHostMallocDefault));
     SMASH_HIPX(hipHostMalloc(reinterpret_cast<void **>(&p->h_recv_base), 8 * 2 * 65,
                              hipHostMallocDefault));
-    SMASH_HIPX(hipEventCreateWithFlags(&p->ev_owner, hipEventDisableTiming));
     SMASH_HIPX(hipEventCreateWithFlags(&p->ev_base, hipEventDisableTiming));
     SMASH_HIPX(hipMemset(p->d_posoff, 0, 4));
   } catch (hip_failure &f) {
@@ -1596,17 +1478,16 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
   }
   if (p->ev_in) (void)hipEventDestroy(p->ev_in);
   if (p->ev_done) (void)hipEventDestroy(p->ev_done);
-  if (p->ev_owner) (void)hipEventDestroy(p->ev_owner);
   if (p->ev_base) (void)hipEventDestroy(p->ev_base);
   if (p->h_owner) (void)hipHostFree(p->h_owner);
   if (p->h_recv_base) (void)hipHostFree(p->h_recv_base);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
                   (void *)p->d_bins, (void *)p->d_cell, (void *)p->d_sp_cell,
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
-                  (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_first,
+                  (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_bcnt, (void *)p->d_boff,
+                  p->d_scan_temp, (void *)p->d_oslot,
                   (void *)p->d_slot, (void *)p->d_tsum, (void *)p->d_tlast,
-                  (void *)p->d_k[0], (void *)p->d_k[1], (void *)p->d_v[0],
-                  (void *)p->d_v[1], p->d_temp, (void *)p->d_table,
+                  p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
                   (void *)p->d_lp, (void *)p->d_lps,
@@ -1718,23 +1599,6 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
     SMASH_HIP(hipEventRecord(p->ev_free[k], s));   // the set's matches are read
   p->set_used[k] = true;
   p->cnt_ready = false;
-  return SMASH_OK;
-}
-
-// the multi-GPU export's in-batch order: stable radix sort of sort_key32,
-// value = pair (the single-GPU de-dup needs no sort: k_dedup_claim)
-static int sort_batch_keys(smash_pipeline *p, hipStream_t s) {
-  const uint64_t n_pairs = p->n_pairs;
-  k_dedup_keys<<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(p->d_nk, p->d_hash, n_pairs,
-                                                             p->d_k[0], p->d_v[0]);
-  hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
-  hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
-  size_t tb = p->temp_bytes;
-  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_pairs, 0, 32, s));
-  if (kb.Current() != p->d_k[0]) {   // keep sorted data in slot 0
-    std::swap(p->d_k[0], p->d_k[1]);
-    std::swap(p->d_v[0], p->d_v[1]);
-  }
   return SMASH_OK;
 }
 
@@ -1959,145 +1823,255 @@ namespace {
 __device__ __forceinline__ uint64_t key_owner(uint64_t hi, int world) {
   return (hi >> 1) % uint64_t(world);
 }
-// The wave's exported keys grouped by owner: for each owner present in the
-// wave, one lane adds the group's key and word totals to the owner's
-// counters and hands every lane of the group its entry and word offsets from
-// the counters' old values (counters in LDS: the block's, below).  One atomic
-// per key on W addresses serialised ~6 M same-address atomics per batch on
-// one L2 channel: 76 ms per launch at W = 1 (profiles/r03/sharded).  Every
-// lane of the wave calls it; `act` marks the lanes with a key.
-struct OwnerSlot {
-  uint64_t entry, word;
+// The export in pair order, without a sort (round 4).  Every keyed pair is
+// exported -- the in-batch first occurrence is the owner's to decide, like
+// the earlier batches' (in-batch duplicates are ~1% of the keys) -- and each
+// owner's segment of the send buffer holds its keys in pair order: a stable
+// multi-split.  Global pair order is (step, rank, pair), so an owner's
+// receive buffer (source ranks in rank order, each segment in pair order)
+// lists this step's keys in global order, and the first claim in that order
+// is the first-wins pair of smashMEM.py:217-228.
+//
+// k_export_count: per block b and owner o, the keyed pairs and their hit
+//   words, packed as keys << 32 | words into bc[o * nblk + b] (owner-major).
+//   An exclusive scan of bc then gives every (owner, block) its offsets in the
+//   owner-major send buffer: the owner's segment start plus the blocks
+//   before it (words < 2^32 per batch: n * 2 * slots <= 1.7e9).
+// k_export_fill: the same per-block grouping, each lane's rank among its
+//   block's keys of the same owner (wave ballots, then the waves before it),
+//   and the scanned block offset: the header, the words and the pair index
+//   of the send slot.
+constexpr uint32_t kExWaves = kB / 64;
+
+// per wave: for every owner present, the group's key count and word total
+// (s_e / s_w[wave][o], written by the group's first lane); each lane gets its
+// rank in the group and the words before it
+struct WaveGroup {
+  uint32_t rank, wbefore;
 };
-__device__ __forceinline__ OwnerSlot wave_owner_slots(bool act, uint32_t ow, uint32_t k,
-                                                      unsigned long long *entry_ctr,
-                                                      unsigned long long *word_ctr) {
+__device__ __forceinline__ WaveGroup wave_owner_groups(bool act, uint32_t ow, uint32_t k,
+                                                       uint32_t *s_e, uint32_t *s_w) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1;
-  OwnerSlot mine{0, 0};
+  WaveGroup mine{0, 0};
   uint64_t todo = __ballot(act);
   while (todo) {
     const int leader = __builtin_ctzll(todo);
     const uint32_t o = uint32_t(__shfl(int(ow), leader, 64));
-    const uint64_t same = __ballot(act && ow == o);
-    // inclusive scan of the group's word counts over the wave
-    uint32_t x = (act && ow == o) ? k : 0u;
-    const uint32_t own = x;
+    const bool in = act && ow == o;
+    const uint64_t same = __ballot(in);
+    uint32_t x = in ? k : 0u;   // inclusive scan of the group's word counts
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(x, d, 64);
       if (lane >= uint32_t(d)) x += y;
     }
     const uint32_t wsum = __shfl(x, 63, 64);
-    unsigned long long be = 0, bw = 0;
     if (lane == uint32_t(leader)) {
-      be = atomicAdd(&entry_ctr[o], (unsigned long long)__popcll(same));
-      bw = atomicAdd(&word_ctr[o], (unsigned long long)wsum);
+      s_e[o] = uint32_t(__popcll(same));
+      s_w[o] = wsum;
     }
-    be = __shfl(be, leader, 64);
-    bw = __shfl(bw, leader, 64);
-    if (act && ow == o) {
-      mine.entry = be + uint64_t(__popcll(same & below));
-      mine.word = bw + (x - own);
+    if (in) {
+      mine.rank = uint32_t(__popcll(same & below));
+      mine.wbefore = x - k;
     }
     todo &= ~same;
   }
   return mine;
 }
-// k_export_count / k_export_fill: the wave groups above add into per-owner
-// counters in LDS, and the block adds its totals (count) or reserves its
-// slots (fill) with one global atomic per owner present: ~2 atomics per
-// owner per 256 pairs instead of 2 per wave (1.2 ms per 6.25 M-pair batch at
-// W = 1 with wave atomics alone, profiles/r03/sharded)
-__global__ __launch_bounds__(kB) void k_export_count(const uint8_t *first, const int32_t *nk,
-                                                     const uint64_t *hash, uint64_t n, int world,
-                                                     unsigned long long *cnt) {
-  __shared__ unsigned long long s_e[64], s_w[64];
-  for (uint32_t o = threadIdx.x; o < 64; o += blockDim.x) s_e[o] = s_w[o] = 0;
-  __syncthreads();
-  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const bool act = q < n && nk[q] >= 0 && first[q];
-  const uint32_t ow = act ? uint32_t(key_owner(hash[2 * q], world)) : 0u;
-  (void)wave_owner_slots(act, ow, act ? uint32_t(nk[q]) : 0u, s_e, s_w);
-  __syncthreads();
-  for (uint32_t o = threadIdx.x; o < uint32_t(world); o += blockDim.x)
-    if (s_e[o]) {
-      atomicAdd(&cnt[o], s_e[o]);
-      atomicAdd(&cnt[128 + o], s_w[o]);
-    }
-}
-__global__ __launch_bounds__(kB) void k_export_fill(const uint8_t *first, const int32_t *nk,
-                                                    const uint64_t *hash, const uint64_t *hits,
-                                                    uint32_t slots, uint64_t n, int world,
-                                                    uint64_t gbase, unsigned long long *cnt,
-                                                    uint64_t *hdr, uint64_t *words,
-                                                    uint32_t *send_q) {
-  __shared__ unsigned long long s_e[64], s_w[64], s_be[64], s_bw[64];
-  for (uint32_t o = threadIdx.x; o < 64; o += blockDim.x) s_e[o] = s_w[o] = 0;
-  __syncthreads();
-  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const bool act = q < n && nk[q] >= 0 && first[q];
-  const uint32_t ow = act ? uint32_t(key_owner(hash[2 * q], world)) : 0u;
-  const uint64_t k = act ? uint64_t(nk[q]) : 0;
-  const OwnerSlot sl = wave_owner_slots(act, ow, uint32_t(k), s_e, s_w);   // within the block
-  __syncthreads();
-  for (uint32_t o = threadIdx.x; o < uint32_t(world); o += blockDim.x) {
-    s_be[o] = s_e[o] ? atomicAdd(&cnt[64 + o], s_e[o]) : 0;     // the block's entry slots
-    s_bw[o] = s_e[o] ? atomicAdd(&cnt[192 + o], s_w[o]) : 0;    // and word slots
+
+__global__ __launch_bounds__(kB) void k_export_count(const int32_t *nk, const uint64_t *hash,
+                                                     uint64_t n, int world, uint32_t nblk,
+                                                     uint64_t *bc) {
+  __shared__ uint32_t s_e[kExWaves][64], s_w[kExWaves][64];
+  const uint32_t wv = threadIdx.x >> 6;
+  for (uint32_t o = threadIdx.x; o < kExWaves * 64; o += blockDim.x) {
+    (&s_e[0][0])[o] = 0;
+    (&s_w[0][0])[o] = 0;
   }
   __syncthreads();
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool act = q < n && nk[q] >= 0;
+  const uint32_t ow = act ? uint32_t(key_owner(hash[2 * q], world)) : 0u;
+  (void)wave_owner_groups(act, ow, act ? uint32_t(nk[q]) : 0u, s_e[wv], s_w[wv]);
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < uint32_t(world); o += blockDim.x) {
+    uint64_t e = 0, w = 0;
+    for (uint32_t v = 0; v < kExWaves; ++v) {
+      e += s_e[v][o];
+      w += s_w[v][o];
+    }
+    bc[uint64_t(o) * nblk + blockIdx.x] = (e << 32) | w;
+  }
+}
+
+// per owner: keys, words (host images: the collectives' split sizes)
+__global__ void k_export_totals(const uint64_t *bc, const uint64_t *boff, int world,
+                                uint32_t nblk, unsigned long long *tot) {
+  const uint32_t o = threadIdx.x;
+  if (o >= uint32_t(world)) return;
+  const uint64_t last = uint64_t(o + 1) * nblk - 1;
+  const uint64_t end = boff[last] + bc[last], beg = boff[uint64_t(o) * nblk];
+  tot[o] = (end >> 32) - (beg >> 32);
+  tot[64 + o] = (end & 0xFFFFFFFFull) - (beg & 0xFFFFFFFFull);
+}
+
+__global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uint64_t *hash,
+                                                    const uint64_t *hits, uint32_t slots,
+                                                    uint64_t n, int world, uint32_t nblk,
+                                                    uint64_t gbase, const uint64_t *boff,
+                                                    uint64_t *hdr, uint64_t *words,
+                                                    uint32_t *send_q) {
+  __shared__ uint32_t s_e[kExWaves][64], s_w[kExWaves][64];
+  const uint32_t wv = threadIdx.x >> 6;
+  for (uint32_t o = threadIdx.x; o < kExWaves * 64; o += blockDim.x) {
+    (&s_e[0][0])[o] = 0;
+    (&s_w[0][0])[o] = 0;
+  }
+  __syncthreads();
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const bool act = q < n && nk[q] >= 0;
+  const uint32_t ow = act ? uint32_t(key_owner(hash[2 * q], world)) : 0u;
+  const uint32_t k = act ? uint32_t(nk[q]) : 0u;
+  const WaveGroup g = wave_owner_groups(act, ow, k, s_e[wv], s_w[wv]);
+  __syncthreads();
   if (!act) return;
-  const uint64_t o = s_be[ow] + sl.entry, w = s_bw[ow] + sl.word;
-  hdr[5 * o] = hash[2 * q];
-  hdr[5 * o + 1] = hash[2 * q + 1];
-  hdr[5 * o + 2] = gbase + q;
-  hdr[5 * o + 3] = k;
-  hdr[5 * o + 4] = w - cnt[128 + ow];   // offset in this owner's word segment
+  uint64_t e = g.rank, w = g.wbefore;
+  for (uint32_t v = 0; v < wv; ++v) {   // the block's earlier waves' keys of this owner
+    e += s_e[v][ow];
+    w += s_w[v][ow];
+  }
+  const uint64_t bo = boff[uint64_t(ow) * nblk + blockIdx.x];
+  const uint64_t seg_w = boff[uint64_t(ow) * nblk] & 0xFFFFFFFFull;   // owner's word segment
+  e += bo >> 32;
+  w += bo & 0xFFFFFFFFull;
+  hdr[5 * e] = hash[2 * q];
+  hdr[5 * e + 1] = hash[2 * q + 1];
+  hdr[5 * e + 2] = gbase + q;
+  hdr[5 * e + 3] = k;
+  hdr[5 * e + 4] = w - seg_w;   // offset in this owner's word segment
   const uint64_t *src = hits + q * 2 * uint64_t(slots);
-  for (uint64_t i = 0; i < k; ++i) words[w + i] = src[i];
-  send_q[o] = uint32_t(q);
+  for (uint32_t i = 0; i < k; ++i) words[w + i] = src[i];
+  send_q[e] = uint32_t(q);
 }
-__global__ void k_owner_keys(const uint64_t *recv, uint64_t n, uint32_t *key, uint32_t *val) {
-  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j < n) { key[j] = sort_key32(recv[5 * j]); val[j] = uint32_t(j); }
-}
+
 // base[0..world]: header prefix per source rank; base[65..65+world]: word
 // prefix per source rank
 __device__ __forceinline__ KeyRef recv_key(const uint64_t *recv, const uint64_t *words,
-                                           const uint64_t *base, int world, uint32_t j) {
+                                           const uint64_t *base, int world, uint64_t j) {
   int r = 0;
   while (r + 1 < world && j >= base[r + 1]) ++r;
   return KeyRef{words + base[65 + r] + recv[5 * j + 4], uint32_t(recv[5 * j + 3]),
                 recv[5 * j + 1]};
 }
-__global__ void k_owner_decide(const uint32_t *key, const uint32_t *val, const uint64_t *recv,
-                               const uint64_t *words, const uint64_t *base, int world,
-                               uint64_t n, uint64_t *table, uint64_t mask, uint64_t *arena,
-                               uint64_t arena_cap, unsigned long long *arena_top,
-                               uint64_t epoch, uint8_t *flags, unsigned long long *stats) {
-  const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t off =
-      wave_alloc(arena_top, s < n ? 2u + uint32_t(recv[5 * val[s] + 3]) : 0u);
-  if (s >= n) return;
-  const uint32_t j = val[s];
-  const KeyRef me = recv_key(recv, words, base, world, j);
-  const uint64_t g = recv[5 * j + 2];
-  bool win = true;   // no same key with a smaller global pair index
-  for (uint64_t t = s; t-- > 0 && key[t] == key[s];) {
-    const uint32_t j2 = val[t];
-    if (recv[5 * j2 + 2] < g && same_key(me, recv_key(recv, words, base, world, j2))) {
-      win = false;
-      break;
+
+// The owner's first-wins decision, the single-GPU claim / decide scheme
+// (k_dedup_claim / k_dedup_decide) over the received keys: key j claims an
+// empty slot with ref = epoch << 40 | (j + 1), or lowers a same-key claim of
+// this launch with atomicMin (the receive order is the global pair order, so
+// the smallest j is the first pair), or finds the key published by an
+// earlier launch (a duplicate).  k_owner_decide: j is kept iff the slot still
+// holds its own claim; the winner writes the record and publishes it.
+__global__ void k_owner_claim(const uint64_t *recv, const uint64_t *words, const uint64_t *base,
+                              int world, uint64_t n, uint64_t *table, uint64_t mask,
+                              const uint64_t *arena, uint64_t epoch, uint64_t *slot_of,
+                              unsigned long long *stats) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  int32_t err = 0;
+  for (uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const KeyRef me = recv_key(recv, words, base, world, j);
+    const uint64_t hi = recv[5 * j];
+    const unsigned long long mine = (epoch << kRefShift) | (j + 1);
+    uint64_t res = kSlotNone;
+    uint64_t i = (hi ^ (hi >> 31)) & mask;
+    uint32_t waits = 0;
+    for (uint64_t probe = 0; probe <= mask;) {
+      unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
+      unsigned long long *sr = sh + 1;
+      unsigned long long cur = __hip_atomic_load(sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == 0) {
+        const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
+        if (prev == 0) {
+          __hip_atomic_store(sr, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          res = i;
+          break;
+        }
+        cur = prev;
+      }
+      if (cur == hi) {
+        const unsigned long long ref =
+            __hip_atomic_load(sr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ref == 0) {   // the claimer is between its CAS and its ref store (k_dedup_claim)
+          if (++waits > (1u << 22)) {
+            err = SMASH_ERR_UNSUPPORTED;
+            break;
+          }
+          continue;
+        }
+        if (ref & kRefPub) {
+          if ((ref >> kRefShift) != epoch &&
+              same_key(arena + ((ref & (kRefPub - 1)) - 1), me)) {
+            res = kSlotOld;
+            break;
+          }
+        } else if ((ref >> kRefShift) == epoch) {
+          const uint64_t j2 = (ref & (kRefPub - 1)) - 1;
+          if (same_key(me, recv_key(recv, words, base, world, j2))) {
+            atomicMin(sr, mine);
+            res = i;
+            break;
+          }
+        }
+      }
+      ++probe;
+      i = (i + 1) & mask;
     }
+    if (res == kSlotNone && err == 0) err = SMASH_ERR_NOMEM;   // the set is full
+    slot_of[j] = res;
   }
-  for (uint64_t t = s + 1; win && t < n && key[t] == key[s]; ++t) {
-    const uint32_t j2 = val[t];
-    if (recv[5 * j2 + 2] < g && same_key(me, recv_key(recv, words, base, world, j2))) win = false;
-  }
+  if (err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)err);
+}
+
+__global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, const uint64_t *base,
+                               int world, uint64_t n, uint64_t *table, uint64_t *arena,
+                               uint64_t arena_cap, unsigned long long *arena_top, uint64_t epoch,
+                               const uint64_t *__restrict__ slot_of, uint8_t *flags,
+                               unsigned long long *stats) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   bool full = false;
-  const bool keep =
-      win && !set_test_insert(table, mask, recv[5 * j], me, arena, arena_cap, off, epoch, &full);
-  flags[j] = keep ? 1 : 0;
+  for (uint64_t b0 = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); b0 < n;
+       b0 += stride) {
+    const uint64_t j = b0 + (threadIdx.x & 63);
+    bool win = false;
+    uint32_t m = 0;
+    if (j < n) {
+      m = uint32_t(recv[5 * j + 3]);
+      const uint64_t sl = slot_of[j];
+      if (sl < kSlotNone) {
+        const unsigned long long ref = __hip_atomic_load(
+            reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        win = ref == ((epoch << kRefShift) | (j + 1));
+      }
+    }
+    const uint32_t need = win ? 2u + m : 0u;
+    const uint64_t off = wave_alloc(arena_top, need);   // (wave-wide)
+    if (win) {
+      if (off + need > arena_cap) {
+        full = true;   // the slot stays a claim: never matched (no kRefPub)
+      } else {
+        const KeyRef me = recv_key(recv, words, base, world, j);
+        uint64_t *rec = arena + off;
+        rec[0] = me.lo;
+        rec[1] = m;
+        for (uint32_t t = 0; t < m; ++t) rec[2 + t] = me.w[t];
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[j] + 1]),
+                           (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (j < n) flags[j] = win ? 1 : 0;
+  }
   if (full) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
 }
 __global__ void k_import(const uint8_t *flags, const uint32_t *send_q, uint64_t n_export,
@@ -2128,50 +2102,39 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
   hipStream_t s = static_cast<hipStream_t>(stream);
   p->last = s;
   const uint64_t n = p->n_pairs;
+  const uint32_t nblk = uint32_t(std::max<uint64_t>(1, (n + kB - 1) / kB));
   SMASH_HIP(hipMemsetAsync(p->d_keep, 0, n ? n : 1, s));
-  if (n) {
-    // in-batch first occurrences (mode 1: no persistent-set probe)
-    if (int rc = sort_batch_keys(p, s)) return rc;
-    k_dedup_first<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
-        p->d_k[0], p->d_v[0], n, p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_table,
-        p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, 0, 1, p->d_keep, p->d_first,
-        p->d_stats);
-  }
-  SMASH_HIP(hipMemsetAsync(p->d_owner, 0, 4 * 64 * 8, s));
-  if (n)
-    k_export_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_first, p->d_nk, p->d_hash, n,
-                                                           world, p->d_owner);
-  // the per-owner counts come to the host (the collectives' split sizes):
-  // the one synchronisation of the exchange
+  // per-owner totals to the host (the collectives' split sizes): the one
+  // synchronisation of the exchange
   unsigned long long *cnt = p->h_owner;
-  SMASH_HIP(hipEventSynchronize(p->ev_owner));   // (the last cursor upload read h_owner)
-  SMASH_HIP(hipMemcpyAsync(cnt, p->d_owner, 8 * 256, hipMemcpyDeviceToHost, s));
-  SMASH_HIP(hipStreamSynchronize(s));
+  std::fill(cnt, cnt + 128, 0ull);
+  if (n) {
+    k_export_count<<<nblk, kB, 0, s>>>(p->d_nk, p->d_hash, n, world, nblk, p->d_bcnt);
+    size_t tb = p->scan_temp_bytes;
+    SMASH_HIP(hipcub::DeviceScan::ExclusiveSum(p->d_scan_temp, tb, p->d_bcnt, p->d_boff,
+                                               uint64_t(world) * nblk, s));
+    k_export_totals<<<1, 64, 0, s>>>(p->d_bcnt, p->d_boff, world, nblk, p->d_owner);
+    SMASH_HIP(hipGetLastError());
+    SMASH_HIP(hipMemcpyAsync(cnt, p->d_owner, 8 * 128, hipMemcpyDeviceToHost, s));
+    SMASH_HIP(hipStreamSynchronize(s));
+  }
   uint64_t tot = 0, wtot = 0;
-  for (int r = 0; r < world; ++r) {   // cursors: entry and word offsets per owner
-    cnt[64 + r] = tot;
-    cnt[192 + r] = wtot;
+  for (int r = 0; r < world; ++r) {
     tot += cnt[r];
-    wtot += cnt[128 + r];
+    wtot += cnt[64 + r];
     h_send_counts[r] = int64_t(cnt[r]);
-    h_send_words[r] = int64_t(cnt[128 + r]);
+    h_send_words[r] = int64_t(cnt[64 + r]);
   }
   p->n_export = tot;
-  if (wtot > p->send_words_cap) {
-    SMASH_HIP(hipStreamSynchronize(s));
+  if (wtot > p->send_words_cap) {   // (the stream is synchronised above)
     if (p->d_send_words) SMASH_HIP(hipFree(p->d_send_words));
     p->send_words_cap = wtot + wtot / 4 + 1024;
     SMASH_HIP(hipMalloc(&p->d_send_words, 8 * p->send_words_cap));
   }
-  // [128 + r] (the word counts, read above) now holds owner r's word-segment
-  // start, for the offsets relative to it (the cursors at [192 + r] move)
-  for (int r = 0; r < world; ++r) cnt[128 + r] = cnt[192 + r];
-  SMASH_HIP(hipMemcpyAsync(p->d_owner, cnt, 8 * 256, hipMemcpyHostToDevice, s));
-  SMASH_HIP(hipEventRecord(p->ev_owner, s));
   if (n)
-    k_export_fill<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(
-        p->d_first, p->d_nk, p->d_hash, p->d_hits, p->slots, n, world, global_base, p->d_owner,
-        p->d_send_hdr, p->d_send_words, p->d_send_q);
+    k_export_fill<<<nblk, kB, 0, s>>>(p->d_nk, p->d_hash, p->d_hits, p->slots, n, world, nblk,
+                                      global_base, p->d_boff, p->d_send_hdr, p->d_send_words,
+                                      p->d_send_q);
   SMASH_HIP(hipGetLastError());
   *d_send = p->d_send_hdr;
   *d_send_words = p->d_send_words;
@@ -2185,10 +2148,6 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   if (!p || world < 1 || world > 64 || !h_recv_counts || !h_recv_words ||
       (n_recv && (!d_recv || !d_flags))) {
     set_error("smash_dedup_owner: bad arguments");
-    return SMASH_ERR_ARG;
-  }
-  if (n_recv > 2 * p->max_pairs) {
-    set_error("smash_dedup_owner: more keys than 2 * cfg.max_pairs");
     return SMASH_ERR_ARG;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -2210,18 +2169,22 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   base[65 + world] = ws;
   p->last = s;
   if (!n_recv) return SMASH_OK;
+  if (n_recv > p->oslot_cap) {   // the claims' slot per received key
+    SMASH_HIP(hipStreamSynchronize(s));
+    if (p->d_oslot) SMASH_HIP(hipFree(p->d_oslot));
+    p->oslot_cap = n_recv + n_recv / 4 + 1024;
+    SMASH_HIP(hipMalloc(reinterpret_cast<void **>(&p->d_oslot), 8 * p->oslot_cap));
+  }
   SMASH_HIP(hipMemcpyAsync(p->d_recv_base, base, 8 * 2 * 65, hipMemcpyHostToDevice, s));
   SMASH_HIP(hipEventRecord(p->ev_base, s));
-  // reuse the sort buffers (phase_map's sorted keys are no longer needed)
-  k_owner_keys<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(d_recv, n_recv, p->d_k[0], p->d_v[0]);
-  hipcub::DoubleBuffer<uint32_t> kb(p->d_k[0], p->d_k[1]);
-  hipcub::DoubleBuffer<uint32_t> vb(p->d_v[0], p->d_v[1]);
-  size_t tb = p->temp_bytes;
-  SMASH_HIP(hipcub::DeviceRadixSort::SortPairs(p->d_temp, tb, kb, vb, n_recv, 0, 32, s));
-  k_owner_decide<<<grid_for(n_recv, kB, 1u << 30), kB, 0, s>>>(
-      kb.Current(), vb.Current(), d_recv, d_recv_words, p->d_recv_base, world, n_recv,
-      p->d_table, p->table_mask, p->d_arena, p->arena_cap, p->d_arena_top, next_epoch(p), d_flags,
-      p->d_stats);
+  const uint64_t epoch = next_epoch(p);
+  k_owner_claim<<<grid_for(n_recv, kB, 8192), kB, 0, s>>>(
+      d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->table_mask, p->d_arena,
+      epoch, p->d_oslot, p->d_stats);
+  SMASH_HIP(hipGetLastError());
+  k_owner_decide<<<grid_for(n_recv, kB, 8192), kB, 0, s>>>(
+      d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->d_arena, p->arena_cap,
+      p->d_arena_top, epoch, p->d_oslot, d_flags, p->d_stats);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }
