@@ -497,6 +497,48 @@ int smash_fastq_index_open(const char *const *r1, uint32_t n1, const char *const
 int smash_fastq_index_pack(smash_fastq_index *ix, uint64_t k0, uint64_t k1, uint8_t *h_reads,
                            char *h_names, uint32_t name_stride);
 void smash_fastq_index_close(smash_fastq_index *ix);
+/* Rank-local ingest for the multi-GPU driver (smash-paper_amd/dist.py): no
+ * rank reads the whole input (smash_mapping.sh:19 streams zcat into
+ * fastqs_to_sam; query.cpp:614-740 holds one ring of reads at a time).
+ *  _scan: the two lists are cut into segments (plain files: 64 MB byte ranges,
+ *    gzip files: whole), dealt to `world` ranks; rank `rank` scans its own on
+ *    `threads` threads -- records per segment, empty records, read-1 order,
+ *    and for gzip restart points every 32 MB of output (zran: compressed
+ *    offset, bits, 32 KB window) -- into *blob (free: _free_blob).
+ *  _open: every rank passes all ranks' blobs (all-gathered by the caller, in
+ *    rank order) and gets the same plan: *n_pairs planned pairs (pairs whose
+ *    two mates are empty dropped) of *len bases (in: 0 or the required one).
+ *    sort_names 0: out-of-order read-1 names are SMASH_ERR_ARG; 1: the input
+ *    must be in order already (SMASH_ERR_UNSUPPORTED otherwise: sorting needs
+ *    the whole input, smash_fastq_index).  Not strict 4-line FASTQ, or a last
+ *    line without a newline: SMASH_ERR_UNSUPPORTED.
+ *  _pack: planned pairs [k0, k1) into h_reads (2 (k1 - k0) len bytes, as
+ *    smash_fastq_index_pack) on the plan's threads, reading only those pairs'
+ *    bytes (plus at most a segment / restart span before each thread's first).
+ *  _stats: bytes scanned and packed by this rank (the share it read). */
+typedef struct smash_fastq_shards smash_fastq_shards;
+typedef struct {
+  uint64_t input_bytes;      /* all files of both lists (on disk) */
+  uint64_t scan_segments;    /* segments this rank scanned */
+  uint64_t scan_bytes;       /* FASTQ bytes this rank scanned (gzip: inflated) */
+  uint64_t scan_bytes_in;    /* file bytes this rank read in the scan */
+  double scan_s;
+  uint64_t pack_pairs;       /* pairs packed */
+  uint64_t pack_bytes;       /* FASTQ bytes parsed by the packs (gzip: inflated) */
+  uint64_t pack_bytes_in;    /* compressed bytes the packs read (gzip) */
+  double pack_s;
+} smash_shard_stats;
+int smash_fastq_shard_scan(const char *const *r1, uint32_t n1, const char *const *r2, uint32_t n2,
+                           uint32_t world, uint32_t rank, uint32_t threads, void **blob,
+                           uint64_t *blob_bytes);
+void smash_fastq_shard_free_blob(void *blob);
+int smash_fastq_shard_open(const char *const *r1, uint32_t n1, const char *const *r2, uint32_t n2,
+                           uint32_t world, uint32_t rank, const void *const *blobs,
+                           const uint64_t *blob_bytes, uint32_t threads, uint32_t *len,
+                           int sort_names, smash_fastq_shards **out, uint64_t *n_pairs);
+int smash_fastq_shard_pack(smash_fastq_shards *h, uint64_t k0, uint64_t k1, uint8_t *h_reads);
+int smash_fastq_shard_stats(smash_fastq_shards *h, smash_shard_stats *stats);
+void smash_fastq_shard_close(smash_fastq_shards *h);
 int smash_count_fastq(smash_pipeline *p, const char *const *r1_paths, uint32_t n1,
                       const char *const *r2_paths, uint32_t n2, int sort_names,
                       uint32_t threads, uint64_t *d_counts, smash_feed_stats *stats,

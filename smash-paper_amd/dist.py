@@ -64,6 +64,23 @@ class TorchComm:
     def all_gather(self, parts, t):
         dist.all_gather(parts, t, group=self.group)
 
+    def all_gather_bytes(self, b):
+        """every rank's byte string, in rank order (the ingest scans)"""
+        g = self.count_group if self.count_group is not None else self.group
+        dev = torch.device("cpu") if self.count_group is not None else self.device
+        W = dist.get_world_size(g)
+        n = torch.tensor([len(b)], dtype=torch.int64, device=dev)
+        ns = [torch.empty_like(n) for _ in range(W)]
+        dist.all_gather(ns, n, group=g)
+        sizes = [int(x.item()) for x in ns]
+        m = max(max(sizes), 1)
+        buf = torch.zeros(m, dtype=torch.uint8, device=dev)
+        if b:
+            buf[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+        parts = [torch.empty_like(buf) for _ in range(W)]
+        dist.all_gather(parts, buf, group=g)
+        return [bytes(parts[r][:sizes[r]].cpu().numpy().tobytes()) for r in range(W)]
+
 
 class ShardedCounter:
     def __init__(self, pipe, rank, world, device, group=None, count_group=None, comm=None):
@@ -168,10 +185,30 @@ class ShardedCounter:
         return torch.where(last >= 0, pick, carried)
 
 
+def open_fastq(sc, r1_paths, r2_paths, sort_names=False, threads=0, read_len=0):
+    """The FASTQ lists of a multi-GPU run, read rank-locally
+    (smashgpu.FastqShards: each rank scans ~1/W of the bytes, the scans are
+    all-gathered over the communicator, and each batch is read from only
+    its own pairs' bytes).  Input the rank-local reader cannot take (not
+    strict 4-line FASTQ, or not in name order when sort_names) goes to
+    smashgpu.FastqIndex, which every rank builds over the whole input --
+    the same decision on every rank, since every rank sees every scan."""
+    import smashgpu as S
+    try:
+        return S.FastqShards(r1_paths, r2_paths, sc.rank, sc.world, sc.comm.all_gather_bytes,
+                             threads=threads, read_len=read_len, sort_names=sort_names)
+    except S.SmashError as e:
+        if getattr(e, "code", None) != S.SMASH_ERR_UNSUPPORTED:
+            raise
+    return S.FastqIndex(r1_paths, r2_paths, threads=threads, read_len=read_len,
+                        sort_names=sort_names)
+
+
 def count_fastq(sc, index, batch, d_counts, look_ahead=True, pin=True):
     """File-fed multi-GPU run (smash_mapping.sh:19-29 over `world` ranks):
-    every rank holds the same smashgpu.FastqIndex (both FASTQ lists indexed
-    once, pairs in samtools sort -n order) and takes, in step s, planned pairs
+    every rank holds the same plan of both FASTQ lists (open_fastq: the
+    rank-local smashgpu.FastqShards, or smashgpu.FastqIndex; pairs in
+    samtools sort -n order) and takes, in step s, planned pairs
     [s W batch + rank batch, + batch): the global name order stays (step,
     rank, pair), which is what ShardedCounter's first-wins de-dup and
     adjacent-dup boundary assume.  Every rank runs the same number of steps

@@ -291,15 +291,28 @@ def cmd_map(args):
         o.write("%d dupes\t%d non-dupes\n" % (st.dupe_pairs, st.key_pairs - st.dupe_pairs))
 
 
-def fastq_pairs_bound(paths, L):
-    """An upper bound on the pairs in the read-1 FASTQ list, for the key-set
-    capacity: a record is at least 2 L + 6 bytes ("@x", seq, "+", qual);
-    gzip is taken at <= 8x compression (FASTQ runs 3-5x).  A bound that is
-    still too small fails the run (SMASH_ERR_NOMEM), never cuts the set."""
+def _is_gzip(path):
+    with open(path, "rb") as f:
+        return f.read(2) == b"\x1f\x8b"
+
+
+def fastq_pairs_bound(r1, r2, L):
+    """The key-set capacity of a file-fed run: at most the pairs of the lists.
+    Plain files: a record is at least 2 L + 6 bytes ("@x", seq, "+", qual),
+    a safe upper bound from the sizes.  With gzip files the pairs are counted
+    (the rank-local scan at world 1: each gzip file inflated once, in bounded
+    buffers), since no compression ratio bounds them; input that scan cannot
+    take falls back to 8x compression.  A set that is still too small fails
+    the run (SMASH_ERR_NOMEM), never cuts it."""
+    if any(_is_gzip(p) for p in r1 + r2):
+        try:
+            return max(S.FastqShards(r1, r2, 0, 1, lambda b: [b]).n, 1)
+        except S.SmashError:
+            pass
     n = 0
-    for p in paths:
+    for p in r1:
         z = os.path.getsize(p)
-        n += (8 * z if p.endswith(".gz") else z) // (2 * L + 6) + 1
+        n += (8 * z if _is_gzip(p) else z) // (2 * L + 6) + 1
     return max(n, 1)
 
 
@@ -320,7 +333,7 @@ def _count_files(args, bins):
     rows, starts = S.read_bins(bins)
     r1, r2 = args.reads1.split(), args.reads2.split()
     L = S.first_read_length(r1)
-    cap = args.dedup_capacity or fastq_pairs_bound(r1, L)
+    cap = args.dedup_capacity or fastq_pairs_bound(r1, r2, L)
     pipe = S.Pipeline(ix, cs, starts, L, args.batch, dedup_capacity=cap)
     counts = torch.zeros(len(starts), dtype=torch.int64, device=torch.device("cuda", args.device))
     pipe.reset()
@@ -331,6 +344,10 @@ def _count_files(args, bins):
     return rows, counts.cpu().numpy(), st
 
 
+class _NoPipe:
+    max_pairs = 0
+
+
 def _count_files_dist(args, bins, world):
     """count over `world` ranks (one process per GPU, torch.distributed over
     RCCL: torchrun sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*): every rank
@@ -339,7 +356,7 @@ def _count_files_dist(args, bins, world):
     are summed over the ranks; rank 0 writes the output."""
     import torch
     import torch.distributed as tdist
-    from dist import ShardedCounter, count_fastq
+    from dist import ShardedCounter, count_fastq, open_fastq
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
@@ -351,7 +368,10 @@ def _count_files_dist(args, bins, world):
     cs = S.read_chrom_sizes(args.chrom_sizes or ref + ".bin/chrom_sizes.txt")
     rows, starts = S.read_bins(bins)
     r1, r2 = args.reads1.split(), args.reads2.split()
-    fq = S.FastqIndex(r1, r2, sort_names=not args.presorted)
+    # the pipeline is made once the plan (pairs, read length) is known: a
+    # placeholder counter carries the communicator for the scan exchange
+    sc = ShardedCounter(_NoPipe(), rank, world, dev, count_group=cpu)
+    fq = open_fastq(sc, r1, r2, sort_names=not args.presorted)
     # an owner keeps the keys it owns for the whole run: ~pairs / world
     cap = args.dedup_capacity or (fq.n // world + fq.n // (8 * world) + (1 << 20))
     pipe = S.Pipeline(ix, cs, starts, fq.L, args.batch, dedup_capacity=cap)

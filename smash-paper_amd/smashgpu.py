@@ -58,6 +58,8 @@ EXPORTS = [
     "smash_phase_map_ahead", "smash_sam_records_packed",
     "smash_text_from_fasta_layout", "smash_index_create_layout", "smash_index_load_layout",
     "smash_phase_search_ahead",
+    "smash_fastq_shard_scan", "smash_fastq_shard_free_blob", "smash_fastq_shard_open",
+    "smash_fastq_shard_pack", "smash_fastq_shard_stats", "smash_fastq_shard_close",
 ]
 
 
@@ -85,6 +87,16 @@ class FeedStats(C.Structure):
     _fields_ = [("pairs", C.c_uint64), ("batches", C.c_uint64), ("wall_s", C.c_double),
                 ("ingest_s", C.c_double), ("wait_s", C.c_double), ("read_len", C.c_uint32),
                 ("parallel", C.c_uint32), ("index_s", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class ShardStats(C.Structure):
+    _fields_ = [("input_bytes", C.c_uint64), ("scan_segments", C.c_uint64),
+                ("scan_bytes", C.c_uint64), ("scan_bytes_in", C.c_uint64), ("scan_s", C.c_double),
+                ("pack_pairs", C.c_uint64), ("pack_bytes", C.c_uint64),
+                ("pack_bytes_in", C.c_uint64), ("pack_s", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -192,6 +204,19 @@ def lib():
     L.smash_fastq_read_parallel.argtypes = [C.POINTER(C.c_char_p), C.c_uint32,
                                             C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
                                             u32p, C.c_uint64, vp, vp, C.c_uint32, u64p]
+    L.smash_fastq_shard_scan.argtypes = [C.POINTER(C.c_char_p), C.c_uint32,
+                                         C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.POINTER(vp), u64p]
+    L.smash_fastq_shard_free_blob.argtypes = [vp]
+    L.smash_fastq_shard_free_blob.restype = None
+    L.smash_fastq_shard_open.argtypes = [C.POINTER(C.c_char_p), C.c_uint32,
+                                         C.POINTER(C.c_char_p), C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.POINTER(vp), u64p, C.c_uint32, u32p,
+                                         C.c_int, C.POINTER(vp), u64p]
+    L.smash_fastq_shard_pack.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
+    L.smash_fastq_shard_stats.argtypes = [vp, C.POINTER(ShardStats)]
+    L.smash_fastq_shard_close.argtypes = [vp]
+    L.smash_fastq_shard_close.restype = None
     L.smash_count_fastq.argtypes = [vp, C.POINTER(C.c_char_p), C.c_uint32,
                                     C.POINTER(C.c_char_p), C.c_uint32, C.c_int, C.c_uint32, vp,
                                     C.POINTER(FeedStats), vp]
@@ -853,6 +878,82 @@ class FastqIndex:
     def close(self):
         if self.h:
             lib().smash_fastq_index_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+SMASH_ERR_UNSUPPORTED = -5
+
+
+class FastqShards:
+    """The rank-local reader of the multi-GPU driver (smash_fastq_shard_*):
+    this rank scans only its share of the segments of both FASTQ lists,
+    `allgather(bytes) -> [bytes of rank 0, ..., rank world-1]` exchanges the
+    scans, and every rank gets the same plan.  Same interface as FastqIndex
+    (.n planned pairs of .L bases, pack(k0, k1, out)), but a pack reads only
+    the bytes of the pairs asked for.  Raises SmashError with .code
+    SMASH_ERR_UNSUPPORTED where FastqIndex must take over (input not strict
+    4-line FASTQ, or not in samtools sort -n order when sort_names)."""
+
+    def __init__(self, r1_paths, r2_paths, rank, world, allgather, threads=0, read_len=0,
+                 sort_names=False):
+        a1 = _cstrs([os.fsencode(p) for p in r1_paths])
+        a2 = _cstrs([os.fsencode(p) for p in r2_paths])
+        T = threads or min(16, os.cpu_count() or 1)
+        blob, nb = vp(), C.c_uint64()
+        L = lib()
+        rc = L.smash_fastq_shard_scan(a1, len(r1_paths), a2, len(r2_paths), world, rank, T,
+                                      C.byref(blob), C.byref(nb))
+        mine = b""
+        err = None
+        if rc == 0:
+            mine = C.string_at(blob.value, nb.value)
+            L.smash_fastq_shard_free_blob(blob)
+        else:
+            err = (rc, L.smash_last_error().decode(errors="replace"))
+        blobs = allgather(mine)     # every rank joins, even after a local failure
+        if err is not None:
+            e = SmashError("smash_fastq_shard_scan failed (%d): %s" % err)
+            e.code = err[0]
+            raise e
+        if any(len(b) == 0 for b in blobs):
+            e = SmashError("smash_fastq_shard_scan failed on another rank")
+            e.code = -1
+            raise e
+        bufs = [C.create_string_buffer(b, len(b)) for b in blobs]
+        ptrs = (vp * world)(*[C.cast(b, vp) for b in bufs])
+        sizes = np.array([len(b) for b in blobs], np.uint64)
+        Lr = C.c_uint32(read_len)
+        n = C.c_uint64()
+        h = vp()
+        rc = L.smash_fastq_shard_open(a1, len(r1_paths), a2, len(r2_paths), world, rank, ptrs,
+                                      _p(sizes, u64p), T, C.byref(Lr), int(bool(sort_names)),
+                                      C.byref(h), C.byref(n))
+        if rc != 0:
+            e = SmashError("smash_fastq_shard_open failed (%d): %s"
+                           % (rc, L.smash_last_error().decode(errors="replace")))
+            e.code = rc
+            raise e
+        self.h, self.n, self.L = h, n.value, Lr.value
+
+    def pack(self, k0, k1, out):
+        ptr = out.data_ptr() if hasattr(out, "data_ptr") else out.ctypes.data
+        check(lib().smash_fastq_shard_pack(self.h, k0, k1, vp(ptr)), "smash_fastq_shard_pack")
+        return out
+
+    def stats(self):
+        st = ShardStats()
+        check(lib().smash_fastq_shard_stats(self.h, C.byref(st)), "smash_fastq_shard_stats")
+        return st.as_dict()
+
+    def close(self):
+        if self.h:
+            lib().smash_fastq_shard_close(self.h)
             self.h = None
 
     def __del__(self):

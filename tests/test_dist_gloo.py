@@ -118,7 +118,7 @@ def _worker_files(rank, world, port, batch, paths, out_q):
     import oracle as O
     import smashgpu as S
     from mock_pipeline import OraclePhasePipeline
-    from dist import ShardedCounter, count_fastq
+    from dist import ShardedCounter, count_fastq, open_fastq
     d = tempfile.mkdtemp()
     fa = os.path.join(d, "tiny.fa")
     with gzip.open(gold("tiny.fa.gz"), "rb") as f, open(fa, "wb") as g:
@@ -129,15 +129,21 @@ def _worker_files(rank, world, port, batch, paths, out_q):
     pipe = OraclePhasePipeline(oix, oix.mappability(), cs, starts, batch)
     cg = dist.new_group(backend="gloo")
     sc = ShardedCounter(pipe, rank, world, torch.device("cpu"), count_group=cg)
-    fq = S.FastqIndex(*paths, threads=2)
+    fq = open_fastq(sc, *paths, threads=2)   # the rank-local reader (scans all-gathered over gloo)
+    assert isinstance(fq, S.FastqShards)
     counts = torch.zeros(len(starts), dtype=torch.int64)
     sc.reset()
     done = count_fastq(sc, fq, batch, counts)
+    rs = fq.stats()
+    assert rs["pack_pairs"] == done
     dist.all_reduce(counts)
     st = torch.tensor([pipe.total, pipe.dups, pipe.kept, done], dtype=torch.int64)
     dist.all_reduce(st)
+    sc_bytes = torch.tensor([rs["scan_bytes"]], dtype=torch.int64)
+    parts = [torch.empty_like(sc_bytes) for _ in range(world)]
+    dist.all_gather(parts, sc_bytes)
     if rank == 0:
-        out_q.put((counts.numpy().tolist(), st.tolist()))
+        out_q.put((counts.numpy().tolist(), st.tolist(), [int(x) for x in parts]))
     dist.destroy_process_group()
 
 
@@ -179,10 +185,14 @@ def test_file_fed_ranks_match_single_process(world, batch, tiny_ix, tmp_path):
         if res is None:
             p.terminate()
     assert res is not None, [p.exitcode for p in procs]
-    got_counts, got_stats = res
+    got_counts, got_stats, scanned = res
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    # each rank scanned a share, not the whole input (every byte once in all)
+    text = sum(len(gzip.open(p, "rb").read()) if p.endswith(".gz") else len(open(p, "rb").read())
+               for p in lanes[0] + lanes[1])
+    assert sum(scanned) >= text and all(x < text for x in scanned), (scanned, text)
     _, reads = S.read_fastq_pairs(*lanes)
     _, starts = load_bins(gold("tiny_bins.txt"))
     cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))

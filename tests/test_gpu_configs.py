@@ -428,9 +428,11 @@ def test_c4_real_driver_files_threads_equal_oracle(c4_run, c4_fastq, W, batch):
     look-ahead packing, short and empty last shares) == the oracle."""
     from thread_ranks import run_files
     dix, cs, starts, _, _, orc = c4_run
-    total, st, done = run_files(dix, c4_fastq, W, batch, starts, cs, capacity=C4_PAIRS)
+    total, st, done, rs = run_files(dix, c4_fastq, W, batch, starts, cs, capacity=C4_PAIRS)
     assert sum(done) == C4_PAIRS
     assert np.array_equal(total, orc[0]) and st == orc[1]
+    # rank-local: each rank packed only its own pairs
+    assert [r["pack_pairs"] for r in rs] == done
 
 
 def _port():
@@ -449,7 +451,8 @@ def test_c4_real_driver_rccl_world1_equals_oracle(c4_run, c4_fastq, monkeypatch)
     with the key hash cut to 18 bits, and dist.count_fastq from the lane
     files -- all == the oracle."""
     import torch.distributed as tdist
-    from dist import ShardedCounter, count_fastq
+    from dist import ShardedCounter, count_fastq, open_fastq
+    from thread_ranks import _NoPipe
     dix, cs, starts, d_reads, _, orc = c4_run
     dev = torch.device("cuda", 0)
     tdist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _port(), rank=0,
@@ -479,8 +482,8 @@ def test_c4_real_driver_rccl_world1_equals_oracle(c4_run, c4_fastq, monkeypatch)
             assert (s.positions, s.dups, s.kept, s.dupe_pairs) == orc[1], bits
             del pipe
         monkeypatch.delenv("SMASH_KEY_HASH_BITS")
-        fq = S.FastqIndex(*c4_fastq)
-        assert fq.n == C4_PAIRS
+        fq = open_fastq(ShardedCounter(_NoPipe(), 0, 1, dev, count_group=cg), *c4_fastq)
+        assert fq.n == C4_PAIRS and isinstance(fq, S.FastqShards)
         pipe = S.Pipeline(dix, cs, starts, fq.L, 70_000, dedup_capacity=C4_PAIRS)
         counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
         sc = ShardedCounter(pipe, 0, 1, dev, count_group=cg)

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 import smashgpu as S
-from dist import ShardedCounter, count_fastq
+from dist import ShardedCounter, count_fastq, open_fastq
 
 
 class ThreadWorld:
@@ -67,6 +67,13 @@ class ThreadComm:
         for s in range(self.tw.world):
             parts[s].copy_(self.tw.slot[s])
         self._done()
+
+    def all_gather_bytes(self, b):
+        self.tw.slot[self.rank] = b
+        self.tw.barrier.wait()
+        got = list(self.tw.slot)
+        self.tw.barrier.wait()
+        return got
 
 
 def _run_threads(world, body):
@@ -140,11 +147,33 @@ def run_resident(ix, d_reads, world, per_rank, starts, cs, ahead2=True, capacity
     return _summary(pipes, counts)
 
 
-def run_files(ix, paths, world, batch, starts, cs, capacity):
-    """dist.count_fastq over `world` ranks, each with its own
-    smashgpu.FastqIndex of the same lists (as smash_cli count runs under
-    torchrun).  Returns (counts, stats, pairs counted per rank)."""
-    fqs = [S.FastqIndex(*paths) for _ in range(world)]
+def run_files(ix, paths, world, batch, starts, cs, capacity, shards=True):
+    """dist.count_fastq over `world` ranks, each opening the lists as
+    smash_cli count does under torchrun (dist.open_fastq: the rank-local
+    reader; shards=False: every rank its own whole-input FastqIndex).
+    Returns (counts, stats, pairs counted per rank, reader stats per rank)."""
+    tw = ThreadWorld(world)
+    fqs = [None] * world
+    errs = [None] * world
+
+    def opener(r):
+        try:
+            if shards:
+                fqs[r] = open_fastq(ShardedCounter(_NoPipe(), r, world, torch.device("cuda"),
+                                                   comm=tw.comm(r)), *paths)
+            else:
+                fqs[r] = S.FastqIndex(*paths)
+        except BaseException as e:   # noqa: BLE001
+            errs[r] = e
+            tw.barrier.abort()
+    th = [threading.Thread(target=opener, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
     L = fqs[0].L
     pipes, counts = make_pipes(ix, world, cs, starts, L, batch, capacity)
     done = [0] * world
@@ -156,4 +185,9 @@ def run_files(ix, paths, world, batch, starts, cs, capacity):
 
     _run_threads(world, body)
     total, st = _summary(pipes, counts)
-    return total, st, done
+    rstats = [f.stats() if hasattr(f, "stats") else None for f in fqs]
+    return total, st, done, rstats
+
+
+class _NoPipe:
+    max_pairs = 0
