@@ -217,3 +217,49 @@ def test_shards_blob_mismatch_is_refused(lanes):
     it = iter([blobs])
     with pytest.raises(S.SmashError, match="not a scan of these files"):
         S.FastqShards(*lanes, rank=0, world=2, allgather=lambda b: next(it))
+
+
+_RSS_SCRIPT = r"""
+import gzip, os, resource, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import smashgpu as S
+paths = [[sys.argv[2]], [sys.argv[3]]]
+S.lib()
+base = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+x = S.FastqShards(*paths, rank=0, world=1, allgather=lambda b: [b], threads=4)
+out = np.zeros((2 * 20000, x.L), np.uint8)
+for k0 in range(0, x.n, 20000):
+    k1 = min(x.n, k0 + 20000)
+    x.pack(k0, k1, out)
+print(x.n, (resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - base) * 1024)
+"""
+
+
+def test_shards_host_memory_is_bounded(tmp_path):
+    """A rank's host memory does not grow with the input: ~400 MB of FASTQ
+    text (gzip, one file per mate) scanned and packed in batches of 20 000
+    pairs raises the process's peak RSS by far less than the text (the
+    readers keep bounded buffers: restart windows, 8 MB cursors, 4 MB input
+    chunks; no whole file)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    recs = [_records("s150", 1), _records("s150", 2)]
+    paths = []
+    for m in (0, 1):
+        f = tmp_path / ("m%d.fq.gz" % m)
+        with gzip.open(f, "wb", compresslevel=1) as g:
+            for c in range(1000):
+                g.write(b"".join(b"@c%04d_%06d\n" % (c, k) + r.split(b"\n", 1)[1]
+                                 for k, r in enumerate(recs[m])))
+        paths.append(str(f))
+    text = 2 * 1000 * sum(len(r) for r in recs[0])
+    res = subprocess.run([sys.executable, "-c", _RSS_SCRIPT,
+                          os.path.join(ROOT, "smash-paper_amd"), *paths],
+                         capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    n, grew = (int(v) for v in res.stdout.split())
+    assert n == 1000 * len(recs[0])
+    assert grew < 96 << 20 and grew < text / 3, (grew, text)
