@@ -68,10 +68,80 @@ struct Source {
   }
 };
 
-// open every path: a file that starts with the gzip magic is inflated into
-// memory (zlib reads concatenated members), another is mapped; a file whose
-// last byte is not '\n' is copied with one appended (every line of every
-// record then ends in '\n').  Files load in parallel.
+// open one file: one that starts with the gzip magic is inflated into memory
+// (zlib reads concatenated members), another is mapped; a file whose last
+// byte is not '\n' is copied with one appended (every line of every record
+// then ends in '\n').  false: why says what failed.
+inline bool load_source(Source &s, std::string &why) {
+  const int fd = open(s.path.c_str(), O_RDONLY);
+  if (fd < 0) {
+    why = "cannot open " + s.path;
+    return false;
+  }
+  struct stat stt;
+  unsigned char magic[2] = {0, 0};
+  const bool ok = fstat(fd, &stt) == 0 && (stt.st_size < 2 || pread(fd, magic, 2, 0) == 2);
+  if (!ok) {
+    close(fd);
+    why = "cannot read " + s.path;
+    return false;
+  }
+  const size_t size = size_t(stt.st_size);
+  if (size >= 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+    close(fd);
+    gzFile g = gzopen(s.path.c_str(), "rb");
+    if (!g) {
+      why = "cannot open " + s.path;
+      return false;
+    }
+    gzbuffer(g, 1 << 20);
+    s.buf.resize(std::max<size_t>(size * 4, 1 << 20));
+    size_t fill = 0;
+    for (;;) {
+      if (fill == s.buf.size()) s.buf.resize(s.buf.size() * 2);
+      const size_t want = std::min<size_t>(s.buf.size() - fill, size_t(1) << 30);
+      const int r = gzread(g, s.buf.data() + fill, unsigned(want));
+      if (r < 0) {
+        why = "read error in " + s.path;
+        gzclose(g);
+        return false;
+      }
+      if (r == 0) break;
+      fill += size_t(r);
+    }
+    gzclose(g);
+    s.buf.resize(fill);
+    if (fill && s.buf.back() != '\n') s.buf.push_back('\n');
+    s.p = s.buf.data();
+    s.n = s.buf.size();
+    return true;
+  }
+  if (size == 0) {
+    close(fd);
+    return true;
+  }
+  void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) {
+    why = "cannot map " + s.path;
+    return false;
+  }
+  s.map = m;
+  s.maplen = size;
+  s.p = static_cast<const char *>(m);
+  s.n = size;
+  if (s.p[size - 1] != '\n') {   // (rare) give the last line its newline
+    s.buf.assign(s.p, s.p + size);
+    s.buf.push_back('\n');
+    munmap(m, size);
+    s.map = nullptr;
+    s.p = s.buf.data();
+    s.n = s.buf.size();
+  }
+  return true;
+}
+
+// open every path (load_source), in parallel
 inline bool load_sources(const std::vector<std::string> &paths, uint32_t T,
                          std::vector<std::unique_ptr<Source>> &out, std::string &msg, int &err) {
   out.clear();
@@ -83,78 +153,8 @@ inline bool load_sources(const std::vector<std::string> &paths, uint32_t T,
   std::atomic<int> bad{0};
   std::vector<std::string> why(out.size());
   run_threads(std::min<uint32_t>(T, uint32_t(out.size())), [&](uint32_t) {
-    for (size_t k; (k = next++) < out.size();) {
-      Source &s = *out[k];
-      const int fd = open(s.path.c_str(), O_RDONLY);
-      if (fd < 0) {
-        why[k] = "cannot open " + s.path;
-        bad = 1;
-        continue;
-      }
-      struct stat stt;
-      unsigned char magic[2] = {0, 0};
-      const bool ok = fstat(fd, &stt) == 0 && (stt.st_size < 2 || pread(fd, magic, 2, 0) == 2);
-      if (!ok) {
-        close(fd);
-        why[k] = "cannot read " + s.path;
-        bad = 1;
-        continue;
-      }
-      const size_t size = size_t(stt.st_size);
-      if (size >= 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
-        close(fd);
-        gzFile g = gzopen(s.path.c_str(), "rb");
-        if (!g) {
-          why[k] = "cannot open " + s.path;
-          bad = 1;
-          continue;
-        }
-        gzbuffer(g, 1 << 20);
-        s.buf.resize(std::max<size_t>(size * 4, 1 << 20));
-        size_t fill = 0;
-        for (;;) {
-          if (fill == s.buf.size()) s.buf.resize(s.buf.size() * 2);
-          const size_t want = std::min<size_t>(s.buf.size() - fill, size_t(1) << 30);
-          const int r = gzread(g, s.buf.data() + fill, unsigned(want));
-          if (r < 0) {
-            why[k] = "read error in " + s.path;
-            bad = 1;
-            break;
-          }
-          if (r == 0) break;
-          fill += size_t(r);
-        }
-        gzclose(g);
-        s.buf.resize(fill);
-        if (fill && s.buf.back() != '\n') s.buf.push_back('\n');
-        s.p = s.buf.data();
-        s.n = s.buf.size();
-        continue;
-      }
-      if (size == 0) {
-        close(fd);
-        continue;
-      }
-      void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
-      close(fd);
-      if (m == MAP_FAILED) {
-        why[k] = "cannot map " + s.path;
-        bad = 1;
-        continue;
-      }
-      s.map = m;
-      s.maplen = size;
-      s.p = static_cast<const char *>(m);
-      s.n = size;
-      if (s.p[size - 1] != '\n') {   // (rare) give the last line its newline
-        s.buf.assign(s.p, s.p + size);
-        s.buf.push_back('\n');
-        munmap(m, size);
-        s.map = nullptr;
-        s.p = s.buf.data();
-        s.n = s.buf.size();
-      }
-    }
+    for (size_t k; (k = next++) < out.size();)
+      if (!load_source(*out[k], why[k])) bad = 1;
   });
   if (bad) {
     for (auto &w : why)

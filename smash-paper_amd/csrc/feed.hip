@@ -115,6 +115,7 @@ struct Feed {
   std::mutex mu;
   std::condition_variable cv;
   Slot slot[3];
+  uint64_t next_slot = 0;  // the producers fill slot[next_slot % 3] in turn (one may hand over)
   int err = 0;
   std::string msg;
   double ingest_s = 0;
@@ -187,8 +188,8 @@ struct Feed {
     const uint8_t *lut = smash::ingest::lut();
     std::vector<uint8_t> keep;
     std::vector<uint64_t> dst;
-    for (uint64_t b = 0;; ++b) {
-      Slot &s = slot[b % 3];
+    for (;;) {
+      Slot &s = slot[next_slot++ % 3];
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return s.state == 0 || err; });
@@ -287,8 +288,8 @@ struct Feed {
       index_s = secs(t0, Clock::now());
       parallel = true;
     }
-    for (uint64_t b = 0, k0 = 0;; ++b) {
-      Slot &s = slot[b % 3];
+    for (uint64_t k0 = 0;;) {
+      Slot &s = slot[next_slot++ % 3];
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return s.state == 0 || err; });
@@ -311,7 +312,317 @@ struct Feed {
     }
   }
 
+  // streaming parallel producer for gzip lane lists (input in name order):
+  // worker threads inflate (or map) the files of both lists in the order the
+  // pairs need them -- the two lists interleaved by cumulative size, at most
+  // 2 T files ahead of the packer -- and index each file's records as it
+  // lands; the packer fills the pinned batches from the files already
+  // indexed, so inflation overlaps packing, copies and compute (the whole-
+  // input parallel producer inflates every file before batch 0).  A file
+  // freed once its last record is packed.  Returns false if it does not
+  // apply (nothing consumed: the caller's producers take the input); if a
+  // later file is not strict 4-line FASTQ, the streaming producer takes over
+  // at the next pair.
+  bool produce_files() {
+    namespace I = smash::ingest;
+    const std::vector<std::string> *pl[2] = {&r1.paths, &r2.paths};
+    bool any_gz = false;
+    std::vector<uint64_t> fsz[2];
+    for (int m = 0; m < 2; ++m)
+      for (const auto &path : *pl[m]) {
+        struct stat st;
+        unsigned char mg[2] = {0, 0};
+        const int fd = open(path.c_str(), O_RDONLY);
+        if (fd < 0 || fstat(fd, &st) != 0) {
+          if (fd >= 0) close(fd);
+          return false;   // (the other producers report it)
+        }
+        if (st.st_size >= 2 && pread(fd, mg, 2, 0) == 2 && mg[0] == 0x1f && mg[1] == 0x8b)
+          any_gz = true;
+        close(fd);
+        fsz[m].push_back(uint64_t(st.st_size));
+      }
+    if (!any_gz) return false;
+    const auto t0 = Clock::now();
+    struct F {
+      std::unique_ptr<I::Source> s;
+      std::vector<const char *> rec;
+      int st = -1;   // -1 pending, 0 indexed, 1 not strict, 2 I/O error
+      std::string why;
+    };
+    std::vector<F> files[2];
+    files[0].resize(pl[0]->size());
+    files[1].resize(pl[1]->size());
+    // loading order: the lists interleaved by cumulative size
+    std::vector<std::pair<int, size_t>> order;
+    {
+      size_t i[2] = {0, 0};
+      uint64_t c[2] = {0, 0};
+      while (i[0] < fsz[0].size() || i[1] < fsz[1].size()) {
+        const int m = i[1] >= fsz[1].size() ? 0 : i[0] >= fsz[0].size() ? 1 : (c[0] <= c[1] ? 0 : 1);
+        c[m] += fsz[m][i[m]];
+        order.emplace_back(m, i[m]++);
+      }
+    }
+    std::vector<size_t> pos_in_order[2];
+    pos_in_order[0].resize(fsz[0].size());
+    pos_in_order[1].resize(fsz[1].size());
+    for (size_t j = 0; j < order.size(); ++j) pos_in_order[order[j].first][order[j].second] = j;
+    std::mutex fm;
+    std::condition_variable fcv;
+    size_t next_job = 0, window = 0;   // jobs claimed; released files (in order) define the window
+    std::vector<uint8_t> released(order.size(), 0);
+    bool stop = false;
+    const size_t ahead = 2 * size_t(T);
+    auto loader = [&] {
+      for (;;) {
+        size_t j;
+        {
+          std::unique_lock<std::mutex> g(fm);
+          fcv.wait(g, [&] { return stop || next_job >= order.size() || next_job < window + ahead; });
+          if (stop || next_job >= order.size()) return;
+          j = next_job++;
+        }
+        F &f = files[order[j].first][order[j].second];
+        auto src = std::make_unique<I::Source>();
+        src->path = (*pl[order[j].first])[order[j].second];
+        std::string why;
+        int st = 0;
+        std::vector<const char *> rec;
+        if (!I::load_source(*src, why)) {
+          st = 2;
+        } else {
+          const char *q = src->p, *e = src->p + src->n;
+          rec.reserve(src->n / 256);
+          while (q < e) {
+            const char *end = I::strict_record(q, e);
+            if (!end) {
+              st = 1;
+              break;
+            }
+            rec.push_back(q);
+            q = end + 1;
+          }
+        }
+        std::lock_guard<std::mutex> g(fm);
+        f.s = std::move(src);
+        f.rec.swap(rec);
+        f.why = why;
+        f.st = st;
+        fcv.notify_all();
+      }
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t t = 0; t < std::max<uint32_t>(1, T); ++t) pool.emplace_back(loader);
+    auto shutdown = [&] {
+      {
+        std::lock_guard<std::mutex> g(fm);
+        stop = true;
+      }
+      fcv.notify_all();
+      for (auto &x : pool) x.join();
+    };
+    auto release = [&](int m, size_t i) {
+      std::lock_guard<std::mutex> g(fm);
+      files[m][i].s.reset();
+      std::vector<const char *>().swap(files[m][i].rec);
+      released[pos_in_order[m][i]] = 1;
+      while (window < order.size() && released[window]) ++window;
+      fcv.notify_all();
+    };
+    // cursors: file, record within it
+    size_t fi[2] = {0, 0}, ri[2] = {0, 0};
+    bool ready[2] = {false, false};   // the cursor's file is loaded (its fields are final)
+    // 0: record ready (*r), 1: list ended, 2: not strict (hand over), 3: I/O error
+    auto get = [&](int m, const char **r) -> int {
+      for (;;) {
+        if (fi[m] >= files[m].size()) return 1;
+        F &f = files[m][fi[m]];
+        if (!ready[m]) {
+          std::unique_lock<std::mutex> g(fm);
+          fcv.wait(g, [&] { return f.st != -1; });
+          ready[m] = true;
+        }
+        if (f.st == 1) return 2;
+        if (f.st == 2) {
+          fail(SMASH_ERR_IO, "smash_count_fastq: " + f.why);
+          return 3;
+        }
+        if (ri[m] < f.rec.size()) {
+          *r = f.rec[ri[m]++];
+          return 0;
+        }
+        release(m, fi[m]);
+        ++fi[m];
+        ri[m] = 0;
+        ready[m] = false;
+      }
+    };
+    const uint64_t CH = 1 << 16;   // pairs gathered per parallel pack
+    std::vector<const char *> pa(CH), pb(CH);
+    std::vector<uint8_t> keep(CH);
+    std::vector<uint64_t> dst(CH);
+    uint64_t emitted = 0;
+    bool first = true;
+    for (;;) {
+      Slot &s = slot[next_slot++ % 3];
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return s.state == 0 || err; });
+        if (err) {
+          shutdown();
+          return true;
+        }
+      }
+      const auto t1 = Clock::now();
+      uint64_t k = 0;   // pairs in the slot
+      int why = 0;      // how the input ended: 0 not yet, 1 end, 2 not strict, 3 error
+      while (k < B && !why) {
+        uint64_t n = 0;
+        const uint64_t want = std::min(CH, B - k);
+        while (n < want) {
+          const int x = get(0, &pa[n]);
+          if (x) {
+            why = x;
+            break;
+          }
+          const int y = get(1, &pb[n]);
+          if (y) {
+            --ri[0];   // (read 1 of an incomplete pair stays unconsumed)
+            why = y;
+            break;
+          }
+          ++n;
+        }
+        if (why == 3) {
+          shutdown();
+          return true;
+        }
+        if (why == 2 && first && emitted == 0 && k == 0 && n == 0) {
+          shutdown();   // nothing consumed: the other producers take it all
+          --next_slot;  // (from this slot on)
+          return false;
+        }
+        // checks (one empty mate, read length), drops, order; then convert
+        std::atomic<int> bad{0};
+        std::atomic<uint64_t> where{~0ull}, disorder{~0ull};
+        par_for(n, T, [&](uint64_t lo, uint64_t hi) {
+          for (uint64_t i = lo; i < hi; ++i) {
+            const I::Rec x = I::parse(pa[i]), y = I::parse(pb[i]);
+            keep[i] = !(x.sn == 0 && y.sn == 0);
+            if (keep[i] && (x.sn == 0 || y.sn == 0 || x.sn != L || y.sn != L)) {
+              uint64_t w = where.load();
+              while (i < w && !where.compare_exchange_weak(w, i)) {
+              }
+              bad = 1;
+            }
+          }
+        });
+        if (bad) {
+          const I::Rec x = I::parse(pa[where]), y = I::parse(pb[where]);
+          const std::string na(x.name, x.nn);
+          fail(SMASH_ERR_ARG, (x.sn == 0 || y.sn == 0)
+                                  ? "smash_count_fastq: one mate of a pair has no bases (" + na + ")"
+                                  : "smash_count_fastq: every mate must have the pipeline's read "
+                                    "length (" + na + ")");
+          shutdown();
+          return true;
+        }
+        uint64_t kk = 0;
+        for (uint64_t i = 0; i < n; ++i) dst[i] = keep[i] ? kk++ : ~0ull;
+        par_for(n, T, [&](uint64_t lo, uint64_t hi) {
+          const char *prev = nullptr;
+          size_t pn = 0;
+          for (uint64_t i = lo; i < hi; ++i) {
+            if (!keep[i]) continue;
+            const I::Rec x = I::parse(pa[i]), y = I::parse(pb[i]);
+            if (!prev) {   // the kept pair before this range
+              for (uint64_t j = i; j-- > 0;)
+                if (keep[j]) {
+                  const I::Rec z = I::parse(pa[j]);
+                  prev = z.name;
+                  pn = z.nn;
+                  break;
+                }
+              if (!prev && have_prev) {
+                prev = prev_name.data();
+                pn = prev_name.size();
+              }
+            }
+            if (prev && strnum_cmp(prev, pn, x.name, x.nn) > 0) {
+              uint64_t w = disorder.load();
+              while (i < w && !disorder.compare_exchange_weak(w, i)) {
+              }
+              break;
+            }
+            prev = x.name;
+            pn = x.nn;
+            uint8_t *d = s.h + (k + dst[i]) * 2 * L;
+            I::convert(d, x.seq, L);
+            I::convert(d + L, y.seq, L);
+          }
+        });
+        if (disorder.load() != ~0ull) {
+          const I::Rec x = I::parse(pa[disorder.load()]);
+          fail(SMASH_ERR_ARG, "smash_count_fastq: pairs are not in samtools sort -n order at read " +
+                                  std::string(x.name, x.nn) + " (use sort_names = 1)");
+          shutdown();
+          return true;
+        }
+        for (uint64_t i = n; i-- > 0;)
+          if (keep[i]) {
+            const I::Rec x = I::parse(pa[i]);
+            prev_name.assign(x.name, x.nn);
+            have_prev = true;
+            break;
+          }
+        k += kk;
+      }
+      const bool end = why != 0;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        ingest_s += secs(t1, Clock::now());
+        if (first) index_s = secs(t0, Clock::now());
+        parallel = true;
+        s.n = k;
+        s.last = end && why != 2;
+        s.state = 1;
+      }
+      cv.notify_all();
+      first = false;
+      emitted += k;
+      if (why == 2) {
+        // a file that is not strict: the streaming producer takes over at
+        // the next pair (each list from its current file, the records
+        // before the cursor skipped: on the strict files before, both
+        // readers see the same records)
+        shutdown();
+        for (int m = 0; m < 2; ++m) {
+          Reader &rd = m ? r2 : r1;
+          std::vector<std::string> rest(pl[m]->begin() + long(std::min(fi[m], pl[m]->size())),
+                                        pl[m]->end());
+          rd.paths.swap(rest);
+          rd.next_path = 0;
+          I::View nm, bs;
+          int e = 0;
+          for (size_t q = 0; q < ri[m]; ++q)
+            if (!rd.record(nm, bs, e)) {
+              fail(e ? e : SMASH_ERR_IO, "smash_count_fastq: " + rd.msg);
+              return true;
+            }
+        }
+        produce_stream();
+        return true;
+      }
+      if (end) {
+        shutdown();
+        return true;
+      }
+    }
+  }
+
   void produce(bool sort_names) {
+    if (!sort_names && produce_files()) return;
     if (produce_parallel(sort_names)) return;
     if (sort_names) produce_sorted();
     else produce_stream();
@@ -353,8 +664,8 @@ struct Feed {
       std::lock_guard<std::mutex> g(mu);
       ingest_s += secs(t0, Clock::now());
     }
-    for (uint64_t b = 0, q0 = 0;; ++b) {
-      Slot &s = slot[b % 3];
+    for (uint64_t q0 = 0;;) {
+      Slot &s = slot[next_slot++ % 3];
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return s.state == 0 || err; });

@@ -125,3 +125,66 @@ def test_feed_refuses_unsorted_stream_and_bad_lengths(gix, setup, tmp_path):
         pipe.count_fastq(["/nonexistent.fq"], r2, c)
     with gzip.open(gold("s100_r1.fq.gz")) as f:
         assert f.read(1) == b"@"
+
+
+def _lane_files(tmp_path, srt, lanes, kinds, fasta_lane=None):
+    """srt's pairs (name order) as len(lanes) lane files per mate: lane k
+    holds pairs [lanes[k], lanes[k + 1]), kind 'gz' or 'fq'; fasta_lane: that
+    lane of mate 1 written as FASTA (not strict 4-line FASTQ)"""
+    p = [[], []]
+    cuts = list(lanes) + [srt.shape[0] // 2]
+    for m in (0, 1):
+        for k in range(len(lanes)):
+            recs = []
+            for q in range(cuts[k], cuts[k + 1]):
+                seq = bytes(srt[2 * q + m]).upper().replace(b"Z", b"N")
+                if fasta_lane == k and m == 0:
+                    recs.append(b">r%012d/%d\n%s\n" % (q, m + 1, seq))
+                else:
+                    recs.append(b"@r%012d/%d\n%s\n+\n%s\n" % (q, m + 1, seq, b"I" * len(seq)))
+            body = b"".join(recs)
+            f = tmp_path / ("m%d_L%d.%s" % (m, k, kinds[k]))
+            f.write_bytes(gzip.compress(body, compresslevel=1) if kinds[k] == "gz" else body)
+            p[m].append(str(f))
+    return p
+
+
+@pytest.mark.parametrize("fasta_lane", [None, 0, 2])
+def test_feed_gzip_lanes_stream_per_file(gix, setup, tmp_path, fasta_lane):
+    """gzip lane lists in name order go through the per-file streaming
+    producer (files inflated and indexed on worker threads as the pairs need
+    them, batches packed from the files already indexed); a lane that is not
+    strict FASTQ hands the rest to the streaming reader (lane 2) or, as the
+    first lane, the whole input (lane 0) -- the counts are the batch path's
+    either way."""
+    cs, starts = setup
+    names, reads = S.read_fastq_pairs([gold("s150_r1.fq.gz")], [gold("s150_r2.fq.gz")])
+    n = len(names)
+    srt = reads.reshape(n, -1)[S.strnum_order(names)].reshape(2 * n, -1)
+    p = _lane_files(tmp_path, srt, [0, 170, 340, 600, 1000], ["gz", "gz", "fq", "gz", "gz"],
+                    fasta_lane)
+    new_names = np.array([b"r%012d/1" % i for i in range(n)], "S16")
+    exp = _batch_path(gix, cs, starts, new_names, srt, 101)
+    got_c, got_s, fs = _feed_path(gix, cs, starts, p[0], p[1], srt.shape[1], 101, False, n)
+    assert (got_c, got_s) == exp
+    assert fs["pairs"] == n
+    if fasta_lane is None:
+        assert fs["parallel"] == 1
+
+
+def test_feed_gzip_lanes_refuse_disorder_and_bad_length(gix, setup, tmp_path):
+    cs, starts = setup
+    names, reads = S.read_fastq_pairs([gold("s100_r1.fq.gz")], [gold("s100_r2.fq.gz")])
+    n = len(names)
+    srt = reads.reshape(n, -1)[S.strnum_order(names)].reshape(2 * n, -1)
+    rev = srt.reshape(n, -1)[::-1].reshape(2 * n, -1)   # names ascend, reads do not matter
+    p = _lane_files(tmp_path, rev, [0, 500], ["gz", "gz"])
+    # swap the two lanes of both mates: names out of order at lane 2's first
+    p = [p[0][::-1], p[1][::-1]]
+    pipe = S.Pipeline(gix, cs, starts, srt.shape[1], 64, dedup_capacity=n)
+    c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    with pytest.raises(S.SmashError, match="sort -n order"):
+        pipe.count_fastq(p[0], p[1], c, sort_names=False)
+    q = _lane_files(tmp_path, srt[:, :-1].copy(), [0, 300], ["gz", "gz"])
+    with pytest.raises(S.SmashError, match="read length"):
+        pipe.count_fastq(q[0], q[1], c, sort_names=False)
