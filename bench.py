@@ -312,8 +312,21 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def drop_cache(paths):
+    """flush the files and drop their pages from the page cache
+    (posix_fadvise DONTNEED after fsync), so the file-fed run reads them
+    from disk, not from the memory the writer just filled"""
+    for q in paths:
+        fd = os.open(q, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        finally:
+            os.close(fd)
+
+
 def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_gz=4000000,
-               gz_lanes=8):
+               gz_lanes=16):
     """The file-fed rate (smash_count_fastq, csrc/feed.hip): the same reads
     written as FASTQ (names in sort -n order) to local disk, then counted from
     the files through the bench's own pipeline (its batches of B pairs) with
@@ -358,6 +371,7 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
         p1, p2 = readgen.write_fastq_lanes(h, os.path.join(tmpdir, kind), lanes, gz=kind == "gz")
         del h
         wr = time.perf_counter() - t0
+        drop_cache(p1 + p2)
         nbytes = sum(os.path.getsize(q) for q in p1 + p2)
         exp = resident(n)
         pipe.reset()
@@ -371,7 +385,26 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
                      "wall_s": round(fs["wall_s"], 3), "index_s": round(fs["index_s"], 3),
                      "ingest_s": round(fs["ingest_s"], 3),
                      "device_waited_s": round(fs["wait_s"], 3), "file_bytes": int(nbytes),
+                     "page_cache": "dropped after writing (fsync + posix_fadvise DONTNEED)",
                      "counts_identical_to_resident": same}
+        if kind == "gz":
+            # the multi-GPU driver's rank-local reader (smashgpu.FastqShards)
+            # on the same lanes at world 1: its scan (every file inflated
+            # once) and the packs of the run's batches
+            drop_cache(p1 + p2)
+            t2 = time.perf_counter()
+            sh = S.FastqShards(p1, p2, 0, 1, lambda b: [b])
+            buf = np.empty((2 * min(B, sh.n), L), np.uint8)
+            for k0 in range(0, sh.n, B):
+                sh.pack(k0, min(sh.n, k0 + B), buf)
+            ss = sh.stats()
+            sh.close()
+            res["gz_shard_reader"] = {
+                "reads_per_s": round(2 * n / (time.perf_counter() - t2), 1),
+                "scan_s": round(ss["scan_s"], 3), "pack_s": round(ss["pack_s"], 3),
+                "scan_bytes": int(ss["scan_bytes"]), "pack_bytes": int(ss["pack_bytes"]),
+                "note": "host only (no device); at W ranks each scans ~1/W of the files and "
+                        "packs only its own batches"}
         log("file-fed %s: %d pairs in %d file(s) per mate, %.3f s -> %.3e reads/s (index %.3f s, "
             "ingest %.3f s, device waited %.3f s, %.1f GB, written in %.1f s, parallel reader %s); "
             "counts == resident: %s"
@@ -392,11 +425,14 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
     gbs = 5 * hp.numel() / (time.perf_counter() - t0) / 1e9
     res["h2d_pinned_GBps"] = round(gbs, 2)
     res["h2d_reads_per_s"] = round(gbs * 1e9 / L, 1)
-    res["method"] = ("smash_count_fastq (csrc/feed.hip) through the bench's pipeline: strict "
-                     "4-line FASTQ read by the parallel reader (csrc/fastq_par.hpp: files mapped "
-                     "or inflated, records indexed by byte range, checked and packed on all "
-                     "host threads), 3 pinned slots, 2 device buffers, H2D on its own stream; "
-                     "batches of %d pairs; FASTQ on local disk, names in sort -n order" % B)
+    res["method"] = ("smash_count_fastq (csrc/feed.hip) through the bench's pipeline: plain "
+                     "strict 4-line FASTQ read by the parallel reader (csrc/fastq_par.hpp: files "
+                     "mapped, records indexed by byte range, checked and packed on all host "
+                     "threads); gzip lanes by the per-file streaming producer (worker threads "
+                     "inflate and index files in pair order, batches packed as they land); "
+                     "3 pinned slots, 2 device buffers, H2D on its own stream; batches of %d "
+                     "pairs; FASTQ on local disk, names in sort -n order, page cache dropped "
+                     "before each read" % B)
     return res
 
 

@@ -19,6 +19,7 @@
 // it from the start.  On strict input both readers give the same pairs.
 #pragma once
 
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -60,13 +61,88 @@ struct Source {
   void *map = nullptr;
   size_t maplen = 0;
   std::vector<char> buf;
+  char *raw = nullptr;   // an inflated file (malloc'd: never zero-filled, only written once)
   Source() = default;
   Source(const Source &) = delete;
   Source &operator=(const Source &) = delete;
   ~Source() {
     if (map) munmap(map, maplen);
+    free(raw);
   }
 };
+
+// libdeflate (the image's libdeflate0 package: whole-buffer gzip decoding,
+// ~2-3x zlib's inflate on FASTQ), bound at run time; absent, zlib reads the
+// file.  Only the three entry points below are used (libdeflate 1.x ABI).
+struct Deflate {
+  void *(*alloc)() = nullptr;
+  void (*release)(void *) = nullptr;
+  int (*gzip_ex)(void *, const void *, size_t, void *, size_t, size_t *, size_t *) = nullptr;
+  Deflate() {
+    void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    alloc = reinterpret_cast<void *(*)()>(dlsym(h, "libdeflate_alloc_decompressor"));
+    release = reinterpret_cast<void (*)(void *)>(dlsym(h, "libdeflate_free_decompressor"));
+    gzip_ex = reinterpret_cast<int (*)(void *, const void *, size_t, void *, size_t, size_t *,
+                                       size_t *)>(dlsym(h, "libdeflate_gzip_decompress_ex"));
+    if (!alloc || !release || !gzip_ex) alloc = nullptr;
+  }
+  bool ok() const { return alloc != nullptr; }
+};
+inline const Deflate &deflate() {
+  static const Deflate d;
+  return d;
+}
+
+// a gzip file (every member, concatenated) into s.raw with libdeflate; the
+// output is sized from the last member's ISIZE and grown on demand.  false:
+// why (an error), or why empty: libdeflate is absent (use zlib)
+inline bool inflate_libdeflate(Source &s, const unsigned char *in, size_t size, std::string &why) {
+  const Deflate &D = deflate();
+  if (!D.ok()) return false;
+  void *dec = D.alloc();
+  if (!dec) return false;
+  const size_t isize = size >= 4 ? size_t(in[size - 4]) | size_t(in[size - 3]) << 8 |
+                                       size_t(in[size - 2]) << 16 | size_t(in[size - 1]) << 24
+                                 : 0;
+  size_t cap = std::max<size_t>({isize + 1, size * 4, size_t(1) << 16});
+  char *out = static_cast<char *>(malloc(cap + 1));
+  size_t in_off = 0, fill = 0;
+  bool ok = out != nullptr;
+  while (ok && in_off + 2 <= size && in[in_off] == 0x1f && in[in_off + 1] == 0x8b) {
+    size_t used = 0, got = 0;
+    const int r = D.gzip_ex(dec, in + in_off, size - in_off, out + fill, cap - fill, &used, &got);
+    if (r == 3) {   // LIBDEFLATE_INSUFFICIENT_SPACE: larger output, the member again
+      cap *= 2;
+      char *o2 = static_cast<char *>(realloc(out, cap + 1));
+      if (!o2) {
+        ok = false;
+        break;
+      }
+      out = o2;
+      continue;
+    }
+    if (r != 0) {   // LIBDEFLATE_BAD_DATA / SHORT_OUTPUT
+      why = "corrupt gzip data in " + s.path;
+      ok = false;
+      break;
+    }
+    in_off += used;
+    fill += got;
+  }
+  D.release(dec);
+  if (!ok) {
+    if (why.empty()) why = "out of host memory inflating " + s.path;
+    free(out);
+    return false;
+  }
+  // (trailing bytes that are no gzip member are ignored, as gzip -dc does)
+  if (fill && out[fill - 1] != '\n') out[fill++] = '\n';
+  s.raw = out;
+  s.p = out;
+  s.n = fill;
+  return true;
+}
 
 // open one file: one that starts with the gzip magic is inflated into memory
 // (zlib reads concatenated members), another is mapped; a file whose last
@@ -88,6 +164,18 @@ inline bool load_source(Source &s, std::string &why) {
   }
   const size_t size = size_t(stt.st_size);
   if (size >= 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+    if (deflate().ok()) {
+      void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+      close(fd);
+      if (m == MAP_FAILED) {
+        why = "cannot map " + s.path;
+        return false;
+      }
+      madvise(m, size, MADV_SEQUENTIAL);
+      const bool ok = inflate_libdeflate(s, static_cast<const unsigned char *>(m), size, why);
+      munmap(m, size);
+      return ok;
+    }
     close(fd);
     gzFile g = gzopen(s.path.c_str(), "rb");
     if (!g) {

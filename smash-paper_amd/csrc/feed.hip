@@ -370,16 +370,18 @@ struct Feed {
     for (size_t j = 0; j < order.size(); ++j) pos_in_order[order[j].first][order[j].second] = j;
     std::mutex fm;
     std::condition_variable fcv;
-    size_t next_job = 0, window = 0;   // jobs claimed; released files (in order) define the window
-    std::vector<uint8_t> released(order.size(), 0);
+    // jobs claimed; a loader claims job j only while j < need + ahead, need
+    // = the latest loading position of the packer's current files (the
+    // packer never waits for a file no loader may claim)
+    size_t next_job = 0, need = 0;
     bool stop = false;
-    const size_t ahead = 2 * size_t(T);
+    const size_t ahead = std::max<size_t>(4, 2 * size_t(T));
     auto loader = [&] {
       for (;;) {
         size_t j;
         {
           std::unique_lock<std::mutex> g(fm);
-          fcv.wait(g, [&] { return stop || next_job >= order.size() || next_job < window + ahead; });
+          fcv.wait(g, [&] { return stop || next_job >= order.size() || next_job < need + ahead; });
           if (stop || next_job >= order.size()) return;
           j = next_job++;
         }
@@ -426,15 +428,22 @@ struct Feed {
       std::lock_guard<std::mutex> g(fm);
       files[m][i].s.reset();
       std::vector<const char *>().swap(files[m][i].rec);
-      released[pos_in_order[m][i]] = 1;
-      while (window < order.size() && released[window]) ++window;
-      fcv.notify_all();
     };
     // cursors: file, record within it
     size_t fi[2] = {0, 0}, ri[2] = {0, 0};
+    std::vector<std::pair<int, size_t>> done_files;   // read past, records maybe still in a run
     bool ready[2] = {false, false};   // the cursor's file is loaded (its fields are final)
-    // 0: record ready (*r), 1: list ended, 2: not strict (hand over), 3: I/O error
-    auto get = [&](int m, const char **r) -> int {
+    auto set_need = [&] {
+      size_t x = 0;
+      for (int m = 0; m < 2; ++m)
+        if (fi[m] < files[m].size()) x = std::max(x, pos_in_order[m][fi[m]]);
+      std::lock_guard<std::mutex> g(fm);
+      need = x;
+      fcv.notify_all();
+    };
+    // the cursor's file with records left: 0 ok, 1 list ended, 2 not strict
+    // (hand over), 3 I/O error
+    auto avail = [&](int m) -> int {
       for (;;) {
         if (fi[m] >= files[m].size()) return 1;
         F &f = files[m][fi[m]];
@@ -448,20 +457,20 @@ struct Feed {
           fail(SMASH_ERR_IO, "smash_count_fastq: " + f.why);
           return 3;
         }
-        if (ri[m] < f.rec.size()) {
-          *r = f.rec[ri[m]++];
-          return 0;
-        }
-        release(m, fi[m]);
+        if (ri[m] < f.rec.size()) return 0;
+        done_files.emplace_back(m, fi[m]);   // freed once the run holding its records is packed
         ++fi[m];
         ri[m] = 0;
         ready[m] = false;
+        set_need();
       }
     };
-    const uint64_t CH = 1 << 16;   // pairs gathered per parallel pack
-    std::vector<const char *> pa(CH), pb(CH);
-    std::vector<uint8_t> keep(CH);
-    std::vector<uint64_t> dst(CH);
+    auto release_done = [&] {
+      for (auto &x : done_files) release(x.first, x.second);
+      done_files.clear();
+    };
+    std::vector<uint8_t> keep;
+    std::vector<uint64_t> dst;
     uint64_t emitted = 0;
     bool first = true;
     for (;;) {
@@ -478,31 +487,27 @@ struct Feed {
       uint64_t k = 0;   // pairs in the slot
       int why = 0;      // how the input ended: 0 not yet, 1 end, 2 not strict, 3 error
       while (k < B && !why) {
-        uint64_t n = 0;
-        const uint64_t want = std::min(CH, B - k);
-        while (n < want) {
-          const int x = get(0, &pa[n]);
-          if (x) {
-            why = x;
-            break;
-          }
-          const int y = get(1, &pb[n]);
-          if (y) {
-            --ri[0];   // (read 1 of an incomplete pair stays unconsumed)
-            why = y;
-            break;
-          }
-          ++n;
-        }
+        // a run of pairs inside the two cursors' current files: record ri0 +
+        // i of one, ri1 + i of the other
+        const int x = avail(0);
+        const int y = x ? 0 : avail(1);
+        why = x ? x : y;
         if (why == 3) {
           shutdown();
           return true;
         }
-        if (why == 2 && first && emitted == 0 && k == 0 && n == 0) {
+        if (why == 2 && first && emitted == 0 && k == 0) {
           shutdown();   // nothing consumed: the other producers take it all
           --next_slot;  // (from this slot on)
           return false;
         }
+        if (why) break;
+        const F &f0 = files[0][fi[0]], &f1 = files[1][fi[1]];
+        const uint64_t n = std::min<uint64_t>({B - k, f0.rec.size() - ri[0], f1.rec.size() - ri[1]});
+        const char *const *pa = f0.rec.data() + ri[0];
+        const char *const *pb = f1.rec.data() + ri[1];
+        keep.resize(n);
+        dst.resize(n);
         // checks (one empty mate, read length), drops, order; then convert
         std::atomic<int> bad{0};
         std::atomic<uint64_t> where{~0ull}, disorder{~0ull};
@@ -577,6 +582,9 @@ struct Feed {
             break;
           }
         k += kk;
+        ri[0] += n;
+        ri[1] += n;
+        release_done();   // the runs' records before this one are converted
       }
       const bool end = why != 0;
       {

@@ -161,7 +161,7 @@ def test_feed_gzip_lanes_stream_per_file(gix, setup, tmp_path, fasta_lane):
     names, reads = S.read_fastq_pairs([gold("s150_r1.fq.gz")], [gold("s150_r2.fq.gz")])
     n = len(names)
     srt = reads.reshape(n, -1)[S.strnum_order(names)].reshape(2 * n, -1)
-    p = _lane_files(tmp_path, srt, [0, 170, 340, 600, 1000], ["gz", "gz", "fq", "gz", "gz"],
+    p = _lane_files(tmp_path, srt, [0, 100, 200, 350, 500], ["gz", "gz", "fq", "gz", "gz"],
                     fasta_lane)
     new_names = np.array([b"r%012d/1" % i for i in range(n)], "S16")
     exp = _batch_path(gix, cs, starts, new_names, srt, 101)
