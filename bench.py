@@ -355,7 +355,7 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
     # warm-up: the first call pins the feed's slots (3 x 2 B L bytes) and
     # allocates its device buffers, which the pipeline keeps for later calls
     # (a service's steady state; the first call's wall time is reported)
-    h = d_reads[:2 * min(P, 10000)].cpu().numpy()
+    h = d_reads[:2 * min(P, 10000), :L].contiguous().cpu().numpy()
     w1, w2 = readgen.write_fastq_lanes(h, os.path.join(tmpdir, "warm"), 1)
     c = torch.zeros(len(starts), dtype=torch.int64, device=dev)
     pipe.reset()
@@ -367,7 +367,7 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
 
     for kind, n, lanes in (("plain", n_plain, 1), ("gz", n_gz, gz_lanes)):
         t0 = time.perf_counter()
-        h = d_reads[:2 * n].cpu().numpy()
+        h = d_reads[:2 * n, :L].contiguous().cpu().numpy()
         p1, p2 = readgen.write_fastq_lanes(h, os.path.join(tmpdir, kind), lanes, gz=kind == "gz")
         del h
         wr = time.perf_counter() - t0
@@ -414,7 +414,7 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
         for q in p1 + p2:
             os.remove(q)
     # the pinned host -> device copy rate of one batch of reads
-    hp = torch.from_numpy(d_reads[:2 * min(P, 1000000)].cpu().numpy()).pin_memory()
+    hp = torch.from_numpy(d_reads[:2 * min(P, 1000000)].cpu().numpy()).pin_memory()   # (rows)
     dd = torch.empty_like(hp, device=dev)
     dd.copy_(hp, non_blocking=True)
     torch.cuda.synchronize()
@@ -424,7 +424,7 @@ def feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir, n_plain=None, n_g
     torch.cuda.synchronize()
     gbs = 5 * hp.numel() / (time.perf_counter() - t0) / 1e9
     res["h2d_pinned_GBps"] = round(gbs, 2)
-    res["h2d_reads_per_s"] = round(gbs * 1e9 / L, 1)
+    res["h2d_reads_per_s"] = round(gbs * 1e9 / d_reads.shape[1], 1)
     res["method"] = ("smash_count_fastq (csrc/feed.hip) through the bench's pipeline: plain "
                      "strict 4-line FASTQ read by the parallel reader (csrc/fastq_par.hpp: files "
                      "mapped, records indexed by byte range, checked and packed on all host "
@@ -495,12 +495,21 @@ def main():
     import readgen
     gen = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000 + rank)
     d_reads = gen.generate(P)
+    # the device's native read layout: each mate in a 16-byte aligned,
+    # zero-padded row (smash_read_stride: 160 B at 150 bp), which the search
+    # copies straight into LDS (no record build); SMASH_BENCH_ROWS=0: dense
+    # [2P, L] mates, searched through k_prep's records (A/B)
+    rows = os.environ.get("SMASH_BENCH_ROWS", "1") != "0"
+    if rows:
+        d_reads = S.to_rows(d_reads, L)
     torch.cuda.synchronize()
-    log("reads: %d pairs x %d bp per rank in HBM (%.1f GB), batches of %d (%.1fs since start)"
-        % (P, L, d_reads.numel() / 1e9, B, time.time() - t0))
+    log("reads: %d pairs x %d bp per rank in HBM (%.1f GB, rows of %d B), batches of %d "
+        "(%.1fs since start)" % (P, L, d_reads.numel() / 1e9, d_reads.shape[1], B,
+                                 time.time() - t0))
     # the key set: every key of the run (single GPU), or the keys this rank
     # owns ((hash >> 1) % world of all ranks' keys: ~P as well)
-    pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20))
+    pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),
+                      read_stride=d_reads.shape[1] if rows else 0)
     counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
     nb = (P + B - 1) // B
 
@@ -609,7 +618,7 @@ def main():
         import oracle as O
         t2 = time.time()
         ns = min(4000, 2 * P)
-        sample = d_reads[:ns].cpu().numpy()
+        sample = d_reads[:ns, :L].contiguous().cpu().numpy()
         oix, mp = host_index(S, O, dix, T, sp, sz, names, sample_reads=sample)
         log("host copy of the index for the oracle: %.1fs" % (time.time() - t2))
         # algorithmic bytes per read: 64 B x the 64-byte line transitions of
@@ -676,12 +685,12 @@ def main():
             op = O.Pipeline(oix, mp, cs, starts)
             # calibrate, then a bounded sample of ~cpu_seconds of the same reads
             n0 = min(P, 64 * threads)
-            h0 = d_reads[:2 * n0].cpu().numpy()
+            h0 = d_reads[:2 * n0, :L].contiguous().cpu().numpy()
             t3 = time.perf_counter()
             op.run(h0, threads=threads)
             dt0 = time.perf_counter() - t3
             n1 = int(min(P, max(n0, n0 * args.cpu_seconds / max(dt0, 1e-3))))
-            h1 = d_reads[:2 * n1].cpu().numpy()
+            h1 = d_reads[:2 * n1, :L].contiguous().cpu().numpy()
             op = O.Pipeline(oix, mp, cs, starts)
             t3 = time.perf_counter()
             err = op.run(h1, threads=threads)

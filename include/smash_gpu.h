@@ -215,14 +215,23 @@ typedef struct {
   int64_t hit_window;        /* smashMEM arg 4 (10000) */
   uint64_t dedup_capacity;   /* distinct pair keys the persistent set holds
                                 (exact keys: ~16 hit words per key of arena) */
+  uint32_t read_stride;      /* bytes from one mate to the next in d_reads: 0 or
+                                read_len (dense), or smash_read_stride(read_len):
+                                the device's native rows (16-byte aligned d_reads,
+                                the bytes past read_len of every row zero) -- the
+                                search copies each mate straight from its row
+                                instead of building a record of it first */
 } smash_pipeline_cfg;
+
+/* The native row of a mate of read_len bases (bytes; a multiple of 16). */
+uint32_t smash_read_stride(uint32_t read_len);
 
 int smash_pipeline_create(const smash_index *ix, const smash_pipeline_cfg *cfg,
                           smash_pipeline **out);
 void smash_pipeline_free(smash_pipeline *p);
 
 /* One batch of n_pairs pairs: d_reads holds 2*n_pairs mates of cfg->read_len
- * bytes, mate 2q = read 1, 2q+1 = read 2 of pair q (Pair::run alternation,
+ * bytes (rows of cfg->read_stride), mate 2q = read 1, 2q+1 = read 2 of pair q (Pair::run alternation,
  * query.cpp:486-505), pairs in name order (samtools sort -n).  Runs map ->
  * resolve -> tag -> filter -> de-dup (first wins, against every earlier
  * batch) -> adjacent de-dup (carried across batches) -> bin, adding into

@@ -154,6 +154,9 @@ int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint
                    bool sync_check, const SearchWs *ws = nullptr);
 // record bytes of n reads of up to max_len bases (k_prep)
 uint64_t search_rec_bytes(uint64_t n_reads, uint32_t max_len);
+// the search takes these reads as direct rows (no records): native stride,
+// 16-byte aligned (mam.hip; SMASH_DIRECT_ROWS=0 turns it off for A/B)
+bool search_direct(const uint8_t *seqs, uint64_t stride, uint32_t len);
 // one pipeline batch whose search waits for in_ev (null: for all earlier
 // work on s) instead of for everything on s (pipeline.hip)
 int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,

@@ -592,8 +592,9 @@ inline int plan_pairs(const PairIndex &px, uint32_t T, uint32_t L, bool check_or
 // read 2, prepared) and, with names, read-1 names (stride bytes, NUL padded;
 // false if one does not fit), T threads
 inline bool pack_pairs(const PairIndex &px, const Plan &pl, uint64_t k0, uint64_t k1, uint8_t *out,
-                       char *names, uint32_t stride, uint32_t T) {
+                       char *names, uint32_t stride, uint32_t T, uint32_t row = 0) {
   const uint32_t L = pl.L;
+  const uint64_t RW = row ? row : L;   // bytes per mate row (the bytes past L: left as they are)
   const uint64_t n = k1 - k0;
   const uint32_t R = std::max<uint32_t>(1, std::min<uint64_t>(T * 4, (n + 4095) / 4096));
   std::atomic<uint32_t> next{0};
@@ -603,9 +604,9 @@ inline bool pack_pairs(const PairIndex &px, const Plan &pl, uint64_t k0, uint64_
       for (uint64_t k = k0 + n * r / R, hi = k0 + n * (r + 1) / R; k < hi; ++k) {
         const uint64_t i = pl.idx.empty() ? k : pl.idx[k];
         const Rec a = parse(px.r1[i]), b = parse(px.r2[i]);
-        uint8_t *d = out + (k - k0) * 2 * L;
+        uint8_t *d = out + (k - k0) * 2 * RW;
         convert(d, a.seq, L);
-        convert(d + L, b.seq, L);
+        convert(d + RW, b.seq, L);
         if (names) {
           if (a.nn >= stride) {
             bad = 1;

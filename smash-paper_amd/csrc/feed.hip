@@ -36,6 +36,7 @@ using smash::ingest::strnum_cmp;
 
 namespace smash {
 uint32_t pipe_read_len(const smash_pipeline *p);
+uint32_t pipe_stride(const smash_pipeline *p);
 uint64_t pipe_max_pairs(const smash_pipeline *p);
 int pipe_device(const smash_pipeline *p);
 void *&pipe_feed(smash_pipeline *p, void (*freer)(void *));
@@ -96,8 +97,10 @@ struct FeedBufs {
       ok = hipMalloc(&d[k], b) == hipSuccess &&
            hipEventCreateWithFlags(&copied[k], hipEventDisableTiming) == hipSuccess &&
            hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
-    for (auto *&x : h)
+    for (auto *&x : h) {
       ok = ok && hipHostMalloc(reinterpret_cast<void **>(&x), b, hipHostMallocDefault) == hipSuccess;
+      if (ok) memset(x, 0, b);   // the rows' pads stay zero: packing writes only [0, L) of a row
+    }
     return ok;
   }
 };
@@ -106,6 +109,7 @@ void free_feed(void *f) { delete static_cast<FeedBufs *>(f); }
 struct Feed {
   smash_pipeline *p;
   uint32_t L, T;
+  uint32_t S;   // bytes per mate row in the batches (the pipeline's read stride)
   uint64_t B;
   Reader r1, r2;
   Chunk c1, c2;
@@ -233,9 +237,9 @@ struct Feed {
           pn = nn;
           const uint8_t *a = reinterpret_cast<const uint8_t *>(c1.bases.data() + c1.boff[i]);
           const uint8_t *bb = reinterpret_cast<const uint8_t *>(c2.bases.data() + c2.boff[i]);
-          uint8_t *d = s.h + dst[i] * 2 * L;
+          uint8_t *d = s.h + dst[i] * 2 * S;
           for (uint32_t j = 0; j < L; ++j) d[j] = lut[a[j]];
-          for (uint32_t j = 0; j < L; ++j) d[L + j] = lut[bb[j]];
+          for (uint32_t j = 0; j < L; ++j) d[S + j] = lut[bb[j]];
         }
       });
       if (disorder.load() != ~0ull) {
@@ -297,7 +301,7 @@ struct Feed {
       }
       const auto t1 = Clock::now();
       const uint64_t k = std::min(B, pl.n_out - k0);
-      I::pack_pairs(px, pl, k0, k0 + k, s.h, nullptr, 0, T);
+      I::pack_pairs(px, pl, k0, k0 + k, s.h, nullptr, 0, T, S);
       k0 += k;
       const bool end = k0 >= pl.n_out;
       {
@@ -562,9 +566,9 @@ struct Feed {
             }
             prev = x.name;
             pn = x.nn;
-            uint8_t *d = s.h + (k + dst[i]) * 2 * L;
+            uint8_t *d = s.h + (k + dst[i]) * 2 * S;
             I::convert(d, x.seq, L);
-            I::convert(d + L, y.seq, L);
+            I::convert(d + S, y.seq, L);
           }
         });
         if (disorder.load() != ~0ull) {
@@ -682,8 +686,10 @@ struct Feed {
       const auto t1 = Clock::now();
       const uint64_t k = std::min(B, np - q0);
       par_for(k, T, [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t i = lo; i < hi; ++i)
-          memcpy(s.h + i * 2 * L, reads.data() + perm[q0 + i] * 2 * L, 2 * L);
+        for (uint64_t i = lo; i < hi; ++i) {
+          memcpy(s.h + i * 2 * S, reads.data() + perm[q0 + i] * 2 * L, L);
+          memcpy(s.h + i * 2 * S + S, reads.data() + perm[q0 + i] * 2 * L + L, L);
+        }
       });
       q0 += k;
       const bool end = q0 >= np;
@@ -714,11 +720,12 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
   auto f = std::make_unique<Feed>();
   f->p = p;
   f->L = smash::pipe_read_len(p);
+  f->S = smash::pipe_stride(p);
   f->B = smash::pipe_max_pairs(p);
   f->T = threads ? threads : 1;
   for (uint32_t i = 0; i < n1; ++i) f->r1.paths.emplace_back(r1[i]);
   for (uint32_t i = 0; i < n2; ++i) f->r2.paths.emplace_back(r2[i]);
-  const uint64_t bytes = 2 * f->B * f->L;
+  const uint64_t bytes = 2 * f->B * f->S;
   SMASH_HIP(hipSetDevice(smash::pipe_device(p)));
   hipStream_t cs = static_cast<hipStream_t>(stream);
   void *&fb_slot = smash::pipe_feed(p, free_feed);
@@ -767,7 +774,7 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
       if (s.n) {
         // the copy into dbuf[d] waits for the compute that last read it
         if (b >= 2 && hipStreamWaitEvent(xs, done[d], 0) != hipSuccess) { rc = SMASH_ERR_HIP; break; }
-        if (hipMemcpyAsync(dbuf[d], s.h, 2 * s.n * f->L, hipMemcpyHostToDevice, xs) != hipSuccess ||
+        if (hipMemcpyAsync(dbuf[d], s.h, 2 * s.n * f->S, hipMemcpyHostToDevice, xs) != hipSuccess ||
             hipEventRecord(copied[d], xs) != hipSuccess) {
           rc = SMASH_ERR_HIP;
           break;

@@ -147,9 +147,9 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
         "consume", "S_ALU", "S_COPY", "S_BM", "S_KT", "S_IDX", "S_BYTE", "S_CMP", "S_USCAN",
         "S_EX", "A_BS", "A_BS_DONE", "A_XL_DONE", "A_RUN_DONE", "A_CHAIN_DONE", "A_EXPAND",
         "A_AFTER", "A_TOP", "A_TRAV", "A_DONE", "TOP.!clean", "TOP.codes1", "TOP.codes2",
-        "TOP.kt", "TOP.filter", "TOP.kcache", "dma"};
+        "TOP.kt", "TOP.filter", "TOP.kcache", "dma", "rowbad"};
     std::fprintf(stderr, "[k_mam_sm] wave iterations running each region (%%):");
-    for (int k = 0; k < 27; ++k)
+    for (int k = 0; k < 28; ++k)
       if (ws[64 + k])
         std::fprintf(stderr, " %s %.1f", regions[k], 100.0 * double(ws[64 + k]) / double(ws[0] ? ws[0] : 1));
     std::fprintf(stderr, "\n");
@@ -164,8 +164,12 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
               hipStream_t s, bool sync_check, const SearchWs *ws) {
   constexpr int B = kSmBlock;
   const sm::Geom g = sm::make_geom(lens ? 255 : len);
+  // direct rows: the reads are the device's native rows (16-byte aligned,
+  // 4 w_row bytes apart, zero padded: smash_read_stride) -- the search DMAs
+  // each straight from its row and needs no records
+  const bool direct = !lens && search_direct(seqs, stride, len);
   // read records (k_prep): the caller's workspace, else the index's buffer
-  const uint64_t need = n_reads * g.chunks * 16;
+  const uint64_t need = direct ? 0 : n_reads * g.chunks * 16;
   uint32_t *rec = ws ? reinterpret_cast<uint32_t *>(ws->rec) : nullptr;
   if (ws && need > ws->rec_bytes) {
     set_error("k_mam_sm: search workspace too small");
@@ -182,11 +186,12 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   }
   if (!ws) rec = ix->d_rec;
   const uint32_t ga = sm::prep_groups(lens ? 255 : len);
-  // k_prep (LDS-staged, the default: profiles/r03/sched) or, with
-  // SMASH_PREP_LDS=0, k_prep_direct (no LDS: it fits beside a running search
-  // but moves ~2x the bytes)
+  // records (not for direct rows): k_prep (LDS-staged, the default:
+  // profiles/r03/sched) or, with SMASH_PREP_LDS=0, k_prep_direct (no LDS: it
+  // fits beside a running search but moves ~2x the bytes)
   const char *pl = std::getenv("SMASH_PREP_LDS");
-  if (!(pl && pl[0] == '0') || n_reads * ga >= (1ull << 32)) {
+  if (direct) {
+  } else if (!(pl && pl[0] == '0') || n_reads * ga >= (1ull << 32)) {
     const uint32_t per = sm::prep_per_block(g, stride);
     const size_t plds = sm::prep_lds_bytes(g, stride, per);
     sm::k_prep<<<unsigned((n_reads + per - 1) / per), 256, plds, s>>>(
@@ -208,6 +213,9 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(rec);
   c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
+  c.rows = direct ? reinterpret_cast<const uint4 *>(seqs) : nullptr;
+  c.direct = direct ? 1u : 0u;
+  sm::bad_table(ix->in_text, &c.bad_tab_lo, &c.bad_tab_hi);
   c.lin_blocks = 8;
   c.pad = 0;
   c.grab = 16;
@@ -235,7 +243,8 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
         {reinterpret_cast<uint64_t>(ix->d_lcp8), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_uniq), N + 64},
         {reinterpret_cast<uint64_t>(ix->d_kmer), 16ull << (2 * ix->kmer_k)},
-        {reinterpret_cast<uint64_t>(rec), n_reads * g.chunks * 16}};
+        {direct ? reinterpret_cast<uint64_t>(seqs) : reinterpret_cast<uint64_t>(rec),
+         direct ? n_reads * stride : n_reads * g.chunks * 16}};
     c.lo = ~0ull; c.hi = 0;
     for (int k = 0; k < 7; ++k) {
       c.lo = std::min<uint64_t>(c.lo, spans[k][0]);
@@ -302,6 +311,12 @@ int probe_check(const smash_index *ix) {
   std::fprintf(stderr, "%s\n", msg);
   set_error(msg);
   return SMASH_ERR_HIP;
+}
+
+bool search_direct(const uint8_t *seqs, uint64_t stride, uint32_t len) {
+  static const bool off = std::getenv("SMASH_DIRECT_ROWS") && std::getenv("SMASH_DIRECT_ROWS")[0] == '0';
+  return !off && len && stride == 4ull * sm::make_geom(len).w_row &&
+         (reinterpret_cast<uint64_t>(seqs) & 15) == 0;
 }
 
 uint64_t search_rec_bytes(uint64_t n_reads, uint32_t max_len) {
@@ -373,6 +388,10 @@ using namespace smash;
 
 // Synchronous w.r.t. the probe check: a probe outside the index fails this
 // call (the pipeline uses the asynchronous form and checks at stats time).
+extern "C" uint32_t smash_read_stride(uint32_t read_len) {
+  return read_len && read_len <= 255 ? 4 * sm::make_geom(read_len).w_row : 0;
+}
+
 extern "C" int smash_map_batch(const smash_index *ix, int mode, uint32_t min_len,
                                const uint8_t *d_seqs, uint64_t stride,
                                const uint16_t *d_lens, uint32_t len,

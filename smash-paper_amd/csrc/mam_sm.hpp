@@ -481,6 +481,14 @@ struct Ctx {
   // k_prep records and the LDS row geometry
   const uint4 *rec;
   uint32_t chunks, c_bad, w_row, w_raw;
+  // direct rows (rows != null): the reads themselves, one 16-byte aligned,
+  // zero-padded row of w_row words per mate (smash_read_stride): no
+  // records; the row is DMA'd from its read and the bad mask computed from
+  // it in LDS by the wave (row_bad); bad_tab: the 8-byte table of the
+  // expected byte per low-3-bit code (a c g t if they occur in the text)
+  const uint4 *rows;
+  uint32_t direct;        // rows != null (0 / 1)
+  uint32_t bad_tab_lo, bad_tab_hi;
   uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
   uint32_t pad;           // experiment: dependent ALU ops added per iteration (0 = none)
   uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
@@ -515,6 +523,42 @@ template <class IdxT>
 __device__ __forceinline__ uint64_t idx_val(const uint4 &v, uint32_t ao) {
   if (sizeof(IdxT) == 8) return (ao & 8) ? hi64(v) : lo64(v);
   return dword_at(v, ao >> 2);
+}
+
+// Direct rows: the bad-mask nibble of the 4 bytes of w (bit j: byte j is not
+// a base that occurs in the text), bases at or past `live` (0..4) masked.
+// One permute looks up the byte each low-3-bit code would have to be
+// (tab_hi:tab_lo, a c g t where they occur in the text, else a byte that
+// can never match), a xor marks the mismatching bytes, the zero-byte test
+// gathers their high bits and one multiply packs them (as gt4).
+__device__ __forceinline__ uint32_t bad_nibble(uint32_t w, uint32_t tab_lo, uint32_t tab_hi,
+                                               uint32_t live) {
+  const uint32_t expect = SM_PERM(tab_hi, tab_lo, w & 0x07070707u);
+  const uint32_t z = expect ^ w;
+  const uint32_t nz = (((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+  const uint32_t nib = (nz * 0x00204081u) >> 28;
+  return live >= 4 ? nib : nib & ((1u << live) - 1u);
+}
+
+// the same mask for one row, one lane alone (the host emulation's form of
+// the wave's computation in k_mam_sm)
+__device__ inline Bad row_bad_mask(const uint32_t *row, uint32_t L, uint32_t tab_lo,
+                                            uint32_t tab_hi) {
+  uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t k = 0; 4 * k < L && k < 64; ++k)
+    m[k >> 3] |= bad_nibble(row[k], tab_lo, tab_hi, L - 4 * k) << (4 * (k & 7));
+  return Bad{m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7]};
+}
+
+// the bad_nibble table from the bytes that occur in the text
+inline void bad_table(const uint64_t in_text[4], uint32_t *lo, uint32_t *hi) {
+  uint8_t t[8];
+  for (uint32_t c = 0; c < 8; ++c) t[c] = uint8_t(0x80u | (c ^ 1u));   // never equal: low bits differ
+  const uint8_t letters[4] = {'a', 'c', 'g', 't'};
+  for (uint8_t b : letters)
+    if ((in_text[b >> 6] >> (b & 63)) & 1ull) t[b & 7] = b;
+  *lo = uint32_t(t[0]) | uint32_t(t[1]) << 8 | uint32_t(t[2]) << 16 | uint32_t(t[3]) << 24;
+  *hi = uint32_t(t[4]) | uint32_t(t[5]) << 8 | uint32_t(t[6]) << 16 | uint32_t(t[7]) << 24;
 }
 
 // One lane = one read at a time.  Each iteration: (1) the lanes with a
@@ -642,7 +686,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     const uint64_t live = __ballot(st != S_EXIT);
     if (live == 0) break;
     if (STATS) { w_iters += 1; w_active += __popcll(live); }
-    if (CHECK && st >= S_COPY &&
+    const uint32_t st_ld = S_COPY + c.direct;   // the lowest state that loads
+    if (CHECK && st >= st_ld &&
         (addr < c.lo || addr >= c.hi || (need2 && (addr2 < c.lo || addr2 >= c.hi)))) {
       if (atomicAdd(c.viol, 1ull) == 0) {
         c.viol[1] = st; c.viol[2] = op; c.viol[3] = addr; c.viol[4] = need2 ? addr2 : 0;
@@ -654,7 +699,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
     uint64_t v3 = 0;
     const uint64_t amask = st >= S_BYTE ? ~uint64_t(0) : ~uint64_t(15);
-    if (st >= S_COPY) v = SM_LOAD16ST(addr & amask, st);
+    if (st >= st_ld) v = SM_LOAD16ST(addr & amask, st);
     if (need2) {
       if (pf) v2 = SM_LOADPF16(addr2 & ~uint64_t(15));
       else v2 = SM_LOAD16ST(addr2 & amask, st);
@@ -671,12 +716,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           st = S_EXIT;
         } else {
           L = c.lens ? c.lens[rd] : c.len0;
-          // the lane loads the bad-mask chunks; the read's bytes go to its
-          // LDS row by DMA (below)
+          // records: the lane loads the bad-mask chunks, the read's bytes go
+          // to its LDS row by DMA (below); direct rows: the row is DMA'd
+          // from the read and the wave computes the mask next iteration
           addr = reinterpret_cast<uint64_t>(c.rec + rd * c.chunks);
           addr2 = addr + 16;
-          need2 = c.c_bad > 1;
+          need2 = !c.direct && c.c_bad > 1;
           pf = false; pfr = false;
+          bad = Bad{0, 0, 0, 0, 0, 0, 0, 0};
           st = S_COPY;
         }
       }
@@ -691,7 +738,42 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         const uint32_t ln = uint32_t(__builtin_ctzll(fm_));
         fm_ &= fm_ - 1;
         const uint64_t rl = __shfl(rd, int(ln), 64);
-        SM_DMA_ROW(ldsw + ln * c.w_row, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
+        if (c.direct)
+          SM_DMA_ROW(ldsw + ln * c.w_row, c.rows + rl * (c.w_row >> 2), c.w_row >> 2, lane);
+        else
+          SM_DMA_ROW(ldsw + ln * c.w_row, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
+      }
+    }
+    // direct rows: the rows DMA'd last iteration have landed (every earlier
+    // vector-memory operation of the wave is done: vmcnt(0)); the bad mask of
+    // each, one row word per lane, assembled only when a base is bad
+    if (c.direct) {
+      uint64_t cm = __ballot(st == S_COPY && !fresh);
+      if (cm) {
+        SM_REGION(27);
+#ifdef SM_HOST_LANE
+        if (st == S_COPY && !fresh) bad = row_bad_mask(row, L, c.bad_tab_lo, c.bad_tab_hi);
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        while (cm) {
+          const uint32_t ln = uint32_t(__builtin_ctzll(cm));
+          cm &= cm - 1;
+          const uint32_t lr = uint32_t(__shfl(int(L), int(ln), 64));
+          const uint32_t b0 = 4 * lane;
+          const uint32_t w = b0 < lr ? ldsw[ln * c.w_row + lane] : 0u;
+          const uint32_t nib = b0 < lr ? bad_nibble(w, c.bad_tab_lo, c.bad_tab_hi, lr - b0) : 0u;
+          if (__ballot(nib != 0)) {   // rare: a read with a bad base
+            uint32_t x = nib << (4 * (lane & 7));
+            x |= __shfl_xor(x, 1, 64);
+            x |= __shfl_xor(x, 2, 64);
+            x |= __shfl_xor(x, 4, 64);
+            const uint32_t m0 = __shfl(x, 0, 64), m1 = __shfl(x, 8, 64), m2 = __shfl(x, 16, 64),
+                           m3 = __shfl(x, 24, 64), m4 = __shfl(x, 32, 64), m5 = __shfl(x, 40, 64),
+                           m6 = __shfl(x, 48, 64), m7 = __shfl(x, 56, 64);
+            if (lane == ln) bad = Bad{m0, m1, m2, m3, m4, m5, m6, m7};
+          }
+        }
+#endif
       }
     }
     if (st < S_ALU || fresh) continue;
@@ -729,8 +811,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       case S_COPY: {                                 // bad-mask chunks 0 (v), 1 (v2)
         SM_REGION(2);
-        bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
-        bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
+        if (!c.direct) {   // (direct rows: the wave set the mask above)
+          bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
+          bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
+        }
         need2 = false;
         prefix = 0; depth = 0; start = 0; end = N - 1; have_pos = false; nem = 0;
         skip_f = false; fm = 0; ktr_set = false;

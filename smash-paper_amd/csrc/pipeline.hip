@@ -48,6 +48,7 @@ struct smash_pipeline {
   const smash_index *ix = nullptr;
   int device = 0;
   uint32_t read_len = 0, min_len = 20, slots = 0, n_contig = 0, nbins = 0;
+  uint32_t stride = 0;   // bytes from one mate to the next in d_reads (cfg.read_stride)
   int32_t min_excess = 4;
   int64_t hit_window = 10000;
   uint64_t max_pairs = 0;
@@ -1266,6 +1267,11 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     set_error("smash_pipeline_create: bad configuration");
     return SMASH_ERR_ARG;
   }
+  if (cfg->read_stride && cfg->read_stride != cfg->read_len &&
+      cfg->read_stride != smash_read_stride(cfg->read_len)) {
+    set_error("smash_pipeline_create: read_stride must be 0, read_len or smash_read_stride(read_len)");
+    return SMASH_ERR_ARG;
+  }
   if (!ix->rcref) {   // the SMASH chain maps with -rcref (smash_mapping.sh:19)
     set_error("smash_pipeline_create: the count chain needs the -rcref text layout");
     return SMASH_ERR_ARG;
@@ -1280,6 +1286,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->ix = ix;
     p->device = ix->device;
     p->read_len = cfg->read_len;
+    p->stride = cfg->read_stride ? cfg->read_stride : cfg->read_len;
     p->min_len = cfg->min_len;
     p->slots = cfg->read_len - cfg->min_len + 1;
     p->n_contig = cfg->n_contig;
@@ -1340,7 +1347,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     for (int k = 0; k < 2; ++k) {
       p->d_match_s[k] = dalloc<uint64_t>(2 * P * p->slots);
       p->d_nmatch_s[k] = dalloc<uint32_t>(2 * P);
-      p->d_rec_s[k] = dalloc<uint8_t>(p->rec_bytes);
+      // (the records: only for dense input, allocated by the first search that needs them)
       p->d_work_s[k] = dalloc<unsigned long long>(1);
       SMASH_HIPX(hipStreamCreateWithFlags(&p->xs[k], hipStreamNonBlocking));
       SMASH_HIPX(hipEventCreateWithFlags(&p->ev_found[k], hipEventDisableTiming));
@@ -1452,6 +1459,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
 
 namespace smash {
 uint32_t pipe_read_len(const smash_pipeline *p) { return p->read_len; }
+uint32_t pipe_stride(const smash_pipeline *p) { return p->stride; }
 uint64_t pipe_max_pairs(const smash_pipeline *p) { return p->max_pairs; }
 int pipe_device(const smash_pipeline *p) { return p->device; }
 void *&pipe_feed(smash_pipeline *p, void (*freer)(void *)) {
@@ -1520,9 +1528,13 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
     p->ix->kev[0] = p->ev[2 * p->n_ev];          // recorded around k_mam_sm itself
     p->ix->kev[1] = p->ev[2 * p->n_ev + 1];
   }
-  const SearchWs ws{p->d_rec_s[k], p->rec_bytes, p->d_work_s[k],
+  if (!search_direct(d_reads, p->stride, p->read_len) && !p->d_rec_s[k]) {   // k_prep's records
+    SMASH_HIP(hipStreamSynchronize(xs));
+    SMASH_HIP(hipMalloc(reinterpret_cast<void **>(&p->d_rec_s[k]), p->rec_bytes));
+  }
+  const SearchWs ws{p->d_rec_s[k], p->d_rec_s[k] ? p->rec_bytes : 0, p->d_work_s[k],
                     p->set_used[k] && !p->gate_prep ? p->ev_free[k] : nullptr};
-  const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->read_len, nullptr,
+  const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->stride, nullptr,
                                 p->read_len, 2 * n_pairs, p->d_match_s[k], p->slots,
                                 p->d_nmatch_s[k], xs, false, &ws);   // probe check at stats time
   p->ix->kev[0] = p->ix->kev[1] = nullptr;
@@ -1786,7 +1798,7 @@ static int count_batches_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_
     SMASH_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
     rc = hipEventRecord(in_ev, s) == hipSuccess ? SMASH_OK : SMASH_ERR_HIP;
   }
-  const uint64_t L2 = 2 * uint64_t(p->read_len);
+  const uint64_t L2 = 2 * uint64_t(p->stride);
   for (uint64_t b0 = 0; rc == SMASH_OK && b0 < n_pairs; b0 += batch_pairs) {
     const uint64_t n = std::min(batch_pairs, n_pairs - b0);
     rc = smash::count_batch_ev(p, d_reads + b0 * L2, n, d_counts, s, in_ev);

@@ -60,6 +60,7 @@ EXPORTS = [
     "smash_phase_search_ahead",
     "smash_fastq_shard_scan", "smash_fastq_shard_free_blob", "smash_fastq_shard_open",
     "smash_fastq_shard_pack", "smash_fastq_shard_stats", "smash_fastq_shard_close",
+    "smash_read_stride",
 ]
 
 
@@ -80,7 +81,8 @@ class PipelineCfg(C.Structure):
                 ("h_tag_offsets", u32p), ("h_small_chr", u8p),
                 ("h_chrom_off", i64p), ("nbins", C.c_uint32),
                 ("h_bin_starts", i64p), ("min_excess", C.c_int32),
-                ("hit_window", C.c_int64), ("dedup_capacity", C.c_uint64)]
+                ("hit_window", C.c_int64), ("dedup_capacity", C.c_uint64),
+                ("read_stride", C.c_uint32)]
 
 
 class FeedStats(C.Structure):
@@ -217,6 +219,8 @@ def lib():
     L.smash_fastq_shard_stats.argtypes = [vp, C.POINTER(ShardStats)]
     L.smash_fastq_shard_close.argtypes = [vp]
     L.smash_fastq_shard_close.restype = None
+    L.smash_read_stride.argtypes = [C.c_uint32]
+    L.smash_read_stride.restype = C.c_uint32
     L.smash_count_fastq.argtypes = [vp, C.POINTER(C.c_char_p), C.c_uint32,
                                     C.POINTER(C.c_char_p), C.c_uint32, C.c_int, C.c_uint32, vp,
                                     C.POINTER(FeedStats), vp]
@@ -414,12 +418,31 @@ def read_bins(path):
     return rows, np.array([int(r[2]) for r in rows], np.int64)
 
 
+def read_stride(read_len):
+    """bytes of the device's native row for a mate of read_len bases
+    (smash_read_stride): batches laid out in such rows (16-byte aligned, zero
+    padded) are searched without a record build"""
+    return int(lib().smash_read_stride(read_len))
+
+
+def to_rows(d_reads, read_len=None):
+    """a [2n, L] uint8 device tensor of mates as the native rows [2n, stride]
+    (zero padded)"""
+    import torch
+    L = read_len or d_reads.shape[1]
+    rows = torch.zeros((d_reads.shape[0], read_stride(L)), dtype=torch.uint8, device=d_reads.device)
+    rows[:, :L] = d_reads[:, :L]
+    return rows
+
+
 class Pipeline:
-    """prepare_matches + mappability_tag + smashMEM + varbin on the device."""
+    """prepare_matches + mappability_tag + smashMEM + varbin on the device.
+    read_stride: the bytes from one mate to the next in the batches (0:
+    read_len, dense; read_stride(read_len): native rows, see to_rows)."""
 
     def __init__(self, index: Index, chrom_sizes: dict, bin_starts, read_len,
                  max_pairs, min_len=20, min_excess=4, hit_window=10000,
-                 dedup_capacity=None):
+                 dedup_capacity=None, read_stride=0):
         self.index = index
         sizes = index.contig_sizes
         self.tag, self.small, self.off = contig_tables(index.contigs, sizes, chrom_sizes)
@@ -428,18 +451,19 @@ class Pipeline:
                                _p(self.tag, u32p), _p(self.small, u8p),
                                _p(self.off, i64p), len(self.bins), _p(self.bins, i64p),
                                min_excess, hit_window,
-                               dedup_capacity or max_pairs)
+                               dedup_capacity or max_pairs, read_stride)
         h = vp()
         check(lib().smash_pipeline_create(index.h, C.byref(self.cfg), C.byref(h)),
               "smash_pipeline_create")
         self.h = h
         self.read_len = read_len
+        self.stride = read_stride or read_len
         self.max_pairs = max_pairs
         self.slots = read_len - min_len + 1
 
     def count_batch(self, d_reads, n_pairs, d_counts, stream=None):
         """d_reads: device uint8 [2*n_pairs, read_len] (torch tensor or ptr)."""
-        check(lib().smash_count_batch(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+        check(lib().smash_count_batch(self.h, _reads(d_reads, n_pairs, self.stride), n_pairs,
                                       _ptr(d_counts),
                                       vp(_stream(stream))), "smash_count_batch")
 
@@ -466,33 +490,33 @@ class Pipeline:
         searches need not wait for the work queued on the stream before this
         call -- consecutive runs over the same reads overlap."""
         if resident:
-            check(lib().smash_count_batches_ready(self.h, _reads(d_reads, n_pairs, self.read_len),
+            check(lib().smash_count_batches_ready(self.h, _reads(d_reads, n_pairs, self.stride),
                                                   n_pairs, batch_pairs,
                                                   _ptr(d_counts), vp(_stream(stream)), None),
                   "smash_count_batches_ready")
             return
-        check(lib().smash_count_batches(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+        check(lib().smash_count_batches(self.h, _reads(d_reads, n_pairs, self.stride), n_pairs,
                                         batch_pairs,
                                         _ptr(d_counts), vp(_stream(stream))),
               "smash_count_batches")
 
     def phase_map(self, d_reads, n_pairs, stream=None):
-        check(lib().smash_phase_map(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+        check(lib().smash_phase_map(self.h, _reads(d_reads, n_pairs, self.stride), n_pairs,
                                     vp(_stream(stream))),
               "smash_phase_map")
 
     def phase_map_ahead(self, d_reads, n_pairs, d_next, n_next, stream=None):
         """phase_map, and the next batch's search issued at once on the
         pipeline's other search stream (smash_phase_map_ahead)."""
-        check(lib().smash_phase_map_ahead(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
-                                          _reads(d_next, n_next, self.read_len) if n_next else None,
+        check(lib().smash_phase_map_ahead(self.h, _reads(d_reads, n_pairs, self.stride), n_pairs,
+                                          _reads(d_next, n_next, self.stride) if n_next else None,
                                           n_next,
                                           vp(_stream(stream))), "smash_phase_map_ahead")
 
     def phase_search_ahead(self, d_reads, n_pairs, stream=None):
         """after phase_export of batch b: batch b + 2's search into the set
         b used (smash_phase_search_ahead)."""
-        check(lib().smash_phase_search_ahead(self.h, _reads(d_reads, n_pairs, self.read_len), n_pairs,
+        check(lib().smash_phase_search_ahead(self.h, _reads(d_reads, n_pairs, self.stride), n_pairs,
                                              vp(_stream(stream))), "smash_phase_search_ahead")
 
     def phase_export(self, world, global_base, stream=None):

@@ -135,3 +135,59 @@ def test_full_key_set_fails_loudly(gix, monkeypatch):
     cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
     with pytest.raises(S.SmashError, match="key set full"):
         run_emulated(gix, reads, 2, 150, 6, starts, cs, True, capacity=150)
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+@pytest.mark.parametrize("how", ["rows", "rows_records", "rows_phases"])
+def test_native_rows_equal_dense(gix, s, how, monkeypatch):
+    """The device's native read layout (smash_read_stride rows, zero padded,
+    16-byte aligned): the search copies each mate straight from its row and
+    the wave computes its bad mask in LDS (mam_sm.hpp direct rows).  Counts
+    and statistics equal the dense [2n, L] input's (k_prep records) for
+    count_batches, for the same rows through k_prep (SMASH_DIRECT_ROWS=0:
+    records built from strided rows), and through the multi-GPU phase calls;
+    the per-read MAM triples of smash_map_batch agree too."""
+    reads = interleaved_reads(s)
+    n = reads.shape[0] // 2
+    L = reads.shape[1]
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    dense = torch.from_numpy(np.ascontiguousarray(reads)).cuda()
+    rows = S.to_rows(dense)
+    assert rows.shape[1] == S.read_stride(L) and rows.shape[1] % 16 == 0
+    assert rows.data_ptr() % 16 == 0 and int(rows[:, L:].abs().sum()) == 0
+    if how == "rows_records":
+        monkeypatch.setenv("SMASH_DIRECT_ROWS", "0")
+
+    def run(d, stride, batch=173):
+        pipe = S.Pipeline(gix, cs, starts, L, batch, dedup_capacity=n, read_stride=stride)
+        pipe.reset()
+        c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+        if how == "rows_phases" and stride:
+            tail = torch.empty(2, dtype=torch.int64, device="cuda")
+            for b0 in range(0, n, batch):
+                b1 = min(n, b0 + batch)
+                pipe.phase_map(d[2 * b0:2 * b1], b1 - b0)
+                hdr, words, cnt, wcnt = pipe.phase_export(1, b0)
+                flags = torch.empty(max(int(cnt.sum()), 1), dtype=torch.uint8, device="cuda")
+                pipe.dedup_owner(hdr.clone(), int(cnt.sum()), words.clone(), cnt, wcnt, flags)
+                pipe.phase_import(flags)
+                pipe.phase_positions(tail)
+                pipe.phase_bin(None, c)
+        else:
+            pipe.count_batches(d, n, batch, c)
+        st = pipe.stats()
+        return c.cpu().numpy().tolist(), (st.positions, st.dups, st.kept, st.dupe_pairs, st.matches)
+
+    assert run(rows, rows.shape[1]) == run(dense, 0)
+    # smash_map_batch over rows (stride = the native row) == over dense mates
+    cap = L - 20 + 1
+    got = []
+    for d, stride in ((dense, L), (rows, rows.shape[1])):
+        o = torch.zeros(2 * n * cap, dtype=torch.int64, device="cuda")
+        nn = torch.zeros(2 * n, dtype=torch.int32, device="cuda")
+        S.lib().smash_map_batch(gix.h, S.SMASH_MODE_MAM, 20, S._ptr(d), stride, None, L, 2 * n,
+                                S._ptr(o), cap, S._ptr(nn), S.vp(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        got.append((o.cpu().numpy().tolist(), nn.cpu().numpy().tolist()))
+    assert got[0] == got[1]

@@ -52,9 +52,13 @@ def _edge_reads(ix, L, n, rng):
 
 
 @pytest.mark.parametrize("L", [15, 32, 33, 100, 128, 129, 150, 255])
-def test_state_machine_edge_reads(emu, tiny_ix, L):
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_state_machine_edge_reads(emu, tiny_ix, L, direct, monkeypatch):
     """bytes absent from the text, 'n' (present), windows at the read end,
-    homopolymers; read lengths around the record/bad-mask boundaries."""
+    homopolymers; read lengths around the record/bad-mask boundaries.
+    direct: the reads as native rows (the bad mask computed from the LDS
+    row, mam_sm.hpp row_bad_mask) or as k_prep records."""
+    monkeypatch.setenv("SMASH_SM_DIRECT", direct)
     rng = np.random.default_rng(L)
     reads = _edge_reads(tiny_ix, L, 120, rng)
     extra = [b"z" * L, b"n" * L, b"a" * L, (b"acgt" * 64)[:L], (b"c" * (L // 2) + b"z" + b"c" * L)[:L]]

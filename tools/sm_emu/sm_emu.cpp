@@ -94,14 +94,19 @@ static void emu_dma_row(uint32_t *dst, const uint4 *src, uint32_t n, const uint4
   // one instruction: its lanes' chunks coalesce per line; the lane's own
   // bad-mask load next iteration is one more request per line it touches
   emu_req[0] += ((reinterpret_cast<uint64_t>(src + n) - 1) >> 6) - (reinterpret_cast<uint64_t>(src) >> 6) + 1;
-  emu_req[0] += ((reinterpret_cast<uint64_t>(src) - 1) >> 6) - (reinterpret_cast<uint64_t>(rec0) >> 6) + 1;
+  if (rec0 != src)   // (records: the lane's own load of the bad-mask chunks)
+    emu_req[0] += ((reinterpret_cast<uint64_t>(src) - 1) >> 6) - (reinterpret_cast<uint64_t>(rec0) >> 6) + 1;
   for (uint32_t k = 0; k < n; ++k) {
     const uint4 v = emu_load16(reinterpret_cast<uint64_t>(src + k));
     std::memcpy(dst + 4 * k, &v, 16);
   }
-  emu_last[7] = reinterpret_cast<uint64_t>(rec0) >> 6;   // chunks 0, 1: the line chunk 2 opened
+  if (rec0 != src) emu_last[7] = reinterpret_cast<uint64_t>(rec0) >> 6;   // chunks 0, 1: the line chunk 2 opened
 }
-#define SM_DMA_ROW(dst, src, n, lane) emu_dma_row(dst, src, n, (src) - c.c_bad)
+// (direct rows: the row is the read itself, no bad-mask chunks before it)
+#define SM_DMA_ROW(dst, src, n, lane) emu_dma_row(dst, src, n, c.direct ? (src) : (src) - c.c_bad)
+// direct rows: the bad mask from the lane's own row (the device computes it
+// with the whole wave)
+#define SM_HOST_LANE
 #define SM_DMA_ROW_HOST
 #define PAD_KEEP(x) ((void)(x))
 // v_perm_b32 on the host: byte i of the result from selector byte i (0-7 a
@@ -194,13 +199,25 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
                uint64_t *viol, uint32_t lin_blocks, uint64_t *counters) {
   const sm::Geom g = sm::make_geom(L);
   if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
+  // direct rows (the device's path for native-row input, the default here as
+  // in bench.py; SMASH_SM_DIRECT=0: records built by k_prep)
+  const bool direct = !(std::getenv("SMASH_SM_DIRECT") && std::getenv("SMASH_SM_DIRECT")[0] == '0');
+  const uint64_t rw = 4ull * g.w_row;   // native row bytes
+  std::vector<uint4> rows_mem(direct ? n * rw / 16 + 4 : 0);
+  uint8_t *rows_p = direct ? reinterpret_cast<uint8_t *>(rows_mem.data()) : nullptr;
+  while (direct && (reinterpret_cast<uint64_t>(rows_p) & 63)) rows_p += 16;
+  for (uint64_t q = 0; direct && q < n; ++q) {
+    std::memset(rows_p + q * rw, 0, rw);
+    std::memcpy(rows_p + q * rw, reads + q * stride, L);
+  }
   // 64-byte aligned, as the device's allocation (records are whole lines)
   std::vector<uint4> rec_mem(n * g.chunks + 4);
   uint4 *rec_p = rec_mem.data();
   while (reinterpret_cast<uint64_t>(rec_p) & 63) ++rec_p;
   struct { uint4 *p; size_t n; uint4 *data() { return p; } size_t size() const { return n; } } rec{
       rec_p, size_t(n * g.chunks)};
-  if (prep_records(reads, stride, nullptr, L, n, in_text, g, reinterpret_cast<uint32_t *>(rec.data()),
+  if (!direct &&
+      prep_records(reads, stride, nullptr, L, n, in_text, g, reinterpret_cast<uint32_t *>(rec.data()),
                    !(std::getenv("SMASH_PREP_LDS") && std::getenv("SMASH_PREP_LDS")[0] == '1')))
     return -1;
   threadIdx.x = 0;
@@ -210,6 +227,9 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   (void)BM;   // (round 3: the filter's presence bits live in KT)
   c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
   c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
+  c.rows = direct ? reinterpret_cast<const uint4 *>(rows_p) : nullptr;
+  c.direct = direct ? 1u : 0u;
+  sm::bad_table(in_text, &c.bad_tab_lo, &c.bad_tab_hi);
   c.lin_blocks = lin_blocks;
   c.pad = 0;
   c.grab = 1;
@@ -230,8 +250,8 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   unsigned long long v[10] = {0};
   c.viol = v;
   emu_spans = spans;
-  emu_rec_lo = reinterpret_cast<uint64_t>(rec.data());
-  emu_rec_hi = emu_rec_lo + rec.size() * sizeof(uint4);
+  emu_rec_lo = direct ? reinterpret_cast<uint64_t>(rows_p) : reinterpret_cast<uint64_t>(rec.data());
+  emu_rec_hi = emu_rec_lo + (direct ? n * rw : rec.size() * sizeof(uint4));
   emu_bad = 0;
   for (int k = 0; k < 8; ++k) { emu_probes[k] = emu_lines[k] = 0; emu_last[k] = ~0ull; }
   emu_req[0] = emu_req[1] = 0;
