@@ -716,6 +716,10 @@ def main():
                                           "%.1f s" % (nm, dtm),
                    "end_to_end_reads_per_s": round(2 * n1 / dt, 1),
                    "cores_note": note,
+                   "port_vs_reference": "the port maps 1.64x the reference binary's rate on "
+                                        "1 core, 1.04x on 8 (profiles/r03/"
+                                        "cpu_calibration_c1.log): an upper bound on the "
+                                        "reference CPU path",
                    "index_load_s": round(time.time() - t2 - dt - dtm - dt0, 1),
                    "bin_counts_identical_to_device": exact}
             log("cpu baseline: %.3e reads/s end to end, %.3e mapping only, on %d threads; "

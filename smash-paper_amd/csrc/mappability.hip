@@ -282,19 +282,26 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     const bool fast = (satf | satr) == 0 && ib + kMPer <= i1;
     uint32_t umask = 0;
     if (fast) {
-      // away from the contig ends (m <= 255) the edge rules cannot zero a byte
-      const bool edge = ib < 272 || ib + kMPer + 256 > S;
 #pragma unroll
       for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
-        const uint64_t i = ib + q;
-        uint32_t rb = byte_of(fw, q) + 1;                  // <= 255: U < 255 here
-        uint32_t lb = byte_of(rw, 15 - q) + 1;
-        if (edge) {
-          rb = uint64_t(rb) + i >= S ? 0u : rb;
-          lb = uint64_t(lb) >= i ? 0u : lb;
-        }
+        const uint32_t rb = byte_of(fw, q) + 1;            // <= 255: U < 255 here
+        const uint32_t lb = byte_of(rw, 15 - q) + 1;
         ob[q >> 1] |= (lb | (rb << 8)) << (16 * (q & 1));
         umask |= uint32_t(rb - 1u < c.k) << q;             // 1 <= rb <= k
+      }
+      // the edge rules can zero a byte only near the contig ends (m <= 256):
+      // a separate pass for those chunks
+      if (ib < 272 || ib + kMPer + 256 > S) {
+        const uint32_t rem = S - ib < 0xFFFFFFFFull ? uint32_t(S - ib) : 0xFFFFFFFFu, ib32 = uint32_t(ib < 272 ? ib : 272);
+#pragma unroll
+        for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
+          const uint32_t sh = 16 * (q & 1);
+          if (byte_of(fw, q) + 1 + q >= rem) {             // right + i >= S (:666)
+            ob[q >> 1] &= ~(0xFF00u << sh);
+            umask &= ~(1u << q);
+          }
+          if (byte_of(rw, 15 - q) + 1 >= ib32 + q) ob[q >> 1] &= ~(0xFFu << sh);   // left >= i
+        }
       }
       mine = uint32_t(__popc(umask));
       if (binned && umask) {
@@ -317,6 +324,10 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         }
       }
     }
+    // U at the first unsaturated position after / above the chunk, loaded
+    // once (the saturated bases of the chunk all bound through it)
+    const uint32_t ufn = !fast && satf && fnext != kNone ? uint32_t(U[fnext]) : 0u;
+    const uint32_t urn = !fast && satr && rnext != kNone ? uint32_t(U[rnext]) : 0u;
 #pragma unroll 4
     for (uint32_t q = 0; q < uint32_t(kMPer) && !fast; ++q) {
       const uint64_t i = ib + q;
@@ -329,11 +340,12 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       } else if (i + 256 >= S) {
         right = 0;
       } else {
-        uint64_t y = kNone;   // next unsaturated text position after xf + q
-        for (uint32_t q2 = q + 1; q2 < uint32_t(kMPer) && y == kNone; ++q2)
-          if (!((satf >> q2) & 1)) y = xf + q2;
-        if (y == kNone) y = fnext;
-        const uint64_t ub = y == kNone ? kNone : U[y] + 1 + (y - (xf + q));
+        // the next unsaturated text position after xf + q: in the chunk (its
+        // U byte is in fw), else fnext
+        const uint32_t above = ~satf & 0xFFFFu & (0xFFFFFFFEu << q);
+        const uint32_t q2 = above ? uint32_t(__builtin_ctz(above)) : 0u;
+        const uint64_t ub = above ? uint64_t(byte_of(fw, q2)) + 1 + (q2 - q)
+                            : fnext == kNone ? kNone : ufn + 1 + (fnext - (xf + q));
         if (ub != kNone && i + ub < S) right = 255;
         else if (defer) {
           right = 255;
@@ -351,11 +363,12 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       } else if (i <= 256) {
         left = 0;
       } else {
-        uint64_t y = kNone;   // next unsaturated text position above xr - q
-        for (uint32_t q2 = q; q2-- > 0 && y == kNone;)
-          if (!((satr >> q2) & 1)) y = xr - q2;
-        if (y == kNone) y = rnext;
-        const uint64_t ub = y == kNone ? kNone : U[y] + 1 + (y - (xr - q));
+        // the next unsaturated text position above xr - q: in the chunk
+        // (base q2 < q, the largest: rw byte 15 - q2), else rnext
+        const uint32_t below = ~satr & ((1u << q) - 1u);
+        const uint32_t q2 = below ? 31u - uint32_t(__builtin_clz(below)) : 0u;
+        const uint64_t ub = below ? uint64_t(byte_of(rw, 15 - q2)) + 1 + (q - q2)
+                            : rnext == kNone ? kNone : urn + 1 + (rnext - (xr - q));
         if (ub != kNone && ub < i) left = 255;
         else if (defer) {
           left = 255;
@@ -381,7 +394,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         }
       }
     }
-    if (c.fix) {   // list the deferred bytes: one atomic per wave
+    if (c.fix && __ballot((fixr | fixl) != 0)) {   // list the deferred bytes: one atomic per wave
       const uint32_t nf = uint32_t(__popc(fixr) + __popc(fixl));
       const uint32_t lane = threadIdx.x & 63;
       uint32_t x = nf;

@@ -33,6 +33,13 @@ enum Stat { S_PAIRS, S_KEYPAIRS, S_DUPEPAIRS, S_POS, S_DUPS, S_KEPT, S_MATCHES, 
 // reduction (a kernel with LDS cannot share a CU with the search, whose
 // blocks hold all of it); the host sums the rows.  S_ERR lives in row 0.
 constexpr uint32_t kStatStride = 16, kStatStripes = 16, kStatWords = kStatStride * kStatStripes;
+// the multi-GPU export's header per key (smash_phase_export): {hash hi, hash
+// lo, nk << 40 | word offset in the owner's segment} = SMASH_EXPORT_HDR_WORDS
+// (round 3 also sent the global pair index and kept nk and the offset in
+// words of their own: 40 B per key, now 24)
+constexpr uint32_t kHdrWords = 3;
+constexpr uint64_t kHdrOffMask = (uint64_t(1) << 40) - 1;
+static_assert(kHdrWords == SMASH_EXPORT_HDR_WORDS, "smash_gpu.h's export header");
 }  // namespace
 
 // The post-stage kernels run beside the next batch's k_mam_sm (no LDS, so
@@ -138,7 +145,7 @@ struct smash_pipeline {
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
   unsigned long long *d_owner = nullptr;  // per owner: [0,64) keys [64,128) words (k_export_totals)
-  uint64_t *d_send_hdr = nullptr; // [n_export][5] {hi, lo, global index, nk, word offset}
+  uint64_t *d_send_hdr = nullptr; // [n_export][kHdrWords] {hi, lo, nk << 40 | word offset}
   uint64_t *d_send_words = nullptr;   // the exported keys' hit words, grouped by owner
   uint64_t send_words_cap = 0;
   uint64_t *d_recv_base = nullptr;    // [2 * 65] owner side: header / word prefix per source
@@ -1441,7 +1448,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       if (b > 0 && b < 64) p->hash_mask = (1ull << b) - 1;
     }
     p->d_owner = dalloc<unsigned long long>(4 * 64);
-    p->d_send_hdr = dalloc<uint64_t>(5 * P);
+    p->d_send_hdr = dalloc<uint64_t>(uint64_t(kHdrWords) * P);
     p->d_recv_base = dalloc<uint64_t>(2 * 65);
     SMASH_HIPX(hipHostMalloc(reinterpret_cast<void **>(&p->h_owner), 8 * 256, hipHostMallocDefault));
     SMASH_HIPX(hipHostMalloc(reinterpret_cast<void **>(&p->h_recv_base), 8 * 2 * 65,
@@ -1822,8 +1829,8 @@ extern "C" int smash_count_batches_ready(smash_pipeline *p, const uint8_t *d_rea
 }
 
 // ---- multi-GPU de-dup exchange ------------------------------------------------
-// Each rank exports its in-batch-first keys to owner = (hash hi >> 1) % world: a
-// 5-word header {hi, lo, global pair index, nk, word offset} per key and the
+// Each rank exports its keyed pairs to owner = (hash hi >> 1) % world: a
+// 3-word header {hi, lo, nk << 40 | word offset} per key and the
 // key's nk hit words (hash + canonical key bytes + index).
 // The owner decides first-wins over the exact keys and answers one byte per
 // header.
@@ -1957,11 +1964,10 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
   const uint64_t seg_w = boff[uint64_t(ow) * nblk] & 0xFFFFFFFFull;   // owner's word segment
   e += bo >> 32;
   w += bo & 0xFFFFFFFFull;
-  hdr[5 * e] = hash[2 * q];
-  hdr[5 * e + 1] = hash[2 * q + 1];
-  hdr[5 * e + 2] = gbase + q;
-  hdr[5 * e + 3] = k;
-  hdr[5 * e + 4] = w - seg_w;   // offset in this owner's word segment
+  (void)gbase;   // the receive order is the global order: no pair index travels
+  hdr[kHdrWords * e] = hash[2 * q];
+  hdr[kHdrWords * e + 1] = hash[2 * q + 1];
+  hdr[kHdrWords * e + 2] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
   const uint64_t *src = hits + q * 2 * uint64_t(slots);
   for (uint32_t i = 0; i < k; ++i) words[w + i] = src[i];
   send_q[e] = uint32_t(q);
@@ -1973,8 +1979,9 @@ __device__ __forceinline__ KeyRef recv_key(const uint64_t *recv, const uint64_t 
                                            const uint64_t *base, int world, uint64_t j) {
   int r = 0;
   while (r + 1 < world && j >= base[r + 1]) ++r;
-  return KeyRef{words + base[65 + r] + recv[5 * j + 4], uint32_t(recv[5 * j + 3]),
-                recv[5 * j + 1]};
+  const uint64_t nw = recv[kHdrWords * j + 2];
+  return KeyRef{words + base[65 + r] + (nw & kHdrOffMask), uint32_t(nw >> 40),
+                recv[kHdrWords * j + 1]};
 }
 
 // The owner's first-wins decision, the single-GPU claim / decide scheme
@@ -1992,7 +1999,7 @@ __global__ void k_owner_claim(const uint64_t *recv, const uint64_t *words, const
   int32_t err = 0;
   for (uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < n; j += stride) {
     const KeyRef me = recv_key(recv, words, base, world, j);
-    const uint64_t hi = recv[5 * j];
+    const uint64_t hi = recv[kHdrWords * j];
     const unsigned long long mine = (epoch << kRefShift) | (j + 1);
     uint64_t res = kSlotNone;
     uint64_t i = (hi ^ (hi >> 31)) & mask;
@@ -2057,7 +2064,7 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
     bool win = false;
     uint32_t m = 0;
     if (j < n) {
-      m = uint32_t(recv[5 * j + 3]);
+      m = uint32_t(recv[kHdrWords * j + 2] >> 40);
       const uint64_t sl = slot_of[j];
       if (sl < kSlotNone) {
         const unsigned long long ref = __hip_atomic_load(

@@ -6,11 +6,13 @@ SURVEY.md Appendix A.11) is (step, rank, pair).  Everything is per-rank except
 the two dependencies the reference's sequential scripts carry:
 
 * smashMEM.py's global first-wins pair de-dup (smashMEM.py:149,217-228): the
-  in-batch-first keys -- a header {hash, global pair index, length} plus the
-  key's canonical hit words -- are sent to owner rank = (hash >> 1) % world
-  (all_to_all of the counts, the headers and the words), the owner decides
-  first-wins by global pair index over the exact keys against its persistent
-  key set and returns one flag per key (all_to_all back);
+  keyed pairs -- a header {hash, length, word offset} plus the key's
+  canonical hit words -- are sent to owner rank = (hash >> 1) % world, each
+  owner's segment in pair order (all_to_all of the counts, the headers and
+  the words); the receive order (source ranks in rank order) is then the
+  global pair order, so the owner decides first-wins in receive order over
+  the exact keys against its persistent key set and returns one flag per key
+  (all_to_all back);
 * varbin.py's adjacent de-dup (varbin.py:56-58) compares with the previous
   emitted position: all_gather of every rank's {count, last pos0} gives each
   rank the last position emitted before its shard.
@@ -149,7 +151,7 @@ class ShardedCounter:
         self._mark("counts")
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
         n_recv, n_words = sum(rcv), sum(rcw)
-        recv = torch.empty((max(n_recv, 1), 5), dtype=torch.int64, device=dev)
+        recv = torch.empty((max(n_recv, 1), hdr.shape[1]), dtype=torch.int64, device=dev)
         self.comm.all_to_all(recv[:n_recv], hdr[:sum(snd)], rcv, snd)
         recv_words = torch.empty(max(n_words, 1), dtype=torch.int64, device=dev)
         self.comm.all_to_all(recv_words[:n_words], words[:sum(sndw)], rcw, sndw)

@@ -440,6 +440,9 @@ class Pipeline:
     read_stride: the bytes from one mate to the next in the batches (0:
     read_len, dense; read_stride(read_len): native rows, see to_rows)."""
 
+    # u64 words per key in phase_export's headers (SMASH_EXPORT_HDR_WORDS)
+    hdr_words = 3
+
     def __init__(self, index: Index, chrom_sizes: dict, bin_starts, read_len,
                  max_pairs, min_len=20, min_excess=4, hit_window=10000,
                  dedup_capacity=None, read_stride=0):
@@ -520,7 +523,7 @@ class Pipeline:
                                              vp(_stream(stream))), "smash_phase_search_ahead")
 
     def phase_export(self, world, global_base, stream=None):
-        """(headers [n, 5] int64, words [w] int64, per-owner key counts,
+        """(headers [n, hdr_words] int64, words [w] int64, per-owner key counts,
         per-owner word counts) -- the tensors alias pipeline-owned device
         memory, valid until the next export."""
         import torch
@@ -531,8 +534,9 @@ class Pipeline:
                                        _p(wcounts, i64p), C.byref(ds), C.byref(dw),
                                        vp(_stream(stream))), "smash_phase_export")
         n, w = int(counts.sum()), int(wcounts.sum())
-        hdr = device_view(ds.value, 40 * n, torch.int64).view(n, 5) if n else \
-            torch.zeros((0, 5), dtype=torch.int64, device="cuda")
+        H = self.hdr_words
+        hdr = device_view(ds.value, 8 * H * n, torch.int64).view(n, H) if n else \
+            torch.zeros((0, H), dtype=torch.int64, device="cuda")
         words = device_view(dw.value, 8 * w, torch.int64) if w else \
             torch.zeros(0, dtype=torch.int64, device="cuda")
         return hdr, words, counts, wcounts

@@ -67,9 +67,10 @@ class OraclePhasePipeline:
         pass                               # (likewise)
 
     def phase_export(self, world, gbase):
-        """smash_phase_export's layout: per owner, 5-word headers {hi, lo,
-        global index, nk, word offset in the owner segment} and the keys'
-        hit words (tid << 48 | pos0)."""
+        """smash_phase_export's layout: per owner, in pair order, 3-word
+        headers {hi, lo, nk << 40 | word offset in the owner segment} and the
+        keys' hit words (tid << 48 | pos0).  No pair index travels: the
+        receive order is the global order (dedup_owner relies on it)."""
         first = {}
         for q, k in enumerate(self.kept_hits):
             if k is not None and tuple(k) not in first:
@@ -83,13 +84,13 @@ class OraclePhasePipeline:
             seg = []
             for k, q in sorted(groups[w], key=lambda t: t[1]):
                 h = self.hashes[q]
-                rows.append((to_i64(h[0]), to_i64(h[1]), gbase + q, len(k), len(seg)))
+                rows.append((to_i64(h[0]), to_i64(h[1]), (len(k) << 40) | len(seg)))
                 seg += [to_i64((tid << 48) | pos) for tid, pos in k]
                 self.order.append(q)
             words += seg
             counts.append(len(groups[w]))
             wcounts.append(len(seg))
-        hdr = torch.tensor(rows, dtype=torch.int64).reshape(-1, 5)
+        hdr = torch.tensor(rows, dtype=torch.int64).reshape(-1, 3)
         return (hdr, torch.tensor(words, dtype=torch.int64), np.array(counts, np.int64),
                 np.array(wcounts, np.int64))
 
@@ -100,12 +101,13 @@ class OraclePhasePipeline:
         wb = np.cumsum([0] + list(recv_words))
         best = {}
         keys = []
-        for j, (hi, lo, g, nk, off) in enumerate(rows):
+        for j, (hi, lo, nw) in enumerate(rows):
+            nk, off = nw >> 40, nw & ((1 << 40) - 1)
             src = int(np.searchsorted(hb, j, side="right")) - 1
             a = int(wb[src]) + off
             k = tuple((to_u64(w) >> 48, to_u64(w) & 0xFFFFFFFFFFFF) for w in words[a:a + nk])
             keys.append(k)
-            if k not in best or g < rows[best[k]][2]:
+            if k not in best:   # the first in receive order = global pair order
                 best[k] = j
         flags = np.zeros(n_recv, np.uint8)
         for k, j in best.items():

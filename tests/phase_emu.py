@@ -74,7 +74,7 @@ def run_emulated(ix, reads, W, per_rank, steps, starts, cs, ahead=False, capacit
                 wparts.append(words[w0:w0 + wcnt[o]])
                 rc.append(cnt[o])
                 rw.append(wcnt[o])
-            recv = torch.cat(hparts) if sum(rc) else torch.zeros((1, 5), dtype=torch.int64, device=dev)
+            recv = torch.cat(hparts) if sum(rc) else torch.zeros((1, sends[0][0].shape[1]), dtype=torch.int64, device=dev)
             rwords = torch.cat(wparts) if sum(rw) else torch.zeros(1, dtype=torch.int64, device=dev)
             n = sum(rc)
             flags = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
