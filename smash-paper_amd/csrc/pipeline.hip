@@ -133,6 +133,7 @@ struct smash_pipeline {
   // emitted position (-1: none), and its inclusive "last valid" scan
   int64_t *d_lp = nullptr, *d_lps = nullptr;
   bool fused_bin = true;
+  uint32_t bin_flush = 0x8000;    // k_emit_bin_lds's 16-bit counter flush threshold
   bool bin_lds = true;            // k_emit_bin_lds when the bins fit (SMASH_BIN_LDS=0: global
                                   // atomics; the LDS form runs in the gap SMASH_GATE_POST leaves)
   bool pos_dirty = false;         // the positions arrays are not materialised yet
@@ -1125,12 +1126,20 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
 // k_emit_bin with the counts summed on chip: a global atomic per position
 // (one lane per random bin, executed at the memory side) is the slow shape
 // of an atomic (MI355X_MICROARCH.md, Global float atomics).  The bins are
-// cut in parts of kBinPart u32 LDS counters; block (x, part) walks the pairs
+// cut in parts of kBinPart LDS counters; block (x, part) walks the pairs
 // of its x slice, bins every emitted position as k_emit_bin does, counts the
 // ones in its part in LDS and adds the part to the global counts once, lane
-// i -> bin i (whole contiguous rows).  Every part re-walks the pairs (hit
-// words and bisects: cheap next to the atomics); part 0 keeps the stats.
-constexpr uint32_t kBinPart = 38912;   // <= 152 KB of counters: one 1024-thread block per CU
+// i -> bin i (whole contiguous rows).  Every part re-walks the pairs (the
+// walk, a chain of dependent loads per pair at 16 waves per CU, is the
+// kernel's cost); part 0 keeps the stats.
+//
+// Round 4: the counters are 16-bit, two to an LDS word, so one part holds
+// 77 824 bins (C3's 50 000 in one walk instead of two).  A half never
+// overflows: the increment that takes a half from flush - 1 to flush (the
+// atomic's old value tells exactly one thread) subtracts flush from it and
+// adds flush to the global count; at most 1023 other increments of the block
+// land between the two, and flush + 1023 < 2^16 (flush <= 2^15).
+constexpr uint32_t kBinPart = 77824;   // 16-bit counters: 152 KB, one 1024-thread block per CU
 constexpr uint32_t kBinPartsMax = 4;   // above: k_emit_bin
 // the parts balanced: ceil(nbins / parts) bins each (50 k bins: 2 x 25 000,
 // not 24 576 + 24 576 + 848 -- every part re-walks all the pairs)
@@ -1145,11 +1154,11 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
     const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
     uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats,
-    uint32_t part) {
-  __shared__ uint32_t hc[kBinPart];
+    uint32_t part, uint32_t flush) {
+  __shared__ uint32_t hc[kBinPart / 2];   // bin b0 + i: half i & 1 of word i >> 1
   const uint32_t b0 = blockIdx.y * part;
   const uint32_t b1 = b0 + part < nbins ? b0 + part : nbins;
-  for (uint32_t i = threadIdx.x; i < part; i += blockDim.x) hc[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (part + 1) / 2; i += blockDim.x) hc[i] = 0;
   __syncthreads();
   const int64_t prev0 = *prev_p;
   unsigned long long d = 0, k = 0, t = 0;
@@ -1171,7 +1180,14 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
         ++d;
       } else {
         const uint32_t b = bin_of(p + co, bins, nbins, cell, ncell, cshift);
-        if (b >= b0 && b < b1) atomicAdd(&hc[b - b0], 1u);
+        if (b >= b0 && b < b1) {
+          const uint32_t sh = 16 * ((b - b0) & 1);
+          const uint32_t old = atomicAdd(&hc[(b - b0) >> 1], 1u << sh);
+          if (((old >> sh) & 0xFFFFu) == flush - 1) {
+            atomicSub(&hc[(b - b0) >> 1], flush << sh);
+            atomicAdd(&counts[b], (unsigned long long)flush);
+          }
+        }
         ++k;
       }
       prev = p;
@@ -1187,8 +1203,10 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     atomicAdd(&stats[S_DUPS], sd);
     atomicAdd(&stats[S_KEPT], sk);
   }
-  for (uint32_t i = threadIdx.x; b0 + i < b1; i += blockDim.x)
-    if (hc[i]) atomicAdd(&counts[b0 + i], (unsigned long long)hc[i]);
+  for (uint32_t i = threadIdx.x; b0 + i < b1; i += blockDim.x) {
+    const uint32_t c = (hc[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+    if (c) atomicAdd(&counts[b0 + i], (unsigned long long)c);
+  }
 }
 
 // the batch's tail {count, last position} (lps_last: lps[n - 1]; count 0:
@@ -1410,6 +1428,11 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       p->fused_bin = !(e && e[0] == '0');
       const char *l = getenv("SMASH_BIN_LDS");   // profiles/r03/binlds: 1.39 vs 2.18 ms
       p->bin_lds = !(l && l[0] == '0');
+      // SMASH_BIN_FLUSH (tests): k_emit_bin_lds's flush threshold, a power of
+      // two in [2, 2^15] (default 2^15)
+      const char *fl = getenv("SMASH_BIN_FLUSH");
+      const unsigned long f = fl ? std::strtoul(fl, nullptr, 10) : 0;
+      if (f >= 2 && f <= 0x8000 && !(f & (f - 1))) p->bin_flush = uint32_t(f);
       auto on = [](const char *v, bool dflt) {
         const char *x = getenv(v);
         return x && x[0] ? x[0] == '1' : dflt;
@@ -1735,7 +1758,7 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
       k_emit_bin_lds<<<grid, 1024, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
           p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
-          p->d_stats, part);
+          p->d_stats, part, p->bin_flush);
     } else if (n) {
       k_emit_bin<<<grid_for(n, kB, 8192), kB, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,

@@ -331,8 +331,9 @@ def test_key_set_exact_under_hash_collisions(gix, tiny_ix, bits, monkeypatch):
 @pytest.mark.parametrize("batch", [7, 1000])
 @pytest.mark.parametrize("s", ["s100", "s150"])
 def test_fused_positions_bins_agree(gix, s, batch, monkeypatch):
-    """k_count_last + k_emit_bin (positions and varbin in one pass) and the
-    two-kernel path (k_emit, then k_bin over the written positions) give the
+    """k_count_last + k_emit_bin (positions and varbin in one pass; global
+    atomics, and 16-bit LDS counters with the default and a tiny flush
+    threshold) and the two-kernel path (k_emit, then k_bin over the written positions) give the
     same counts, statistics and, read back after every batch, positions
     (the adjacent de-dup line carried across batches both ways)."""
     reads = interleaved_reads(s)
@@ -353,7 +354,10 @@ def test_fused_positions_bins_agree(gix, s, batch, monkeypatch):
     monkeypatch.setenv("SMASH_BIN_LDS", "0")   # global bin atomics (k_emit_bin), not LDS
     c = run()
     monkeypatch.setenv("SMASH_BIN_LDS", "1")
+    monkeypatch.setenv("SMASH_BIN_FLUSH", "2")   # 16-bit LDS counters flushed every 2
+    d = run()
+    monkeypatch.delenv("SMASH_BIN_FLUSH")
     monkeypatch.setenv("SMASH_FUSED_BIN", "0")
     b = run()
     assert a[1]["error"] == 0
-    assert a == b and a == c
+    assert a == b and a == c and a == d
