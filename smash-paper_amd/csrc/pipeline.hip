@@ -1977,23 +1977,49 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
   const uint32_t k = act ? uint32_t(nk[q]) : 0u;
   const WaveGroup g = wave_owner_groups(act, ow, k, s_e[wv], s_w[wv]);
   __syncthreads();
-  if (!act) return;
-  uint64_t e = g.rank, w = g.wbefore;
-  for (uint32_t v = 0; v < wv; ++v) {   // the block's earlier waves' keys of this owner
-    e += s_e[v][ow];
-    w += s_w[v][ow];
+  uint64_t w = 0;
+  if (act) {
+    uint64_t e = g.rank;
+    w = g.wbefore;
+    for (uint32_t v = 0; v < wv; ++v) {   // the block's earlier waves' keys of this owner
+      e += s_e[v][ow];
+      w += s_w[v][ow];
+    }
+    const uint64_t bo = boff[uint64_t(ow) * nblk + blockIdx.x];
+    const uint64_t seg_w = boff[uint64_t(ow) * nblk] & 0xFFFFFFFFull;   // owner's word segment
+    e += bo >> 32;
+    w += bo & 0xFFFFFFFFull;
+    (void)gbase;   // the receive order is the global order: no pair index travels
+    hdr[kHdrWords * e] = hash[2 * q];
+    hdr[kHdrWords * e + 1] = hash[2 * q + 1];
+    hdr[kHdrWords * e + 2] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
+    send_q[e] = uint32_t(q);
   }
-  const uint64_t bo = boff[uint64_t(ow) * nblk + blockIdx.x];
-  const uint64_t seg_w = boff[uint64_t(ow) * nblk] & 0xFFFFFFFFull;   // owner's word segment
-  e += bo >> 32;
-  w += bo & 0xFFFFFFFFull;
-  (void)gbase;   // the receive order is the global order: no pair index travels
-  hdr[kHdrWords * e] = hash[2 * q];
-  hdr[kHdrWords * e + 1] = hash[2 * q + 1];
-  hdr[kHdrWords * e + 2] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
-  const uint64_t *src = hits + q * 2 * uint64_t(slots);
-  for (uint32_t i = 0; i < k; ++i) words[w + i] = src[i];
-  send_q[e] = uint32_t(q);
+  // the keys' words, the wave together: word t of the wave's concatenated
+  // key lists (lane order) is word t - pre(l) of lane l's key, so
+  // consecutive lanes store consecutive words of an owner's segment (a
+  // lane-per-key loop stores 64 scattered words per instruction)
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t incl = k;   // inclusive scan of the word counts over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= uint32_t(d)) incl += y;
+  }
+  const uint32_t total = __shfl(incl, 63, 64);
+  const uint64_t row = q * 2 * uint64_t(slots);
+  for (uint32_t t0 = 0; t0 < total; t0 += 64) {   // (wave-uniform: every shuffle has all lanes)
+    const uint32_t t = t0 + lane;
+    // the lane whose key holds word t: the first l with incl(l) > t
+    uint32_t l = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+      if (uint32_t(__shfl(int(incl), int(l + step - 1), 64)) <= t) l += step;
+    l = l < 63u ? l : 63u;   // (t >= total: a lane past the end)
+    const uint32_t before = l ? uint32_t(__shfl(int(incl), int(l - 1), 64)) : 0u;
+    const uint64_t wl = __shfl(w, int(l), 64), rl = __shfl(row, int(l), 64);
+    if (t < total) words[wl + (t - before)] = hits[rl + (t - before)];
+  }
 }
 
 // base[0..world]: header prefix per source rank; base[65..65+world]: word
