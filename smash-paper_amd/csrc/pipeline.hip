@@ -681,7 +681,8 @@ __device__ bool same_key(const KeyRef &a, const KeyRef &b) {
 // every lane of the wave calls it, need = 0 for lanes without a key; the
 // lane gets the offset of its `need` words.  A key that turns out present
 // leaves its reserved words unused.
-__device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need) {
+__device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need, uint32_t *incl_out = nullptr,
+                               uint32_t *total_out = nullptr) {
   const uint32_t lane = threadIdx.x & 63;
   uint32_t x = need;   // inclusive prefix over the wave
 #pragma unroll
@@ -693,7 +694,39 @@ __device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need) {
   unsigned long long base = 0;
   if (lane == 63 && total) base = atomicAdd(top, (unsigned long long)total);
   base = __shfl(base, 63, 64);
+  if (incl_out) *incl_out = x;
+  if (total_out) *total_out = total;
   return uint64_t(base) + x - need;
+}
+
+// The key records {hash lo, nk, hit words} of a wave's winners, written by
+// the whole wave: wave_alloc gave the wave one contiguous arena range
+// (lane l's record at off(l), incl = the inclusive prefix of the record
+// sizes), so word t of the range belongs to the first lane l with
+// incl(l) > t and consecutive lanes store consecutive words (a lane-per-record
+// loop stores 64 words a record apart per instruction).  ok: the lane's
+// record fits the arena; lo / m / src: its hash lo, word count and words.
+// Every lane of the wave calls it (wave-uniform trip count).
+__device__ __forceinline__ void wave_fill_records(uint64_t *arena, uint64_t off, uint32_t incl,
+                                                  uint32_t total, bool ok, uint64_t lo, uint32_t m,
+                                                  const uint64_t *src) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t srcv = reinterpret_cast<uint64_t>(src);
+  for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+    const uint32_t t = t0 + lane;
+    uint32_t l = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+      if (uint32_t(__shfl(int(incl), int(l + step - 1), 64)) <= t) l += step;
+    l = l < 63u ? l : 63u;
+    const uint32_t before = l ? uint32_t(__shfl(int(incl), int(l - 1), 64)) : 0u;
+    const uint32_t r = t - before;   // word r of lane l's record
+    const bool lok = __shfl(int(ok), int(l), 64) != 0;
+    const uint64_t loff = __shfl(off, int(l), 64), llo = __shfl(lo, int(l), 64);
+    const uint32_t lm = uint32_t(__shfl(int(m), int(l), 64));
+    const uint64_t *ls = reinterpret_cast<const uint64_t *>(__shfl(srcv, int(l), 64));
+    if (t < total && lok) arena[loff + r] = r == 0 ? llo : r == 1 ? uint64_t(lm) : ls[r - 2];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -830,16 +863,15 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
       dp += win ? 0 : 1;
     }
     const uint32_t need = win ? 2u + uint32_t(m) : 0u;
-    const uint64_t off = wave_alloc(arena_top, need);
+    uint32_t incl, total;
+    const uint64_t off = wave_alloc(arena_top, need, &incl, &total);
+    const bool ok = win && off + need <= arena_cap;
+    wave_fill_records(arena, off, incl, total, ok, win ? hash[2 * q + 1] : 0ull,
+                      win ? uint32_t(m) : 0u, hits + (in ? q : 0) * 2 * uint64_t(slots));
     if (win) {
-      if (off + need > arena_cap) {
+      if (!ok) {
         full = true;   // the slot stays a claim: never matched (no kRefPub)
       } else {
-        uint64_t *rec = arena + off;
-        const uint64_t *w = hits + q * 2 * uint64_t(slots);
-        rec[0] = hash[2 * q + 1];
-        rec[1] = uint64_t(m);
-        for (int32_t j = 0; j < m; ++j) rec[2 + j] = w[j];
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[q] + 1]),
                            (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2123,16 +2155,16 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
       }
     }
     const uint32_t need = win ? 2u + m : 0u;
-    const uint64_t off = wave_alloc(arena_top, need);   // (wave-wide)
+    uint32_t incl, total;
+    const uint64_t off = wave_alloc(arena_top, need, &incl, &total);   // (wave-wide)
+    const bool ok = win && off + need <= arena_cap;
+    KeyRef me{words, 0u, 0ull};
+    if (win) me = recv_key(recv, words, base, world, j);
+    wave_fill_records(arena, off, incl, total, ok, me.lo, win ? m : 0u, me.w);
     if (win) {
-      if (off + need > arena_cap) {
+      if (!ok) {
         full = true;   // the slot stays a claim: never matched (no kRefPub)
       } else {
-        const KeyRef me = recv_key(recv, words, base, world, j);
-        uint64_t *rec = arena + off;
-        rec[0] = me.lo;
-        rec[1] = m;
-        for (uint32_t t = 0; t < m; ++t) rec[2 + t] = me.w[t];
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[j] + 1]),
                            (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
