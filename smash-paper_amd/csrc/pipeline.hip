@@ -134,6 +134,8 @@ struct smash_pipeline {
   int64_t *d_lp = nullptr, *d_lps = nullptr;
   bool fused_bin = true;
   uint32_t bin_flush = 0x8000;    // k_emit_bin_lds's 16-bit counter flush threshold
+  uint32_t coop_copy = 7;         // wave-cooperative key-word copies, bit 0: export, 1: single-GPU
+                                  // decide, 2: owner decide (SMASH_COOP_COPY=0: per lane)
   bool bin_lds = true;            // k_emit_bin_lds when the bins fit (SMASH_BIN_LDS=0: global
                                   // atomics; the LDS form runs in the gap SMASH_GATE_POST leaves)
   bool pos_dirty = false;         // the positions arrays are not materialised yet
@@ -709,7 +711,16 @@ __device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need, uint32_t 
 // Every lane of the wave calls it (wave-uniform trip count).
 __device__ __forceinline__ void wave_fill_records(uint64_t *arena, uint64_t off, uint32_t incl,
                                                   uint32_t total, bool ok, uint64_t lo, uint32_t m,
-                                                  const uint64_t *src) {
+                                                  const uint64_t *src, bool coop) {
+  if (!coop) {   // (SMASH_COOP_COPY=0: one record per lane, the round-3 form)
+    if (ok) {
+      uint64_t *rec = arena + off;
+      rec[0] = lo;
+      rec[1] = m;
+      for (uint32_t j = 0; j < m; ++j) rec[2 + j] = src[j];
+    }
+    return;
+  }
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t srcv = reinterpret_cast<uint64_t>(src);
   for (uint32_t t0 = 0; t0 < total; t0 += 64) {
@@ -719,7 +730,10 @@ __device__ __forceinline__ void wave_fill_records(uint64_t *arena, uint64_t off,
     for (uint32_t step = 32; step; step >>= 1)
       if (uint32_t(__shfl(int(incl), int(l + step - 1), 64)) <= t) l += step;
     l = l < 63u ? l : 63u;
-    const uint32_t before = l ? uint32_t(__shfl(int(incl), int(l - 1), 64)) : 0u;
+    // (the shuffle runs on every lane, outside the select: a cross-lane read
+    // under a partial exec mask returns 0 from the lanes it excludes)
+    const uint32_t prev = uint32_t(__shfl(int(incl), int((l + 63u) & 63u), 64));
+    const uint32_t before = l ? prev : 0u;
     const uint32_t r = t - before;   // word r of lane l's record
     const bool lok = __shfl(int(ok), int(l), 64) != 0;
     const uint64_t loff = __shfl(off, int(l), 64), llo = __shfl(lo, int(l), 64);
@@ -840,7 +854,7 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
                                uint64_t *table, uint64_t *arena, uint64_t arena_cap,
                                unsigned long long *arena_top, uint64_t epoch,
                                const uint64_t *__restrict__ slot_of, uint8_t *keep,
-                               uint32_t *cnt, int64_t *lp, unsigned long long *stats) {
+                               uint32_t *cnt, int64_t *lp, unsigned long long *stats, bool coop) {
   SMASH_BESIDE_SEARCH();
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   unsigned long long kp = 0, dp = 0;
@@ -867,7 +881,7 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
     const uint64_t off = wave_alloc(arena_top, need, &incl, &total);
     const bool ok = win && off + need <= arena_cap;
     wave_fill_records(arena, off, incl, total, ok, win ? hash[2 * q + 1] : 0ull,
-                      win ? uint32_t(m) : 0u, hits + (in ? q : 0) * 2 * uint64_t(slots));
+                      win ? uint32_t(m) : 0u, hits + (in ? q : 0) * 2 * uint64_t(slots), coop);
     if (win) {
       if (!ok) {
         full = true;   // the slot stays a claim: never matched (no kRefPub)
@@ -1465,6 +1479,8 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       const char *fl = getenv("SMASH_BIN_FLUSH");
       const unsigned long f = fl ? std::strtoul(fl, nullptr, 10) : 0;
       if (f >= 2 && f <= 0x8000 && !(f & (f - 1))) p->bin_flush = uint32_t(f);
+      const char *cc = getenv("SMASH_COOP_COPY");
+      if (cc) p->coop_copy = uint32_t(std::strtoul(cc, nullptr, 10)) & 7u;
       auto on = [](const char *v, bool dflt) {
         const char *x = getenv(v);
         return x && x[0] ? x[0] == '1' : dflt;
@@ -1728,7 +1744,7 @@ static int dedup_local(smash_pipeline *p, hipStream_t s) {
   k_dedup_decide<<<grid_for(n, kB, 8192), kB, 0, s>>>(
       p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_nmajor, p->d_chrom_off, n, p->d_table,
       p->d_arena, p->arena_cap, p->d_arena_top, epoch, p->d_slot, p->d_keep, p->d_cnt, p->d_lp,
-      p->d_stats);
+      p->d_stats, (p->coop_copy & 2u) != 0);
   SMASH_HIP(hipGetLastError());
   p->cnt_ready = true;
   return SMASH_OK;
@@ -1995,7 +2011,7 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
                                                     uint64_t n, int world, uint32_t nblk,
                                                     uint64_t gbase, const uint64_t *boff,
                                                     uint64_t *hdr, uint64_t *words,
-                                                    uint32_t *send_q) {
+                                                    uint32_t *send_q, bool coop) {
   __shared__ uint32_t s_e[kExWaves][64], s_w[kExWaves][64];
   const uint32_t wv = threadIdx.x >> 6;
   for (uint32_t o = threadIdx.x; o < kExWaves * 64; o += blockDim.x) {
@@ -2026,7 +2042,12 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
     hdr[kHdrWords * e + 1] = hash[2 * q + 1];
     hdr[kHdrWords * e + 2] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
     send_q[e] = uint32_t(q);
+    if (!coop) {   // (SMASH_COOP_COPY=0: one key per lane, the round-3 form)
+      const uint64_t *src = hits + q * 2 * uint64_t(slots);
+      for (uint32_t i = 0; i < k; ++i) words[w + i] = src[i];
+    }
   }
+  if (!coop) return;
   // the keys' words, the wave together: word t of the wave's concatenated
   // key lists (lane order) is word t - pre(l) of lane l's key, so
   // consecutive lanes store consecutive words of an owner's segment (a
@@ -2048,7 +2069,10 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
     for (uint32_t step = 32; step; step >>= 1)
       if (uint32_t(__shfl(int(incl), int(l + step - 1), 64)) <= t) l += step;
     l = l < 63u ? l : 63u;   // (t >= total: a lane past the end)
-    const uint32_t before = l ? uint32_t(__shfl(int(incl), int(l - 1), 64)) : 0u;
+    // (the shuffle runs on every lane, outside the select: a cross-lane read
+    // under a partial exec mask returns 0 from the lanes it excludes)
+    const uint32_t prev = uint32_t(__shfl(int(incl), int((l + 63u) & 63u), 64));
+    const uint32_t before = l ? prev : 0u;
     const uint64_t wl = __shfl(w, int(l), 64), rl = __shfl(row, int(l), 64);
     if (t < total) words[wl + (t - before)] = hits[rl + (t - before)];
   }
@@ -2136,7 +2160,7 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
                                int world, uint64_t n, uint64_t *table, uint64_t *arena,
                                uint64_t arena_cap, unsigned long long *arena_top, uint64_t epoch,
                                const uint64_t *__restrict__ slot_of, uint8_t *flags,
-                               unsigned long long *stats) {
+                               unsigned long long *stats, bool coop) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   bool full = false;
   for (uint64_t b0 = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); b0 < n;
@@ -2160,7 +2184,7 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
     const bool ok = win && off + need <= arena_cap;
     KeyRef me{words, 0u, 0ull};
     if (win) me = recv_key(recv, words, base, world, j);
-    wave_fill_records(arena, off, incl, total, ok, me.lo, win ? m : 0u, me.w);
+    wave_fill_records(arena, off, incl, total, ok, me.lo, win ? m : 0u, me.w, coop);
     if (win) {
       if (!ok) {
         full = true;   // the slot stays a claim: never matched (no kRefPub)
@@ -2234,7 +2258,7 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
   if (n)
     k_export_fill<<<nblk, kB, 0, s>>>(p->d_nk, p->d_hash, p->d_hits, p->slots, n, world, nblk,
                                       global_base, p->d_boff, p->d_send_hdr, p->d_send_words,
-                                      p->d_send_q);
+                                      p->d_send_q, (p->coop_copy & 1u) != 0);
   SMASH_HIP(hipGetLastError());
   *d_send = p->d_send_hdr;
   *d_send_words = p->d_send_words;
@@ -2284,7 +2308,7 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   SMASH_HIP(hipGetLastError());
   k_owner_decide<<<grid_for(n_recv, kB, 8192), kB, 0, s>>>(
       d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->d_arena, p->arena_cap,
-      p->d_arena_top, epoch, p->d_oslot, d_flags, p->d_stats);
+      p->d_arena_top, epoch, p->d_oslot, d_flags, p->d_stats, (p->coop_copy & 4u) != 0);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }

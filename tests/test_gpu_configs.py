@@ -405,7 +405,44 @@ def test_c4_real_driver_threads_equal_oracle(c4_run, W, per_rank, bits, ahead2, 
         monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
     total, st = run_resident(dix, d_reads, W, per_rank, starts, cs, ahead2=ahead2)
     assert orc[1][3] > 100
-    assert np.array_equal(total, orc[0]) and st == orc[1]
+    assert st == orc[1], (st, orc[1], single[1])
+    assert np.array_equal(total, orc[0])
+
+
+def test_c4_real_driver_variants(c4_run, monkeypatch):
+    """The W = 8 driver, and one pipeline over 24 batches (the key records
+    written by one launch and compared by later ones), with each kernel form
+    the knobs select (SMASH_COOP_COPY=0: per-lane key-word copies instead of
+    the wave-cooperative ones; SMASH_BIN_LDS=0: global bin atomics) == the
+    oracle, all reported before the first failure is raised (a failing form
+    is then named by the others)."""
+    from thread_ranks import run_resident
+    dix, cs, starts, d_reads, single, orc = c4_run
+    res = {}
+    for name, env in [("coop0", {"SMASH_COOP_COPY": "0"}), ("binglobal", {"SMASH_BIN_LDS": "0"}),
+                      ("default", {})]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        total, st = run_resident(dix, d_reads, 8, 10_000, starts, cs)
+        res[name] = (st, bool(np.array_equal(total, orc[0])))
+        for k in env:
+            monkeypatch.delenv(k)
+    for name, env in [("single_batches", {}), ("single_batches_coop0", {"SMASH_COOP_COPY": "0"})]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        one = S.Pipeline(dix, cs, starts, 150, 10_000, dedup_capacity=C4_PAIRS)
+        one.reset()
+        c1 = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+        for b0 in range(0, C4_PAIRS, 10_000):
+            one.count_batch(d_reads[2 * b0:2 * (b0 + 10_000)], 10_000, c1)
+        s1 = one.stats()
+        res[name] = ((s1.positions, s1.dups, s1.kept, s1.dupe_pairs),
+                     bool(np.array_equal(c1.cpu().numpy().astype(np.uint64), orc[0])))
+        for k in env:
+            monkeypatch.delenv(k)
+    print("variants:", res, "oracle:", orc[1], "single:", single[1],
+          "single counts == oracle:", bool(np.array_equal(single[0], orc[0])))
+    assert all(st == orc[1] and eq for st, eq in res.values()), (res, orc[1], single[1])
 
 
 @pytest.fixture(scope="module")
