@@ -202,7 +202,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
   __shared__ int64_t s_bs[kLdsBins];
   __shared__ unsigned long long s_tot;
   __shared__ uint32_t s_o0;
-  __shared__ uint64_t s_f[kMB], s_r[kMB];   // per chunk: first unsaturated (fwd / rc text order)
+  __shared__ uint64_t s_f[kMB / 64], s_r[kMB / 64];   // per wave: first unsaturated (fwd / rc)
   __shared__ uint64_t s_ftail, s_rtail;
   __shared__ uint32_t s_seg;
   __shared__ Seg s_segs[kMaxSegLds];   // the segment table, once per block
@@ -249,25 +249,30 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     const bool any_sat = __syncthreads_or((satf | satr) != 0);
     uint64_t fnext = kNone, rnext = kNone;   // first unsaturated chunk after / before mine
     if (any_sat) {
-      // suffix-min of the forward chunk heads over later chunks, prefix-min of
-      // the rc chunk heads over earlier chunks (higher text positions)
-      s_f[threadIdx.x] = ff;
-      s_r[threadIdx.x] = fr;
+      // the min of the forward chunk heads over later chunks, and of the rc
+      // chunk heads over earlier chunks (higher text positions): within the
+      // wave by shuffles, across the block's waves through LDS (one barrier;
+      // a block-wide LDS scan took 16)
+      const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      uint64_t xs = ff, xp = fr;   // inclusive suffix-min / prefix-min in the wave
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t a = __shfl_down(xs, d, 64), b = __shfl_up(xp, d, 64);
+        if (lane + d < 64) xs = a < xs ? a : xs;
+        if (lane >= d) xp = b < xp ? b : xp;
+      }
+      const uint64_t after = __shfl_down(xs, 1, 64), before = __shfl_up(xp, 1, 64);
+      if (lane == 0) s_f[wv] = xs;    // the wave's minima
+      if (lane == 63) s_r[wv] = xp;
       if (threadIdx.x == 0) {
         s_ftail = next_unsat_dir(dir, ndir, sp + t0 + kMTile);
         s_rtail = next_unsat_dir(dir, ndir, xr + 1);       // above the tile's rc range
       }
       __syncthreads();
-      for (uint32_t d = 1; d < uint32_t(kMB); d <<= 1) {
-        const uint64_t a = threadIdx.x + d < uint32_t(kMB) ? s_f[threadIdx.x + d] : kNone;
-        const uint64_t b = threadIdx.x >= d ? s_r[threadIdx.x - d] : kNone;
-        __syncthreads();
-        s_f[threadIdx.x] = a < s_f[threadIdx.x] ? a : s_f[threadIdx.x];
-        s_r[threadIdx.x] = b < s_r[threadIdx.x] ? b : s_r[threadIdx.x];
-        __syncthreads();
-      }
-      fnext = threadIdx.x + 1 < uint32_t(kMB) ? s_f[threadIdx.x + 1] : kNone;
-      rnext = threadIdx.x > 0 ? s_r[threadIdx.x - 1] : kNone;
+      fnext = lane < 63 ? after : kNone;
+      rnext = lane > 0 ? before : kNone;
+      for (uint32_t w = wv + 1; w < uint32_t(kMB / 64); ++w) fnext = s_f[w] < fnext ? s_f[w] : fnext;
+      for (uint32_t w = 0; w < wv; ++w) rnext = s_r[w] < rnext ? s_r[w] : rnext;
       if (fnext == kNone) fnext = s_ftail;
       if (rnext == kNone) rnext = s_rtail;
     }

@@ -678,31 +678,27 @@ __device__ bool same_key(const KeyRef &a, const KeyRef &b) {
   return true;
 }
 
-// arena space for the wave's keys with ONE atomic per wave (an atomic per
-// key serialises ~2 M same-address atomics per batch on one L2 channel):
-// every lane of the wave calls it, need = 0 for lanes without a key; the
-// lane gets the offset of its `need` words.  A key that turns out present
-// leaves its reserved words unused.
-__device__ uint64_t wave_alloc(unsigned long long *top, uint32_t need, uint32_t *incl_out = nullptr,
-                               uint32_t *total_out = nullptr) {
+// the wave's inclusive prefix of v (every lane calls it) and its total
+__device__ __forceinline__ uint32_t wave_incl(uint32_t v, uint32_t &total) {
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t x = need;   // inclusive prefix over the wave
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= uint32_t(d)) x += y;
+    const uint32_t y = __shfl_up(v, d, 64);
+    if (lane >= uint32_t(d)) v += y;
   }
-  const uint32_t total = __shfl(x, 63, 64);
-  unsigned long long base = 0;
-  if (lane == 63 && total) base = atomicAdd(top, (unsigned long long)total);
-  base = __shfl(base, 63, 64);
-  if (incl_out) *incl_out = x;
-  if (total_out) *total_out = total;
-  return uint64_t(base) + x - need;
+  total = __shfl(v, 63, 64);
+  return v;
 }
 
+// the decide kernels take kDecGroups groups of 64 consecutive keys per wave
+// per trip and reserve their arena space with ONE atomic: the arena top is a
+// single address, and one atomic per 64 keys (~100 k per 6.25 M-pair batch)
+// serialised on its L2 channel for ~1 ms
+constexpr uint32_t kDecGroups = 4;
+
 // The key records {hash lo, nk, hit words} of a wave's winners, written by
-// the whole wave: wave_alloc gave the wave one contiguous arena range
+// the whole wave: the decide kernels give each group of 64 keys one
+// contiguous arena range
 // (lane l's record at off(l), incl = the inclusive prefix of the record
 // sizes), so word t of the range belongs to the first lane l with
 // incl(l) > t and consecutive lanes store consecutive words (a lane-per-record
@@ -846,7 +842,7 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
   if (err) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)err);
 }
 
-// one wave per 64 consecutive pairs per trip (wave_alloc is wave-wide)
+// one wave per kDecGroups x 64 consecutive pairs per trip (wave-wide scans)
 __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *__restrict__ hash,
                                const uint64_t *__restrict__ hits, uint32_t slots,
                                const uint32_t *__restrict__ nmajor,
@@ -859,52 +855,72 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   unsigned long long kp = 0, dp = 0;
   bool full = false;
-  for (uint64_t base = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); base < n;
-       base += stride) {
-    const uint64_t q = base + (threadIdx.x & 63);
-    const bool in = q < n;
-    const int32_t m = in ? nk[q] : -1;
-    bool win = false;
-    if (m >= 0) {
-      const uint64_t sl = slot_of[q];
-      if (sl < kSlotNone) {
-        const unsigned long long ref = __hip_atomic_load(
-            reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        win = ref == ((epoch << kRefShift) | (q + 1));
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t b0 = (uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u)) * kDecGroups;
+       b0 < n; b0 += stride * kDecGroups) {
+    bool wins[kDecGroups];
+    uint32_t needs[kDecGroups], incls[kDecGroups], tots[kDecGroups];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < kDecGroups; ++g) {
+      const uint64_t q = b0 + 64 * g + lane;
+      const int32_t m = q < n ? nk[q] : -1;
+      bool win = false;
+      if (m >= 0) {
+        const uint64_t sl = slot_of[q];
+        if (sl < kSlotNone) {
+          const unsigned long long ref = __hip_atomic_load(
+              reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT);
+          win = ref == ((epoch << kRefShift) | (q + 1));
+        }
+        ++kp;
+        dp += win ? 0 : 1;
       }
-      ++kp;
-      dp += win ? 0 : 1;
+      wins[g] = win;
+      needs[g] = win ? 2u + uint32_t(m) : 0u;
+      incls[g] = wave_incl(needs[g], tots[g]);
+      sum += tots[g];
     }
-    const uint32_t need = win ? 2u + uint32_t(m) : 0u;
-    uint32_t incl, total;
-    const uint64_t off = wave_alloc(arena_top, need, &incl, &total);
-    const bool ok = win && off + need <= arena_cap;
-    wave_fill_records(arena, off, incl, total, ok, win ? hash[2 * q + 1] : 0ull,
-                      win ? uint32_t(m) : 0u, hits + (in ? q : 0) * 2 * uint64_t(slots), coop);
-    if (win) {
-      if (!ok) {
-        full = true;   // the slot stays a claim: never matched (no kRefPub)
-      } else {
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[q] + 1]),
-                           (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long wbase = 0;
+    if (lane == 63 && sum) wbase = atomicAdd(arena_top, (unsigned long long)sum);
+    wbase = __shfl(wbase, 63, 64);
+#pragma unroll
+    for (uint32_t g = 0; g < kDecGroups; ++g) {
+      const uint64_t q = b0 + 64 * g + lane;
+      const bool in = q < n;
+      const int32_t m = in ? nk[q] : -1;
+      const bool win = wins[g];
+      const uint32_t need = needs[g], incl = incls[g], total = tots[g];
+      const uint64_t off = uint64_t(wbase) + incl - need;
+      wbase += total;
+      const bool ok = win && off + need <= arena_cap;
+      wave_fill_records(arena, off, incl, total, ok, win ? hash[2 * q + 1] : 0ull,
+                        win ? uint32_t(m) : 0u, hits + (in ? q : 0) * 2 * uint64_t(slots), coop);
+      if (win) {
+        if (!ok) {
+          full = true;   // the slot stays a claim: never matched (no kRefPub)
+        } else {
+          __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[q] + 1]),
+                             (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
-    }
-    if (in) {
-      keep[q] = win ? 1 : 0;
-      const uint32_t c = win ? nmajor[q] : 0;   // k_count_last
-      cnt[q] = c;
-      int64_t last = -1;
-      if (c) {
-        const uint64_t *h = hits + q * 2 * uint64_t(slots);
-        for (int32_t j = m - 1; j >= 0; --j)
-          if (chrom_off[uint32_t(h[j] >> 48)] >= 0) {
-            last = int64_t(h[j] & 0xFFFFFFFFFFFFull);
-            break;
-          }
+      if (in) {
+        keep[q] = win ? 1 : 0;
+        const uint32_t c = win ? nmajor[q] : 0;   // k_count_last
+        cnt[q] = c;
+        int64_t last = -1;
+        if (c) {
+          const uint64_t *h = hits + q * 2 * uint64_t(slots);
+          for (int32_t j = m - 1; j >= 0; --j)
+            if (chrom_off[uint32_t(h[j] >> 48)] >= 0) {
+              last = int64_t(h[j] & 0xFFFFFFFFFFFFull);
+              break;
+            }
+        }
+        lp[q] = last;
       }
-      lp[q] = last;
     }
   }
   wave_stats(stats, S_KEYPAIRS, kp, S_DUPEPAIRS, dp, full ? SMASH_ERR_NOMEM : 0);
@@ -1741,7 +1757,7 @@ static int dedup_local(smash_pipeline *p, hipStream_t s) {
                                                      p->d_table, p->table_mask, p->d_arena, epoch,
                                                      p->d_slot, p->d_stats);
   SMASH_HIP(hipGetLastError());
-  k_dedup_decide<<<grid_for(n, kB, 8192), kB, 0, s>>>(
+  k_dedup_decide<<<grid_for((n + kDecGroups - 1) / kDecGroups, kB, 8192), kB, 0, s>>>(
       p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_nmajor, p->d_chrom_off, n, p->d_table,
       p->d_arena, p->arena_cap, p->d_arena_top, epoch, p->d_slot, p->d_keep, p->d_cnt, p->d_lp,
       p->d_stats, (p->coop_copy & 2u) != 0);
@@ -2163,38 +2179,58 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
                                unsigned long long *stats, bool coop) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   bool full = false;
-  for (uint64_t b0 = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); b0 < n;
-       b0 += stride) {
-    const uint64_t j = b0 + (threadIdx.x & 63);
-    bool win = false;
-    uint32_t m = 0;
-    if (j < n) {
-      m = uint32_t(recv[kHdrWords * j + 2] >> 40);
-      const uint64_t sl = slot_of[j];
-      if (sl < kSlotNone) {
-        const unsigned long long ref = __hip_atomic_load(
-            reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
-        win = ref == ((epoch << kRefShift) | (j + 1));
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t c0 = (uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u)) * kDecGroups;
+       c0 < n; c0 += stride * kDecGroups) {
+    bool wins[kDecGroups];
+    uint32_t needs[kDecGroups], incls[kDecGroups], tots[kDecGroups];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < kDecGroups; ++g) {
+      const uint64_t j = c0 + 64 * g + lane;
+      bool win = false;
+      uint32_t m = 0;
+      if (j < n) {
+        m = uint32_t(recv[kHdrWords * j + 2] >> 40);
+        const uint64_t sl = slot_of[j];
+        if (sl < kSlotNone) {
+          const unsigned long long ref = __hip_atomic_load(
+              reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT);
+          win = ref == ((epoch << kRefShift) | (j + 1));
+        }
       }
+      wins[g] = win;
+      needs[g] = win ? 2u + m : 0u;
+      incls[g] = wave_incl(needs[g], tots[g]);
+      sum += tots[g];
     }
-    const uint32_t need = win ? 2u + m : 0u;
-    uint32_t incl, total;
-    const uint64_t off = wave_alloc(arena_top, need, &incl, &total);   // (wave-wide)
-    const bool ok = win && off + need <= arena_cap;
-    KeyRef me{words, 0u, 0ull};
-    if (win) me = recv_key(recv, words, base, world, j);
-    wave_fill_records(arena, off, incl, total, ok, me.lo, win ? m : 0u, me.w, coop);
-    if (win) {
-      if (!ok) {
-        full = true;   // the slot stays a claim: never matched (no kRefPub)
-      } else {
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[j] + 1]),
-                           (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long wbase = 0;
+    if (lane == 63 && sum) wbase = atomicAdd(arena_top, (unsigned long long)sum);
+    wbase = __shfl(wbase, 63, 64);
+#pragma unroll
+    for (uint32_t g = 0; g < kDecGroups; ++g) {
+      const uint64_t j = c0 + 64 * g + lane;
+      const bool win = wins[g];
+      const uint32_t need = needs[g], incl = incls[g], total = tots[g];
+      const uint32_t m = win ? need - 2u : 0u;
+      const uint64_t off = uint64_t(wbase) + incl - need;
+      wbase += total;
+      const bool ok = win && off + need <= arena_cap;
+      KeyRef me{words, 0u, 0ull};
+      if (win) me = recv_key(recv, words, base, world, j);
+      wave_fill_records(arena, off, incl, total, ok, me.lo, win ? m : 0u, me.w, coop);
+      if (win) {
+        if (!ok) {
+          full = true;   // the slot stays a claim: never matched (no kRefPub)
+        } else {
+          __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[j] + 1]),
+                             (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
+      if (j < n) flags[j] = win ? 1 : 0;
     }
-    if (j < n) flags[j] = win ? 1 : 0;
   }
   if (full) atomicCAS(&stats[S_ERR], 0ull, (unsigned long long)(unsigned)SMASH_ERR_NOMEM);
 }
@@ -2306,7 +2342,7 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
       d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->table_mask, p->d_arena,
       epoch, p->d_oslot, p->d_stats);
   SMASH_HIP(hipGetLastError());
-  k_owner_decide<<<grid_for(n_recv, kB, 8192), kB, 0, s>>>(
+  k_owner_decide<<<grid_for((n_recv + kDecGroups - 1) / kDecGroups, kB, 8192), kB, 0, s>>>(
       d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->d_arena, p->arena_cap,
       p->d_arena_top, epoch, p->d_oslot, d_flags, p->d_stats, (p->coop_copy & 4u) != 0);
   SMASH_HIP(hipGetLastError());
