@@ -686,6 +686,39 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     const uint64_t live = __ballot(st != S_EXIT);
     if (live == 0) break;
     if (STATS) { w_iters += 1; w_active += __popcll(live); }
+    // direct rows: the rows DMA'd last iteration (the lanes still in S_COPY)
+    // have landed -- waited for here, before this iteration's loads are
+    // issued, where nothing else is outstanding; the bad mask of each, one
+    // row word per lane, assembled only when a base is bad
+    if (c.direct) {
+      uint64_t cm = __ballot(st == S_COPY);
+      if (cm) {
+        SM_REGION(27);
+#ifdef SM_HOST_LANE
+        if (st == S_COPY) bad = row_bad_mask(row, L, c.bad_tab_lo, c.bad_tab_hi);
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        while (cm) {
+          const uint32_t ln = uint32_t(__builtin_ctzll(cm));
+          cm &= cm - 1;
+          const uint32_t lr = uint32_t(__shfl(int(L), int(ln), 64));
+          const uint32_t b0 = 4 * lane;
+          const uint32_t w = b0 < lr ? ldsw[ln * c.w_row + lane] : 0u;
+          const uint32_t nib = b0 < lr ? bad_nibble(w, c.bad_tab_lo, c.bad_tab_hi, lr - b0) : 0u;
+          if (__ballot(nib != 0)) {   // rare: a read with a bad base
+            uint32_t x = nib << (4 * (lane & 7));
+            x |= __shfl_xor(x, 1, 64);
+            x |= __shfl_xor(x, 2, 64);
+            x |= __shfl_xor(x, 4, 64);
+            const uint32_t m0 = __shfl(x, 0, 64), m1 = __shfl(x, 8, 64), m2 = __shfl(x, 16, 64),
+                           m3 = __shfl(x, 24, 64), m4 = __shfl(x, 32, 64), m5 = __shfl(x, 40, 64),
+                           m6 = __shfl(x, 48, 64), m7 = __shfl(x, 56, 64);
+            if (lane == ln) bad = Bad{m0, m1, m2, m3, m4, m5, m6, m7};
+          }
+        }
+#endif
+      }
+    }
     const uint32_t st_ld = S_COPY + c.direct;   // the lowest state that loads
     if (CHECK && st >= st_ld &&
         (addr < c.lo || addr >= c.hi || (need2 && (addr2 < c.lo || addr2 >= c.hi)))) {
@@ -742,38 +775,6 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           SM_DMA_ROW(ldsw + ln * c.w_row, c.rows + rl * (c.w_row >> 2), c.w_row >> 2, lane);
         else
           SM_DMA_ROW(ldsw + ln * c.w_row, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
-      }
-    }
-    // direct rows: the rows DMA'd last iteration have landed (every earlier
-    // vector-memory operation of the wave is done: vmcnt(0)); the bad mask of
-    // each, one row word per lane, assembled only when a base is bad
-    if (c.direct) {
-      uint64_t cm = __ballot(st == S_COPY && !fresh);
-      if (cm) {
-        SM_REGION(27);
-#ifdef SM_HOST_LANE
-        if (st == S_COPY && !fresh) bad = row_bad_mask(row, L, c.bad_tab_lo, c.bad_tab_hi);
-#else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        while (cm) {
-          const uint32_t ln = uint32_t(__builtin_ctzll(cm));
-          cm &= cm - 1;
-          const uint32_t lr = uint32_t(__shfl(int(L), int(ln), 64));
-          const uint32_t b0 = 4 * lane;
-          const uint32_t w = b0 < lr ? ldsw[ln * c.w_row + lane] : 0u;
-          const uint32_t nib = b0 < lr ? bad_nibble(w, c.bad_tab_lo, c.bad_tab_hi, lr - b0) : 0u;
-          if (__ballot(nib != 0)) {   // rare: a read with a bad base
-            uint32_t x = nib << (4 * (lane & 7));
-            x |= __shfl_xor(x, 1, 64);
-            x |= __shfl_xor(x, 2, 64);
-            x |= __shfl_xor(x, 4, 64);
-            const uint32_t m0 = __shfl(x, 0, 64), m1 = __shfl(x, 8, 64), m2 = __shfl(x, 16, 64),
-                           m3 = __shfl(x, 24, 64), m4 = __shfl(x, 32, 64), m5 = __shfl(x, 40, 64),
-                           m6 = __shfl(x, 48, 64), m7 = __shfl(x, 56, 64);
-            if (lane == ln) bad = Bad{m0, m1, m2, m3, m4, m5, m6, m7};
-          }
-        }
-#endif
       }
     }
     if (st < S_ALU || fresh) continue;
