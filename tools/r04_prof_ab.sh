@@ -14,7 +14,7 @@ ARGS="--steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-feed --no-c5"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv \
     -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-feed --no-c5 \
     > "$O/prof.json" 2> "$O/prof.log"
-T=$(ls "$O"/prof/*/run_kernel_trace.csv 2>/dev/null | head -1 || true)
+T=$(ls "$O"/prof/run_kernel_trace.csv "$O"/prof/*/run_kernel_trace.csv 2>/dev/null | head -1 || true)
 if [ -n "$T" ]; then
   python3 "$R/tools/step_breakdown.py" "$T" 4 4 > "$O/step_breakdown.txt" || true
   python3 "$R/tools/roofline_from_trace.py" "$T" "$O/prof.json" > "$O/roofline_from_trace.txt" || true
