@@ -134,6 +134,7 @@ struct smash_pipeline {
   int64_t *d_lp = nullptr, *d_lps = nullptr;
   bool fused_bin = true;
   uint32_t bin_flush = 0x8000;    // k_emit_bin_lds's 16-bit counter flush threshold
+  uint32_t *d_binpart = nullptr;  // [kBinBlocks][nbins]: k_emit_bin_lds's per-block counts
   uint32_t coop_copy = 7;         // wave-cooperative key-word copies, bit 0: export, 1: single-GPU
                                   // decide, 2: owner decide (SMASH_COOP_COPY=0: per lane)
   bool bin_lds = true;            // k_emit_bin_lds when the bins fit (SMASH_BIN_LDS=0: global
@@ -1203,6 +1204,7 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
 // land between the two, and flush + 1023 < 2^16 (flush <= 2^15).
 constexpr uint32_t kBinPart = 77824;   // 16-bit counters: 152 KB, one 1024-thread block per CU
 constexpr uint32_t kBinPartsMax = 4;   // above: k_emit_bin
+constexpr uint32_t kBinBlocks = 256;   // k_emit_bin_lds blocks per part (one per CU)
 // the parts balanced: ceil(nbins / parts) bins each (50 k bins: 2 x 25 000,
 // not 24 576 + 24 576 + 848 -- every part re-walks all the pairs)
 inline uint32_t bin_parts(uint32_t nbins) { return (nbins + kBinPart - 1) / kBinPart; }
@@ -1216,7 +1218,7 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
     const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
     uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats,
-    uint32_t part, uint32_t flush) {
+    uint32_t part, uint32_t flush, uint32_t *binpart) {
   __shared__ uint32_t hc[kBinPart / 2];   // bin b0 + i: half i & 1 of word i >> 1
   const uint32_t b0 = blockIdx.y * part;
   const uint32_t b1 = b0 + part < nbins ? b0 + part : nbins;
@@ -1265,9 +1267,22 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     atomicAdd(&stats[S_DUPS], sd);
     atomicAdd(&stats[S_KEPT], sk);
   }
-  for (uint32_t i = threadIdx.x; b0 + i < b1; i += blockDim.x) {
-    const uint32_t c = (hc[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-    if (c) atomicAdd(&counts[b0 + i], (unsigned long long)c);
+  // the block's counts as plain coalesced stores (k_bin_reduce sums the
+  // blocks): a global atomic per non-zero bin per block was ~9 M atomics per
+  // batch at 50 000 bins, most of the kernel
+  uint32_t *out = binpart + uint64_t(blockIdx.x) * nbins;
+  for (uint32_t i = threadIdx.x; b0 + i < b1; i += blockDim.x)
+    out[b0 + i] = (hc[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+}
+
+// counts[b] += the blocks' partial counts of bin b (one thread per bin; the
+// only writer of counts after k_emit_bin_lds on the stream)
+__global__ void k_bin_reduce(const uint32_t *__restrict__ binpart, uint32_t blocks, uint32_t nbins,
+                             unsigned long long *counts) {
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
+    unsigned long long t = 0;
+    for (uint32_t k = 0; k < blocks; ++k) t += binpart[uint64_t(k) * nbins + b];
+    if (t) counts[b] += t;
   }
 }
 
@@ -1485,6 +1500,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_prev = dalloc<int64_t>(2);
     p->d_lp = dalloc<int64_t>(P);
     p->d_lps = dalloc<int64_t>(P);
+    p->d_binpart = dalloc<uint32_t>(uint64_t(kBinBlocks) * (p->nbins ? p->nbins : 1));
     {
       const char *e = getenv("SMASH_FUSED_BIN");   // 0: k_emit + k_bin (A/B)
       p->fused_bin = !(e && e[0] == '0');
@@ -1592,7 +1608,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
-                  (void *)p->d_lp, (void *)p->d_lps,
+                  (void *)p->d_lp, (void *)p->d_lps, (void *)p->d_binpart,
                   (void *)p->d_send_q, (void *)p->d_owner, (void *)p->d_fb, (void *)p->d_l16,
                   (void *)p->d_post_ws, (void *)p->d_arena, (void *)p->d_arena_top,
                   (void *)p->d_send_hdr, (void *)p->d_send_words, (void *)p->d_recv_base})
@@ -1818,11 +1834,14 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
     const uint32_t parts = bin_parts(p->nbins);
     if (n && p->bin_lds && parts <= kBinPartsMax) {
       const uint32_t part = bin_part_size(p->nbins);
-      const dim3 grid(unsigned(std::min<uint64_t>(256, (n + 1023) / 1024)), parts);
+      const unsigned gx = unsigned(std::min<uint64_t>(kBinBlocks, (n + 1023) / 1024));
+      const dim3 grid(gx, parts);
       k_emit_bin_lds<<<grid, 1024, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
           p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
-          p->d_stats, part, p->bin_flush);
+          p->d_stats, part, p->bin_flush, p->d_binpart);
+      k_bin_reduce<<<grid_for(p->nbins, kB, 1024), kB, 0, s>>>(
+          p->d_binpart, gx, p->nbins, reinterpret_cast<unsigned long long *>(d_counts));
     } else if (n) {
       k_emit_bin<<<grid_for(n, kB, 8192), kB, 0, s>>>(
           p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
