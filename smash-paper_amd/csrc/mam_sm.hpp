@@ -594,6 +594,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   uint32_t *row = ldsw + threadIdx.x * c.w_row;
   const uint8_t *P = reinterpret_cast<const uint8_t *>(row);
   const uint32_t lane = threadIdx.x & 63;
+  // direct rows: the bytes of row word `lane` inside the read (0..4)
+  const uint32_t row_live = 4 * lane < c.len0 ? (c.len0 - 4 * lane < 4 ? c.len0 - 4 * lane : 4u) : 0u;
 
   uint64_t q_next = 0, q_end = 0;   // this wave's claimed, unassigned reads
   uint32_t st = S_NEW, op = 0, pend = A_NONE;
@@ -701,10 +703,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         while (cm) {
           const uint32_t ln = uint32_t(__builtin_ctzll(cm));
           cm &= cm - 1;
-          const uint32_t lr = uint32_t(__shfl(int(L), int(ln), 64));
-          const uint32_t b0 = 4 * lane;
-          const uint32_t w = b0 < lr ? ldsw[ln * c.w_row + lane] : 0u;
-          const uint32_t nib = b0 < lr ? bad_nibble(w, c.bad_tab_lo, c.bad_tab_hi, lr - b0) : 0u;
+          // (direct rows have one length, c.len0: row_live is this lane's
+          // live bytes of word `lane`, 0 past the read)
+          const uint32_t w = row_live ? ldsw[ln * c.w_row + lane] : 0u;
+          const uint32_t nib = row_live ? bad_nibble(w, c.bad_tab_lo, c.bad_tab_hi, row_live) : 0u;
           if (__ballot(nib != 0)) {   // rare: a read with a bad base
             uint32_t x = nib << (4 * (lane & 7));
             x |= __shfl_xor(x, 1, 64);
