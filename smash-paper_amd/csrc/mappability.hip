@@ -212,6 +212,11 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     for (uint32_t k = threadIdx.x; k < nseg; k += blockDim.x) s_segs[k] = segs[k];
   __syncthreads();
   const Seg *tab = lds_segs ? s_segs : segs;
+  // thread 0's running unique count of the block's tiles in one contig,
+  // added when the contig changes and at the end (an atomic per tile on ~25
+  // contig addresses serialised ~60 k same-address atomics on chr1's)
+  unsigned long long run_tot = 0;
+  uint64_t run_contig = ~0ull;
   for (uint64_t T = blockIdx.x; T < ntiles_all; T += gridDim.x) {
     if (threadIdx.x == 0) s_seg = seg_of(tab, nseg, T);
     __syncthreads();
@@ -219,7 +224,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     const uint64_t sp = g.sp, S = g.S, i0 = g.i0, i1 = g.i1;
     const int64_t abs0 = g.abs0;
     const bool binned = abs0 >= 0 && c.nbins;
-    unsigned long long *contig_count = contig_counts ? contig_counts + g.contig : nullptr;
+    const bool contig_count = contig_counts != nullptr;
     const uint64_t t0 = i0 + (T - g.tile0) * kMTile;
     if (threadIdx.x <= kLdsBins) s_bin[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
@@ -447,9 +452,17 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       const uint32_t o = o0 + threadIdx.x;   // ordinal o counts into bin o - 1 (0: the last)
       atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], s_bin[threadIdx.x]);
     }
-    if (threadIdx.x == 0 && s_tot && contig_count) atomicAdd(contig_count, s_tot);
+    if (threadIdx.x == 0 && contig_count) {
+      if (g.contig != run_contig) {
+        if (run_tot) atomicAdd(contig_counts + run_contig, run_tot);
+        run_tot = 0;
+        run_contig = g.contig;
+      }
+      run_tot += s_tot;
+    }
     __syncthreads();
   }
+  if (threadIdx.x == 0 && run_tot) atomicAdd(contig_counts + run_contig, run_tot);
 }
 
 // settle the listed bytes: exact m, zeroed at its threshold, else min(m, 255)
