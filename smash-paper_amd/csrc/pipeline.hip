@@ -1227,15 +1227,39 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
   const int64_t prev0 = *prev_p;
   unsigned long long d = 0, k = 0, t = 0;
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += stride) {
-    if (!keep[q]) continue;
-    const int32_t m = nk[q];
-    if (m <= 0) continue;
-    int64_t prev = q ? lps[q - 1] : -1;
-    if (prev < 0) prev = prev0;
+  // a pair's inputs are fetched one trip ahead (keep, nk, lps[q - 1] and its
+  // first 4 hit words as one 32-byte row prefix): the walk is a chain of
+  // dependent loads per pair, and the next pair's part of it now overlaps
+  // this pair's bin lookups
+  struct Ahead {
+    uint32_t kp;
+    int32_t m;
+    int64_t lp;
+    uint4 h0, h1;
+  };
+  auto fetch = [&](uint64_t x) {
+    Ahead a{0u, 0, -1, make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (x < n) {
+      a.kp = keep[x];
+      a.m = nk[x];
+      a.lp = x ? lps[x - 1] : -1;
+      const uint4 *r = reinterpret_cast<const uint4 *>(hits + x * 2 * uint64_t(slots));
+      a.h0 = r[0];
+      a.h1 = r[1];
+    }
+    return a;
+  };
+  uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  Ahead cur = fetch(q);
+  for (; q < n; q += stride) {
+    const Ahead nxt = fetch(q + stride);
+    const int32_t m = cur.kp ? cur.m : 0;
+    int64_t prev = cur.lp < 0 ? prev0 : cur.lp;
     const uint64_t *h = hits + q * 2 * uint64_t(slots);
     for (int32_t i = 0; i < m; ++i) {
-      const uint64_t w = h[i];
+      const uint4 &hv = i < 2 ? cur.h0 : cur.h1;
+      const uint64_t w = i >= 4 ? h[i]
+                                : (i & 1) ? (uint64_t(hv.w) << 32 | hv.z) : (uint64_t(hv.y) << 32 | hv.x);
       const int64_t co = chrom_off[uint32_t(w >> 48)];
       if (co < 0) continue;
       const int64_t p = int64_t(w & 0xFFFFFFFFFFFFull);
@@ -1256,6 +1280,7 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
       }
       prev = p;
     }
+    cur = nxt;
   }
   __shared__ unsigned long long sd, sk, st;
   if (threadIdx.x == 0) { sd = 0; sk = 0; st = 0; }
@@ -1267,9 +1292,8 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     atomicAdd(&stats[S_DUPS], sd);
     atomicAdd(&stats[S_KEPT], sk);
   }
-  // the block's counts as plain coalesced stores (k_bin_reduce sums the
-  // blocks): a global atomic per non-zero bin per block was ~9 M atomics per
-  // batch at 50 000 bins, most of the kernel
+  // the block's counts as plain coalesced stores, k_bin_reduce sums the
+  // blocks (no global atomic per non-zero bin per block)
   uint32_t *out = binpart + uint64_t(blockIdx.x) * nbins;
   for (uint32_t i = threadIdx.x; b0 + i < b1; i += blockDim.x)
     out[b0 + i] = (hc[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
