@@ -49,7 +49,7 @@ METRIC = ("reads/sec mapped+binned (hg19, 150 bp) at 1/2/4/8 MI355X; "
 CONFIGS = {
     # BASELINE.json configs[2]: hg19, 50 M x 150 bp, sample_bins/50000 (the
     # metric's config); configs[3] (C4) is this at N = 8: 400 M reads
-    "c3": dict(genome="hg19", read_len=150, pairs=25_000_000, batch=6_250_000, bins="50000",
+    "c3": dict(genome="hg19", read_len=150, pairs=25_000_000, batch=12_500_000, bins="50000",
                seed=3, workload="C3 hg19-shaped, 50 M x 150 bp SMASH reads per rank "
                                 "(25 M pairs, 4 batches, one run), sample_bins/50000"),
     # configs[1]: hg19 1M x 100 bp, sample_bins/100000 (synthesized 2-way split)
@@ -312,6 +312,24 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def fit_batch(B, P, L, free, min_len=20, floor=1_000_000):
+    """the largest B / 2^k (>= floor) whose pipeline buffers fit in `free`
+    bytes of HBM: two search sets' match rows and the hit rows (slots u64
+    per mate each, slots = L - min_len + 1), ~256 B of other per-pair state,
+    the key set (~128 B per key of capacity) and 8 GB for the exchange and
+    file-fed buffers"""
+    slots = L - min_len + 1
+    cap = P + P // 8 + (1 << 20)
+
+    def need(b):
+        return b * (3 * 2 * slots * 8 + 256) + cap * 128 + (8 << 30)
+    while B > floor and need(B) > free:
+        B //= 2
+    log("batch %d pairs: %.1f GB of pipeline buffers, %.1f GB of HBM free"
+        % (B, need(B) / 1e9, free / 1e9))
+    return B
+
+
 def drop_cache(paths):
     """flush the files and drop their pages from the page cache
     (posix_fadvise DONTNEED after fsync), so the file-fed run reads them
@@ -506,6 +524,12 @@ def main():
     log("reads: %d pairs x %d bp per rank in HBM (%.1f GB, rows of %d B), batches of %d "
         "(%.1fs since start)" % (P, L, d_reads.numel() / 1e9, d_reads.shape[1], B,
                                  time.time() - t0))
+    # the batch: the config's (C3: 12.5 M pairs, 2 per step) when the
+    # pipeline's buffers fit in what the index and the reads leave of HBM,
+    # else halved until they do (profiles/r04/sched: 12.5 M-pair batches
+    # 3.56-3.60e8 reads/s vs 3.47-3.48e8 at 6.25 M on one box)
+    if not args.batch:
+        B = fit_batch(B, P, L, torch.cuda.mem_get_info(dev)[0])
     # the key set: every key of the run (single GPU), or the keys this rank
     # owns ((hash >> 1) % world of all ranks' keys: ~P as well)
     pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),
