@@ -750,9 +750,15 @@ def main():
                 "device==oracle counts: %s" % (cpu["value"], nm / dtm, threads, exact))
     out["roofline"] = roof
     out["cpu_baseline"] = cpu
+    # the side measurements must not cost the line: a failure is recorded in
+    # its object (and the log) instead
     if rank == 0 and world == 1 and not args.no_feed:
-        out["host_boundary"] = feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir,
-                                          n_plain=args.feed_pairs)
+        try:
+            out["host_boundary"] = feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir,
+                                              n_plain=args.feed_pairs)
+        except Exception as e:   # noqa: BLE001
+            log("file-fed measurement failed: %r" % (e,))
+            out["host_boundary"] = {"error": repr(e)}
     if cfg["genome"] == "hg19" and not args.no_c5:
         out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)
     out["deterministic_counts"] = same
