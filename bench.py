@@ -312,22 +312,25 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
-def fit_batch(B, P, L, free, min_len=20, floor=1_000_000):
-    """the largest B / 2^k (>= floor) whose pipeline buffers fit in `free`
-    bytes of HBM: two search sets' match rows and the hit rows (slots u64
-    per mate each, slots = L - min_len + 1), ~256 B of other per-pair state,
-    the key set (~128 B per key of capacity) and 8 GB for the exchange and
-    file-fed buffers"""
+def fit_batch(B, P, L, free, min_len=20, headroom=12 << 30):
+    """the largest batch ceil(P / k) <= B (k = 1, 2, ...) whose pipeline
+    buffers leave `headroom` of the free HBM: two search sets' match rows and
+    the hit rows (slots u64 per mate each, slots = L - min_len + 1), ~130 B
+    of other per-pair state, the key set (~170 B per key of capacity); the
+    headroom is for the file-fed buffers (2 x 2 B x 160 B) and the multi-GPU
+    exchange buffers"""
     slots = L - min_len + 1
     cap = P + P // 8 + (1 << 20)
 
     def need(b):
-        return b * (3 * 2 * slots * 8 + 256) + cap * 128 + (8 << 30)
-    while B > floor and need(B) > free:
-        B //= 2
-    log("batch %d pairs: %.1f GB of pipeline buffers, %.1f GB of HBM free"
-        % (B, need(B) / 1e9, free / 1e9))
-    return B
+        return b * (3 * 2 * slots * 8 + 130) + cap * 170
+    k = max(1, -(-P // B))
+    while -(-P // k) > 1_000_000 and need(-(-P // k)) + headroom > free:
+        k += 1
+    b = -(-P // k)
+    log("batch %d pairs (%d per step): %.1f GB of pipeline buffers, %.1f GB of HBM free"
+        % (b, k, need(b) / 1e9, free / 1e9))
+    return b
 
 
 def drop_cache(paths):
@@ -525,9 +528,10 @@ def main():
         "(%.1fs since start)" % (P, L, d_reads.numel() / 1e9, d_reads.shape[1], B,
                                  time.time() - t0))
     # the batch: the config's (C3: 12.5 M pairs, 2 per step) when the
-    # pipeline's buffers fit in what the index and the reads leave of HBM,
-    # else halved until they do (profiles/r04/sched: 12.5 M-pair batches
-    # 3.56-3.60e8 reads/s vs 3.47-3.48e8 at 6.25 M on one box)
+    # pipeline's buffers leave 12 GB of what the index and the reads leave of
+    # HBM, else P / 3, P / 4, ... (at hg19 with 150 bp reads: P / 3 = 8.33 M;
+    # profiles/r04/sched: 3.50-3.52e8 reads/s vs 3.47-3.48e8 at 6.25 M and
+    # 3.56-3.60e8 at 12.5 M, which leaves only ~4 GB)
     if not args.batch:
         B = fit_batch(B, P, L, torch.cuda.mem_get_info(dev)[0])
     # the key set: every key of the run (single GPU), or the keys this rank
