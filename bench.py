@@ -533,7 +533,12 @@ def main():
     # profiles/r04/sched: 3.50-3.52e8 reads/s vs 3.47-3.48e8 at 6.25 M and
     # 3.56-3.60e8 at 12.5 M, which leaves only ~4 GB)
     if not args.batch:
-        B = fit_batch(B, P, L, torch.cuda.mem_get_info(dev)[0])
+        free = torch.cuda.mem_get_info(dev)[0]
+        if sharded:   # every rank must run the same batches: the least free HBM decides
+            f = torch.tensor([free], dtype=torch.int64, device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            free = int(f.item())
+        B = fit_batch(B, P, L, free)
     # the key set: every key of the run (single GPU), or the keys this rank
     # owns ((hash >> 1) % world of all ranks' keys: ~P as well)
     pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),
