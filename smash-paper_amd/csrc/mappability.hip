@@ -198,18 +198,21 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
                                                  const uint32_t *__restrict__ tile_o0,
                                                  unsigned long long *bin_counts,
                                                  unsigned long long *contig_counts) {
-  __shared__ unsigned long long s_bin[kLdsBins + 1];
-  __shared__ int64_t s_bs[kLdsBins];
-  __shared__ unsigned long long s_tot;
-  __shared__ uint32_t s_o0;
+  // per-tile LDS, double-buffered by tile parity: a tile's counts are read
+  // and cleared by their flushers while the faster threads already count the
+  // next tile into the other buffer (two barriers per tile, not four)
+  __shared__ unsigned long long s_bin[2][kLdsBins + 1];
+  __shared__ int64_t s_bs[2][kLdsBins];
+  __shared__ unsigned long long s_tot[2];
   __shared__ uint64_t s_f[kMB / 64], s_r[kMB / 64];   // per wave: first unsaturated (fwd / rc)
   __shared__ uint64_t s_ftail, s_rtail;
-  __shared__ uint32_t s_seg;
   __shared__ Seg s_segs[kMaxSegLds];   // the segment table, once per block
   const uint64_t N = c.N;
   const bool lds_segs = nseg <= uint32_t(kMaxSegLds);
   if (lds_segs)
     for (uint32_t k = threadIdx.x; k < nseg; k += blockDim.x) s_segs[k] = segs[k];
+  if (threadIdx.x <= kLdsBins) s_bin[0][threadIdx.x] = s_bin[1][threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_tot[0] = s_tot[1] = 0;
   __syncthreads();
   const Seg *tab = lds_segs ? s_segs : segs;
   // thread 0's running unique count of the block's tiles in one contig,
@@ -217,24 +220,19 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
   // contig addresses serialised ~60 k same-address atomics on chr1's)
   unsigned long long run_tot = 0;
   uint64_t run_contig = ~0ull;
-  for (uint64_t T = blockIdx.x; T < ntiles_all; T += gridDim.x) {
-    if (threadIdx.x == 0) s_seg = seg_of(tab, nseg, T);
-    __syncthreads();
-    const Seg g = tab[s_seg];
+  uint32_t par = 0;
+  for (uint64_t T = blockIdx.x; T < ntiles_all; T += gridDim.x, par ^= 1u) {
+    const Seg g = tab[seg_of(tab, nseg, T)];   // (every thread: same LDS words, broadcast)
     const uint64_t sp = g.sp, S = g.S, i0 = g.i0, i1 = g.i1;
     const int64_t abs0 = g.abs0;
     const bool binned = abs0 >= 0 && c.nbins;
     const bool contig_count = contig_counts != nullptr;
     const uint64_t t0 = i0 + (T - g.tile0) * kMTile;
-    if (threadIdx.x <= kLdsBins) s_bin[threadIdx.x] = 0;
-    if (threadIdx.x == 0) {
-      s_tot = 0;
-      s_o0 = binned ? tile_o0[T] : 0;
-    }
-    __syncthreads();
-    const uint32_t o0 = s_o0;
-    if (binned && threadIdx.x < kLdsBins)
-      s_bs[threadIdx.x] = o0 + threadIdx.x < c.nbins ? c.bins[o0 + threadIdx.x] : INT64_MAX;
+    const uint32_t o0 = binned ? tile_o0[T] : 0;
+    unsigned long long *sbin = s_bin[par];
+    const int64_t *s_bsp = s_bs[par];
+    if (binned && threadIdx.x < kLdsBins)   // (read after the barrier below)
+      s_bs[par][threadIdx.x] = o0 + threadIdx.x < c.nbins ? c.bins[o0 + threadIdx.x] : INT64_MAX;
     // this thread's 16 bases: U at the forward positions (ascending) and at
     // the reverse-complement positions (descending; byte 15 - q is base q)
     const uint64_t ib = t0 + uint64_t(threadIdx.x) * kMPer;
@@ -317,15 +315,15 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       if (binned && umask) {
         const int64_t a0 = abs0 + int64_t(ib) + __builtin_ctz(umask);
         const int64_t a1 = abs0 + int64_t(ib) + 31 - __builtin_clz(umask);
-        while (d < uint32_t(kLdsBins) && a0 >= s_bs[d]) ++d;
-        if (d < uint32_t(kLdsBins) && a1 < s_bs[d]) {       // [a0, a1] in one bin
-          atomicAdd(&s_bin[d], (unsigned long long)__popc(umask));
+        while (d < uint32_t(kLdsBins) && a0 >= s_bsp[d]) ++d;
+        if (d < uint32_t(kLdsBins) && a1 < s_bsp[d]) {       // [a0, a1] in one bin
+          atomicAdd(&sbin[d], (unsigned long long)__popc(umask));
         } else {
           for (uint32_t m = umask; m; m &= m - 1) {
             const int64_t a = abs0 + int64_t(ib) + __builtin_ctz(m);
-            while (d < uint32_t(kLdsBins) && a >= s_bs[d]) ++d;
+            while (d < uint32_t(kLdsBins) && a >= s_bsp[d]) ++d;
             if (d < uint32_t(kLdsBins)) {
-              atomicAdd(&s_bin[d], 1ull);
+              atomicAdd(&sbin[d], 1ull);
             } else {
               const uint32_t o = bisect_right(c, a);
               atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], 1ull);
@@ -394,9 +392,9 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         ++mine;
         if (binned) {
           const int64_t a = abs0 + int64_t(i);
-          while (d < uint32_t(kLdsBins) && a >= s_bs[d]) ++d;
+          while (d < uint32_t(kLdsBins) && a >= s_bsp[d]) ++d;
           if (d < uint32_t(kLdsBins)) {
-            atomicAdd(&s_bin[d], 1ull);
+            atomicAdd(&sbin[d], 1ull);
           } else {
             const uint32_t o = bisect_right(c, a);
             atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], 1ull);
@@ -446,11 +444,18 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         }
       }
     }
-    if (mine) atomicAdd(&s_tot, mine);
+    if (mine) atomicAdd(&s_tot[par], mine);
     __syncthreads();
-    if (binned && threadIdx.x <= kLdsBins && s_bin[threadIdx.x]) {
-      const uint32_t o = o0 + threadIdx.x;   // ordinal o counts into bin o - 1 (0: the last)
-      atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], s_bin[threadIdx.x]);
+    // flush this tile's buffer and clear it for tile T + 2 gridDim.x (the
+    // next tile counts into the other one; every thread passes the next
+    // tile's barrier, after these clears, before it counts into this one)
+    if (threadIdx.x <= kLdsBins) {
+      const unsigned long long v = sbin[threadIdx.x];
+      if (binned && v) {
+        const uint32_t o = o0 + threadIdx.x;   // ordinal o counts into bin o - 1 (0: the last)
+        atomicAdd(&bin_counts[o == 0 ? c.nbins - 1 : o - 1], v);
+      }
+      sbin[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0 && contig_count) {
       if (g.contig != run_contig) {
@@ -458,9 +463,9 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
         run_tot = 0;
         run_contig = g.contig;
       }
-      run_tot += s_tot;
+      run_tot += s_tot[par];
     }
-    __syncthreads();
+    if (threadIdx.x == 0) s_tot[par] = 0;
   }
   if (threadIdx.x == 0 && run_tot) atomicAdd(contig_counts + run_contig, run_tot);
 }
