@@ -290,13 +290,22 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     const bool fast = (satf | satr) == 0 && ib + kMPer <= i1;
     uint32_t umask = 0;
     if (fast) {
+      // the output byte pairs [left, right] = [rc U + 1, fwd U + 1] by byte
+      // permutes (U < 255 here: + 0x01 per byte cannot carry): word 2m holds
+      // bases 4m, 4m + 1 (fwd dword m bytes 0, 1; rc dword 3 - m bytes 3, 2),
+      // word 2m + 1 bases 4m + 2, 4m + 3 (bytes 2, 3; 1, 0)
+      const uint32_t f1[4] = {fw.x + 0x01010101u, fw.y + 0x01010101u, fw.z + 0x01010101u,
+                              fw.w + 0x01010101u};
+      const uint32_t r1[4] = {rw.x + 0x01010101u, rw.y + 0x01010101u, rw.z + 0x01010101u,
+                              rw.w + 0x01010101u};
 #pragma unroll
-      for (uint32_t q = 0; q < uint32_t(kMPer); ++q) {
-        const uint32_t rb = byte_of(fw, q) + 1;            // <= 255: U < 255 here
-        const uint32_t lb = byte_of(rw, 15 - q) + 1;
-        ob[q >> 1] |= (lb | (rb << 8)) << (16 * (q & 1));
-        umask |= uint32_t(rb - 1u < c.k) << q;             // 1 <= rb <= k
+      for (uint32_t m = 0; m < 4; ++m) {
+        ob[2 * m] = __builtin_amdgcn_perm(f1[m], r1[3 - m], 0x05020403u);
+        ob[2 * m + 1] = __builtin_amdgcn_perm(f1[m], r1[3 - m], 0x07000601u);
       }
+#pragma unroll
+      for (uint32_t q = 0; q < uint32_t(kMPer); ++q)
+        umask |= uint32_t(byte_of(fw, q) < c.k) << q;      // 1 <= right = U + 1 <= k
       // the edge rules can zero a byte only near the contig ends (m <= 256):
       // a separate pass for those chunks
       if (ib < 272 || ib + kMPer + 256 > S) {
