@@ -538,7 +538,9 @@ def main():
             f = torch.tensor([free], dtype=torch.int64, device=dev)
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
             free = int(f.item())
-        B = fit_batch(B, P, L, free)
+        # (one process: 6 GB beside the pipeline hold the file-fed buffers of
+        # 6.25 M-pair feed batches; under torchrun, 12 GB for the exchange)
+        B = fit_batch(B, P, L, free, headroom=(12 << 30) if sharded else (6 << 30))
     # the key set: every key of the run (single GPU), or the keys this rank
     # owns ((hash >> 1) % world of all ranks' keys: ~P as well)
     pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),
@@ -762,6 +764,9 @@ def main():
     # the side measurements must not cost the line: a failure is recorded in
     # its object (and the log) instead
     if rank == 0 and world == 1 and not args.no_feed:
+        # the file-fed batches: at most 6.25 M pairs (2 x 2 B x 160 B of
+        # device buffers beside the pipeline)
+        os.environ.setdefault("SMASH_FEED_BATCH", str(min(B, 6_250_000)))
         try:
             out["host_boundary"] = feed_bench(S, pipe, starts, L, d_reads, P, B, dev, tmpdir,
                                               n_plain=args.feed_pairs)

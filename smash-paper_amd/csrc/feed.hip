@@ -722,6 +722,12 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
   f->L = smash::pipe_read_len(p);
   f->S = smash::pipe_stride(p);
   f->B = smash::pipe_max_pairs(p);
+  // SMASH_FEED_BATCH: pairs per file-fed batch below the pipeline's
+  // max_pairs (the device buffers are 2 x 2 B x stride bytes)
+  if (const char *fb_env = std::getenv("SMASH_FEED_BATCH")) {
+    const uint64_t b = std::strtoull(fb_env, nullptr, 10);
+    if (b > 0 && b < f->B) f->B = b;
+  }
   f->T = threads ? threads : 1;
   for (uint32_t i = 0; i < n1; ++i) f->r1.paths.emplace_back(r1[i]);
   for (uint32_t i = 0; i < n2; ++i) f->r2.paths.emplace_back(r2[i]);
