@@ -773,10 +773,14 @@ def main():
         except Exception as e:   # noqa: BLE001
             log("file-fed measurement failed: %r" % (e,))
             out["host_boundary"] = {"error": repr(e)}
-    if cfg["genome"] == "hg19" and not args.no_c5:
-        out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)
     out["deterministic_counts"] = same
     out["stats_last_step"] = st.as_dict()
+    if cfg["genome"] == "hg19" and not args.no_c5:
+        # the scan needs ~12 GB of its own (its map.bin output and the
+        # comparison): the C3 pipeline and its file-fed buffers go first
+        pipe.close()
+        torch.cuda.empty_cache()
+        out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if sharded:

@@ -623,11 +623,16 @@ class Pipeline:
                                         _p(hits, u64p), None), "smash_pipeline_peek")
         return nk, keep, hits.reshape(n_pairs, 2 * self.slots)
 
+    def close(self):
+        """free the pipeline's device buffers now (its streams are
+        synchronised first); the object is unusable afterwards"""
+        if self.h:
+            lib().smash_pipeline_free(self.h)
+            self.h = None
+
     def __del__(self):
         try:
-            if self.h:
-                lib().smash_pipeline_free(self.h)
-                self.h = None
+            self.close()
         except Exception:
             pass
 
