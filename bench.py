@@ -538,9 +538,10 @@ def main():
             f = torch.tensor([free], dtype=torch.int64, device=dev)
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
             free = int(f.item())
-        # (one process: 6 GB beside the pipeline hold the file-fed buffers of
-        # 6.25 M-pair feed batches; under torchrun, 12 GB for the exchange)
-        B = fit_batch(B, P, L, free, headroom=(12 << 30) if sharded else (6 << 30))
+        # (one GPU: 6 GB beside the pipeline hold the file-fed buffers of
+        # 6.25 M-pair feed batches, or the world-1 exchange; N > 1 GPUs: 12 GB
+        # for the exchange with the other ranks)
+        B = fit_batch(B, P, L, free, headroom=(12 << 30) if world > 1 else (6 << 30))
     # the key set: every key of the run (single GPU), or the keys this rank
     # owns ((hash >> 1) % world of all ranks' keys: ~P as well)
     pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),
