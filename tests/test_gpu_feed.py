@@ -71,6 +71,21 @@ def test_feed_sorted_equals_batch_path(gix, setup, s, batch):
     assert fs["batches"] == -(-len(names) // batch)
 
 
+def test_feed_batch_knob_below_max_pairs(gix, setup, monkeypatch):
+    """SMASH_FEED_BATCH: file-fed batches smaller than the pipeline's
+    max_pairs (bench.py feeds 12.5 M-pair pipelines in 6.25 M-pair batches):
+    the same counts and statistics as the batch path at that batch size."""
+    cs, starts = setup
+    r1, r2 = [gold("s150_r1.fq.gz")], [gold("s150_r2.fq.gz")]
+    names, reads = S.read_fastq_pairs(r1, r2)
+    exp = _batch_path(gix, cs, starts, names, reads, 41)
+    monkeypatch.setenv("SMASH_FEED_BATCH", "41")
+    got_c, got_s, fs = _feed_path(gix, cs, starts, r1, r2, reads.shape[1], 5000, True,
+                                  len(names))
+    assert (got_c, got_s) == exp
+    assert fs["batches"] == -(-len(names) // 41)
+
+
 @pytest.mark.parametrize("gz", [False, True])
 def test_feed_streams_input_in_name_order(gix, setup, tmp_path, gz):
     """Pairs rewritten in name order (tools/readgen.py write_fastq): the
