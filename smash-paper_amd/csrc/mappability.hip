@@ -220,25 +220,50 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
   // contig addresses serialised ~60 k same-address atomics on chr1's)
   unsigned long long run_tot = 0;
   uint64_t run_contig = ~0ull;
+  // a tile's inputs are fetched one trip ahead (its segment, bin ordinal,
+  // bin starts and this thread's two U blocks): the waves waited on these
+  // loads for most of their cycles (profiles/r04/c5pmc)
+  struct TileIn {
+    uint32_t seg, o0;
+    int64_t bs;
+    uint4 fw, rw;
+  };
+  auto fetch = [&](uint64_t T) {
+    TileIn x;
+    x.seg = seg_of(tab, nseg, T);   // (every thread: same LDS words, broadcast)
+    const Seg &g = tab[x.seg];
+    const bool binned = g.abs0 >= 0 && c.nbins;
+    x.o0 = binned ? tile_o0[T] : 0;
+    x.bs = binned && threadIdx.x < kLdsBins
+               ? (x.o0 + threadIdx.x < c.nbins ? c.bins[x.o0 + threadIdx.x] : INT64_MAX)
+               : INT64_MAX;
+    const uint64_t ib = g.i0 + (T - g.tile0) * kMTile + uint64_t(threadIdx.x) * kMPer;
+    const uint64_t xf = g.sp + ib, xr = g.sp + 2 * g.S - ib;
+    x.fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    x.rw = xr >= 15 ? load16u(U + xr - 15) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    return x;
+  };
   uint32_t par = 0;
+  TileIn cur{};
+  if (uint64_t(blockIdx.x) < ntiles_all) cur = fetch(blockIdx.x);
   for (uint64_t T = blockIdx.x; T < ntiles_all; T += gridDim.x, par ^= 1u) {
-    const Seg g = tab[seg_of(tab, nseg, T)];   // (every thread: same LDS words, broadcast)
+    TileIn nxt{};
+    if (T + gridDim.x < ntiles_all) nxt = fetch(T + gridDim.x);
+    const Seg g = tab[cur.seg];
     const uint64_t sp = g.sp, S = g.S, i0 = g.i0, i1 = g.i1;
     const int64_t abs0 = g.abs0;
     const bool binned = abs0 >= 0 && c.nbins;
     const bool contig_count = contig_counts != nullptr;
     const uint64_t t0 = i0 + (T - g.tile0) * kMTile;
-    const uint32_t o0 = binned ? tile_o0[T] : 0;
+    const uint32_t o0 = cur.o0;
     unsigned long long *sbin = s_bin[par];
     const int64_t *s_bsp = s_bs[par];
-    if (binned && threadIdx.x < kLdsBins)   // (read after the barrier below)
-      s_bs[par][threadIdx.x] = o0 + threadIdx.x < c.nbins ? c.bins[o0 + threadIdx.x] : INT64_MAX;
+    if (binned && threadIdx.x < kLdsBins) s_bs[par][threadIdx.x] = cur.bs;   // (read after the barrier below)
     // this thread's 16 bases: U at the forward positions (ascending) and at
     // the reverse-complement positions (descending; byte 15 - q is base q)
     const uint64_t ib = t0 + uint64_t(threadIdx.x) * kMPer;
     const uint64_t xf = sp + ib, xr = sp + 2 * S - ib;   // xr - q: base ib + q
-    const uint4 fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
-    const uint4 rw = xr >= 15 ? load16u(U + xr - 15) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    const uint4 fw = cur.fw, rw = cur.rw;
     // bit q: U == 255 at base ib + q (or past the text), 4 bytes per step:
     // a byte is 0xFF iff its complement is zero
     uint32_t satf = sat_mask16(fw), satr = rev16(sat_mask16(rw));
@@ -475,6 +500,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
       run_tot += s_tot[par];
     }
     if (threadIdx.x == 0) s_tot[par] = 0;
+    cur = nxt;
   }
   if (threadIdx.x == 0 && run_tot) atomicAdd(contig_counts + run_contig, run_tot);
 }
@@ -561,7 +587,15 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     }
     int cus = 0;
     SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
-    const uint64_t grid = std::min<uint64_t>(ntiles, uint64_t(cus) * 8);   // resident blocks
+    // resident blocks only: the tiles are dealt block-stride, so a block that
+    // is not resident from the start waits for a whole block's share of the
+    // tiles (at 147+ VGPRs 3 blocks of 256 fit per CU, not the 8 a fixed
+    // grid of cus * 8 assumed)
+    int per_cu = 0;
+    SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void *>(k_mapscan<IdxT>), kMB, 0));
+    if (per_cu < 1) per_cu = 1;
+    const uint64_t grid = std::min<uint64_t>(ntiles, uint64_t(cus) * uint64_t(per_cu));
     k_mapscan<IdxT><<<unsigned(grid), kMB, 0, s>>>(
         c, static_cast<const IdxT *>(ix->d_isa), ix->d_uniq, ix->d_nsdir, ndir, d_segs, nseg,
         ntiles, out, d_o0, reinterpret_cast<unsigned long long *>(d_bin_counts),
