@@ -49,6 +49,9 @@
 // on the block's critical path.
 #include "common.hpp"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace smash {
 namespace {
 
@@ -189,8 +192,8 @@ __global__ void k_tilebins(MapCtx c, const Seg *segs, uint32_t nseg, uint64_t nt
 // every contig's bases in ONE launch (per-contig launches and their tails
 // dominated the scan): block-stride over the tiles of all segments; out: the
 // scan's map.bin bytes (or null)
-template <class IdxT>
-__global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restrict__ ISA,
+template <class IdxT, int W, bool PF_U>
+__global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__restrict__ ISA,
                                                  const uint8_t *__restrict__ U,
                                                  const uint64_t *__restrict__ dir, uint64_t ndir,
                                                  const Seg *__restrict__ segs, uint32_t nseg,
@@ -221,8 +224,9 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
   unsigned long long run_tot = 0;
   uint64_t run_contig = ~0ull;
   // a tile's inputs are fetched one trip ahead (its segment, bin ordinal,
-  // bin starts and this thread's two U blocks): the waves waited on these
-  // loads for most of their cycles (profiles/r04/c5pmc)
+  // bin starts, and with PF_U this thread's two U blocks): the waves waited
+  // on these loads for most of their cycles (profiles/r04/c5pmc); PF_U's
+  // registers cost more occupancy than the early U loads buy
   struct TileIn {
     uint32_t seg, o0;
     int64_t bs;
@@ -237,6 +241,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     x.bs = binned && threadIdx.x < kLdsBins
                ? (x.o0 + threadIdx.x < c.nbins ? c.bins[x.o0 + threadIdx.x] : INT64_MAX)
                : INT64_MAX;
+    if (!PF_U) return x;
     const uint64_t ib = g.i0 + (T - g.tile0) * kMTile + uint64_t(threadIdx.x) * kMPer;
     const uint64_t xf = g.sp + ib, xr = g.sp + 2 * g.S - ib;
     x.fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -263,7 +268,11 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     // the reverse-complement positions (descending; byte 15 - q is base q)
     const uint64_t ib = t0 + uint64_t(threadIdx.x) * kMPer;
     const uint64_t xf = sp + ib, xr = sp + 2 * S - ib;   // xr - q: base ib + q
-    const uint4 fw = cur.fw, rw = cur.rw;
+    uint4 fw = cur.fw, rw = cur.rw;
+    if (!PF_U) {
+      fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
+      rw = xr >= 15 ? load16u(U + xr - 15) : make_uint4(~0u, ~0u, ~0u, ~0u);
+    }
     // bit q: U == 255 at base ib + q (or past the text), 4 bytes per step:
     // a byte is 0xFF iff its complement is zero
     uint32_t satf = sat_mask16(fw), satr = rev16(sat_mask16(rw));
@@ -370,7 +379,7 @@ __global__ __launch_bounds__(kMB) void k_mapscan(MapCtx c, const IdxT *__restric
     // once (the saturated bases of the chunk all bound through it)
     const uint32_t ufn = !fast && satf && fnext != kNone ? uint32_t(U[fnext]) : 0u;
     const uint32_t urn = !fast && satr && rnext != kNone ? uint32_t(U[rnext]) : 0u;
-#pragma unroll 4
+#pragma unroll 1
     for (uint32_t q = 0; q < uint32_t(kMPer) && !fast; ++q) {
       const uint64_t i = ib + q;
       if (i >= i1) break;
@@ -589,18 +598,35 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     SMASH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
     // resident blocks only: the tiles are dealt block-stride, so a block that
     // is not resident from the start waits for a whole block's share of the
-    // tiles (at 147+ VGPRs 3 blocks of 256 fit per CU, not the 8 a fixed
-    // grid of cus * 8 assumed)
-    int per_cu = 0;
-    SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void *>(k_mapscan<IdxT>), kMB, 0));
-    if (per_cu < 1) per_cu = 1;
-    const uint64_t grid = std::min<uint64_t>(ntiles, uint64_t(cus) * uint64_t(per_cu));
-    k_mapscan<IdxT><<<unsigned(grid), kMB, 0, s>>>(
-        c, static_cast<const IdxT *>(ix->d_isa), ix->d_uniq, ix->d_nsdir, ndir, d_segs, nseg,
-        ntiles, out, d_o0, reinterpret_cast<unsigned long long *>(d_bin_counts),
-        reinterpret_cast<unsigned long long *>(d_contig_counts));
-    SMASH_HIP(hipGetLastError());
+    // tiles (the occupancy query, not a fixed cus * 8)
+    // the register budget: 5 waves per SIMD (96 VGPRs, a few spilled) with
+    // the U blocks loaded in their own trip beat the compiler's choice (3
+    // waves at 150+ VGPRs) with them fetched a trip ahead: 6.9 vs 8.5 ms
+    // over hg19 (profiles/r04/c5waves).  SMASH_MAPSCAN_WAVES (A/B): 0 (the
+    // compiler's choice), 4 or 5, a trailing 'n' = no fetch a trip ahead
+    const char *ev = getenv("SMASH_MAPSCAN_WAVES");
+    if (!ev || !*ev) ev = "5n";
+    const int wv = atoi(ev);
+    const bool pf = !strchr(ev, 'n');
+    const IdxT *isa = static_cast<const IdxT *>(ix->d_isa);
+    auto *bcp = reinterpret_cast<unsigned long long *>(d_bin_counts);
+    auto *ccp = reinterpret_cast<unsigned long long *>(d_contig_counts);
+    auto launch = [&](auto kfn) -> hipError_t {
+      int per_cu = 0;
+      hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void *>(kfn), kMB, 0);
+      if (e != hipSuccess) return e;
+      if (per_cu < 1) per_cu = 1;
+      const uint64_t grid = std::min<uint64_t>(ntiles, uint64_t(cus) * uint64_t(per_cu));
+      kfn<<<unsigned(grid), kMB, 0, s>>>(c, isa, ix->d_uniq, ix->d_nsdir, ndir, d_segs, nseg,
+                                         ntiles, out, d_o0, bcp, ccp);
+      return hipGetLastError();
+    };
+    hipError_t le;
+    if (wv == 4) le = pf ? launch(k_mapscan<IdxT, 4, true>) : launch(k_mapscan<IdxT, 4, false>);
+    else if (wv == 5) le = pf ? launch(k_mapscan<IdxT, 5, true>) : launch(k_mapscan<IdxT, 5, false>);
+    else le = pf ? launch(k_mapscan<IdxT, 1, true>) : launch(k_mapscan<IdxT, 1, false>);
+    SMASH_HIP(le);
   }
   if (d_segs) SMASH_HIP(hipFreeAsync(d_segs, s));
   if (d_o0) SMASH_HIP(hipFreeAsync(d_o0, s));
