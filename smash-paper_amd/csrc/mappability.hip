@@ -603,7 +603,7 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     // the U blocks loaded in their own trip beat the compiler's choice (3
     // waves at 150+ VGPRs) with them fetched a trip ahead: 6.9 vs 8.5 ms
     // over hg19 (profiles/r04/c5waves).  SMASH_MAPSCAN_WAVES (A/B): 0 (the
-    // compiler's choice), 4 or 5, a trailing 'n' = no fetch a trip ahead
+    // compiler's choice), 4, 5 or 6, a trailing 'n' = no fetch a trip ahead
     const char *ev = getenv("SMASH_MAPSCAN_WAVES");
     if (!ev || !*ev) ev = "5n";
     const int wv = atoi(ev);
@@ -625,6 +625,7 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     hipError_t le;
     if (wv == 4) le = pf ? launch(k_mapscan<IdxT, 4, true>) : launch(k_mapscan<IdxT, 4, false>);
     else if (wv == 5) le = pf ? launch(k_mapscan<IdxT, 5, true>) : launch(k_mapscan<IdxT, 5, false>);
+    else if (wv == 6) le = pf ? launch(k_mapscan<IdxT, 6, true>) : launch(k_mapscan<IdxT, 6, false>);
     else le = pf ? launch(k_mapscan<IdxT, 1, true>) : launch(k_mapscan<IdxT, 1, false>);
     SMASH_HIP(le);
   }
