@@ -953,6 +953,37 @@ __device__ __forceinline__ void wave_scan(uint64_t &s, int64_t &l) {
   }
 }
 
+// a lane's kScanPer consecutive (cnt, lp): 16-byte loads when the run is
+// whole (q0 is a multiple of 16, the arrays are 256-byte aligned), one
+// element per load at the batch's end (4 + 8 loads per lane instead of 32:
+// the lanes' runs are 64 / 128 bytes apart, so each element load of a wave
+// touched 64 lines)
+__device__ __forceinline__ void scan_run(const uint32_t *__restrict__ cnt,
+                                         const int64_t *__restrict__ lp, uint64_t q0, uint64_t n,
+                                         uint32_t (&c)[kScanPer], int64_t (&v)[kScanPer]) {
+  if (q0 + kScanPer <= n) {
+    const uint4 *cv = reinterpret_cast<const uint4 *>(cnt + q0);
+    const longlong2 *lv = reinterpret_cast<const longlong2 *>(lp + q0);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer / 4; ++k) {
+      const uint4 x = cv[k];
+      c[4 * k] = x.x; c[4 * k + 1] = x.y; c[4 * k + 2] = x.z; c[4 * k + 3] = x.w;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer / 2; ++k) {
+      const longlong2 y = lv[k];
+      v[2 * k] = y.x; v[2 * k + 1] = y.y;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+      const bool ok = q0 + k < n;
+      c[k] = ok ? cnt[q0 + k] : 0;
+      v[k] = ok ? lp[q0 + k] : -1;
+    }
+  }
+}
+
 __global__ void k_scan_tiles(const uint32_t *__restrict__ cnt, const int64_t *__restrict__ lp,
                              uint64_t n, uint64_t *tsum, int64_t *tlast) {
   SMASH_BESIDE_SEARCH();
@@ -961,12 +992,14 @@ __global__ void k_scan_tiles(const uint32_t *__restrict__ cnt, const int64_t *__
   uint64_t s = 0;
   int64_t l = -1;
   if (t * kScanTile < n) {
+    uint32_t c[kScanPer];
+    int64_t v[kScanPer];
+    scan_run(cnt, lp, q0, n, c, v);
 #pragma unroll
-    for (uint32_t k = 0; k < kScanPer; ++k)
-      if (q0 + k < n) {
-        s += cnt[q0 + k];
-        l = last_valid(l, lp[q0 + k]);
-      }
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+      s += c[k];
+      l = last_valid(l, v[k]);
+    }
   }
   wave_scan(s, l);
   if ((threadIdx.x & 63) == 63 && t * kScanTile < n) {
@@ -1014,11 +1047,9 @@ __global__ void k_scan_apply(const uint32_t *__restrict__ cnt, const int64_t *__
   int64_t v[kScanPer];
   uint64_t s = 0;
   int64_t l = -1;
+  scan_run(cnt, lp, q0, live ? n : 0, c, v);
 #pragma unroll
   for (uint32_t k = 0; k < kScanPer; ++k) {
-    const bool ok = live && q0 + k < n;
-    c[k] = ok ? cnt[q0 + k] : 0;
-    v[k] = ok ? lp[q0 + k] : -1;
     s += c[k];
     l = last_valid(l, v[k]);
   }
@@ -1031,6 +1062,20 @@ __global__ void k_scan_apply(const uint32_t *__restrict__ cnt, const int64_t *__
   if (!live) return;
   es += tsum[t];
   el = last_valid(tlast[t], el);
+  if (q0 + kScanPer <= n) {   // whole run: 16-byte stores (posoff's are 4 bytes off alignment)
+    uint32_t po[kScanPer];
+    int64_t lo[kScanPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+      es += c[k];
+      el = last_valid(el, v[k]);
+      po[k] = uint32_t(es);
+      lo[k] = el;
+    }
+    __builtin_memcpy(posoff + q0 + 1, po, sizeof(po));
+    __builtin_memcpy(lps + q0, lo, sizeof(lo));
+    return;
+  }
 #pragma unroll
   for (uint32_t k = 0; k < kScanPer; ++k) {
     if (q0 + k >= n) break;
