@@ -182,17 +182,17 @@ __device__ __forceinline__ uint32_t rev16(uint32_t m) { return __brev(m) >> 16; 
 
 // bin ordinal (bisect_right of abs0 + the tile's first base) per tile
 __global__ void k_tilebins(MapCtx c, const Seg *segs, uint32_t nseg, uint64_t ntiles,
-                           uint32_t *o0) {
+                           uint64_t tile, uint32_t *o0) {
   const uint64_t T = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (T >= ntiles) return;
   const Seg g = segs[seg_of(segs, nseg, T)];
-  o0[T] = g.abs0 >= 0 ? bisect_right(c, g.abs0 + int64_t(g.i0 + (T - g.tile0) * kMTile)) : 0;
+  o0[T] = g.abs0 >= 0 ? bisect_right(c, g.abs0 + int64_t(g.i0 + (T - g.tile0) * tile)) : 0;
 }
 
 // every contig's bases in ONE launch (per-contig launches and their tails
 // dominated the scan): block-stride over the tiles of all segments; out: the
 // scan's map.bin bytes (or null)
-template <class IdxT, int W, bool PF_U>
+template <class IdxT, int W, bool PF_U, int SUB>
 __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__restrict__ ISA,
                                                  const uint8_t *__restrict__ U,
                                                  const uint64_t *__restrict__ dir, uint64_t ndir,
@@ -210,6 +210,11 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
   __shared__ uint64_t s_f[kMB / 64], s_r[kMB / 64];   // per wave: first unsaturated (fwd / rc)
   __shared__ uint64_t s_ftail, s_rtail;
   __shared__ Seg s_segs[kMaxSegLds];   // the segment table, once per block
+  // a tile is SUB sub-tiles of kMTile bases, one after the other: the
+  // tile's fixed work (segment, bin ordinal, bin starts, the counts' flush,
+  // two barriers) once per SUB x 4 096 bases
+  static_assert(!PF_U || SUB == 1, "the U fetch ahead covers one sub-tile");
+  constexpr uint64_t kTile = kMTile * SUB;
   const uint64_t N = c.N;
   const bool lds_segs = nseg <= uint32_t(kMaxSegLds);
   if (lds_segs)
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
                ? (x.o0 + threadIdx.x < c.nbins ? c.bins[x.o0 + threadIdx.x] : INT64_MAX)
                : INT64_MAX;
     if (!PF_U) return x;
-    const uint64_t ib = g.i0 + (T - g.tile0) * kMTile + uint64_t(threadIdx.x) * kMPer;
+    const uint64_t ib = g.i0 + (T - g.tile0) * kTile + uint64_t(threadIdx.x) * kMPer;
     const uint64_t xf = g.sp + ib, xr = g.sp + 2 * g.S - ib;
     x.fw = xf + 16 <= N + 64 ? load16u(U + xf) : make_uint4(~0u, ~0u, ~0u, ~0u);
     x.rw = xr >= 15 ? load16u(U + xr - 15) : make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -259,14 +264,20 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
     const int64_t abs0 = g.abs0;
     const bool binned = abs0 >= 0 && c.nbins;
     const bool contig_count = contig_counts != nullptr;
-    const uint64_t t0 = i0 + (T - g.tile0) * kMTile;
+    const uint64_t t0 = i0 + (T - g.tile0) * kTile;
     const uint32_t o0 = cur.o0;
     unsigned long long *sbin = s_bin[par];
     const int64_t *s_bsp = s_bs[par];
     if (binned && threadIdx.x < kLdsBins) s_bs[par][threadIdx.x] = cur.bs;   // (read after the barrier below)
+    unsigned long long mine = 0;
+    uint32_t d = 0;   // bin ordinal offset from o0 (monotone over the thread's bases)
+    for (uint32_t r = 0; r < uint32_t(SUB); ++r) {
+    // (block-uniform: a sub-tile past the segment's end is skipped whole, so
+    // a thread's rc position xr never falls below the contig's own text)
+    if (r && t0 + r * kMTile >= i1) break;
     // this thread's 16 bases: U at the forward positions (ascending) and at
     // the reverse-complement positions (descending; byte 15 - q is base q)
-    const uint64_t ib = t0 + uint64_t(threadIdx.x) * kMPer;
+    const uint64_t ib = t0 + r * kMTile + uint64_t(threadIdx.x) * kMPer;
     const uint64_t xf = sp + ib, xr = sp + 2 * S - ib;   // xr - q: base ib + q
     uint4 fw = cur.fw, rw = cur.rw;
     if (!PF_U) {
@@ -302,7 +313,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
       if (lane == 0) s_f[wv] = xs;    // the wave's minima
       if (lane == 63) s_r[wv] = xp;
       if (threadIdx.x == 0) {
-        s_ftail = next_unsat_dir(dir, ndir, sp + t0 + kMTile);
+        s_ftail = next_unsat_dir(dir, ndir, sp + t0 + (r + 1) * kMTile);
         s_rtail = next_unsat_dir(dir, ndir, xr + 1);       // above the tile's rc range
       }
       __syncthreads();
@@ -316,8 +327,6 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
     uint32_t ob[2 * kMPer / 4] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t fixr = 0, fixl = 0;   // bases whose right / left byte k_mapfix settles
     const bool defer = out && c.fix && c.k < 255;
-    unsigned long long mine = 0;
-    uint32_t d = 0;   // bin ordinal offset from o0 (monotone over the thread's bases)
     // fast path (most chunks): no saturated byte and every base inside
     // [i0, i1): straight-line selects, the unique bases as a mask, and their
     // bin counted with one LDS atomic when the 16 bases share a bin
@@ -354,7 +363,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
           if (byte_of(rw, 15 - q) + 1 >= ib32 + q) ob[q >> 1] &= ~(0xFFu << sh);   // left >= i
         }
       }
-      mine = uint32_t(__popc(umask));
+      mine += uint32_t(__popc(umask));
       if (binned && umask) {
         const int64_t a0 = abs0 + int64_t(ib) + __builtin_ctz(umask);
         const int64_t a1 = abs0 + int64_t(ib) + 31 - __builtin_clz(umask);
@@ -487,6 +496,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
         }
       }
     }
+    }   // sub-tiles
     if (mine) atomicAdd(&s_tot[par], mine);
     __syncthreads();
     // flush this tile's buffer and clear it for tile T + 2 gridDim.x (the
@@ -562,6 +572,23 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     SMASH_HIP(hipMemcpyAsync(ix->d_nsdir, h.data(), 8 * ndir, hipMemcpyHostToDevice, s));
     SMASH_HIP(hipStreamSynchronize(s));   // h is a host local
   }
+  // the register budget: 5 waves per SIMD (96 VGPRs, a few spilled) with
+  // the U blocks loaded in their own trip beat the compiler's choice (3
+  // waves at 150+ VGPRs) with them fetched a trip ahead: 6.9 vs 8.5 ms
+  // over hg19 (profiles/r04/c5waves).  SMASH_MAPSCAN_WAVES (A/B): 0 (the
+  // compiler's choice), 4, 5 or 6, a trailing 'n' = no fetch a trip ahead.
+  // Sub-tiles: the tile's fixed work once per 4 x 4 096 bases cut the scan
+  // from 6.9 to ~5.0 ms (profiles/r04/c5sub).  SMASH_MAPSCAN_SUB (A/B): 1,
+  // 2, 4 or 8 sub-tiles per tile at 5 waves without the fetch ahead; the
+  // other budgets take 1
+  const char *ev = getenv("SMASH_MAPSCAN_WAVES");
+  if (!ev || !*ev) ev = "5n";
+  const int wv = atoi(ev);
+  const bool pf = !strchr(ev, 'n');
+  const char *es = getenv("SMASH_MAPSCAN_SUB");
+  int sub = es && *es ? atoi(es) : 4;
+  if (pf || wv != 5 || (sub != 2 && sub != 4 && sub != 8)) sub = 1;
+  const uint64_t tile = kMTile * uint64_t(sub);
   // the segments of [begin, end): one per contig part, tiles numbered across
   std::vector<Seg> segs;
   uint64_t ntiles = 0, g0 = 0;
@@ -577,7 +604,7 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
       sg.abs0 = h_chrom_off ? h_chrom_off[q / 2] : -1;
       sg.contig = q / 2;
       segs.push_back(sg);
-      ntiles += (b - a + kMTile - 1) / kMTile;
+      ntiles += (b - a + tile - 1) / tile;
     }
     g0 += S;
   }
@@ -591,7 +618,7 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_o0), 4 * ntiles, s));
     const uint32_t nseg = uint32_t(segs.size());
     if (c.nbins) {
-      k_tilebins<<<unsigned((ntiles + 255) / 256), 256, 0, s>>>(c, d_segs, nseg, ntiles, d_o0);
+      k_tilebins<<<unsigned((ntiles + 255) / 256), 256, 0, s>>>(c, d_segs, nseg, ntiles, tile, d_o0);
       SMASH_HIP(hipGetLastError());
     }
     int cus = 0;
@@ -599,15 +626,6 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     // resident blocks only: the tiles are dealt block-stride, so a block that
     // is not resident from the start waits for a whole block's share of the
     // tiles (the occupancy query, not a fixed cus * 8)
-    // the register budget: 5 waves per SIMD (96 VGPRs, a few spilled) with
-    // the U blocks loaded in their own trip beat the compiler's choice (3
-    // waves at 150+ VGPRs) with them fetched a trip ahead: 6.9 vs 8.5 ms
-    // over hg19 (profiles/r04/c5waves).  SMASH_MAPSCAN_WAVES (A/B): 0 (the
-    // compiler's choice), 4, 5 or 6, a trailing 'n' = no fetch a trip ahead
-    const char *ev = getenv("SMASH_MAPSCAN_WAVES");
-    if (!ev || !*ev) ev = "5n";
-    const int wv = atoi(ev);
-    const bool pf = !strchr(ev, 'n');
     const IdxT *isa = static_cast<const IdxT *>(ix->d_isa);
     auto *bcp = reinterpret_cast<unsigned long long *>(d_bin_counts);
     auto *ccp = reinterpret_cast<unsigned long long *>(d_contig_counts);
@@ -623,10 +641,13 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
       return hipGetLastError();
     };
     hipError_t le;
-    if (wv == 4) le = pf ? launch(k_mapscan<IdxT, 4, true>) : launch(k_mapscan<IdxT, 4, false>);
-    else if (wv == 5) le = pf ? launch(k_mapscan<IdxT, 5, true>) : launch(k_mapscan<IdxT, 5, false>);
-    else if (wv == 6) le = pf ? launch(k_mapscan<IdxT, 6, true>) : launch(k_mapscan<IdxT, 6, false>);
-    else le = pf ? launch(k_mapscan<IdxT, 1, true>) : launch(k_mapscan<IdxT, 1, false>);
+    if (wv == 5 && !pf && sub == 2) le = launch(k_mapscan<IdxT, 5, false, 2>);
+    else if (wv == 5 && !pf && sub == 4) le = launch(k_mapscan<IdxT, 5, false, 4>);
+    else if (wv == 5 && !pf && sub == 8) le = launch(k_mapscan<IdxT, 5, false, 8>);
+    else if (wv == 4) le = pf ? launch(k_mapscan<IdxT, 4, true, 1>) : launch(k_mapscan<IdxT, 4, false, 1>);
+    else if (wv == 5) le = pf ? launch(k_mapscan<IdxT, 5, true, 1>) : launch(k_mapscan<IdxT, 5, false, 1>);
+    else if (wv == 6) le = pf ? launch(k_mapscan<IdxT, 6, true, 1>) : launch(k_mapscan<IdxT, 6, false, 1>);
+    else le = pf ? launch(k_mapscan<IdxT, 1, true, 1>) : launch(k_mapscan<IdxT, 1, false, 1>);
     SMASH_HIP(le);
   }
   if (d_segs) SMASH_HIP(hipFreeAsync(d_segs, s));

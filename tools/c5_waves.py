@@ -1,6 +1,6 @@
 """tools/c5_waves.py -- A/B of k_mapscan's register budget on one index in
 one process: SMASH_MAPSCAN_WAVES = 0 (the compiler's choice), 4, 5, 6 waves
-per SIMD, each scanned `reps` times (C5: hg19, k = 36, 50 000 bins); every
+per SIMD (W:SUB also sets SMASH_MAPSCAN_SUB), each scanned `reps` times (C5: hg19, k = 36, 50 000 bins); every
 variant's map.bin must equal the index build's and its counts the first
 variant's.  Prints one JSON line per variant."""
 import json
@@ -26,7 +26,9 @@ def main():
     args = types.SimpleNamespace(no_cpu_baseline=True)
     ref = None
     for v in variants:
-        os.environ["SMASH_MAPSCAN_WAVES"] = v
+        w, _, sub = v.partition(":")   # "5n:2": SMASH_MAPSCAN_SUB=2
+        os.environ["SMASH_MAPSCAN_WAVES"] = w
+        os.environ["SMASH_MAPSCAN_SUB"] = sub
         r = bench.c5_scan(args, dix, contigs, "50000", 1, 0, dev, None, None, reps=reps)
         key = (r["unique_kmers"], r["map_identical_to_index_build"])
         ref = ref or key
