@@ -577,17 +577,17 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
   // waves at 150+ VGPRs) with them fetched a trip ahead: 6.9 vs 8.5 ms
   // over hg19 (profiles/r04/c5waves).  SMASH_MAPSCAN_WAVES (A/B): 0 (the
   // compiler's choice), 4, 5 or 6, a trailing 'n' = no fetch a trip ahead.
-  // Sub-tiles: the tile's fixed work once per 8 x 4 096 bases cut the scan
-  // from 6.9 to ~4.6 ms (profiles/r04/c5sub).  SMASH_MAPSCAN_SUB (A/B): 1,
-  // 2, 4, 8 or 16 sub-tiles per tile at 5 waves without the fetch ahead;
-  // the other budgets take 1
+  // Sub-tiles: the tile's fixed work once per 16 x 4 096 bases cut the scan
+  // from 6.9 to ~4.3 ms (profiles/r04/c5sub).  SMASH_MAPSCAN_SUB (A/B): 1,
+  // 2, 4, 8, 16 or 32 sub-tiles per tile at 5 waves without the fetch
+  // ahead; the other budgets take 1
   const char *ev = getenv("SMASH_MAPSCAN_WAVES");
   if (!ev || !*ev) ev = "5n";
   const int wv = atoi(ev);
   const bool pf = !strchr(ev, 'n');
   const char *es = getenv("SMASH_MAPSCAN_SUB");
-  int sub = es && *es ? atoi(es) : 8;
-  if (pf || wv != 5 || (sub != 2 && sub != 4 && sub != 8 && sub != 16)) sub = 1;
+  int sub = es && *es ? atoi(es) : 16;
+  if (pf || wv != 5 || (sub != 2 && sub != 4 && sub != 8 && sub != 16 && sub != 32)) sub = 1;
   const uint64_t tile = kMTile * uint64_t(sub);
   // the segments of [begin, end): one per contig part, tiles numbered across
   std::vector<Seg> segs;
@@ -645,6 +645,7 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     else if (wv == 5 && !pf && sub == 4) le = launch(k_mapscan<IdxT, 5, false, 4>);
     else if (wv == 5 && !pf && sub == 8) le = launch(k_mapscan<IdxT, 5, false, 8>);
     else if (wv == 5 && !pf && sub == 16) le = launch(k_mapscan<IdxT, 5, false, 16>);
+    else if (wv == 5 && !pf && sub == 32) le = launch(k_mapscan<IdxT, 5, false, 32>);
     else if (wv == 4) le = pf ? launch(k_mapscan<IdxT, 4, true, 1>) : launch(k_mapscan<IdxT, 4, false, 1>);
     else if (wv == 5) le = pf ? launch(k_mapscan<IdxT, 5, true, 1>) : launch(k_mapscan<IdxT, 5, false, 1>);
     else if (wv == 6) le = pf ? launch(k_mapscan<IdxT, 6, true, 1>) : launch(k_mapscan<IdxT, 6, false, 1>);
