@@ -51,7 +51,7 @@ CONFIGS = {
     # metric's config); configs[3] (C4) is this at N = 8: 400 M reads
     "c3": dict(genome="hg19", read_len=150, pairs=25_000_000, batch=12_500_000, bins="50000",
                seed=3, workload="C3 hg19-shaped, 50 M x 150 bp SMASH reads per rank "
-                                "(25 M pairs, 4 batches, one run), sample_bins/50000"),
+                                "(25 M pairs, one run in batches), sample_bins/50000"),
     # configs[1]: hg19 1M x 100 bp, sample_bins/100000 (synthesized 2-way split)
     "c2": dict(genome="hg19", read_len=100, pairs=500_000, batch=500_000, bins="100000", seed=2,
                workload="C2 hg19-shaped 1M x 100 bp SMASH reads, sample_bins/100000"),
@@ -196,16 +196,30 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
     bc = torch.zeros(len(starts), dtype=torch.int64, device=dev)
     cc = torch.zeros(len(dix.contigs), dtype=torch.int64, device=dev)
     out = torch.empty(2 * (g1 - g0), dtype=torch.uint8, device=dev)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * reps)]
+    # C5 from the index arrays (SA, ISA, LCP bytes + overflow): each rep first
+    # rebuilds, from SA + the LCP bytes, the per-position unique lengths U and
+    # their directory over the text window the rank's bases read
+    # (smash_mappability_prepare: longSA.cpp:628-641's m[r] in rank order,
+    # scattered to SA[r] by three streaming partition passes), then scans
+    # (k_mapscan, k_mapfix).  U is poisoned in that window first, so the scan
+    # can only see what the timed rebuild wrote.
+    lo, hi = S.mappability_window(dix, g0, g1)
+    N = dix.info.N
+    U = S.device_view(dix.info.d_uniq, N + 64, torch.uint8)
+    U[lo:hi].fill_(0x55)
 
     def step(i, timed):
         bc.zero_()
         cc.zero_()
         if timed:
-            ev[2 * i].record()
+            ev[3 * i].record()
+        S.mappability_prepare(dix, g0, g1)
+        if timed:
+            ev[3 * i + 1].record()
         S.mappability_scan(dix, g0, g1, k, out, off, d_bins, len(starts), bc, cc)
         if timed:
-            ev[2 * i + 1].record()
+            ev[3 * i + 2].record()
         if world > 1:
             dist.all_reduce(bc)
             dist.all_reduce(cc)
@@ -225,31 +239,47 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)) / reps
+    prep_ms = sum(ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(reps)) / reps
+    scan_ms = sum(ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(reps)) / reps
+    kms = prep_ms + scan_ms
     # the scan reproduces the index build's map.bin (compared on the device)
     dmap = S.device_view(dix.info.d_map, dix.info.map_bytes, torch.uint8)
     same_map = bool(torch.equal(out, dmap[2 + 2 * g0:2 + 2 * g1]))
     n_uniq = int(cc.sum().item())
     value = total * reps / el
-    # streaming scan (mappability.hip): U at the forward and at the reverse-
-    # complement position (1 B each, sequential) + the 2 map.bin bytes
-    bpb = 4
-    achieved = (g1 - g0) * bpb / (kms / 1e3) / 1e9
+    # the bytes the step streams: the rebuild reads all of SA (idx_bytes per
+    # rank) and the LCP bytes (1 B), and per position of the window writes +
+    # reads a u32 entry twice (passes 1 -> 2 -> 3) and writes U (1 B); the
+    # directory reads U once (1 B); the scan reads U at the forward and at the
+    # reverse-complement position (1 B each) and writes the 2 map.bin bytes
+    nw = hi - lo
+    prep_bytes = N * (dix.info.idx_bytes + 1) + nw * (4 + 8 + 5 + 1)
+    scan_bytes = (g1 - g0) * 4
+    achieved = (prep_bytes + scan_bytes) / (kms / 1e3) / 1e9
     res = {"metric": "bases/sec mappability self-scan (hg19, every 36-mer; map.bin + unique "
-                     "counts, C5)",
+                     "counts, C5) from the index arrays",
            "value": value, "unit": "bases/s", "ms_per_scan": 1000.0 * el / reps,
            "scaling": "strong", "bases": total, "k": k, "bins": int(len(starts)),
-           "roofline": {"bound": "hbm", "kernel": "k_mapscan", "achieved": round(achieved, 2),
+           "prepare_ms": round(prep_ms, 3), "scan_ms": round(scan_ms, 3),
+           "window_positions": int(nw),
+           "roofline": {"bound": "hbm", "kernel": "smash_mappability_prepare (k_upart1-3, "
+                                                  "k_nsdir) + k_mapscan + k_mapfix",
+                        "achieved": round(achieved, 2),
                         "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5),
-                        "traffic": None, "bytes_per_base": bpb,
-                        "bytes_method": "U byte at the forward + at the reverse-complement "
-                                        "position + 2 output bytes per base (saturated-run "
-                                        "fallback reads not counted)",
+                        "traffic": None,
+                        "bytes_per_base": round((prep_bytes + scan_bytes) / (g1 - g0), 2),
+                        "bytes_method": "streamed bytes of the rebuild of U from SA + LCP "
+                                        "(SA %d B + LCP 1 B per rank; 4 + 8 + 5 + 1 B per "
+                                        "window position) + the scan (4 B per base); SURVEY "
+                                        "section 8d's gather model (ISA + 2 random LCP lines, "
+                                        "146 B per base) prices the same output at %.0f GB/s"
+                                        % (dix.info.idx_bytes,
+                                           146.0 * (g1 - g0) / (kms / 1e3) / 1e9),
                         "avg_kernel_ms": round(kms, 3)},
            "map_identical_to_index_build": same_map, "unique_kmers": n_uniq,
            "cpu_baseline": None}
-    log("C5: %d reps %.3f s -> %.3e bases/s; scan %.1f ms; unique %d-mers %d; map == build: %s"
-        % (reps, el, value, kms, k, n_uniq, same_map))
+    log("C5: %d reps %.3f s -> %.3e bases/s; prepare %.2f ms + scan %.2f ms; unique %d-mers %d; "
+        "map == build: %s" % (reps, el, value, prep_ms, scan_ms, k, n_uniq, same_map))
     if oix is not None and rank == 0 and world == 1 and not args.no_cpu_baseline:
         # oracle/smash_oracle.c orc_mappability_range on every host thread,
         # contiguous sub-windows of one window in the middle of the genome
@@ -312,19 +342,24 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
-def fit_batch(B, P, L, free, min_len=20, headroom=12 << 30):
+def fit_batch(B, P, L, free, min_len=20, headroom=12 << 30, nbins=50_000, max_batch=None):
     """the largest batch ceil(P / k) <= B (k = 1, 2, ...) whose pipeline
     buffers leave `headroom` of the free HBM: two search sets' match rows and
     the hit rows (slots u64 per mate each, slots = L - min_len + 1), ~130 B
-    of other per-pair state, the key set (~170 B per key of capacity); the
-    headroom is for the file-fed buffers (2 x 2 B x 160 B) and the multi-GPU
-    exchange buffers"""
+    of other per-pair state, the key set (~170 B per key of capacity), and
+    k_emit_bin_lds's per-block counts (256 x 4 B per bin, up to 311 296
+    bins); the headroom is for the file-fed buffers (2 x 2 B x 160 B) and the
+    multi-GPU exchange buffers.  Never above max_batch (the library's
+    smash_pipeline_max_batch: max_pairs * 2 * slots < 2^32)."""
     slots = L - min_len + 1
     cap = P + P // 8 + (1 << 20)
+    fixed = cap * 170 + (256 * 4 * nbins if nbins <= 4 * 77824 else 0)
 
     def need(b):
-        return b * (3 * 2 * slots * 8 + 130) + cap * 170
+        return b * (3 * 2 * slots * 8 + 130) + fixed
     k = max(1, -(-P // B))
+    while max_batch and -(-P // k) > max_batch:
+        k += 1
     while -(-P // k) > 1_000_000 and need(-(-P // k)) + headroom > free:
         k += 1
     b = -(-P // k)
@@ -541,7 +576,8 @@ def main():
         # (one GPU: 6 GB beside the pipeline hold the file-fed buffers of
         # 6.25 M-pair feed batches, or the world-1 exchange; N > 1 GPUs: 12 GB
         # for the exchange with the other ranks)
-        B = fit_batch(B, P, L, free, headroom=(12 << 30) if world > 1 else (6 << 30))
+        B = fit_batch(B, P, L, free, headroom=(12 << 30) if world > 1 else (6 << 30),
+                      nbins=len(starts), max_batch=S.pipeline_max_batch(L))
     # the key set: every key of the run (single GPU), or the keys this rank
     # owns ((hash >> 1) % world of all ranks' keys: ~P as well)
     pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),

@@ -193,6 +193,21 @@ int smash_mappability_scan(const smash_index *ix, uint64_t begin, uint64_t end,
                            uint64_t *d_bin_counts, uint64_t *d_contig_counts,
                            void *stream);
 
+/* C5's own preparation from the index arrays: rebuilds, from the suffix     */
+/* array and the LCP bytes (m[r] = max(LCP[r], LCP[r+1]) in rank order,       */
+/* longSA.cpp:628-641, scattered to text position SA[r]), the per-position    */
+/* unique lengths U -- and their directory -- that smash_mappability_scan of  */
+/* the same [begin, end) reads, in place in the index (the values are the     */
+/* index build's).  Three streaming partition passes (csrc/uniq_build.hip);   */
+/* ~4 B per position of scratch HBM.  Asynchronous on `stream`; no search or  */
+/* scan may run on the index concurrently.                                    */
+int smash_mappability_prepare(const smash_index *ix, uint64_t begin, uint64_t end,
+                              void *stream);
+/* The text window [*lo, *hi) that smash_mappability_prepare(begin, end)     */
+/* rebuilds (the forward and reverse-complement positions of those bases).    */
+int smash_mappability_window(const smash_index *ix, uint64_t begin, uint64_t end,
+                             uint64_t *lo, uint64_t *hi);
+
 /* ========================================================================== */
 /* Pipeline: prepare_matches (query.cpp:231-306) + mappability_tag           */
 /* (mappability_tag.cpp:93-124) + smashMEM.py filters & global pair de-dup   */
@@ -226,6 +241,15 @@ typedef struct {
 /* The native row of a mate of read_len bases (bytes; a multiple of 16). */
 uint32_t smash_read_stride(uint32_t read_len);
 
+/* The largest cfg.max_pairs smash_pipeline_create accepts for mates of
+ * read_len bases: a batch's hit rows hold 2 * (read_len - min_len + 1) u64
+ * per pair, and the batch's position offsets and export word prefixes are
+ * 32-bit, so max_pairs * 2 * slots < 2^32 (16 393 004 pairs at 150 bp with
+ * min_len 20).  0 when read_len / min_len are out of range. */
+uint64_t smash_pipeline_max_batch(uint32_t read_len, uint32_t min_len);
+
+/* SMASH_ERR_ARG for a bad configuration, max_pairs above
+ * smash_pipeline_max_batch included (checked before the index is touched). */
 int smash_pipeline_create(const smash_index *ix, const smash_pipeline_cfg *cfg,
                           smash_pipeline **out);
 void smash_pipeline_free(smash_pipeline *p);

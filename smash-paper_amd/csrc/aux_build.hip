@@ -2,6 +2,7 @@
 // index (results-preserving; see mam_device.hpp):
 //
 //  U[x]  (u8, one per text position) = min(255, max(LCP[ISA[x]], LCP[ISA[x]+1]))
+//        (built from SA + L8 by uniq_build.hip)
 //        The suffix at x is alone in its SA interval at depth d iff U[x] < d
 //        (d <= 255).  This is what the reference's suffix-link chain
 //        (longSA.cpp:523-534 + expand_link, longSA.h:158-174) tests one step
@@ -21,18 +22,6 @@
 
 namespace smash {
 namespace {
-
-template <class IdxT>
-__global__ void k_uniq(const IdxT *__restrict__ ISA, const uint8_t *__restrict__ L8,
-                       uint64_t N, uint8_t *U) {
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x < N; x += stride) {
-    const uint64_t r = ISA[x];
-    const uint8_t a = L8[r];
-    const uint8_t b = r + 1 < N ? L8[r + 1] : 0;
-    U[x] = a > b ? a : b;
-  }
-}
 
 __device__ inline int acgt2(uint8_t c) {
   switch (c) {
@@ -126,8 +115,7 @@ void build_aux_t(smash_index *ix, hipStream_t s) {
   const uint64_t N = ix->N;
   if (!ix->d_uniq) ix->d_uniq = dalloc<uint8_t>(N + 64);
   SMASH_HIPX(hipMemsetAsync(ix->d_uniq + N, 0, 64, s));
-  k_uniq<IdxT><<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
-      static_cast<const IdxT *>(ix->d_isa), ix->d_lcp8, N, ix->d_uniq);
+  build_uniq_range(ix, 0, N, s);   // from SA + L8 (uniq_build.hip)
   // k: floor(log4 N) characters, <= 16 (about one suffix per k-mer: a root
   // descent lands on a singleton or a short run; hg19: 4^16 x 16 B = 69 GB)
   int K = 4;

@@ -134,6 +134,8 @@ uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, satu
 void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
 void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
 void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
+// U for text positions [lo, hi) from SA + L8 (uniq_build.hip; lo rounded down to 64)
+void build_uniq_range(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s);
 // mam.hip: smash_map_batch without the per-launch synchronisation of the
 // probe check (sync_check = false: the caller runs probe_check later)
 // caller-owned search workspace (the pipeline's double-buffered sets): the

@@ -40,6 +40,18 @@
 #ifndef SM_HOOK_BS
 #define SM_HOOK_BS(size, depth)   // host emulation: interval statistics
 #endif
+// host emulation: where the binary-search compares start and stop (offsets
+// from the probed suffix's start), and how far the L8 runs reach (kind 0:
+// expand_link after ISA loads, 1: the traverse's final run around an SA rank)
+#ifndef SM_HOOK_CMPBS
+#define SM_HOOK_CMPBS(begin, sp, off)
+#endif
+#ifndef SM_HOOK_RUN
+#define SM_HOOK_RUN(begin, kind, ext_l, ext_r)
+#endif
+#ifndef SM_HOOK_BYTE
+#define SM_HOOK_BYTE(pos)
+#endif
 #ifndef SM_LOAD16
 #define SM_LOAD16(a) ::smash::sm::load16u(a)
 #endif
@@ -650,6 +662,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // left blocks are the 16 bytes ENDING at es (from 0 when es < 15), right
   // blocks start at ee + 1
   auto bs_probe = [&]() {   // compare P' with T[sp + cbase + lc ...] (sp = SA[m])
+    SM_HOOK_CMPBS(true, sp, cbase + lc);
     addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
     need2 = c.pf && lo < m;
@@ -939,6 +952,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_BYTE: {                                 // is_leftmaximal: T[pos-1]
         SM_REGION(6);
+        SM_HOOK_BYTE(pos);
         if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
           if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
           ++nem;
@@ -972,6 +986,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           depth += lc; lc = 0;
           a = A_AFTER;
         } else {                                      // O_BS: probe m decided
+          SM_HOOK_CMPBS(false, sp, cbase + lc);
           need2 = false;
           bool left;                                  // keep [lo, m) (else (m, hi))
           if (bsm == BS_INSERT) {
@@ -1113,6 +1128,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         xd = depth + best; xrun = true;
         cbase = depth; cap = best;
         es = bi; ee = bi;
+        SM_HOOK_RUN(true, 1, 0, 0);
         a = ex_start(start, end) ? A_NONE : A_RUN_DONE;
       }
     }
@@ -1121,6 +1137,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       const uint64_t hb = xrun ? end : N - 1;
       nblk = 0;
       if (!xrun && start - es >= thresh) {            // expand_link gives up (longSA.h:164)
+        SM_HOOK_RUN(false, 0, start - es, 99);
         depth = 0; start = 0; end = N - 1; have_pos = false;
         a = A_TOP;
       } else if (ee < hb && !rdone) {
@@ -1133,6 +1150,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     if (a == A_RUN_DONE) {
       SM_REGION(13);
+      SM_HOOK_RUN(false, xrun ? 1 : 0, xrun ? bi - es : start - es, xrun ? ee - bi : ee - end);
       if (xrun) {                                     // traverse result
         start = es; end = ee; depth = xd; pos = bpos; have_pos = start == end;
         a = A_AFTER;
@@ -1165,6 +1183,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       xd = depth; xrun = false;
       cbase = 0; cap = depth;
       es = start; ee = end;
+      SM_HOOK_RUN(true, 0, 0, 0);
       a = ex_start(0, N - 1) ? A_NONE : A_RUN_DONE;
     }
     if (a == A_AFTER) {

@@ -47,10 +47,14 @@
 // the bin ordinal of each tile's first base comes from k_tilebins (one thread
 // per tile, all bisections in flight at once) instead of a 16-load bisection
 // on the block's critical path.
-#include "common.hpp"
+#include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <iterator>
+
+#include "common.hpp"
 
 namespace smash {
 namespace {
@@ -115,9 +119,10 @@ __device__ __forceinline__ uint32_t byte_of(const uint4 &v, uint32_t q) {
 // dir[t] = the first text position p in [t << 12, (t + 1) << 12) with
 // U[p] < 255, else kNone
 __global__ __launch_bounds__(kMB) void k_nsdir(const uint8_t *__restrict__ U, uint64_t N,
-                                               uint64_t *__restrict__ dir, uint64_t ndir) {
+                                               uint64_t *__restrict__ dir, uint64_t t0,
+                                               uint64_t t1) {
   __shared__ unsigned long long s_first;
-  for (uint64_t t = blockIdx.x; t < ndir; t += gridDim.x) {
+  for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
     if (threadIdx.x == 0) s_first = kNone;
     __syncthreads();
     const uint64_t p0 = (t << kDirShift) + uint64_t(threadIdx.x) * kMPer;
@@ -132,6 +137,47 @@ __global__ __launch_bounds__(kMB) void k_nsdir(const uint8_t *__restrict__ U, ui
     if (threadIdx.x == 0) dir[t] = s_first;
     __syncthreads();
   }
+}
+
+// dir[t] = min(dir[t], dir[t + 1], ...): the first unsaturated position at or
+// after tile t, from each tile's own first (a min scan of the reversed
+// directory on the device; entries already propagated are fixed points)
+hipError_t dir_suffix_min(uint64_t *dir, uint64_t ndir, hipStream_t s) {
+  uint64_t *tmp = nullptr;
+  void *tb = nullptr;
+  size_t nb = 0;
+  auto in = std::make_reverse_iterator(dir + ndir);
+  auto out = std::make_reverse_iterator(static_cast<uint64_t *>(nullptr) + ndir);
+  hipError_t e = hipcub::DeviceScan::InclusiveScan(nullptr, nb, in, out, hipcub::Min(), ndir, s);
+  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void **>(&tmp), 8 * ndir, s);
+  if (e == hipSuccess) e = hipMallocAsync(&tb, nb, s);
+  if (e == hipSuccess)
+    e = hipcub::DeviceScan::InclusiveScan(tb, nb, in, std::make_reverse_iterator(tmp + ndir),
+                                          hipcub::Min(), ndir, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(dir, tmp, 8 * ndir, hipMemcpyDeviceToDevice, s);
+  if (tmp) (void)hipFreeAsync(tmp, s);
+  if (tb) (void)hipFreeAsync(tb, s);
+  return e;
+}
+
+// the directory entries of text positions [lo, hi) from U, then propagated
+hipError_t build_nsdir(const smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
+  const uint64_t ndir = (ix->N + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
+  if (!ix->d_nsdir) {
+    hipError_t e = hipMalloc(&ix->d_nsdir, 8 * ndir);
+    if (e != hipSuccess) return e;
+    lo = 0;
+    hi = ix->N;
+  }
+  const uint64_t t0 = lo >> kDirShift;
+  const uint64_t t1 = std::min(ndir, (hi + (uint64_t(1) << kDirShift) - 1) >> kDirShift);
+  if (t0 < t1)
+    k_nsdir<<<unsigned(std::min<uint64_t>(t1 - t0, 65536)), kMB, 0, s>>>(ix->d_uniq, ix->N,
+                                                                      ix->d_nsdir, t0, t1);
+  hipError_t e = hipGetLastError();
+  // (the scan covers entry t1 too: a window tile without an unsaturated
+  // position takes the propagated entry after the window)
+  return e == hipSuccess ? dir_suffix_min(ix->d_nsdir, std::min(ndir, t1 + 1), s) : e;
 }
 
 // an unsaturated text position >= p (kNone: none before N): the first one
@@ -556,22 +602,11 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
     SMASH_HIP(hipMemsetAsync(c.nfix, 0, 8, s));
     c.fix_cap = kFixCap;
   }
-  // the directory of unsaturated U positions, once per index: first one per
-  // 4096 positions, then the suffix minimum (host side, 12 MB at hg19)
+  // the directory of unsaturated U positions, once per index (unless
+  // smash_mappability_prepare built it): first one per 4096 positions, then
+  // the suffix minimum (12 MB at hg19)
   const uint64_t ndir = (ix->N + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
-  if (!ix->d_nsdir) {
-    SMASH_HIP(hipMalloc(&ix->d_nsdir, 8 * ndir));
-    k_nsdir<<<unsigned(ndir < 65536 ? ndir : 65536), kMB, 0, s>>>(ix->d_uniq, ix->N, ix->d_nsdir,
-                                                                   ndir);
-    SMASH_HIP(hipGetLastError());
-    std::vector<uint64_t> h(ndir);
-    SMASH_HIP(hipMemcpyAsync(h.data(), ix->d_nsdir, 8 * ndir, hipMemcpyDeviceToHost, s));
-    SMASH_HIP(hipStreamSynchronize(s));
-    for (uint64_t t = ndir - 1; t-- > 0;)
-      if (h[t] == kNone) h[t] = h[t + 1];
-    SMASH_HIP(hipMemcpyAsync(ix->d_nsdir, h.data(), 8 * ndir, hipMemcpyHostToDevice, s));
-    SMASH_HIP(hipStreamSynchronize(s));   // h is a host local
-  }
+  if (!ix->d_nsdir) SMASH_HIP(build_nsdir(ix, 0, ix->N, s));
   // the register budget: 5 waves per SIMD (96 VGPRs, a few spilled) with
   // the U blocks loaded in their own trip beat the compiler's choice (3
   // waves at 150+ VGPRs) with them fetched a trip ahead: 6.9 vs 8.5 ms
@@ -699,4 +734,61 @@ extern "C" int smash_mappability_scan(const smash_index *ix, uint64_t begin, uin
                             d_bin_counts, d_contig_counts, s);
   return scan_t<uint64_t>(ix, begin, end, k, d_map_out, h_chrom_off, d_bin_starts, nbins,
                           d_bin_counts, d_contig_counts, s);
+}
+
+// The text window the scan of forward bases [begin, end) reads U in: every
+// contig piece's forward positions and their reverse-complement positions
+// (sp + 2S - i, longSA.cpp:667), with a 4 096-position margin (the scan's
+// neighbouring-chunk loads and directory tiles)
+static void scan_window(const smash_index *ix, uint64_t begin, uint64_t end, uint64_t *lo,
+                        uint64_t *hi) {
+  uint64_t a0 = ~0ull, b0 = 0, g0 = 0;
+  for (uint32_t q = 0; q < ix->n_seq; q += 2) {
+    const uint64_t S = ix->sizes[q], sp = ix->startpos[q];
+    const uint64_t a = begin > g0 ? begin - g0 : 0;
+    const uint64_t b = end < g0 + S ? end - g0 : S;
+    if (a < b && g0 < end) {
+      a0 = std::min(a0, sp + a);
+      b0 = std::max(b0, sp + 2 * S - a + 1);
+    }
+    g0 += S;
+  }
+  const uint64_t m = uint64_t(1) << kDirShift;
+  *lo = a0 == ~0ull ? 0 : (a0 > m ? a0 - m : 0);
+  *hi = a0 == ~0ull ? 0 : std::min(ix->N, b0 + m);
+}
+
+extern "C" int smash_mappability_prepare(const smash_index *ix, uint64_t begin, uint64_t end,
+                                         void *stream) {
+  if (!ix || end < begin || !ix->rcref || !ix->d_uniq) {
+    set_error("smash_mappability_prepare: bad arguments (or an index without -rcref / U)");
+    return SMASH_ERR_ARG;
+  }
+  uint64_t total = 0;
+  for (uint32_t q = 0; q < ix->n_seq; q += 2) total += ix->sizes[q];
+  if (end > total) {
+    set_error("smash_mappability_prepare: range past the last forward base");
+    return SMASH_ERR_ARG;
+  }
+  if (begin == end) return SMASH_OK;
+  SMASH_HIP(hipSetDevice(ix->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint64_t lo = 0, hi = 0;
+  scan_window(ix, begin, end, &lo, &hi);
+  try {
+    build_uniq_range(const_cast<smash_index *>(ix), lo, hi, s);
+  } catch (hip_failure &f) {
+    set_error(f.what);
+    return f.what.find("hipMalloc") != std::string::npos ? SMASH_ERR_NOMEM : SMASH_ERR_HIP;
+  }
+  SMASH_HIP(build_nsdir(ix, lo & ~uint64_t(63), hi, s));
+  return SMASH_OK;
+}
+
+extern "C" int smash_mappability_window(const smash_index *ix, uint64_t begin, uint64_t end,
+                                        uint64_t *lo, uint64_t *hi) {
+  if (!ix || !lo || !hi || end < begin) return SMASH_ERR_ARG;
+  scan_window(ix, begin, end, lo, hi);
+  *lo &= ~uint64_t(63);
+  return SMASH_OK;
 }

@@ -1290,7 +1290,7 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
       a.lp = x ? lps[x - 1] : -1;
       const uint4 *r = reinterpret_cast<const uint4 *>(hits + x * 2 * uint64_t(slots));
       a.h0 = r[0];
-      a.h1 = r[1];
+      if (slots > 1) a.h1 = r[1];   // (a one-slot row is 16 B: r[1] is the next pair's)
     }
     return a;
   };
@@ -1344,14 +1344,15 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     out[b0 + i] = (hc[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
 }
 
-// counts[b] += the blocks' partial counts of bin b (one thread per bin; the
-// only writer of counts after k_emit_bin_lds on the stream)
+// counts[b] += the blocks' partial counts of bin b (one thread per bin), as
+// an atomic: the caller's counts may be shared with other pipelines or
+// streams (at most nbins atomics per batch, none for an empty bin)
 __global__ void k_bin_reduce(const uint32_t *__restrict__ binpart, uint32_t blocks, uint32_t nbins,
                              unsigned long long *counts) {
   for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
     unsigned long long t = 0;
     for (uint32_t k = 0; k < blocks; ++k) t += binpart[uint64_t(k) * nbins + b];
-    if (t) counts[b] += t;
+    if (t) atomicAdd(&counts[b], t);
   }
 }
 
@@ -1427,12 +1428,19 @@ PostCfg post_cfg(const smash_pipeline *p) {
 
 using namespace smash;
 
+extern "C" uint64_t smash_pipeline_max_batch(uint32_t read_len, uint32_t min_len) {
+  if (read_len == 0 || read_len > 255 || min_len < 2 || read_len < min_len) return 0;
+  const uint64_t slots = read_len - min_len + 1;
+  return ((1ull << 32) - 1) / (2 * slots);
+}
+
 extern "C" int smash_pipeline_create(const smash_index *ix,
                                      const smash_pipeline_cfg *cfg,
                                      smash_pipeline **out) {
   if (!ix || !cfg || !out || cfg->read_len == 0 || cfg->read_len > 255 ||
       cfg->min_len < 2 || cfg->read_len < cfg->min_len || cfg->max_pairs == 0 ||
-      cfg->max_pairs > 0xFFFFFFFFull || cfg->n_contig * 2 != ix->n_seq ||
+      cfg->max_pairs > smash_pipeline_max_batch(cfg->read_len, cfg->min_len) ||
+      cfg->n_contig * 2 != ix->n_seq ||
       !cfg->h_tag_offsets || !cfg->h_small_chr || !cfg->h_chrom_off ||
       !cfg->h_bin_starts || cfg->nbins == 0) {
     set_error("smash_pipeline_create: bad configuration");
@@ -1569,12 +1577,14 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_prev = dalloc<int64_t>(2);
     p->d_lp = dalloc<int64_t>(P);
     p->d_lps = dalloc<int64_t>(P);
-    p->d_binpart = dalloc<uint32_t>(uint64_t(kBinBlocks) * (p->nbins ? p->nbins : 1));
     {
       const char *e = getenv("SMASH_FUSED_BIN");   // 0: k_emit + k_bin (A/B)
       p->fused_bin = !(e && e[0] == '0');
       const char *l = getenv("SMASH_BIN_LDS");   // profiles/r03/binlds: 1.39 vs 2.18 ms
-      p->bin_lds = !(l && l[0] == '0');
+      // (k_emit_bin_lds only where its parts fit: above kBinPartsMax parts,
+      // k_emit_bin with global atomics, and no per-block count buffer)
+      p->bin_lds = !(l && l[0] == '0') && p->fused_bin && bin_parts(p->nbins) <= kBinPartsMax;
+      if (p->bin_lds) p->d_binpart = dalloc<uint32_t>(uint64_t(kBinBlocks) * p->nbins);
       // SMASH_BIN_FLUSH (tests): k_emit_bin_lds's flush threshold, a power of
       // two in [2, 2^15] (default 2^15)
       const char *fl = getenv("SMASH_BIN_FLUSH");
@@ -1901,7 +1911,7 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
   const int64_t *prev = d_prev ? d_prev : p->d_prev;
   if (p->fused_bin) {
     const uint32_t parts = bin_parts(p->nbins);
-    if (n && p->bin_lds && parts <= kBinPartsMax) {
+    if (n && p->bin_lds) {   // (set only when parts <= kBinPartsMax)
       const uint32_t part = bin_part_size(p->nbins);
       const unsigned gx = unsigned(std::min<uint64_t>(kBinBlocks, (n + 1023) / 1024));
       const dim3 grid(gx, parts);
@@ -2030,7 +2040,10 @@ __device__ __forceinline__ uint64_t key_owner(uint64_t hi, int world) {
 //   words, packed as keys << 32 | words into bc[o * nblk + b] (owner-major).
 //   An exclusive scan of bc then gives every (owner, block) its offsets in the
 //   owner-major send buffer: the owner's segment start plus the blocks
-//   before it (words < 2^32 per batch: n * 2 * slots <= 1.7e9).
+//   before it.  Exact while a batch's words stay below 2^32: a pair exports
+//   at most 2 * slots words, and smash_pipeline_create refuses max_pairs *
+//   2 * slots >= 2^32 (smash_pipeline_max_batch; 16.39 M pairs at 150 bp,
+//   3.28e9 words at the bench's 12.5 M).
 // k_export_fill: the same per-block grouping, each lane's rank among its
 //   block's keys of the same owner (wave ballots, then the waves before it),
 //   and the scanned block offset: the header, the words and the pair index

@@ -60,7 +60,8 @@ EXPORTS = [
     "smash_phase_search_ahead",
     "smash_fastq_shard_scan", "smash_fastq_shard_free_blob", "smash_fastq_shard_open",
     "smash_fastq_shard_pack", "smash_fastq_shard_stats", "smash_fastq_shard_close",
-    "smash_read_stride",
+    "smash_read_stride", "smash_pipeline_max_batch",
+    "smash_mappability_prepare", "smash_mappability_window",
 ]
 
 
@@ -221,6 +222,10 @@ def lib():
     L.smash_fastq_shard_close.restype = None
     L.smash_read_stride.argtypes = [C.c_uint32]
     L.smash_read_stride.restype = C.c_uint32
+    L.smash_mappability_prepare.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
+    L.smash_mappability_window.argtypes = [vp, C.c_uint64, C.c_uint64, u64p, u64p]
+    L.smash_pipeline_max_batch.argtypes = [C.c_uint32, C.c_uint32]
+    L.smash_pipeline_max_batch.restype = C.c_uint64
     L.smash_count_fastq.argtypes = [vp, C.POINTER(C.c_char_p), C.c_uint32,
                                     C.POINTER(C.c_char_p), C.c_uint32, C.c_int, C.c_uint32, vp,
                                     C.POINTER(FeedStats), vp]
@@ -423,6 +428,12 @@ def read_stride(read_len):
     (smash_read_stride): batches laid out in such rows (16-byte aligned, zero
     padded) are searched without a record build"""
     return int(lib().smash_read_stride(read_len))
+
+
+def pipeline_max_batch(read_len, min_len=20):
+    """The largest batch (pairs) a Pipeline of read_len-base mates accepts:
+    max_pairs * 2 * (read_len - min_len + 1) < 2^32 (include/smash_gpu.h)."""
+    return int(lib().smash_pipeline_max_batch(read_len, min_len))
 
 
 def to_rows(d_reads, read_len=None):
@@ -697,6 +708,22 @@ def mappability_scan(index: Index, begin, end, k=36, d_map_out=None, chrom_off=N
                                        _ptr(d_bin_starts), nbins, _ptr(d_bin_counts),
                                        _ptr(d_contig_counts), vp(_stream(stream))),
           "smash_mappability_scan")
+
+
+def mappability_prepare(index: Index, begin, end, stream=None):
+    """C5's preparation from the index arrays (smash_mappability_prepare):
+    U and its directory for the scan of forward bases [begin, end), rebuilt
+    from SA + the LCP bytes, in place."""
+    check(lib().smash_mappability_prepare(index.h, begin, end, vp(_stream(stream))),
+          "smash_mappability_prepare")
+
+
+def mappability_window(index: Index, begin, end):
+    """the text window [lo, hi) mappability_prepare(begin, end) rebuilds"""
+    lo, hi = C.c_uint64(), C.c_uint64()
+    check(lib().smash_mappability_window(index.h, begin, end, C.byref(lo), C.byref(hi)),
+          "smash_mappability_window")
+    return int(lo.value), int(hi.value)
 
 
 def unpack_records(words, n, cap):

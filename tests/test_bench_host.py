@@ -29,3 +29,15 @@ def test_fit_batch_picks_the_largest_fitting_divisor():
         b = fit(12_500_000, P, L, free * GB)
         k = -(-P // b)
         assert b == -(-P // k)
+
+
+def test_fit_batch_respects_the_library_batch_bound():
+    """max_batch (smash_pipeline_max_batch: max_pairs * 2 * slots < 2^32)
+    caps the batch even when the HBM would hold a larger one."""
+    fit = _bench().fit_batch
+    GB = 1_000_000_000
+    P = 25_000_000
+    mb = ((1 << 32) - 1) // (2 * 231)          # 250 bp mates
+    b = fit(P, P, 250, 10_000 * GB, max_batch=mb)
+    assert b <= mb and b == -(-P // -(-P // b))
+    assert fit(12_500_000, P, 150, 10_000 * GB, max_batch=((1 << 32) - 1) // 262) == 12_500_000

@@ -238,11 +238,11 @@ def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, tmp_path):
 
 
 def test_c3_full_run_properties(hg19):
-    """The C3 run as stated, 25 M pairs (50 M mates) in 4 batches of 6.25 M
-    (the bench's split) with one key set and the adjacent-dup state carried: the
-    counts sum to ReadsKept, every pair is accounted for, and the same reads
-    in another batch split give the same counts (the oracle cannot run 50 M
-    reads here)."""
+    """The C3 run as stated, 25 M pairs (50 M mates) in 2 batches of 12.5 M
+    (the bench's split), and again in 4 of 6.25 M and 15 of 1.7 M, with one key
+    set and the adjacent-dup state carried: the counts sum to ReadsKept,
+    every pair is accounted for, and every batch split gives the same counts
+    and stats (the oracle cannot run 50 M reads here)."""
     contigs, _, dix = hg19
     cs = _chrom_sizes(contigs)
     src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
@@ -252,7 +252,8 @@ def test_c3_full_run_properties(hg19):
     g = readgen.Generator(dix, contigs, 150, seed=3)
     d_reads = g.generate(P)
     outs = []
-    for batch in (6_250_000, 1_700_000):
+    torch.cuda.empty_cache()
+    for batch in (12_500_000, 6_250_000, 1_700_000):
         pipe = S.Pipeline(dix, cs, starts, 150, batch, dedup_capacity=P)
         counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
         pipe.reset()
@@ -265,7 +266,8 @@ def test_c3_full_run_properties(hg19):
         assert st.positions == st.kept + st.dups
         outs.append((counts.cpu().numpy(), st.as_dict()))
         del pipe
-    assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+    for c, d in outs[1:]:
+        assert np.array_equal(outs[0][0], c) and outs[0][1] == d
 
 
 # ---------------------------------------------------------------------------
@@ -341,6 +343,51 @@ def test_c5_mappability_scan_full_genome(hg19, hg19_oracle):
         assert u == int(((r >= 1) & (r <= 36)).sum())
         n_uniq += u
     assert int(cc.sum().item()) == int(((dev[1::2] >= 1) & (dev[1::2] <= 36)).sum())
+
+
+def test_c5_prepare_rebuilds_u_full_genome(hg19, hg19_oracle, monkeypatch):
+    """C5 from the index arrays at full size (smash_mappability_prepare,
+    csrc/uniq_build.hip: 369 level-1 buckets in 12 chunks at hg19): U
+    poisoned and rebuilt from SA + L8 by the partition passes equals the
+    gather form's U (ISA -> L8, the definition) byte for byte, and the scan
+    over it equals the index build's map.bin (built from the exact LCP,
+    longSA.cpp:612-690); one rank's eighth (its own window only, the rest of U
+    poisoned) equals its slice."""
+    contigs, _, dix = hg19
+    oix, mp = hg19_oracle
+    total = int(sum(dix.contig_sizes))
+    N = dix.info.N
+    U = S.device_view(dix.info.d_uniq, N + 64, torch.uint8)
+    monkeypatch.setenv("SMASH_UNIQ_GATHER", "1")
+    S.mappability_prepare(dix, 0, total)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("SMASH_UNIQ_GATHER")
+    gathered = U[:N].clone()
+    U[:N].fill_(0x55)
+    S.mappability_prepare(dix, 0, total)
+    torch.cuda.synchronize()
+    assert torch.equal(U[:N], gathered)
+    del gathered
+    out = torch.empty(2 * total, dtype=torch.uint8, device="cuda")
+    S.mappability_scan(dix, 0, total, 36, out, None, None, 0, None, None)
+    want = torch.from_numpy(mp[2:]).cuda()
+    assert torch.equal(out, want)
+    keep = U[:N].clone()
+    try:
+        g0, g1 = total * 3 // 8, total * 4 // 8
+        lo, hi = S.mappability_window(dix, g0, g1)
+        assert hi - lo < N // 4
+        U[:N].fill_(0xAA)
+        S.mappability_prepare(dix, g0, g1)
+        part = torch.empty(2 * (g1 - g0), dtype=torch.uint8, device="cuda")
+        S.mappability_scan(dix, g0, g1, 36, part, None, None, 0, None, None)
+        torch.cuda.synchronize()
+        assert torch.equal(U[lo:hi], keep[lo:hi])
+        assert torch.equal(part, want[2 * g0:2 * g1])
+    finally:
+        U[:N].copy_(keep)
+        S.mappability_prepare(dix, 0, total)
+        torch.cuda.synchronize()
 
 
 # ---------------------------------------------------------------------------
@@ -534,20 +581,25 @@ def test_c4_real_driver_rccl_world1_equals_oracle(c4_run, c4_fastq, monkeypatch)
         tdist.destroy_process_group()
 
 
+@pytest.mark.timeout(900)
 def test_c3_production_batch_equals_oracle(hg19, hg19_oracle):
-    """C3 at the bench's production batch size: 6.6 M pairs of the bench's
+    """C3 at the bench's production batch size: 12.6 M pairs of the bench's
     workload (seed 3, 150 bp, sample_bins/50000) counted as bench.py counts a
-    run -- smash_count_batches_ready over batches of 6.25 M pairs, one key set
-    and the adjacent-dup state carried into the second, short batch -- equal
-    the oracle's whole chain over the same 13.2 M reads (smashMEM.py:147-228,
-    varbin.py:52-92).  ~2 minutes of oracle time on 16 threads."""
+    run -- smash_count_batches_ready over batches of 12.5 M pairs (the
+    bench's fit_batch choice on one GPU: 3.28e9 hit words per batch, within
+    smash_pipeline_max_batch's 2^32 bound), one key set and the adjacent-dup
+    state carried into the second, short batch -- equal the oracle's whole
+    chain over the same 25.2 M reads (smashMEM.py:147-228, varbin.py:52-92).
+    ~4 minutes of oracle time on 16 threads."""
     import readgen
     contigs, _, dix = hg19
     oix, mp = hg19_oracle
     cs = _chrom_sizes(contigs)
     src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
     starts = np.array([int(l.split("\t")[2]) for l in open(src)], np.int64)
-    P, B = 6_600_000, 6_250_000
+    P, B = 12_600_000, 12_500_000
+    assert B <= S.pipeline_max_batch(150)
+    torch.cuda.empty_cache()
     d_reads = readgen.Generator(dix, contigs, 150, seed=3000).generate(P)
     pipe = S.Pipeline(dix, cs, starts, 150, B, dedup_capacity=P + P // 8 + (1 << 20))
     counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")

@@ -116,3 +116,65 @@ def test_mid_scan_any_partition(mid, parts):
         bc = bc + b1
     assert np.array_equal(np.concatenate(maps), full)
     assert np.array_equal(cc, fcc) and np.array_equal(bc, fbc)
+
+
+def host_uniq(oix):
+    """U[x] = min(255, max(LCP[ISA[x]], LCP[ISA[x] + 1])) on the host from the
+    oracle's own index (longSA.cpp:628-641 before the +1 and the edge rules)"""
+    L8 = oix.L8.astype(np.int64)
+    Lp = np.append(L8[1:], 0)
+    isa = oix.ISA.astype(np.int64)
+    return np.maximum(L8[isa], Lp[isa]).astype(np.uint8)
+
+
+@pytest.mark.parametrize("form", ["partition", "gather"])
+def test_prepare_rebuilds_u_from_the_suffix_array(mid, form, monkeypatch):
+    """smash_mappability_prepare (C5's preparation from SA + L8,
+    csrc/uniq_build.hip): U poisoned on the device, rebuilt for the whole
+    genome, equals the host's U from the oracle's ISA + LCP, and the scan over
+    it equals the oracle's map.bin (longSA.cpp:612-690); SMASH_UNIQ_GATHER=1
+    runs the gather form for A/B."""
+    oix, dix, off, starts = mid
+    if form == "gather":
+        monkeypatch.setenv("SMASH_UNIQ_GATHER", "1")
+    N = dix.info.N
+    U = S.device_view(dix.info.d_uniq, N + 64, torch.uint8)
+    want = host_uniq(oix)
+    assert np.array_equal(U[:N].cpu().numpy(), want)     # the index build's
+    U[:N].fill_(0x55)
+    total = sum(dix.contig_sizes)
+    S.mappability_prepare(dix, 0, total)
+    torch.cuda.synchronize()
+    assert np.array_equal(U[:N].cpu().numpy(), want)
+    mp, _, _ = scan(dix, 0, total, 36, off, starts)
+    assert np.array_equal(mp, oix.mappability()[2:])
+
+
+@pytest.mark.parametrize("parts", [3, 8])
+def test_prepare_per_partition(mid, parts):
+    """Each part of a partition of the forward bases (a rank's share of C5)
+    rebuilds only its window (its forward and reverse-complement positions)
+    and scans it: poisoned U outside the rebuilt windows is never read, the
+    concatenated maps equal the oracle's."""
+    oix, dix, off, starts = mid
+    total = sum(dix.contig_sizes)
+    N = dix.info.N
+    U = S.device_view(dix.info.d_uniq, N + 64, torch.uint8)
+    want = torch.from_numpy(host_uniq(oix)).cuda()
+    rng = np.random.default_rng(100 + parts)
+    cuts = [0] + sorted(int(x) for x in rng.integers(1, total, parts - 1)) + [total]
+    omap = oix.mappability()[2:]
+    try:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            lo, hi = S.mappability_window(dix, a, b)
+            assert 0 <= lo < hi <= N
+            U[:N].fill_(0xAA)
+            S.mappability_prepare(dix, a, b)
+            torch.cuda.synchronize()
+            assert torch.equal(U[lo:hi], want[lo:hi]), (a, b, lo, hi)
+            m, _, _ = scan(dix, a, b, 36, off, starts)
+            assert np.array_equal(m, omap[2 * a:2 * b]), (a, b)
+    finally:
+        U[:N].copy_(want)
+        S.mappability_prepare(dix, 0, total)   # (the directory too)
+        torch.cuda.synchronize()

@@ -113,3 +113,32 @@ def test_fasta_forward_layout_edge_cases(tmp_path):
         assert T0.tobytes() == want, c
         assert n0 == n1[0::2] and list(sz0) == list(sz1[0::2])
         assert list(sp0) == [sum(len(f) + 1 for f in fw[:k]) for k in range(len(fw))]
+
+
+def test_pipeline_refuses_batches_past_the_32bit_word_bound():
+    """max_pairs * 2 * slots must stay below 2^32 (the batch's u32 position
+    offsets and the export's packed keys << 32 | words prefix,
+    csrc/pipeline.hip k_export_count): smash_pipeline_create refuses a larger
+    batch with SMASH_ERR_ARG before it touches the index or the device."""
+    import ctypes as C
+    assert S.pipeline_max_batch(150, 20) == ((1 << 32) - 1) // (2 * 131) == 16_393_004
+    assert S.pipeline_max_batch(100, 20) == ((1 << 32) - 1) // (2 * 81)
+    assert S.pipeline_max_batch(255, 20) == ((1 << 32) - 1) // (2 * 236)
+    assert S.pipeline_max_batch(19, 20) == 0 and S.pipeline_max_batch(256, 20) == 0
+    assert 12_500_000 <= S.pipeline_max_batch(150, 20)   # the bench's C3 batch fits
+
+    class FakeIndex:   # never dereferenced past the size check
+        buf = C.create_string_buffer(4096)
+        h = C.cast(buf, C.c_void_p)
+        contigs = ["chr1", "chr2"]
+        contig_sizes = [1000, 1000]
+
+    starts = np.array([0, 500, 1000], np.int64)
+    for L, B in ((150, 16_393_005), (150, 25_000_000), (250, 12_500_000)):
+        assert B > S.pipeline_max_batch(L, 20)
+        try:
+            S.Pipeline(FakeIndex(), {"chr1": 0, "chr2": 1000}, starts, L, B)
+        except S.SmashError as e:
+            assert "(-1)" in str(e) and "bad configuration" in str(e), e
+        else:
+            raise AssertionError("batch of %d pairs at %d bp accepted" % (B, L))

@@ -137,6 +137,39 @@ static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16], emu_f[16 * 8];
 #define SM_HOOK_F(j, bits) (++emu_f[8 * ((j) < 16 ? (j) : 15) + (bits)])
 #define SM_HOOK_BS(size, depth) \
   do { ++emu_bs_size[(size) < 64 ? (size) : 64]; ++emu_bs_depth[(depth) < 255 ? (depth) : 255]; } while (0)
+// opportunity statistics (tools/emu_profile.py --opp): [off0][stop] of every
+// binary-search compare, weighted by the text lines it cost; L8 runs by
+// (kind, left extension, right extension), weighted by all lines they cost
+static uint64_t emu_cmp_n[64 * 64], emu_cmp_lines[64 * 64], emu_cmp_off0, emu_cmp_l0;
+static uint64_t emu_run_n[2 * 10 * 10], emu_run_lines[2 * 10 * 10], emu_run_l0[2];
+static uint64_t emu_byte_n, emu_byte_other;
+static const uint8_t *emu_T;
+static uint64_t emu_lines_all() {
+  uint64_t t = 0;
+  for (int k = 0; k < 8; ++k) t += emu_lines[k];
+  return t;
+}
+static void emu_hook_cmpbs(bool begin, uint64_t sp, uint64_t off) {
+  (void)sp;
+  if (begin) { emu_cmp_off0 = off; emu_cmp_l0 = emu_lines[0]; return; }
+  const uint64_t a = emu_cmp_off0 < 63 ? emu_cmp_off0 : 63, b = off < 63 ? off : 63;
+  emu_cmp_n[64 * a + b] += 1;
+  emu_cmp_lines[64 * a + b] += emu_lines[0] - emu_cmp_l0;
+}
+static void emu_hook_run(bool begin, int kind, uint64_t el, uint64_t er) {
+  if (begin) { emu_run_l0[kind] = emu_lines_all(); return; }
+  const uint64_t a = el < 9 ? el : 9, b = er < 9 ? er : 9;
+  emu_run_n[100 * kind + 10 * a + b] += 1;
+  emu_run_lines[100 * kind + 10 * a + b] += emu_lines_all() - emu_run_l0[kind];
+}
+static void emu_hook_byte(uint64_t pos) {
+  ++emu_byte_n;
+  const uint8_t ch = emu_T[pos - 1];
+  if (ch != 'a' && ch != 'c' && ch != 'g' && ch != 't') ++emu_byte_other;
+}
+#define SM_HOOK_CMPBS(begin, sp, off) emu_hook_cmpbs(begin, sp, off)
+#define SM_HOOK_RUN(begin, kind, el, er) emu_hook_run(begin, kind, el, er)
+#define SM_HOOK_BYTE(pos) emu_hook_byte(pos)
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
 
 thread_local dim3 threadIdx, blockIdx, blockDim;
@@ -222,6 +255,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
     return -1;
   threadIdx.x = 0;
   sm::Ctx<IdxT> c;
+  emu_T = T;
   c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);
   c.L8 = L8; c.U = U; c.KT = KT;
   (void)BM;   // (round 3: the filter's presence bits live in KT)
@@ -282,6 +316,22 @@ extern "C" void sm_emu_bs_hist(uint64_t *size, uint64_t *depth, int reset) {
   for (int k = 0; k < 65; ++k) { size[k] = emu_bs_size[k]; if (reset) emu_bs_size[k] = 0; }
   for (int k = 0; k < 256; ++k) { depth[k] = emu_bs_depth[k]; if (reset) emu_bs_depth[k] = 0; }
   for (int k = 0; k < 12; ++k) { depth[244 + k] = emu_bm[k]; if (reset) emu_bm[k] = 0; }
+}
+
+// the opportunity statistics since the last reset: cmp_n[4096], cmp_lines[4096],
+// run_n[200], run_lines[200], byte[2]
+extern "C" void sm_emu_opp(uint64_t *cmp_n, uint64_t *cmp_lines, uint64_t *run_n,
+                           uint64_t *run_lines, uint64_t *byte, int reset) {
+  for (int k = 0; k < 4096; ++k) {
+    cmp_n[k] = emu_cmp_n[k]; cmp_lines[k] = emu_cmp_lines[k];
+    if (reset) emu_cmp_n[k] = emu_cmp_lines[k] = 0;
+  }
+  for (int k = 0; k < 200; ++k) {
+    run_n[k] = emu_run_n[k]; run_lines[k] = emu_run_lines[k];
+    if (reset) emu_run_n[k] = emu_run_lines[k] = 0;
+  }
+  byte[0] = emu_byte_n; byte[1] = emu_byte_other;
+  if (reset) emu_byte_n = emu_byte_other = 0;
 }
 
 extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int idx_bytes,
