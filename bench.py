@@ -155,13 +155,15 @@ def host_index(S, O, dix, T, sp, sz, names, sample_reads=None):
     (what the host emulation of the kernel looks up)."""
     i = dix.info
     N = i.N
-    dt = np.uint32 if i.idx_bytes == 4 else np.uint64
-    SA = S.download(i.d_sa, N * i.idx_bytes, dt)
-    ISA = S.download(i.d_isa, N * i.idx_bytes, dt)
+    # SA / ISA as the device holds them: with packed index words (hg19) the
+    # oracle reads their element bits (pos_mask), the emulation of k_mam_sm
+    # their hints too
+    SA, ISA = dix.download_sa_isa(plain=False)
     L8 = S.download(i.d_lcp8, N)
     ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
     mp = S.download(i.d_map, i.map_bytes)
-    oix = O.Index(T, sp, sz, names, SA=SA, ISA=ISA, L8=L8, ovf=ovf)
+    oix = O.Index(T, sp, sz, names, SA=SA, ISA=ISA, L8=L8, ovf=ovf,
+                  pos_mask=dix.pos_mask if i.pos_bits else None)
     U = S.download(i.d_uniq, N + 64)
     KT = np.zeros(2 << (2 * i.kmer_k), np.uint64)          # calloc: pages on first touch
     if sample_reads is not None:
@@ -333,6 +335,8 @@ def bench_c5(args, cfg, world, rank, local, dist):
              "scaling": r.pop("scaling"), "vs_baseline": None, "dtype": "u8/u64 (integer)",
              "data": "synthetic (tools/synth.py hg19-shaped genome)",
              "config": {"workload": cfg["workload"], "genome": cfg["genome"],
+                   "index_words": "packed (SA / ISA hints, DESIGN section 3)"
+                                  if dix.info.pos_bits else "plain",
                         "bases": r.pop("bases"), "k": r.pop("k"), "bins": r.pop("bins"),
                         "parallelism": "%d contiguous base ranges, all_reduce counts" % world}}
     out_j.update(r)
@@ -668,6 +672,8 @@ def main():
         "data": "synthetic (tools/synth.py hg19-shaped genome; SMASH reads generated on the "
                 "device, tools/readgen.hip, seeded)",
         "config": {"workload": cfg["workload"], "genome": cfg["genome"],
+                   "index_words": "packed (SA / ISA hints, DESIGN section 3)"
+                                  if dix.info.pos_bits else "plain",
                    "genome_bp": int(sum(len(s) for _, s in contigs)),
                    "text_N": int(dix.info.N), "pairs_per_rank": P, "read_len": L,
                    "reads_per_step": 2 * P * world, "batch_pairs": B, "batches_per_step": nb,
@@ -698,7 +704,7 @@ def main():
         # on the host (tools/sm_emu: the same source, one lane) over this
         # index and a sample of the same reads
         import sm_emu
-        emu = sm_emu.Emu(oix, copy=False)
+        emu = sm_emu.Emu(oix, copy=False, packed=bool(dix.info.pos_bits))
         _, emu_it = emu.map(sample)
         lines = sum(v[1] for v in emu.counters.values())
         b_read = 64.0 * lines / ns

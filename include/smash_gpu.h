@@ -116,8 +116,8 @@ typedef struct {
   uint64_t n_lcp_overflow; /* entries with LCP >= 255 */
   uint64_t map_bytes;      /* 2 + 2 * sum(forward contig sizes) */
   const uint8_t *d_text;   /* N + 64 bytes (zero padded) */
-  const void *d_sa;        /* N x idx_bytes */
-  const void *d_isa;       /* N x idx_bytes */
+  const void *d_sa;        /* N x idx_bytes (pos_bits: positions in the low bits) */
+  const void *d_isa;       /* N x idx_bytes (pos_bits: ranks in the low bits) */
   const uint8_t *d_lcp8;   /* N, min(LCP,255) */
   const uint64_t *d_lcp_ovf; /* n_lcp_overflow x {idx, val} sorted by idx */
   const uint8_t *d_map;    /* map.bin image */
@@ -136,9 +136,20 @@ typedef struct {
   const uint64_t *d_bitmap;/* NULL (round 3: the presence bits are in d_kmer) */
   uint64_t in_text[4];     /* 256-bit set of bytes occurring in the text */
   uint32_t rcref;          /* 1: c ` rc(c) layout; 0: forward only, no map.bin */
-  uint32_t reserved;
+  uint32_t pos_bits;       /* 0: plain SA / ISA elements; 33: 8-byte elements
+                              whose bits 33..63 hold the search's hints (DESIGN
+                              section 3, packed index words): the element is
+                              its low 33 bits.  smash_index_save writes plain
+                              elements either way (SMASH_PACK_IDX=0 at create /
+                              load: never packed) */
 } smash_index_info;
 int smash_index_query(const smash_index *ix, smash_index_info *out);
+/* Packed index words: pack != 0 puts the search's hints
+ * into the high bits of the 8-byte SA / ISA elements (what create / load do
+ * by default when N < 2^33), 0 strips them.  Results never change; the
+ * search reads fewer random lines with them.  A no-op for 4-byte elements.
+ * Synchronous; no search may run on the index meanwhile. */
+int smash_index_pack(smash_index *ix, int pack, void *stream);
 
 /* ========================================================================== */
 /* Search: replaces longSA::MAM(Aligner&) (longSA.cpp:503-536) for a batch   */

@@ -30,7 +30,8 @@ class OrcIndex(C.Structure):
     _fields_ = [("N", C.c_uint64), ("logN", C.c_uint64), ("T", u8p),
                 ("SA", C.c_void_p), ("ISA", C.c_void_p), ("idx_bytes", C.c_uint32),
                 ("L8", u8p), ("ovf", u64p), ("n_ovf", C.c_uint64),
-                ("n_seq", C.c_uint32), ("startpos", u64p), ("sizes", u64p)]
+                ("n_seq", C.c_uint32), ("startpos", u64p), ("sizes", u64p),
+                ("pos_mask", C.c_uint64)]
 
 
 class OrcCounters(C.Structure):
@@ -209,7 +210,7 @@ class Index:
     unless arrays are given (e.g. downloaded from the device)."""
 
     def __init__(self, T, startpos, sizes, names, SA=None, ISA=None, LCP=None,
-                 L8=None, ovf=None, padded_text=False):
+                 L8=None, ovf=None, padded_text=False, pos_mask=None):
         N = len(T) - (64 if padded_text else 0)
         if padded_text:
             self.T = T
@@ -240,7 +241,10 @@ class Index:
                           self.SA.itemsize, _p(self.L8, u8p),
                           _p(self.ovf, u64p) if len(self.ovf) else None,
                           len(self.ovf), len(self.startpos),
-                          _p(self.startpos, u64p), _p(self.sizes, u64p))
+                          _p(self.startpos, u64p), _p(self.sizes, u64p), pos_mask or 0)
+        # SA / ISA as given may be the device's packed words: the oracle reads
+        # their element bits only (pos_mask), the emulator their hints too
+        self.pos_mask = pos_mask
 
     @property
     def LCP(self):

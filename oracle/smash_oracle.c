@@ -227,8 +227,9 @@ typedef struct {
   uint32_t isz;      /* element bytes of SA/ISA */
 } ctx_t;
 
-static inline uint64_t idx_at(const void *a, uint32_t isz, uint64_t k) {
-  return isz == 4 ? ((const uint32_t *)a)[k] : ((const uint64_t *)a)[k];
+static inline uint64_t idx_at(const orc_index *ix, const void *a, uint32_t isz, uint64_t k) {
+  const uint64_t m = ix->pos_mask ? ix->pos_mask : ~(uint64_t)0;
+  return (isz == 4 ? ((const uint32_t *)a)[k] : ((const uint64_t *)a)[k]) & m;
 }
 
 /* vec_uchar::operator[] (longSA.h:34-39) */
@@ -252,11 +253,11 @@ static inline void tick(uint64_t *loads, uint64_t *lines, uint64_t *last,
 }
 static inline uint64_t SAat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->sa_loads, &x->c->sa_lines, &x->c->last_sa, k * x->isz);
-  return idx_at(x->ix->SA, x->isz, k);
+  return idx_at(x->ix, x->ix->SA, x->isz, k);
 }
 static inline uint64_t ISAat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->isa_loads, &x->c->isa_lines, &x->c->last_isa, k * x->isz);
-  return idx_at(x->ix->ISA, x->isz, k);
+  return idx_at(x->ix, x->ix->ISA, x->isz, k);
 }
 static inline int64_t Tat(const ctx_t *x, uint64_t k) {
   if (x->c) tick(&x->c->ref_loads, &x->c->ref_lines, &x->c->last_ref, k);
@@ -708,8 +709,8 @@ int orc_mappability(const orc_index *ix, uint8_t *out) {
   for (uint32_t chrom = 0; chrom < ix->n_seq; chrom += 2) {
     const uint64_t sp = ix->startpos[chrom], sz = ix->sizes[chrom];
     for (uint64_t i = 0; i < sz; ++i) {
-      const uint64_t sapos = idx_at(ix->ISA, ix->idx_bytes, i + sp);
-      const uint64_t rcsapos = idx_at(ix->ISA, ix->idx_bytes, sp + 2 * sz - i);
+      const uint64_t sapos = idx_at(ix, ix->ISA, ix->idx_bytes, i + sp);
+      const uint64_t rcsapos = idx_at(ix, ix->ISA, ix->idx_bytes, sp + 2 * sz - i);
       if (ml[sapos] + i >= sz) ml[sapos] = 0;
       if (ml[rcsapos] >= i) ml[rcsapos] = 0;
       out[w++] = (uint8_t)(ml[rcsapos] < 255 ? ml[rcsapos] : 255);
@@ -733,8 +734,8 @@ uint64_t orc_mappability_range(const orc_index *ix, uint64_t g0, uint64_t g1,
     const uint64_t sp = ix->startpos[chrom], sz = ix->sizes[chrom];
     const uint64_t a = g0 > g ? g0 - g : 0, b = g1 < g + sz ? g1 - g : sz;
     for (uint64_t i = a; i < b; ++i) {
-      const uint64_t sapos = idx_at(ix->ISA, ix->idx_bytes, i + sp);
-      const uint64_t rcsapos = idx_at(ix->ISA, ix->idx_bytes, sp + 2 * sz - i);
+      const uint64_t sapos = idx_at(ix, ix->ISA, ix->idx_bytes, i + sp);
+      const uint64_t rcsapos = idx_at(ix, ix->ISA, ix->idx_bytes, sp + 2 * sz - i);
       uint64_t right = min_len_at(ix, sapos), left = min_len_at(ix, rcsapos);
       if (right + i >= sz) right = 0;                  /* :666 */
       if (left >= i) left = 0;                         /* :667 */
@@ -1084,7 +1085,7 @@ void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT) 
   const uint64_t N = ix->N;
   const uint32_t isz = ix->idx_bytes == 4 ? 4 : 8;
   for (uint64_t x = 0; x < N; ++x) {
-    const uint64_t r = idx_at(ix->ISA, isz, x);
+    const uint64_t r = idx_at(ix, ix->ISA, isz, x);
     const uint8_t a = ix->L8[r], b = r + 1 < N ? ix->L8[r + 1] : 0;
     U[x] = a > b ? a : b;
   }
@@ -1093,7 +1094,7 @@ void orc_build_accel(const orc_index *ix, uint32_t K, uint8_t *U, uint64_t *KT) 
   for (uint64_t w = 0; w < nk; ++w) { KT[2 * w] = 1; KT[2 * w + 1] = 0; }
   uint64_t prev = ~0ull;
   for (uint64_t r = 0; r < N; ++r) {
-    const uint64_t x = idx_at(ix->SA, isz, r);
+    const uint64_t x = idx_at(ix, ix->SA, isz, r);
     uint64_t code = 0;
     int ok = x + K <= N;
     for (uint32_t k = 0; ok && k < K; ++k) {

@@ -62,6 +62,10 @@ typedef struct {
   uint64_t n_ovf;
   uint32_t n_seq;
   const uint64_t *startpos, *sizes;
+  /* element bits of an SA / ISA word: ~0, or 2^33 - 1 for the device's
+   * packed words (smash-paper_amd/csrc/common.hpp), whose high bits hold the
+   * search's hints (0 is read as ~0) */
+  uint64_t pos_mask;
 } orc_index;
 /* logN = ceil(log(N)/log(2.0)) (longSA.cpp:97) */
 uint64_t orc_logN(uint64_t N);

@@ -79,6 +79,34 @@ inline uint64_t ceil_log2(uint64_t n) {
   return b;
 }
 
+// Packed index words (round 5, pack_index.hip): a 64-bit SA / ISA element
+// needs 33 bits at hg19 (N < 2^33); the search keeps hints for its next
+// probes in the other 31, so they come with the element it loads anyway:
+//   SA[r]  bits  0..32  the text position x = SA[r]
+//                33..35 tag: 0..3 = T[x - 1] (a c g t, the BWT character, for
+//                       is_leftmaximal) and the window below is exact;
+//                       4 = T[x - 1] another byte (or x = 0), window exact;
+//                       5 = the window holds a byte other than a c g t
+//                36..42 min(L8[r], 127)       43..49 min(L8[r + 1], 127)
+//                50..63 T[x + K .. x + K + 7), 2 bits per base (a0 c1 g2 t3,
+//                       base i at bit 50 + 2i; K = the k-mer table's k)
+//   ISA[x] bits  0..32  the rank r = ISA[x]
+//                33..39 min(L8[r - 1], 127)   40..46 min(L8[r], 127)
+//                47..53 min(L8[r + 1], 127)   54..60 min(L8[r + 2], 127)
+// (L8 bytes outside [0, N) are 0).  A capped 127 compares exactly with any
+// depth <= 127; every other reader masks the position bits (IdxArr).
+constexpr uint32_t kPkPosBits = 33;
+constexpr uint64_t kPkPosMask = (uint64_t(1) << kPkPosBits) - 1;
+constexpr uint32_t kPkWindow = 7;   // bases in the SA word
+
+// SA / ISA read through the position mask (~0 for a plain index)
+template <class IdxT>
+struct IdxArr {
+  const IdxT *p;
+  uint64_t mask;
+  __host__ __device__ uint64_t operator[](uint64_t i) const { return uint64_t(p[i]) & mask; }
+};
+
 // Packed match (smash_gpu.h): ref 48 | qoff 8 | len 8
 __host__ __device__ inline uint64_t pack_match(uint64_t ref, uint32_t q,
                                                uint32_t len) {
@@ -106,6 +134,7 @@ struct smash_index {
   uint64_t n_ovf = 0;
   uint8_t *d_map = nullptr;
   uint64_t map_bytes = 0;
+  uint64_t pos_mask = ~0ull;     // kPkPosMask when SA / ISA carry packed hints (pack_index.hip)
   uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
   mutable uint64_t *d_nsdir = nullptr;   // first U < 255 per 4096 positions (mappability.hip)
   uint64_t *d_kmer = nullptr;    // per k-mer: {lo,hi} + (k+2)-mer presence bits (kt_filter)
@@ -134,6 +163,9 @@ uint32_t *build_lcp32(smash_index *ix, hipStream_t s);   // exact LCP (u32, satu
 void finish_lcp(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);  // lcp8 + ovf
 void build_map(smash_index *ix, const uint32_t *d_lcp32, hipStream_t s);   // map.bin
 void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.hip)
+// the packed SA / ISA hints (pack_index.hip; after every build step that reads
+// SA or ISA); pack = false: strip them (plain words)
+void pack_index(smash_index *ix, bool pack, hipStream_t s);
 // U for text positions [lo, hi) from SA + L8 (uniq_build.hip; lo rounded down to 64)
 void build_uniq_range(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s);
 // mam.hip: smash_map_batch without the per-launch synchronisation of the

@@ -159,6 +159,7 @@ extern "C" int smash_index_create_layout(const uint8_t *h_text, uint64_t N,
     SMASH_HIPX(hipStreamSynchronize(s));
     dfree(lcp);
     build_aux(ix.get(), s);
+    pack_index(ix.get(), true, s);   // (after every build step that reads SA / ISA)
     SMASH_HIPX(hipStreamSynchronize(s));
     SMASH_HIPX(hipStreamDestroy(s));
     ix->build_seconds = now_s() - t0;
@@ -292,6 +293,7 @@ extern "C" int smash_index_load_layout(const char *fasta_path, int rcref, int de
     }
     SMASH_HIPX(hipStreamSynchronize(s));
     build_aux(ix.get(), s);
+    pack_index(ix.get(), true, s);
     SMASH_HIPX(hipStreamSynchronize(s));
     SMASH_HIPX(hipStreamDestroy(s));
     ix->build_seconds = now_s() - t0;
@@ -353,6 +355,10 @@ extern "C" int smash_index_save(const smash_index *ix, const char *fasta_path,
     for (int which = 0; which < 2; ++which) {
       std::vector<uint8_t> a(N * ix->idx_bytes);
       SMASH_HIPX(hipMemcpy(a.data(), which ? ix->d_isa : ix->d_sa, a.size(), hipMemcpyDeviceToHost));
+      if (ix->idx_bytes == 8 && ix->pos_mask != ~0ull) {   // the reference's plain elements
+        uint64_t *w = reinterpret_cast<uint64_t *>(a.data());
+        for (uint64_t i = 0; i < N; ++i) w[i] &= ix->pos_mask;
+      }
       if (uint32_t(W) != ix->idx_bytes) {  // widen u32 -> u64
         std::vector<uint64_t> w(N);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(a.data());
@@ -400,6 +406,7 @@ extern "C" int smash_index_query(const smash_index *ix, smash_index_info *o) {
   o->idx_bytes = ix->idx_bytes;
   o->n_seq = ix->n_seq;
   o->rcref = ix->rcref ? 1 : 0;
+  o->pos_bits = ix->pos_mask == kPkPosMask ? kPkPosBits : 0;
   o->n_lcp_overflow = ix->n_ovf;
   o->map_bytes = ix->map_bytes;
   o->d_text = ix->d_text;

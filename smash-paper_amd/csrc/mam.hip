@@ -208,7 +208,11 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   if (ws && ws->gate) SMASH_HIP(hipStreamWaitEvent(s, ws->gate, 0));
   sm::Ctx<IdxT> c;
   const DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
-  c.T = x.T; c.SA = x.SA; c.ISA = x.ISA; c.L8 = x.L8; c.U = x.U; c.KT = x.KT;
+  c.T = x.T; c.SA = x.SA.p; c.ISA = x.ISA.p; c.L8 = x.L8; c.U = x.U; c.KT = x.KT;
+  // packed SA / ISA words (pack_index.hip): the search reads their hints
+  c.pm = ix->pos_mask;
+  c.pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask ? 1u : 0u;
+  if (const char *e = std::getenv("SMASH_SM_PK")) c.pk = c.pk && std::atoi(e) != 0;
   c.N = x.N; c.logN = uint32_t(x.logN); c.K = uint32_t(x.K); c.B = uint32_t(x.B);
   c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(rec);

@@ -12,8 +12,8 @@ namespace smash {
 template <class IdxT>
 struct DevIndex {
   const uint8_t *T;     // text (+64 zero bytes)
-  const IdxT *SA;
-  const IdxT *ISA;
+  IdxArr<IdxT> SA;      // positions only (the packed hints masked off)
+  IdxArr<IdxT> ISA;
   const uint8_t *L8;    // min(LCP,255)
   const uint8_t *U;     // per-position unique-length bytes (aux_build.hip)
   const uint64_t *KT;   // k-mer -> {lo, hi} + (k+2)-mer presence bits (common.hpp)
@@ -26,8 +26,8 @@ template <class IdxT>
 inline DevIndex<IdxT> make_dev_index(const smash_index *ix) {
   DevIndex<IdxT> x;
   x.T = ix->d_text;
-  x.SA = static_cast<const IdxT *>(ix->d_sa);
-  x.ISA = static_cast<const IdxT *>(ix->d_isa);
+  x.SA = IdxArr<IdxT>{static_cast<const IdxT *>(ix->d_sa), ix->pos_mask};
+  x.ISA = IdxArr<IdxT>{static_cast<const IdxT *>(ix->d_isa), ix->pos_mask};
   x.L8 = ix->d_lcp8;
   x.U = ix->d_uniq;
   x.KT = ix->d_kmer;

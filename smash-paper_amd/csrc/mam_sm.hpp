@@ -486,6 +486,8 @@ struct Ctx {
   // the index (DevIndex fields, flattened: every field is a live SGPR)
   const uint8_t *T;
   const IdxT *SA, *ISA;
+  uint64_t pm;            // position bits of an SA / ISA word (common.hpp kPkPosMask, or ~0)
+  uint32_t pk;            // the words carry the packed hints (common.hpp): 0 / 1
   const uint8_t *L8, *U;
   const uint64_t *KT;     // k-mer table: {lo, hi} + (k+2)-mer presence bits (common.hpp)
   uint64_t N;
@@ -536,6 +538,19 @@ __device__ __forceinline__ uint64_t idx_val(const uint4 &v, uint32_t ao) {
   if (sizeof(IdxT) == 8) return (ao & 8) ? hi64(v) : lo64(v);
   return dword_at(v, ao >> 2);
 }
+
+// packed-word hints (common.hpp): the 7-bit capped L8 byte at bit b of w is
+// known to be < xd (a run stops there): exact below 127, and 127 only stands
+// for >= 127
+__device__ __forceinline__ bool pk_below(uint64_t w, uint32_t b, uint32_t xd) {
+  const uint32_t c = uint32_t(w >> b) & 127u;
+  return c < xd && c < 127u;
+}
+__device__ __forceinline__ bool pk_above(uint64_t w, uint32_t b, uint32_t xd) {
+  return (uint32_t(w >> b) & 127u) >= xd;
+}
+// the lowercase base of 2-bit code q (a0 c1 g2 t3)
+__device__ __forceinline__ uint32_t pk_char(uint32_t q) { return (0x74676361u >> (8 * q)) & 0xFFu; }
 
 // Direct rows: the bad-mask nibble of the 4 bytes of w (bit j: byte j is not
 // a base that occurs in the text), bases at or past `live` (0..4) masked.
@@ -661,18 +676,58 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // blocks in one iteration (S_EXB), or the one side with room; false: none
   // left blocks are the 16 bytes ENDING at es (from 0 when es < 15), right
   // blocks start at ee + 1
-  auto bs_probe = [&]() {   // compare P' with T[sp + cbase + lc ...] (sp = SA[m])
+  // probe m decided: P' agrees with S_m on lc characters past cbase; ranout:
+  // P' ran out (it is a prefix of S_m), else its next byte pb differs from
+  // the text's tb (signed chars, like the reference)
+  auto bs_decide = [&](bool ranout, uint32_t pb, uint32_t tb) {
+    bool left;                                  // keep [lo, m) (else (m, hi))
+    if (bsm == BS_INSERT) {
+      left = ranout || int8_t(pb) < int8_t(tb);
+      if (lc > best) { best = lc; bpos = sp; bi = m; }
+    } else {                                    // in the run iff lcp reaches cap
+      left = (lc >= cap) == (bsm == BS_LEFT);
+    }
+    if (left) { hi = m; lR = lc; }
+    else { lo = m + 1; lL = lc; }
+  };
+  // compare P' with T[sp + cbase + lc ...] (sp = the SA word of probe m).
+  // Packed words: the 7 bases T[x + K ...) in the word decide a compare that
+  // starts and ends inside them without a text probe (true: decided, the
+  // caller goes on at A_BS); a compare that agrees on all of them goes on in
+  // the text after them
+  auto bs_probe = [&]() -> bool {
     SM_HOOK_CMPBS(true, sp, cbase + lc);
-    addr = reinterpret_cast<uint64_t>(c.T + sp + cbase + lc);
+    const uint32_t o = cbase + lc;
+    if (c.pk && ((sp >> kPkPosBits) & 7u) != 5u && o >= c.K && o < c.K + kPkWindow) {
+      const uint32_t rem = cap - lc, nav = c.K + kPkWindow - o;
+      const uint32_t lim = rem < nav ? rem : nav;
+      const uint32_t w = uint32_t(sp >> (50 + 2 * (o - c.K)));
+      const uint32_t off = prefix + o;
+      uint32_t k = 0, tb = 0;
+      for (; k < lim; ++k) {
+        tb = pk_char((w >> (2 * k)) & 3u);
+        if (P[off + k] != tb) break;
+      }
+      lc += k;
+      if (k < lim || k == rem) {
+        SM_HOOK_CMPBS(false, sp, cbase + lc);
+        bs_decide(k == rem, k == rem ? 0u : uint32_t(P[off + k]), tb);
+        pf = false; pfr = false; need2 = false;
+        return true;
+      }
+    }
+    addr = reinterpret_cast<uint64_t>(c.T + (sp & c.pm) + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
     need2 = c.pf && lo < m;
     pfr = c.pf && m + 1 < hi;
     pf = c.pf != 0;
     st = S_CMP; op = O_BS;
+    return false;
   };
   auto lblock = [&](uint64_t e) { return reinterpret_cast<uint64_t>(c.L8 + (e >= 15 ? e - 15 : 0)); };
-  auto ex_start = [&](uint64_t lb, uint64_t hb) {
-    const bool l = es > lb, r = ee < hb;
+  // (ls / rs: that side's end is known already, from packed-word L8 bytes)
+  auto ex_start = [&](uint64_t lb, uint64_t hb, bool ls, bool rs) {
+    const bool l = !ls && es > lb, r = !rs && ee < hb;
     nblk = 0;
     rdone = !r;
     addr = l ? lblock(es) : reinterpret_cast<uint64_t>(c.L8 + ee + 1);
@@ -805,6 +860,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
 #endif
     const uint32_t ao = st >= S_BYTE ? 0u : uint32_t(addr) & 15;   // element offset in v
     uint32_t a = A_NONE;
+    // the ISA words of an expand_link's two ends (this iteration only: the
+    // decide chain runs A_EXPAND right after the consume that loads them)
+    uint64_t xwl = 0, xwr = 0;
+    bool xw = false;
     SM_REGION(0);
     // the scan states' byte masks, one computation shared by all four (their
     // bodies would otherwise each pay for it): bit i of mv / mv2 is byte i of
@@ -935,15 +994,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
           sp = iv;
           // 16 bytes first: a binary-search probe usually decides early
-          bs_probe();
+          if (bs_probe()) a = A_BS;
         } else if (op == O_ISAJ) {
-          start = end = iv; have_pos = false;
+          start = end = iv & c.pm; have_pos = false;
+          xwl = xwr = iv; xw = c.pk != 0;
           a = A_EXPAND;
         } else if (op == O_NS_SA2) {                  // suffix link, both ends
-          addr = ia(c.ISA, iv + 1); addr2 = ia(c.ISA, iv2 + 1);
+          addr = ia(c.ISA, (iv & c.pm) + 1); addr2 = ia(c.ISA, (iv2 & c.pm) + 1);
           op = O_NS_ISA2;
         } else {                                      // O_NS_ISA2
-          start = iv; end = iv2; need2 = false;
+          start = iv & c.pm; end = iv2 & c.pm; need2 = false;
+          xwl = iv; xwr = iv2; xw = c.pk != 0;
           ++prefix; have_pos = false;
           if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
           else a = A_EXPAND;
@@ -952,12 +1013,12 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_BYTE: {                                 // is_leftmaximal: T[pos-1]
         SM_REGION(6);
-        SM_HOOK_BYTE(pos);
+        SM_HOOK_BYTE(pos & c.pm);
         if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
-          if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
+          if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & c.pm, prefix, depth);
           ++nem;
         }
-        uscan_start(pos, depth);
+        uscan_start(pos & c.pm, depth);
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
@@ -988,24 +1049,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {                                      // O_BS: probe m decided
           SM_HOOK_CMPBS(false, sp, cbase + lc);
           need2 = false;
-          bool left;                                  // keep [lo, m) (else (m, hi))
-          if (bsm == BS_INSERT) {
-            // P' < S_m iff P' ran out (prefix of S_m) or the first differing
-            // byte of P' is smaller (signed chars, like the reference)
-            const uint32_t tbyte = k < 16 ? byte_at(v, k) : byte_at(v2, k - 16);
-            left = k == rem || int8_t(P[off + k]) < int8_t(tbyte);
-            if (lc > best) { best = lc; bpos = sp; bi = m; }
-          } else {                                    // in the run iff lcp reaches cap
-            left = (lc >= cap) == (bsm == BS_LEFT);
-          }
-          if (left) { hi = m; lR = lc; }
-          else { lo = m + 1; lL = lc; }
+          // P' < S_m iff P' ran out (prefix of S_m) or the first differing
+          // byte of P' is smaller
+          const uint32_t tbyte = k < 16 ? byte_at(v, k) : byte_at(v2, k - 16);
+          bs_decide(k == rem, k == rem ? 0u : uint32_t(P[off + k]), tbyte);
+          const bool left = hi == m;
           if (had_pf && lo < hi) {                    // the next probe's SA element is here
             m = (lo + hi) >> 1;
             SM_HOOK_PF(ia(c.SA, m));
             sp = left ? idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15) : v3;
             lc = lL < lR ? lL : lR;
-            bs_probe();
+            if (bs_probe()) a = A_BS;
           } else {
             a = A_BS;
           }
@@ -1129,7 +1183,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         cbase = depth; cap = best;
         es = bi; ee = bi;
         SM_HOOK_RUN(true, 1, 0, 0);
-        a = ex_start(start, end) ? A_NONE : A_RUN_DONE;
+        // packed: the SA word of rank bi holds L8[bi] and L8[bi + 1], the
+        // run's first stop on either side when it ends at bi
+        const bool ls = c.pk && pk_below(bpos, 36, xd), rs = c.pk && pk_below(bpos, 43, xd);
+        a = ex_start(start, end, ls, rs) ? A_NONE : A_RUN_DONE;
       }
     }
     if (a == A_XL_DONE) {                             // left end known: right side
@@ -1170,7 +1227,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_TOP;
       } else {
         depth = dch - j;
-        addr = ia(c.ISA, pos + j);
+        addr = ia(c.ISA, (pos & c.pm) + j);
         st = S_IDX; op = O_ISAJ;
         a = A_NONE;
       }
@@ -1184,7 +1241,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       cbase = 0; cap = depth;
       es = start; ee = end;
       SM_HOOK_RUN(true, 0, 0, 0);
-      a = ex_start(0, N - 1) ? A_NONE : A_RUN_DONE;
+      // packed: the ISA words of start and end hold L8[start - 1 .. start]
+      // and L8[end + 1 .. end + 2]: a run that ends within one more suffix
+      // on a side needs no L8 probe there
+      bool ls = false, rs = false;
+      if (xw) {
+        if (pk_below(xwl, 40, xd)) ls = true;                      // L8[start] < xd
+        else if (pk_above(xwl, 40, xd) && pk_below(xwl, 33, xd)) { es = start - 1; ls = true; }
+        if (pk_below(xwr, 47, xd)) rs = true;                      // L8[end + 1] < xd
+        else if (pk_above(xwr, 47, xd) && pk_below(xwr, 54, xd)) { ee = end + 1; rs = true; }
+      }
+      a = ex_start(0, N - 1, ls, rs) ? A_NONE : A_RUN_DONE;
     }
     if (a == A_AFTER) {
       SM_REGION(16);
@@ -1200,15 +1267,19 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (!have_pos) {
           addr = ia(c.SA, start);
           st = S_IDX; op = O_SAPOS2;
-        } else if (depth >= c.min_len && prefix != 0 && pos != 0) {
-          addr = reinterpret_cast<uint64_t>(c.T + pos - 1);
+        } else if (depth >= c.min_len && prefix != 0 && (pos & c.pm) != 0 &&
+                   (!c.pk || ((pos >> kPkPosBits) & 7u) >= 4u)) {
+          addr = reinterpret_cast<uint64_t>(c.T + (pos & c.pm) - 1);
           st = S_BYTE;
         } else {
-          if (depth >= c.min_len) {
-            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos, prefix, depth);
+          // (packed: is_leftmaximal from the BWT character in pos's SA word)
+          if (depth >= c.min_len &&
+              (prefix == 0 || (pos & c.pm) == 0 ||
+               P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
+            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & c.pm, prefix, depth);
             ++nem;
           }
-          uscan_start(pos, depth);
+          uscan_start(pos & c.pm, depth);
         }
       }
     }
@@ -1372,7 +1443,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             addr = ia(c.SA, start);
             st = S_IDX; op = O_SAPOS;
           } else {
-            addr = reinterpret_cast<uint64_t>(c.T + pos + depth);
+            addr = reinterpret_cast<uint64_t>(c.T + (pos & c.pm) + depth);
             addr2 = addr + 16;
             need2 = L - prefix - depth > 16;
             st = S_CMP; op = O_EXT; lc = 0;

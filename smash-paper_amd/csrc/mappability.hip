@@ -76,6 +76,7 @@ struct MapCtx {
   uint64_t *fix;                 // [fix_cap][3] {x, byte index in the scan's output, threshold}
   unsigned long long *nfix;
   uint64_t fix_cap;
+  uint64_t pm;                   // position bits of an ISA word (packed hints masked off)
 };
 constexpr uint64_t kFixCap = uint64_t(1) << 23;
 
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
           right = 255;
           fixr |= 1u << q;
         } else {
-          right = min_len_at(c, uint64_t(ISA[xf + q]));
+          right = min_len_at(c, uint64_t(ISA[xf + q]) & c.pm);
           if (right + i >= S) right = 0;
         }
       }
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
           left = 255;
           fixl |= 1u << q;
         } else {
-          left = min_len_at(c, uint64_t(ISA[xr - q]));
+          left = min_len_at(c, uint64_t(ISA[xr - q]) & c.pm);
           if (left >= i) left = 0;
         }
       }
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(kMB, W) void k_mapscan(MapCtx c, const IdxT *__rest
           if (fb < c.fix_cap) {
             c.fix[3 * fb] = x; c.fix[3 * fb + 1] = bi; c.fix[3 * fb + 2] = thr;
           } else {                                 // list full: exact path here
-            const uint64_t mm = min_len_at(c, uint64_t(ISA[x]));
+            const uint64_t mm = min_len_at(c, uint64_t(ISA[x]) & c.pm);
             const uint32_t byte = mm >= thr ? 0u : (mm < 255 ? uint32_t(mm) : 255u);
             const uint32_t sh = 16 * (q & 1) + (side ? 0 : 8);
             ob[q >> 1] = (ob[q >> 1] & ~(0xFFu << sh)) | (byte << sh);
@@ -576,7 +577,7 @@ __global__ void k_mapfix(MapCtx c, const IdxT *__restrict__ ISA, uint8_t *out) {
   const uint64_t n = *c.nfix < c.fix_cap ? *c.nfix : c.fix_cap;
   for (uint64_t e = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < n;
        e += uint64_t(gridDim.x) * blockDim.x) {
-    const uint64_t m = min_len_at(c, uint64_t(ISA[c.fix[3 * e]]));
+    const uint64_t m = min_len_at(c, uint64_t(ISA[c.fix[3 * e]]) & c.pm);
     out[c.fix[3 * e + 1]] = uint8_t(m >= c.fix[3 * e + 2] ? 0 : (m < 255 ? m : 255));
   }
 }
@@ -596,6 +597,7 @@ int scan_t(const smash_index *ix, uint64_t begin, uint64_t end, uint32_t k, uint
   c.fix = nullptr;
   c.nfix = nullptr;
   c.fix_cap = 0;
+  c.pm = ix->pos_mask;
   if (out && k < 255) {
     SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&c.fix), 24 * kFixCap, s));
     SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&c.nfix), 8, s));

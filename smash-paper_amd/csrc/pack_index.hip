@@ -1,0 +1,102 @@
+// smash-paper_amd/csrc/pack_index.hip -- the packed SA / ISA words (round 5).
+//
+// hg19's doubled text needs 33 of an element's 64 bits; the other 31 carry
+// what the search (k_mam_sm, mam_sm.hpp) would otherwise fetch with separate
+// random probes right after loading that element (layout: common.hpp):
+//   * an SA word: the BWT character T[x - 1] (is_leftmaximal,
+//     longSA.cpp:540-546: one text probe per emitted candidate), L8[r] and
+//     L8[r + 1] (the first stops of the traverse's final run around rank r,
+//     longSA.cpp:322-380), and 7 bases T[x + K ...) (a binary-search compare
+//     that starts and ends inside them needs no text probe);
+//   * an ISA word: L8[r - 1 .. r + 2] (the first stops of expand_link's run
+//     around a suffix link's target, longSA.h:158-174).
+// The hints are a pure function of T, SA and L8, so every result is
+// unchanged; readers that want the element mask it (IdxArr, pos_mask), and
+// smash_index_save writes plain elements.
+#include "common.hpp"
+
+#include <cstdlib>
+
+namespace smash {
+namespace {
+
+__device__ __forceinline__ int base_code(uint8_t b) {
+  return b == 'a' ? 0 : b == 'c' ? 1 : b == 'g' ? 2 : b == 't' ? 3 : -1;
+}
+__device__ __forceinline__ uint64_t l8c(const uint8_t *L8, uint64_t N, uint64_t r, int64_t d) {
+  const int64_t q = int64_t(r) + d;
+  if (q < 0 || uint64_t(q) >= N) return 0;
+  const uint32_t v = L8[q];
+  return v < 127u ? v : 127u;
+}
+
+__global__ void k_pack_sa(uint64_t *SA, const uint8_t *__restrict__ T,
+                          const uint8_t *__restrict__ L8, uint64_t N, uint32_t K, bool pack) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < N; r += stride) {
+    const uint64_t x = SA[r] & kPkPosMask;
+    if (!pack) {
+      SA[r] = x;
+      continue;
+    }
+    const int bc = x ? base_code(T[x - 1]) : -1;
+    uint64_t tag = bc >= 0 ? uint64_t(bc) : 4u;
+    uint64_t win = 0;
+    for (uint32_t i = 0; i < kPkWindow; ++i) {   // (T has 64 zero bytes past N)
+      const int c = x + K + i < N ? base_code(T[x + K + i]) : -1;
+      if (c < 0) {
+        tag = 5;
+        win = 0;
+        break;
+      }
+      win |= uint64_t(c) << (2 * i);
+    }
+    SA[r] = x | tag << 33 | l8c(L8, N, r, 0) << 36 | l8c(L8, N, r, 1) << 43 | win << 50;
+  }
+}
+
+__global__ void k_pack_isa(uint64_t *ISA, const uint8_t *__restrict__ L8, uint64_t N, bool pack) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x < N; x += stride) {
+    const uint64_t r = ISA[x] & kPkPosMask;
+    ISA[x] = pack ? r | l8c(L8, N, r, -1) << 33 | l8c(L8, N, r, 0) << 40 |
+                        l8c(L8, N, r, 1) << 47 | l8c(L8, N, r, 2) << 54
+                  : r;
+  }
+}
+
+}  // namespace
+
+void pack_index(smash_index *ix, bool pack, hipStream_t s) {
+  if (ix->idx_bytes != 8 || ix->N > kPkPosMask || !ix->d_kmer) return;
+  const char *e = std::getenv("SMASH_PACK_IDX");   // 0: plain words (A/B)
+  if (pack && e && e[0] == '0') pack = false;
+  if (!pack && ix->pos_mask == ~0ull) return;
+  const uint64_t N = ix->N;
+  k_pack_sa<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(static_cast<uint64_t *>(ix->d_sa),
+                                                      ix->d_text, ix->d_lcp8, N, ix->kmer_k, pack);
+  k_pack_isa<<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(static_cast<uint64_t *>(ix->d_isa),
+                                                       ix->d_lcp8, N, pack);
+  SMASH_HIPX(hipGetLastError());
+  SMASH_HIPX(hipStreamSynchronize(s));
+  ix->pos_mask = pack ? kPkPosMask : ~0ull;
+}
+
+}  // namespace smash
+
+using namespace smash;
+
+extern "C" int smash_index_pack(smash_index *ix, int pack, void *stream) {
+  if (!ix) {
+    set_error("smash_index_pack: null index");
+    return SMASH_ERR_ARG;
+  }
+  try {
+    SMASH_HIPX(hipSetDevice(ix->device));
+    pack_index(ix, pack != 0, static_cast<hipStream_t>(stream));
+  } catch (hip_failure &f) {
+    set_error(f.what);
+    return SMASH_ERR_HIP;
+  }
+  return SMASH_OK;
+}

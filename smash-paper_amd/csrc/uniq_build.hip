@@ -49,11 +49,12 @@ constexpr uint32_t kChunk = 32;                  // level-1 buckets per pass-2/3
 __host__ __device__ inline uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 template <class IdxT>
-__global__ void k_uniq_gather(const IdxT *__restrict__ ISA, const uint8_t *__restrict__ L8,
-                              uint64_t N, uint64_t lo, uint64_t hi, uint8_t *U) {
+__global__ void k_uniq_gather(const IdxT *__restrict__ ISA, uint64_t pm,
+                              const uint8_t *__restrict__ L8, uint64_t N, uint64_t lo,
+                              uint64_t hi, uint8_t *U) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   for (uint64_t x = lo + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x < hi; x += stride) {
-    const uint64_t r = ISA[x];
+    const uint64_t r = uint64_t(ISA[x]) & pm;
     const uint8_t a = L8[r];
     const uint8_t b = r + 1 < N ? L8[r + 1] : 0;
     U[x] = a > b ? a : b;
@@ -124,7 +125,7 @@ __device__ __forceinline__ void tile_scatter(TileLds &t, uint32_t nb, const uint
 
 // pass 1: ranks -> level-1 buckets of the window [lo, hi)
 template <class IdxT>
-__global__ __launch_bounds__(kUT) void k_upart1(const IdxT *__restrict__ SA,
+__global__ __launch_bounds__(kUT) void k_upart1(const IdxT *__restrict__ SA, uint64_t pm,
                                                 const uint8_t *__restrict__ L8, uint64_t N,
                                                 uint64_t lo, uint64_t hi, uint32_t nb,
                                                 unsigned int *cur, uint32_t *E1) {
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(kUT) void k_upart1(const IdxT *__restrict__ SA,
       bk[k] = 0xFFFF;
       ent[k] = 0;
       if (r < N) {
-        const uint64_t x = SA[r];
+        const uint64_t x = uint64_t(SA[r]) & pm;
         const uint8_t a = L8[r], c = r + 1 < N ? L8[r + 1] : uint8_t(0);
         if (x >= lo && x < hi) {
           bk[k] = uint16_t((x - lo) >> kS1);
@@ -229,7 +230,7 @@ void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   const char *e = getenv("SMASH_UNIQ_GATHER");   // 1: the gather form (A/B)
   if (nb1 > kNB1Max || (e && e[0] == '1')) {
     k_uniq_gather<IdxT><<<grid_for(n, 256, 1u << 20), 256, 0, s>>>(
-        static_cast<const IdxT *>(ix->d_isa), ix->d_lcp8, N, lo, hi, ix->d_uniq);
+        static_cast<const IdxT *>(ix->d_isa), ix->pos_mask, ix->d_lcp8, N, lo, hi, ix->d_uniq);
     SMASH_HIPX(hipGetLastError());
     return;
   }
@@ -244,7 +245,7 @@ void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * nb1, s));
   const uint64_t t1 = (N + kUTile - 1) / kUTile;
   k_upart1<IdxT><<<unsigned(std::min<uint64_t>(t1, uint64_t(cus))), kUT, 0, s>>>(
-      static_cast<const IdxT *>(ix->d_sa), ix->d_lcp8, N, lo, hi, nb1, cur, E1);
+      static_cast<const IdxT *>(ix->d_sa), ix->pos_mask, ix->d_lcp8, N, lo, hi, nb1, cur, E1);
   SMASH_HIPX(hipGetLastError());
   for (uint32_t c0 = 0; c0 < nb1; c0 += kChunk) {
     const uint32_t nc = std::min(kChunk, nb1 - c0);

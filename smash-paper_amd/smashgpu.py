@@ -61,7 +61,7 @@ EXPORTS = [
     "smash_fastq_shard_scan", "smash_fastq_shard_free_blob", "smash_fastq_shard_open",
     "smash_fastq_shard_pack", "smash_fastq_shard_stats", "smash_fastq_shard_close",
     "smash_read_stride", "smash_pipeline_max_batch",
-    "smash_mappability_prepare", "smash_mappability_window",
+    "smash_mappability_prepare", "smash_mappability_window", "smash_index_pack",
 ]
 
 
@@ -73,7 +73,7 @@ class IndexInfo(C.Structure):
                 ("device_bytes", C.c_uint64), ("build_seconds", C.c_double),
                 ("kmer_k", C.c_uint32), ("d_uniq", vp), ("d_kmer", vp),
                 ("bitmap_b", C.c_uint32), ("d_bitmap", vp), ("in_text", C.c_uint64 * 4),
-                ("rcref", C.c_uint32), ("reserved", C.c_uint32)]
+                ("rcref", C.c_uint32), ("pos_bits", C.c_uint32)]
 
 
 class PipelineCfg(C.Structure):
@@ -223,6 +223,7 @@ def lib():
     L.smash_read_stride.argtypes = [C.c_uint32]
     L.smash_read_stride.restype = C.c_uint32
     L.smash_mappability_prepare.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
+    L.smash_index_pack.argtypes = [vp, C.c_int, vp]
     L.smash_mappability_window.argtypes = [vp, C.c_uint64, C.c_uint64, u64p, u64p]
     L.smash_pipeline_max_batch.argtypes = [C.c_uint32, C.c_uint32]
     L.smash_pipeline_max_batch.restype = C.c_uint64
@@ -377,6 +378,32 @@ class Index:
     @property
     def N(self):
         return self.info.N
+
+    @property
+    def pos_mask(self):
+        """the element bits of an SA / ISA word (packed index words keep the
+        search's hints above them, smash_index_info.pos_bits)"""
+        b = self.info.pos_bits
+        return (1 << b) - 1 if b else (1 << (8 * self.info.idx_bytes)) - 1
+
+    def pack(self, on=True):
+        """smash_index_pack: put the search's hints into the SA / ISA words
+        (on) or strip them (results are the same either way)"""
+        check(lib().smash_index_pack(self.h, 1 if on else 0, None), "smash_index_pack")
+        check(lib().smash_index_query(self.h, C.byref(self.info)), "smash_index_query")
+
+    def download_sa_isa(self, plain=True):
+        """host copies of SA and ISA (u32 / u64 as in HBM); plain: the
+        elements alone (the packed hints masked off)"""
+        i = self.info
+        dt = np.uint32 if i.idx_bytes == 4 else np.uint64
+        SA = download(i.d_sa, i.N * i.idx_bytes, dt)
+        ISA = download(i.d_isa, i.N * i.idx_bytes, dt)
+        if plain and i.pos_bits:
+            m = dt(self.pos_mask)
+            np.bitwise_and(SA, m, out=SA)
+            np.bitwise_and(ISA, m, out=ISA)
+        return SA, ISA
 
     def __del__(self):
         try:

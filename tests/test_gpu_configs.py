@@ -148,8 +148,13 @@ def test_hg19_device_index_properties_full_size(hg19):
     assert i.idx_bytes == 8 and i.N > (1 << 32)
     r = IchkResult()
     n255 = C.c_ulonglong()
-    rc = _ichk().ichk_run(i.d_text, i.N, i.d_sa, i.d_isa, i.idx_bytes, i.d_lcp8, i.d_lcp_ovf,
-                          i.n_lcp_overflow, 1024, 1 << 16, C.byref(r), C.byref(n255))
+    packed = bool(i.pos_bits)
+    dix.pack(False)   # (the checker reads plain elements; the hints are checked below)
+    try:
+        rc = _ichk().ichk_run(i.d_text, i.N, i.d_sa, i.d_isa, i.idx_bytes, i.d_lcp8, i.d_lcp_ovf,
+                              i.n_lcp_overflow, 1024, 1 << 16, C.byref(r), C.byref(n255))
+    finally:
+        dix.pack(packed)
     assert rc == 0
     assert r.rank0_ok == 1
     assert r.perm_bad == 0, r.perm_first
@@ -170,11 +175,46 @@ def test_hg19_device_index_host_sample(hg19):
     ISA = S.device_view(i.d_isa, 8 * N, torch.int64)
     L8 = S.device_view(i.d_lcp8, N, torch.uint8)
     r = torch.from_numpy(ranks).cuda()
-    a = SA.index_select(0, r - 1).cpu().numpy()
-    b = SA.index_select(0, r).cpu().numpy()
-    back = ISA.index_select(0, torch.from_numpy(b).cuda()).cpu().numpy()
+    pm = dix.pos_mask
+    assert i.pos_bits == 33 and pm == (1 << 33) - 1   # hg19: packed index words
+    wa = SA.index_select(0, r - 1).cpu().numpy().view(np.uint64)
+    wb = SA.index_select(0, r).cpu().numpy().view(np.uint64)
+    a = (wa & np.uint64(pm)).astype(np.int64)
+    b = (wb & np.uint64(pm)).astype(np.int64)
+    wi = ISA.index_select(0, torch.from_numpy(b).cuda()).cpu().numpy().view(np.uint64)
+    back = (wi & np.uint64(pm)).astype(np.int64)
     l8 = L8.index_select(0, r).cpu().numpy().astype(np.int64)
     assert np.array_equal(back, ranks)
+    # the packed hints of these words (csrc/pack_index.hip; layout in
+    # csrc/common.hpp) restated on the host from T and L8 at the same ranks
+    idx = torch.from_numpy(np.concatenate([ranks - 2, ranks - 1, ranks, ranks + 1, ranks + 2])
+                           .clip(0, N - 1)).cuda()
+    near = L8.index_select(0, idx).cpu().numpy().reshape(5, -1).astype(np.uint64)
+    cap = np.minimum(near, 127)
+    cap[4][ranks + 2 > N - 1] = 0
+    cap[3][ranks + 1 > N - 1] = 0
+    sa_hint = wb >> np.uint64(36)
+    assert np.array_equal(sa_hint & np.uint64(127), cap[2])
+    assert np.array_equal((sa_hint >> np.uint64(7)) & np.uint64(127), cap[3])
+    isa_hint = wi >> np.uint64(33)
+    for q, row in enumerate((1, 2, 3, 4)):   # L8[r - 1 .. r + 2]
+        assert np.array_equal((isa_hint >> np.uint64(7 * q)) & np.uint64(127), cap[row]), q
+    K = dix.info.kmer_k
+    lut = np.full(256, 255, np.uint8)
+    for k, ch in enumerate(b"acgt"):
+        lut[ch] = k
+    x = b
+    tag = (wb >> np.uint64(33)) & np.uint64(7)
+    bwt = np.where(x > 0, lut[T[np.maximum(x - 1, 0)]], 255)
+    win = np.stack([np.where(x + K + k < N, lut[T[np.minimum(x + K + k, N - 1)]], 255)
+                    for k in range(7)])
+    dirty = (win == 255).any(0)
+    assert np.array_equal(tag[dirty], np.full(dirty.sum(), 5, np.uint64))
+    clean = ~dirty
+    assert np.array_equal(tag[clean], np.where(bwt[clean] < 4, bwt[clean], 4).astype(np.uint64))
+    w50 = wb[clean] >> np.uint64(50)
+    for k in range(7):
+        assert np.array_equal((w50 >> np.uint64(2 * k)) & np.uint64(3), win[k][clean].astype(np.uint64))
     ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
     big = l8 == 255
     pos = np.searchsorted(ovf[:, 0], ranks[big].astype(np.uint64))
@@ -194,8 +234,7 @@ def hg19_oracle(hg19):
     contigs, (T, sp, sz, names), dix = hg19
     i = dix.info
     N = i.N
-    SA = S.download(i.d_sa, 8 * N, np.uint64)
-    ISA = S.download(i.d_isa, 8 * N, np.uint64)
+    SA, ISA = dix.download_sa_isa(plain=True)
     L8 = S.download(i.d_lcp8, N)
     ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
     mp = S.download(i.d_map, i.map_bytes)
@@ -402,8 +441,15 @@ def test_idx8_pipeline_equals_independent_oracle(monkeypatch, tmp_path):
     monkeypatch.delenv("SMASH_IDX_BYTES")
     i = dix.info
     assert i.idx_bytes == 8
-    assert np.array_equal(S.download(i.d_sa, 8 * i.N, np.uint64), oix.SA.astype(np.uint64))
-    assert np.array_equal(S.download(i.d_isa, 8 * i.N, np.uint64), oix.ISA.astype(np.uint64))
+    dsa, disa = dix.download_sa_isa(plain=True)
+    assert np.array_equal(dsa, oix.SA.astype(np.uint64))
+    assert np.array_equal(disa, oix.ISA.astype(np.uint64))
+    # the packed words (mid is far below 2^33) equal the host restatement
+    import sm_emu
+    assert i.pos_bits == 33
+    psa, pisa = dix.download_sa_isa(plain=False)
+    hsa, hisa = sm_emu.pack_words(oix.T, oix.SA, oix.ISA, oix.L8, i.kmer_k)
+    assert np.array_equal(psa, hsa) and np.array_equal(pisa, hisa)
     reads = _reads(g, 6000, 150, seed=88)
     # MAM triples of every 5th read
     n = reads.shape[0]
@@ -581,39 +627,68 @@ def test_c4_real_driver_rccl_world1_equals_oracle(c4_run, c4_fastq, monkeypatch)
         tdist.destroy_process_group()
 
 
-@pytest.mark.timeout(900)
-def test_c3_production_batch_equals_oracle(hg19, hg19_oracle):
+class _ProductionRun:
     """C3 at the bench's production batch size: 12.6 M pairs of the bench's
-    workload (seed 3, 150 bp, sample_bins/50000) counted as bench.py counts a
-    run -- smash_count_batches_ready over batches of 12.5 M pairs (the
+    workload (seed 3000, 150 bp, sample_bins/50000) counted as bench.py counts
+    a run -- smash_count_batches_ready over batches of 12.5 M pairs (the
     bench's fit_batch choice on one GPU: 3.28e9 hit words per batch, within
     smash_pipeline_max_batch's 2^32 bound), one key set and the adjacent-dup
-    state carried into the second, short batch -- equal the oracle's whole
-    chain over the same 25.2 M reads (smashMEM.py:147-228, varbin.py:52-92).
-    ~4 minutes of oracle time on 16 threads."""
-    import readgen
-    contigs, _, dix = hg19
-    oix, mp = hg19_oracle
-    cs = _chrom_sizes(contigs)
-    src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
-    starts = np.array([int(l.split("\t")[2]) for l in open(src)], np.int64)
-    P, B = 12_600_000, 12_500_000
-    assert B <= S.pipeline_max_batch(150)
-    torch.cuda.empty_cache()
-    d_reads = readgen.Generator(dix, contigs, 150, seed=3000).generate(P)
-    pipe = S.Pipeline(dix, cs, starts, 150, B, dedup_capacity=P + P // 8 + (1 << 20))
-    counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
-    pipe.reset()
-    pipe.count_batches(d_reads, P, B, counts, resident=True)
-    st = pipe.stats()
-    got = counts.cpu().numpy().astype(np.uint64)
-    h = d_reads.cpu().numpy()
-    del d_reads, pipe
-    op = O.Pipeline(oix, mp, cs, starts)
-    for a in range(0, P, 500_000):   # the oracle's state carries across calls
-        assert op.run(h[2 * a:2 * min(P, a + 500_000)], threads=THREADS) == 0
-        print("oracle: %d of %d pairs" % (min(P, a + 500_000), P), flush=True)
-    assert st.pairs == P
-    assert np.array_equal(got, op.counts)
+    state carried into the second, short batch; the oracle's whole chain over
+    the same 25.2 M reads is advanced in PARTS parts by the tests below (each
+    ~25 s of oracle time on 16 threads, so no test runs silent for minutes;
+    the oracle's state carries across its calls)."""
+    P, B, PARTS = 12_600_000, 12_500_000, 10
+
+    def __init__(self, hg19, hg19_oracle):
+        import readgen
+        contigs, _, dix = hg19
+        oix, mp = hg19_oracle
+        cs = _chrom_sizes(contigs)
+        src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
+        starts = np.array([int(l.split("\t")[2]) for l in open(src)], np.int64)
+        P, B = self.P, self.B
+        assert B <= S.pipeline_max_batch(150)
+        torch.cuda.empty_cache()
+        d_reads = readgen.Generator(dix, contigs, 150, seed=3000).generate(P)
+        pipe = S.Pipeline(dix, cs, starts, 150, B, dedup_capacity=P + P // 8 + (1 << 20))
+        counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+        pipe.reset()
+        pipe.count_batches(d_reads, P, B, counts, resident=True)
+        self.st = pipe.stats()
+        self.got = counts.cpu().numpy().astype(np.uint64)
+        self.h = d_reads.cpu().numpy()
+        del d_reads, pipe
+        torch.cuda.empty_cache()
+        self.op = O.Pipeline(oix, mp, cs, starts)
+        self.done = 0
+
+    def advance(self, k):
+        """the oracle over parts 0..k (in order; the ones done are kept)"""
+        P, step = self.P, -(-self.P // self.PARTS)
+        while self.done <= k:
+            a, b = self.done * step, min(P, (self.done + 1) * step)
+            assert self.op.run(self.h[2 * a:2 * b], threads=THREADS) == 0
+            self.done += 1
+
+
+@pytest.fixture(scope="module")
+def c3_production(hg19, hg19_oracle):
+    return _ProductionRun(hg19, hg19_oracle)
+
+
+@pytest.mark.parametrize("part", range(_ProductionRun.PARTS - 1))
+def test_c3_production_batch_oracle_part(c3_production, part):
+    c3_production.advance(part)
+    assert c3_production.op.state.total > 0
+
+
+def test_c3_production_batch_equals_oracle(c3_production):
+    """the device run at the production batch == the oracle's whole chain
+    over the same 12.6 M pairs (smashMEM.py:147-228, varbin.py:52-92)"""
+    r = c3_production
+    r.advance(r.PARTS - 1)
+    st, op = r.st, r.op
+    assert st.pairs == r.P
+    assert np.array_equal(r.got, op.counts)
     assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
     assert st.dupe_pairs == op.n_dupe.value and st.dupe_pairs > 1000

@@ -38,9 +38,7 @@ def gix(tiny_fa):
 def _arrays(ix):
     i = ix.info
     N = i.N
-    dt = np.uint32 if i.idx_bytes == 4 else np.uint64
-    SA = S.download(i.d_sa, N * i.idx_bytes, dt)
-    ISA = S.download(i.d_isa, N * i.idx_bytes, dt)
+    SA, ISA = ix.download_sa_isa(plain=True)
     L8 = S.download(i.d_lcp8, N)
     ovf = S.download(i.d_lcp_ovf, 16 * i.n_lcp_overflow, np.uint64).reshape(-1, 2)
     mp = S.download(i.d_map, i.map_bytes)

@@ -19,11 +19,13 @@ import sm_emu  # noqa: E402
 @pytest.fixture(scope="module")
 def emu(tiny_ix):
     tiny_ix.accel()
-    return sm_emu.Emu(tiny_ix), sm_emu.Emu(tiny_ix, wide=True)
+    # plain 4-byte, plain 8-byte, and the packed 8-byte words (the device's
+    # hg19 index: the search's hints in the SA / ISA words, csrc/common.hpp)
+    return sm_emu.Emu(tiny_ix), sm_emu.Emu(tiny_ix, wide=True), sm_emu.Emu(tiny_ix, packed=True)
 
 
 @pytest.mark.parametrize("s", ["s100", "s150"])
-@pytest.mark.parametrize("wide", [False, True])
+@pytest.mark.parametrize("wide", [0, 1, 2])
 @pytest.mark.parametrize("lin", [2, 1])
 @pytest.mark.parametrize("bm_dual", ["0", "1", "2", "3"])
 def test_state_machine_matches_reference_goldens(emu, s, wide, lin, bm_dual, monkeypatch):
@@ -33,7 +35,7 @@ def test_state_machine_matches_reference_goldens(emu, s, wide, lin, bm_dual, mon
     monkeypatch.setenv("SMASH_SM_BM_DUAL", bm_dual)
     exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
            for l in read_gz_lines("%s_MAM.txt.gz" % s)]
-    got, iters = emu[int(wide)].map(interleaved_reads(s), lin_blocks=lin)
+    got, iters = emu[wide].map(interleaved_reads(s), lin_blocks=lin)
     bad = [i for i in range(len(exp)) if got[i] != exp[i]]
     assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)
     assert iters.min() > 0
@@ -63,10 +65,11 @@ def test_state_machine_edge_reads(emu, tiny_ix, L, direct, monkeypatch):
     reads = _edge_reads(tiny_ix, L, 120, rng)
     extra = [b"z" * L, b"n" * L, b"a" * L, (b"acgt" * 64)[:L], (b"c" * (L // 2) + b"z" + b"c" * L)[:L]]
     reads = np.concatenate([reads, np.array([np.frombuffer(x, np.uint8) for x in extra])])
-    for ml, lin in ((20, 2), (12, 2), (30, 2), (20, 1), (12, 1)):
-        got, _ = emu[0].map(reads, min_len=ml, lin_blocks=lin)
-        for i in range(len(reads)):
-            assert got[i] == tiny_ix.search(reads[i].tobytes(), min_len=ml), (ml, lin, i)
+    for e in (emu[0], emu[2]):
+        for ml, lin in ((20, 2), (12, 2), (30, 2), (20, 1), (12, 1)):
+            got, _ = e.map(reads, min_len=ml, lin_blocks=lin)
+            for i in range(len(reads)):
+                assert got[i] == tiny_ix.search(reads[i].tobytes(), min_len=ml), (e.packed, ml, lin, i)
 
 
 def test_state_machine_on_mid_genome():
@@ -82,11 +85,37 @@ def test_state_machine_on_mid_genome():
     lo = np.arange(256, dtype=np.uint8)
     lo[65:91] += 32
     reads = lo[reads]
-    emu = sm_emu.Emu(ix)
-    for lin in (2, 1):
-        got, _ = emu.map(reads, lin_blocks=lin)
-        for i in range(len(reads)):
-            assert got[i] == ix.search(reads[i].tobytes()), (lin, i)
+    for emu in (sm_emu.Emu(ix), sm_emu.Emu(ix, packed=True)):
+        for lin in (2, 1):
+            got, _ = emu.map(reads, lin_blocks=lin)
+            for i in range(len(reads)):
+                assert got[i] == ix.search(reads[i].tobytes()), (emu.packed, lin, i)
+
+
+def test_packed_words_cut_lines_on_mid_genome():
+    """The packed SA / ISA words (csrc/common.hpp) leave every match as it is
+    and cut the random lines per read: the BWT character, the L8 bytes around
+    a rank and 7 window bases come with the element the search loads anyway."""
+    import oracle as O
+    import synth
+    g = synth.make_genome("mid")
+    ix = O.Index(*O.text_from_contigs(g))
+    ix.accel()
+    r1, r2 = synth.make_reads(g, 1000, 150, seed=46)
+    reads = np.empty((2000, 150), np.uint8)
+    reads[0::2], reads[1::2] = r1, r2
+    lo = np.arange(256, dtype=np.uint8)
+    lo[65:91] += 32
+    reads = lo[np.where(reads == ord("N"), ord("Z"), reads).astype(np.uint8)]
+    plain, packed = sm_emu.Emu(ix, wide=True), sm_emu.Emu(ix, packed=True)
+    a, ia = plain.map(reads)
+    b, ib = packed.map(reads)
+    assert a == b
+    la = sum(v[1] for v in plain.counters.values())
+    lb = sum(v[1] for v in packed.counters.values())
+    assert lb < 0.9 * la, (la / len(reads), lb / len(reads))
+    assert packed.counters["lcp"][1] < 0.5 * plain.counters["lcp"][1]
+    assert ib.sum() < ia.sum()
 
 
 @pytest.mark.parametrize("pf", ["0", "1"])

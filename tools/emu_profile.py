@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--reads", type=int, default=4000)
     ap.add_argument("--len", type=int, default=150)
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--packed", action="store_true",
+                    help="the packed SA / ISA words (8-byte elements, as the device at hg19)")
     a = ap.parse_args()
     import smashgpu as S
     contigs, ix = load_index(a.genome)
@@ -55,7 +57,7 @@ def main():
     reads[0::2] = r1
     reads[1::2] = r2
     reads = S.prepare_reads(reads)
-    emu = sm_emu.Emu(ix, copy=False)
+    emu = sm_emu.Emu(ix, copy=False, packed=a.packed)
     t = time.time()
     got, iters = emu.map(reads)
     dt = time.time() - t

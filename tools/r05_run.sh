@@ -9,7 +9,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
 if [ "$WHAT" != bench ]; then
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread \
+  timeout -k 10 1050 python3 -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread \
       > "$O/tests.log" 2>&1
   timeout -k 10 150 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
 fi

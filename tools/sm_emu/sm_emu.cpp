@@ -229,7 +229,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
                const uint64_t *in_text, uint64_t N, uint64_t logN, const uint8_t *reads,
                uint64_t stride, uint32_t L, uint64_t n, uint32_t min_len, uint64_t *out,
                uint32_t cap, uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
-               uint64_t *viol, uint32_t lin_blocks, uint64_t *counters) {
+               uint64_t *viol, uint32_t lin_blocks, uint64_t *counters, int packed) {
   const sm::Geom g = sm::make_geom(L);
   if (g.w_row > sizeof(sm::ldsw) / 4) return -1;
   // direct rows (the device's path for native-row input, the default here as
@@ -258,6 +258,9 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   emu_T = T;
   c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);
   c.L8 = L8; c.U = U; c.KT = KT;
+  // packed index words (common.hpp): the SA / ISA arrays given carry them
+  c.pk = packed && sizeof(IdxT) == 8 ? 1u : 0u;
+  c.pm = c.pk ? kPkPosMask : ~0ull;
   (void)BM;   // (round 3: the filter's presence bits live in KT)
   c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
   c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
@@ -340,10 +343,10 @@ extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int
                           uint64_t logN, const uint8_t *reads, uint64_t stride, uint32_t L,
                           uint64_t n, uint32_t min_len, uint64_t *out, uint32_t cap,
                           uint32_t *n_out, uint32_t *iters, const uint64_t *spans,
-                          uint64_t *viol, uint32_t lin_blocks, uint64_t *counters) {
+                          uint64_t *viol, uint32_t lin_blocks, uint64_t *counters, int packed) {
   if (idx_bytes == 4)
     return run<uint32_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
-                         min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters);
+                         min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters, 0);
   return run<uint64_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
-                       min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters);
+                       min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters, packed);
 }

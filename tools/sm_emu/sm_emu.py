@@ -60,12 +60,59 @@ IDX_OPS = ("SAPOS", "SAPOS2", "BS_SA", "ISAJ", "NS_SA2", "NS_ISA2")
 CMP_OPS = ("EXT", "BS")
 
 
+POS_BITS = 33          # packed index words (smash-paper_amd/csrc/common.hpp)
+POS_MASK = (1 << POS_BITS) - 1
+WINDOW = 7
+
+
+def pack_words(T, SA, ISA, L8, K):
+    """The packed SA / ISA words (common.hpp layout; the device builds them in
+    pack_index.hip) from plain arrays, on the host: u64 SA and ISA whose
+    bits 33.. hold the BWT character / window tag, the L8 bytes around the
+    rank and 7 bases of T[x + K ..) (SA), and L8[r - 1 .. r + 2] (ISA)."""
+    N = len(SA)
+    assert N <= POS_MASK
+    x = np.asarray(SA, np.uint64)
+    lut = np.full(256, 255, np.uint8)
+    for i, ch in enumerate(b"acgt"):
+        lut[ch] = i
+    Tp = np.zeros(N + 64, np.uint8)
+    Tp[:N] = np.asarray(T[:N], np.uint8)
+    l8 = np.minimum(np.asarray(L8[:N], np.uint64), 127)
+    l8p = np.zeros(N + 4, np.uint64)
+    l8p[1:N + 1] = l8                      # l8p[r + 1] = L8[r], 0 outside [0, N)
+    xi = x.astype(np.int64)
+    bwt = np.where(xi > 0, lut[Tp[np.maximum(xi - 1, 0)]], 255).astype(np.uint64)
+    tag = np.where(bwt < 4, bwt, 4).astype(np.uint64)
+    win = np.zeros(N, np.uint64)
+    dirty = np.zeros(N, bool)
+    for i in range(WINDOW):
+        c = lut[Tp[np.minimum(xi + K + i, N + 63)]]
+        dirty |= c == 255
+        win |= (c.astype(np.uint64) & np.uint64(3)) << np.uint64(2 * i)
+    tag[dirty] = 5
+    win[dirty] = 0
+    r = np.arange(N, dtype=np.int64)
+    sa = (x | (tag << np.uint64(33)) | (l8p[r + 1] << np.uint64(36)) | (l8p[r + 2] << np.uint64(43))
+          | (win << np.uint64(50)))
+    ri = np.asarray(ISA, np.int64)
+    isa = (ri.astype(np.uint64) | (l8p[ri] << np.uint64(33)) | (l8p[ri + 1] << np.uint64(40))
+           | (l8p[ri + 2] << np.uint64(47)) | (l8p[ri + 3] << np.uint64(54)))
+    return sa, isa
+
+
 class Emu:
-    def __init__(self, ix, wide=False, copy=True):
+    def __init__(self, ix, wide=False, copy=True, packed=False):
         """ix: oracle.Index with accel() built; wide: run the 8-byte SA/ISA
         instantiation (the device uses it when N >= 2^32); copy=False uses the
-        index arrays in place (hg19-sized indexes: no second copy)."""
+        index arrays in place (hg19-sized indexes: no second copy); packed:
+        run with the packed index words (the device default at hg19) --
+        built here from ix's plain arrays, or ix's own when they are packed
+        already (ix.pos_mask, e.g. downloaded from the device)."""
         self.ix = ix
+        self.packed = bool(packed)
+        if packed:
+            wide = True
         self.keep = []
         self.spans = []
 
@@ -81,8 +128,13 @@ class Emu:
             return buf.ctypes.data
         self.T = P(ix.T, np.uint8)
         it = np.uint64 if wide else ix.SA.dtype
-        self.SA = P(ix.SA, it)
-        self.ISA = P(ix.ISA, it)
+        if packed and not getattr(ix, "pos_mask", None):
+            sa, isa = pack_words(ix.T, ix.SA, ix.ISA, ix.L8, ix.acc.K)
+            self.SA = P(sa, np.uint64)
+            self.ISA = P(isa, np.uint64)
+        else:
+            self.SA = P(ix.SA, it)
+            self.ISA = P(ix.ISA, it)
         self.L8 = P(ix.L8, np.uint8)
         self.U = P(ix._U, np.uint8)
         self.KT = P(ix._KTF, np.uint64)          # the device layout (orc_build_ktf)
@@ -114,7 +166,7 @@ class Emu:
             out.ctypes.data_as(C.c_void_p), C.c_uint32(cap),
             nout.ctypes.data_as(C.c_void_p), iters.ctypes.data_as(C.c_void_p),
             spans.ctypes.data_as(C.c_void_p), viol.ctypes.data_as(C.c_void_p),
-            C.c_uint32(lin_blocks), ctr.ctypes.data_as(C.c_void_p))
+            C.c_uint32(lin_blocks), ctr.ctypes.data_as(C.c_void_p), C.c_int(int(self.packed)))
         assert rc == 0
         assert viol[0] == 0, ("out-of-range probe", viol.tolist())
         res = []
