@@ -593,7 +593,8 @@ def main():
         from dist import ShardedCounter
         # the per-batch key counts are host integers: exchanged over gloo
         # they need no device synchronisation
-        sc = ShardedCounter(pipe, rank, world, dev, count_group=dist.new_group(backend="gloo"))
+        sc = ShardedCounter(pipe, rank, world, dev, count_group=dist.new_group(backend="gloo"),
+                            plan_pairs=P * world)
 
     resident = os.environ.get("SMASH_BENCH_RESIDENT", "1") != "0"   # (A/B)
     ahead2 = os.environ.get("SMASH_BENCH_AHEAD2", "1") != "0"       # (A/B, sharded step)

@@ -264,6 +264,20 @@ uint64_t smash_pipeline_max_batch(uint32_t read_len, uint32_t min_len);
 int smash_pipeline_create(const smash_index *ix, const smash_pipeline_cfg *cfg,
                           smash_pipeline **out);
 void smash_pipeline_free(smash_pipeline *p);
+/* Grow the persistent pair-key set (smashMEM.py:217-228's `seen`) to hold
+ * `keys` keys: a no-op when it does already; else only while it is empty
+ * (after create / reset, before the first de-dup), SMASH_ERR_ARG when it
+ * holds keys, SMASH_ERR_NOMEM when HBM cannot hold it.  Synchronous.  The
+ * multi-GPU driver sizes each owner's set from the run's pair count and the
+ * owner skew of its first batch (dist.py). */
+int smash_pipeline_reserve_keys(smash_pipeline *p, uint64_t keys, void *stream);
+/* The keys the set takes for sure (a full set is SMASH_ERR_NOMEM in the
+ * pipeline's statistics, never a silent cut). */
+uint64_t smash_pipeline_key_capacity(const smash_pipeline *p);
+/* The data error recorded so far (0: none; the error of smash_stats), as of
+ * the work queued on `stream`: waits for that stream only (not for a search
+ * running on the pipeline's own streams). */
+int smash_pipeline_error(smash_pipeline *p, void *stream, int32_t *err);
 
 /* One batch of n_pairs pairs: d_reads holds 2*n_pairs mates of cfg->read_len
  * bytes (rows of cfg->read_stride), mate 2q = read 1, 2q+1 = read 2 of pair q (Pair::run alternation,

@@ -1428,6 +1428,18 @@ PostCfg post_cfg(const smash_pipeline *p) {
 
 using namespace smash;
 
+// table slots and arena words for a key set of `keys` keys (at least the
+// batch's max_pairs): 2x the keys in power-of-two slots, 16 words per key
+static void key_set_geometry(uint64_t keys, uint64_t max_pairs, uint64_t *slots,
+                             uint64_t *arena_words) {
+  const uint64_t cap = 2 * std::max<uint64_t>(keys, max_pairs);
+  uint64_t pw = 1;
+  while (pw < cap) pw <<= 1;
+  *slots = pw;
+  *arena_words = std::min<uint64_t>(16 * std::max<uint64_t>(keys, max_pairs) + (1u << 20),
+                                    kRefPub - 2);
+}
+
 extern "C" uint64_t smash_pipeline_max_batch(uint32_t read_len, uint32_t min_len) {
   if (read_len == 0 || read_len > 255 || min_len < 2 || read_len < min_len) return 0;
   const uint64_t slots = read_len - min_len + 1;
@@ -1560,17 +1572,15 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
                                                  static_cast<int64_t *>(nullptr), LastValid(), P));
     p->temp_bytes = std::max(b, c3);
     p->d_temp = dalloc<uint8_t>(p->temp_bytes);
-    uint64_t cap = 2 * std::max<uint64_t>(cfg->dedup_capacity, P);
-    uint64_t pw = 1;
-    while (pw < cap) pw <<= 1;
+    // key records: 2 + nk words each; SMASH reads keep ~7 hits per pair, the
+    // arena holds 16 words per key of the capacity (an exhausted arena is a
+    // reported error, SMASH_ERR_NOMEM, never a silent cut; refs hold offset
+    // + 1 below kRefPub)
+    uint64_t pw = 0;
+    key_set_geometry(cfg->dedup_capacity, P, &pw, &p->arena_cap);
     p->table_mask = pw - 1;
     p->d_table = dalloc<uint64_t>(2 * pw);
     SMASH_HIPX(hipMemset(p->d_table, 0, 16 * pw));
-    // key records: 2 + nk words each; SMASH reads keep ~7 hits per pair, the
-    // arena holds 16 words per key of the capacity (an exhausted arena is a
-    // reported error, SMASH_ERR_NOMEM, never a silent cut)
-    p->arena_cap = std::min<uint64_t>(16 * std::max<uint64_t>(cfg->dedup_capacity, P) + (1u << 20),
-                                      kRefPub - 2);   // (refs hold offset + 1 below kRefPub)
     p->d_arena = dalloc<uint64_t>(p->arena_cap);
     p->d_arena_top = dalloc<unsigned long long>(1);
     SMASH_HIPX(hipMemset(p->d_arena_top, 0, 8));
@@ -2465,6 +2475,17 @@ extern "C" int smash_phase_import(smash_pipeline *p, const uint8_t *d_flags_back
   return SMASH_OK;
 }
 
+extern "C" int smash_pipeline_error(smash_pipeline *p, void *stream, int32_t *err) {
+  if (!p || !err) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(p->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // (the owner counts' pinned image is free here: phase_export has read it)
+  SMASH_HIP(hipMemcpyAsync(p->h_owner + 192, p->d_stats + S_ERR, 8, hipMemcpyDeviceToHost, s));
+  SMASH_HIP(hipStreamSynchronize(s));
+  *err = int32_t(p->h_owner[192]);
+  return SMASH_OK;
+}
+
 extern "C" int smash_pipeline_stats(smash_pipeline *p, smash_stats *o) {
   if (!p || !o) return SMASH_ERR_ARG;
   SMASH_HIP(hipSetDevice(p->device));
@@ -2500,6 +2521,44 @@ extern "C" int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_
   if (h_hits) SMASH_HIP(hipMemcpy(h_hits, p->d_hits, 8 * n * 2 * p->slots, hipMemcpyDeviceToHost));
   if (h_hash) SMASH_HIP(hipMemcpy(h_hash, p->d_hash, 16 * n, hipMemcpyDeviceToHost));
   return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_reserve_keys(smash_pipeline *p, uint64_t keys, void *stream) {
+  if (!p) return SMASH_ERR_ARG;
+  uint64_t slots = 0, words = 0;
+  key_set_geometry(keys, p->max_pairs, &slots, &words);
+  if (slots <= p->table_mask + 1 && words <= p->arena_cap) return SMASH_OK;
+  SMASH_HIP(hipSetDevice(p->device));
+  SMASH_HIP(hipDeviceSynchronize());   // (no kernel may hold the old set)
+  unsigned long long top = 0;
+  SMASH_HIP(hipMemcpy(&top, p->d_arena_top, 8, hipMemcpyDeviceToHost));
+  if (top) {
+    set_error("smash_pipeline_reserve_keys: the key set holds keys (reserve before the first batch)");
+    return SMASH_ERR_ARG;
+  }
+  uint64_t *t = nullptr, *a = nullptr;
+  if (hipMalloc(reinterpret_cast<void **>(&t), 16 * slots) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void **>(&a), 8 * words) != hipSuccess) {
+    (void)hipFree(t);
+    set_error("smash_pipeline_reserve_keys: out of device memory for " + std::to_string(keys) +
+              " keys");
+    return SMASH_ERR_NOMEM;
+  }
+  SMASH_HIP(hipFree(p->d_table));
+  SMASH_HIP(hipFree(p->d_arena));
+  p->d_table = t;
+  p->d_arena = a;
+  p->table_mask = slots - 1;
+  p->arena_cap = words;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * slots, s));
+  SMASH_HIP(hipStreamSynchronize(s));
+  return SMASH_OK;
+}
+
+extern "C" uint64_t smash_pipeline_key_capacity(const smash_pipeline *p) {
+  // keys the set takes for sure: half its slots, and 16 words of arena each
+  return p ? std::min<uint64_t>((p->table_mask + 1) / 2, p->arena_cap / 16) : 0;
 }
 
 extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {

@@ -84,14 +84,27 @@ class TorchComm:
         return [bytes(parts[r][:sizes[r]].cpu().numpy().tobytes()) for r in range(W)]
 
 
+class KeySetFull(RuntimeError):
+    """an owner's pair-key set overflowed (SMASH_ERR_NOMEM): counts past this
+    batch would count duplicates again, so the run stops here"""
+
+
 class ShardedCounter:
-    def __init__(self, pipe, rank, world, device, group=None, count_group=None, comm=None):
+    def __init__(self, pipe, rank, world, device, group=None, count_group=None, comm=None,
+                 plan_pairs=0, key_slack=1 << 20):
         """count_group: a CPU (gloo) process group for the per-batch key
         counts, which are host integers after smash_phase_export: exchanged
         there they cost no device synchronisation (None: over `group`).
         comm: the collectives (default TorchComm(device, group, count_group));
         tests pass an in-process transport to run W ranks of this exact step
-        on one device."""
+        on one device.
+        plan_pairs: the pairs of the whole run over all ranks (0: unknown).
+        An owner keeps every key it owns for the whole run, so after the
+        first batch's export each rank grows its key set to plan_pairs x
+        (its share of that batch's keys) x 1.125 + key_slack -- the owner
+        skew measured, not assumed uniform.  Either way a set that overflows
+        stops the run at the batch after the one that overflowed it
+        (KeySetFull), not after the pass."""
         self.pipe = pipe
         self.rank = rank
         self.world = world
@@ -99,6 +112,10 @@ class ShardedCounter:
         self.comm = comm if comm is not None else TorchComm(device, group, count_group)
         self.carried = torch.full((1,), -1, dtype=torch.int64, device=device)
         self.max_pairs = pipe.max_pairs
+        self.plan_pairs = int(plan_pairs)
+        self.key_slack = int(key_slack)
+        self.batch = 0          # batches stepped since the last reset
+        self.key_need = 0       # the first batch's projection (plan_pairs > 0)
         self.timing = {}
         self._t = None
 
@@ -115,11 +132,51 @@ class ShardedCounter:
     def reset(self):
         self.pipe.reset()
         self.carried.fill_(-1)
+        self.batch = 0
 
-    def _recv_counts(self, cnt, wcnt):
-        """what every rank sends me: [keys], [words] per source rank"""
-        rcl = self.comm.exchange_counts([[int(a), int(b)] for a, b in zip(cnt, wcnt)])
-        return [x[0] for x in rcl], [x[1] for x in rcl]
+    def _size_keys(self, sent, received):
+        """grow this owner's key set from the first batch's owner shares
+        (all ranks take part: the batch's key total is all-gathered)"""
+        tot = sum(int.from_bytes(b, "little")
+                  for b in self.comm.all_gather_bytes(int(sent).to_bytes(8, "little")))
+        if not tot:
+            return
+        self.key_need = int(self.plan_pairs * received / tot * 1.125) + self.key_slack
+        if self.key_need > self.pipe.key_capacity:
+            self.pipe.reserve_keys(self.key_need)
+
+    def _raise(self, err, batch, who):
+        import smashgpu as S
+        msg = ("pipeline data error %d (%s) on %s by batch %d; this rank's key capacity %d"
+               % (err, S.ERRORS.get(err, "?"), who, batch, self.pipe.key_capacity))
+        if err == S.SMASH_ERR_NOMEM:
+            raise KeySetFull(msg + " (raise dedup_capacity / the plan's pair count)")
+        raise S.SmashError(msg)
+
+    def finish(self):
+        """the run's end, on every rank together: raise (everywhere) if any
+        rank's last owner decisions recorded a data error"""
+        err = self.pipe.data_error()
+        errs = [int.from_bytes(b, "little", signed=True)
+                for b in self.comm.all_gather_bytes(int(err).to_bytes(8, "little", signed=True))]
+        if min(errs):
+            self._raise(min(errs), self.batch - 1,
+                        "rank %d" % self.rank if err else "rank %d" % errs.index(min(errs)))
+
+    def check_keys(self, batch=None):
+        """this rank alone (a run's end): raise KeySetFull if the owner
+        decisions queued so far recorded a full key set (waits for the
+        exchange stream only)"""
+        err = self.pipe.data_error()
+        if err:
+            self._raise(err, self.batch - 1 if batch is None else batch, "rank %d" % self.rank)
+
+    def _recv_counts(self, cnt, wcnt, err=0):
+        """what every rank sends me: [keys], [words] per source rank, and
+        the largest data error any rank reports (every rank sees every
+        rank's: all of them stop together)"""
+        rcl = self.comm.exchange_counts([[int(a), int(b), int(err)] for a, b in zip(cnt, wcnt)])
+        return [x[0] for x in rcl], [x[1] for x in rcl], min(x[2] for x in rcl)
 
     def step(self, d_reads, n_pairs, step_base, d_counts, next_reads=None, next_pairs=0,
              stride=None, next2_reads=None, next2_pairs=0):
@@ -145,9 +202,17 @@ class ShardedCounter:
         hdr, words, cnt, wcnt = p.phase_export(W, step_base + r * (n_pairs if stride is None
                                                                      else stride))
         self._mark("export")
-        if next_pairs and next2_pairs:
+        # the last batch's owner decision ran before this export, which
+        # synchronised its stream: its data error (a full key set) travels
+        # with the key counts, and every rank stops here together
+        err = p.data_error() if self.batch else 0
+        if next_pairs and next2_pairs and not err:
             p.phase_search_ahead(next2_reads, next2_pairs)
-        rcv, rcw = self._recv_counts(cnt, wcnt)
+        rcv, rcw, gerr = self._recv_counts(cnt, wcnt, err)
+        if gerr:
+            self._raise(gerr, self.batch - 1, "rank %d" % self.rank if err else "another rank")
+        if self.batch == 0 and self.plan_pairs:
+            self._size_keys(sum(int(x) for x in cnt), sum(rcv))
         self._mark("counts")
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
         n_recv, n_words = sum(rcv), sum(rcw)
@@ -172,6 +237,7 @@ class ShardedCounter:
         prev = self._prev(tails[:r], self.carried)
         p.phase_bin(prev, d_counts)
         self.carried = self._prev(tails, self.carried)
+        self.batch += 1
         self._mark("tails_bin")
 
     @staticmethod
@@ -253,4 +319,5 @@ def count_fastq(sc, index, batch, d_counts, look_ahead=True, pin=True):
         if not (look_ahead and s + 1 < steps) and s + 1 < steps:
             nxt = load(s + 1, k ^ 1)
         cur = nxt
+    sc.finish()
     return done

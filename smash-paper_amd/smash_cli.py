@@ -372,11 +372,16 @@ def _count_files_dist(args, bins, world):
     # placeholder counter carries the communicator for the scan exchange
     sc = ShardedCounter(_NoPipe(), rank, world, dev, count_group=cpu)
     fq = open_fastq(sc, r1, r2, sort_names=not args.presorted)
-    # an owner keeps the keys it owns for the whole run: ~pairs / world
+    # an owner keeps the keys it owns for the whole run: ~pairs / world to
+    # start with; unless --dedup-capacity fixes it, ShardedCounter grows each
+    # owner's set after the first batch's export to the run's pairs x that
+    # owner's measured share (a skewed owner is sized, not overflowed), and a
+    # set that still overflows stops every rank at the next batch
     cap = args.dedup_capacity or (fq.n // world + fq.n // (8 * world) + (1 << 20))
     pipe = S.Pipeline(ix, cs, starts, fq.L, args.batch, dedup_capacity=cap)
     counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
-    sc = ShardedCounter(pipe, rank, world, dev, count_group=cpu)
+    sc = ShardedCounter(pipe, rank, world, dev, count_group=cpu,
+                        plan_pairs=0 if args.dedup_capacity else fq.n)
     sc.reset()
     count_fastq(sc, fq, args.batch, counts)
     st = pipe.stats(raise_on_error=False)

@@ -62,6 +62,7 @@ EXPORTS = [
     "smash_fastq_shard_pack", "smash_fastq_shard_stats", "smash_fastq_shard_close",
     "smash_read_stride", "smash_pipeline_max_batch",
     "smash_mappability_prepare", "smash_mappability_window", "smash_index_pack",
+    "smash_pipeline_reserve_keys", "smash_pipeline_key_capacity", "smash_pipeline_error",
 ]
 
 
@@ -224,6 +225,10 @@ def lib():
     L.smash_read_stride.restype = C.c_uint32
     L.smash_mappability_prepare.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
     L.smash_index_pack.argtypes = [vp, C.c_int, vp]
+    L.smash_pipeline_reserve_keys.argtypes = [vp, C.c_uint64, vp]
+    L.smash_pipeline_key_capacity.argtypes = [vp]
+    L.smash_pipeline_key_capacity.restype = C.c_uint64
+    L.smash_pipeline_error.argtypes = [vp, vp, C.POINTER(C.c_int32)]
     L.smash_mappability_window.argtypes = [vp, C.c_uint64, C.c_uint64, u64p, u64p]
     L.smash_pipeline_max_batch.argtypes = [C.c_uint32, C.c_uint32]
     L.smash_pipeline_max_batch.restype = C.c_uint64
@@ -602,6 +607,24 @@ class Pipeline:
     def reset(self, stream=None):
         check(lib().smash_pipeline_reset(self.h, vp(_stream(stream))), "smash_pipeline_reset")
 
+    @property
+    def key_capacity(self):
+        """keys the persistent pair-key set takes for sure"""
+        return int(lib().smash_pipeline_key_capacity(self.h))
+
+    def reserve_keys(self, keys, stream=None):
+        """grow the (empty) key set to `keys` keys (smash_pipeline_reserve_keys)"""
+        check(lib().smash_pipeline_reserve_keys(self.h, int(keys), vp(_stream(stream))),
+              "smash_pipeline_reserve_keys")
+
+    def data_error(self, stream=None):
+        """the data error recorded by the work queued on `stream` (0: none);
+        waits for that stream only (smash_pipeline_error)"""
+        e = C.c_int32()
+        check(lib().smash_pipeline_error(self.h, vp(_stream(stream)), C.byref(e)),
+              "smash_pipeline_error")
+        return int(e.value)
+
     def stats(self, raise_on_error=True):
         """Counters of the run so far.  A data error the device recorded (the
         mappability_tag throw, a full key set) raises SmashError unless
@@ -974,6 +997,7 @@ class FastqIndex:
             pass
 
 
+SMASH_ERR_NOMEM = -4
 SMASH_ERR_UNSUPPORTED = -5
 
 

@@ -4,6 +4,7 @@ exchange code (smash-paper_amd/dist.py) over torch.distributed/gloo with
 world_size 2 on the CPU, checking its collectives, shard bookkeeping and the
 adjacent-dup boundary against a single-process oracle run."""
 import hashlib
+import os
 
 import numpy as np
 import torch
@@ -15,6 +16,9 @@ def key_hash(key):
     d = hashlib.blake2b(repr(key).encode(), digest_size=16).digest()
     hi = int.from_bytes(d[:8], "little") | 1
     lo = int.from_bytes(d[8:], "little") | 1
+    bits = int(os.environ.get("SMASH_KEY_HASH_BITS", "0") or 0)   # (as the library: tests)
+    if 0 < bits < 64:
+        hi = (hi & ((1 << bits) - 1)) | 1
     return hi, lo
 
 
@@ -27,10 +31,12 @@ def to_u64(i):
 
 
 class OraclePhasePipeline:
-    def __init__(self, oix, mapbin, chrom_sizes, bin_starts, max_pairs):
+    def __init__(self, oix, mapbin, chrom_sizes, bin_starts, max_pairs, key_capacity=1 << 40):
         self.oix = oix
         self.map = mapbin
         self.max_pairs = max_pairs
+        self.key_capacity = key_capacity   # smash_pipeline_key_capacity
+        self.error = 0
         sizes = [int(x) for x in oix.sizes[0::2]]
         self.offs = np.cumsum([0] + sizes[:-1]).astype(np.uint32)
         self.small = [1 if ("_gl000" in c or "chrM" in c) else 0 for c in oix.contigs]
@@ -42,6 +48,14 @@ class OraclePhasePipeline:
     def reset(self):
         self.seen = set()
         self.total = self.dups = self.kept = 0
+        self.error = 0
+
+    def reserve_keys(self, keys):
+        assert not self.seen, "smash_pipeline_reserve_keys: the set holds keys"
+        self.key_capacity = max(self.key_capacity, int(keys))
+
+    def data_error(self, stream=None):
+        return self.error
 
     def phase_map(self, d_reads, n_pairs):
         reads = d_reads.numpy()
@@ -114,6 +128,8 @@ class OraclePhasePipeline:
             if k not in self.seen:
                 flags[j] = 1
         self.seen.update(best.keys())
+        if len(self.seen) > self.key_capacity:
+            self.error = -4   # SMASH_ERR_NOMEM: the device's full set (k_owner_claim)
         if n_recv:
             d_flags[:n_recv] = torch.from_numpy(flags)
 

@@ -200,3 +200,113 @@ def test_file_fed_ranks_match_single_process(world, batch, tiny_ix, tmp_path):
     assert op.run(reads, threads=4) == 0
     assert got_counts == op.counts.tolist()
     assert got_stats == [op.state.total, op.state.dups, op.state.kept, reads.shape[0] // 2]
+
+
+def _worker_keys(rank, world, port, per_rank, steps, cap, plan, out_q):
+    """W ranks with the key hash cut to 2 bits (owners 0 and 1 only: a 1.5x
+    skew at W = 3) and a key set of `cap` keys: plan = 0 keeps it (the run
+    must stop with KeySetFull right after the batch that overflows it),
+    plan > 0 lets ShardedCounter size it from the first batch's owner shares"""
+    import sys
+    for p in ("oracle", "tools", "tests", "smash-paper_amd"):
+        sys.path.insert(0, os.path.join(ROOT, p))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["SMASH_KEY_HASH_BITS"] = "2"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gzip, tempfile
+    import oracle as O
+    from mock_pipeline import OraclePhasePipeline
+    from dist import KeySetFull, ShardedCounter
+    d = tempfile.mkdtemp()
+    fa = os.path.join(d, "tiny.fa")
+    with gzip.open(gold("tiny.fa.gz"), "rb") as f, open(fa, "wb") as g:
+        g.write(f.read())
+    oix = O.Index.from_fasta(fa)
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    pipe = OraclePhasePipeline(oix, oix.mappability(), cs, starts, per_rank, key_capacity=cap)
+    sc = ShardedCounter(pipe, rank, world, torch.device("cpu"), plan_pairs=plan, key_slack=8)
+    reads = interleaved_reads("s100")
+    counts = torch.zeros(len(starts), dtype=torch.int64)
+    sc.reset()
+    failed = -1
+    try:
+        for s_ in range(steps):
+            base = s_ * world * per_rank
+            lo = base + rank * per_rank
+            sc.step(torch.from_numpy(reads[2 * lo:2 * (lo + per_rank)].copy()), per_rank, base,
+                    counts)
+        sc.finish()
+    except KeySetFull:
+        failed = sc.batch
+    f = torch.tensor([failed, len(pipe.seen), pipe.key_capacity], dtype=torch.int64)
+    fs = [torch.empty_like(f) for _ in range(world)]
+    dist.all_gather(fs, f)
+    if failed < 0:
+        dist.all_reduce(counts)
+        st = torch.tensor([pipe.total, pipe.dups, pipe.kept], dtype=torch.int64)
+        dist.all_reduce(st)
+    else:
+        st = torch.zeros(3, dtype=torch.int64)
+    if rank == 0:
+        out_q.put(([x.tolist() for x in fs], counts.numpy().tolist(), st.tolist()))
+    dist.destroy_process_group()
+
+
+def _run_keys(world, per_rank, steps, cap, plan):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker_keys, args=(r, world, port, per_rank, steps, cap, plan, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    import queue as _queue
+    res = None
+    for _ in range(600):
+        try:
+            res = q.get(timeout=1)
+            break
+        except _queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        if res is None:
+            p.terminate()
+        p.join(timeout=60)
+    assert res is not None, [p.exitcode for p in procs]
+    return res
+
+
+def test_skewed_owner_overflow_stops_at_the_first_batch():
+    """SMASH_KEY_HASH_BITS=2 at W = 3: owners 0 and 1 hold every key.  A set
+    sized for the uniform share overflows in batch 0, and the step of batch 1
+    stops the run (KeySetFull, smash_pipeline_error) -- not the end of the
+    pass; rank 2 owns nothing and stops with the others at the same batch."""
+    per_rank, steps = 100, 4
+    fs, _, _ = _run_keys(3, per_rank, steps, cap=per_rank // 3, plan=0)
+    failed = [f[0] for f in fs]
+    assert fs[2][1] == 0                          # owner 2 holds no key
+    assert max(f[1] for f in fs[:2]) > per_rank // 3
+    assert failed == [1, 1, 1], fs                # every rank stops in batch 1's step
+
+
+def test_key_set_sized_from_plan_and_first_batch_skew(tiny_ix):
+    """plan_pairs given: after batch 0's export every owner grows its set to
+    its measured share of the run (owners 0 and 1: ~1/2 each, not 1/3), the
+    run completes and equals the single-process chain."""
+    import oracle as O
+    per_rank, steps, world = 100, 4, 3
+    n = world * per_rank * steps
+    fs, counts, st = _run_keys(world, per_rank, steps, cap=per_rank // 3, plan=n)
+    assert all(f[0] < 0 for f in fs), fs
+    assert all(f[1] <= f[2] for f in fs)
+    assert fs[0][2] > n // 3 and fs[1][2] > n // 3   # grown past the uniform share
+    reads = interleaved_reads("s100")[:2 * n]
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    op = O.Pipeline(tiny_ix, tiny_ix.mappability(), cs, starts)
+    assert op.run(reads, threads=4) == 0
+    assert counts == op.counts.tolist()
+    assert st == [op.state.total, op.state.dups, op.state.kept]
