@@ -62,6 +62,11 @@ CONFIGS = {
     "c5": dict(genome="hg19", bins="50000", k=36,
                workload="C5 hg19-shaped mappability self-scan (map.bin + unique 36-mer "
                         "counts per chromosome and per 50 k bin)"),
+    # -maxmatch (longSA::findMEM) on C3's reads: the search mode north_star
+    # names beside MAM, timed alone (not on the SMASH path)
+    "c3mem": dict(genome="hg19", read_len=150, pairs=1_000_000, bins="50000", seed=3, cap=512,
+                  workload="MEM (memsam -maxmatch, longSA::findMEM) of C3's 150 bp SMASH reads "
+                           "on hg19, 2 M reads per launch"),
     # quick functional run
     "mid": dict(genome="mid", read_len=150, pairs=200_000, batch=200_000, bins="synthetic",
                 seed=2, workload="3.2 Mbp synthetic genome, 150 bp (functional check)"),
@@ -346,6 +351,117 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
+def bench_mem(args, cfg, world, rank, local, dist):
+    """--config c3mem: MEM (-maxmatch) of C3-style reads (csrc/mem.hip,
+    smash_match_batch SMASH_MODE_MEM), every launch over all the rank's reads;
+    roofline from the line transitions of mem.hip's own probe sequence
+    (oracle orc_mem_dev: the k-mer table from the root, 8-byte singleton
+    compares, counted) on a sample; CPU baseline the reference's probe
+    sequence (orc_mem, the oracle) on the host's cores; the device's records
+    of a sample equal the oracle's, in emission order."""
+    import torch
+    import smashgpu as S
+    import synth
+    import readgen
+    import oracle as O
+    dev = torch.device("cuda", local)
+    contigs = synth.make_genome(cfg["genome"])
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    dix = S.Index.create(T, sp, sz, names, device=local)
+    log("device index: %.1f s" % dix.info.build_seconds)
+    P, L, cap = cfg["pairs"], cfg["read_len"], cfg["cap"]
+    n = 2 * P
+    d_reads = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000 + rank).generate(P)
+    out = torch.zeros(n * cap * 2, dtype=torch.int64, device=dev)
+    nn = torch.zeros(n, dtype=torch.int32, device=dev)
+
+    def launch():
+        S.match_batch(dix, d_reads, n, L, out, cap, nn, mode="MEM")
+
+    for _ in range(max(1, args.warmup)):
+        launch()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        ev[2 * i].record()
+        launch()
+        ev[2 * i + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.steps)) / args.steps
+    counts = nn.cpu().numpy()
+    value = n * world * args.steps / el
+    log("MEM: %d reads x %d launches in %.3f s -> %.3e reads/s; %.1f ms per launch; %.1f MEMs "
+        "per read (max %d, cap %d)" % (n, args.steps, el, value, kms, counts.mean(), counts.max(),
+                                       cap))
+    res = {"metric": "reads/sec MEM search (memsam -maxmatch, hg19, 150 bp)", "value": value,
+           "unit": "reads/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64 (integer)",
+           "data": "synthetic (tools/synth.py hg19-shaped genome; SMASH reads generated on the "
+                   "device, tools/readgen.hip, seeded)",
+           "config": {"workload": cfg["workload"], "genome": cfg["genome"], "reads": n,
+                      "read_len": L, "cap_per_read": cap, "kernel": "k_mem (csrc/mem.hip)",
+                      "parallelism": "dp%d: read shards" % world},
+           "mems_per_read": round(float(counts.mean()), 2), "mems_max": int(counts.max()),
+           "records_cut": int((counts > cap).sum()), "roofline": None, "cpu_baseline": None}
+    if rank == 0:
+        t2 = time.time()
+        ns = 2000
+        sample = d_reads[:ns].cpu().numpy()
+        oix, _ = host_index(S, O, dix, T, sp, sz, names, sample_reads=sample)
+        log("host copy of the index: %.1f s" % (time.time() - t2))
+        _, per, ctr = O.mem_batch(oix, sample, threads=host_cores()[0], device_probes=True,
+                                  count=True)
+        lines = {"text": ctr.ref_lines / ns, "sa": ctr.sa_lines / ns, "isa": ctr.isa_lines / ns,
+                 "lcp": ctr.lcp_lines / ns, "kmer": ctr.kt_lines / ns}
+        b_read = 64.0 * sum(lines.values())
+        achieved = n * b_read / (kms / 1e3) / 1e9
+        res["roofline"] = {
+            "bound": "hbm", "kernel": "k_mem", "achieved": round(achieved, 2), "peak": 8000.0,
+            "unit": "GB/s", "frac": round(achieved / 8000.0, 5), "traffic": None,
+            "bytes_per_read": round(b_read, 1), "avg_kernel_ms": round(kms, 3),
+            "lines_per_read": {k: round(v, 2) for k, v in lines.items()},
+            "lines_G_per_s": round(n * sum(lines.values()) / (kms / 1e3) / 1e9, 2),
+            "bytes_method": "64 B x line transitions of mem.hip's probe sequence (oracle "
+                            "orc_mem_dev on the downloaded index, %d reads)" % ns}
+        # the device's records == the oracle's, in emission order
+        o = out.view(n, 2 * cap)[:200].cpu().numpy().view(np.uint64)
+        same = all(S.unpack_records(o[i], counts[i], cap) == oix.search(sample[i].tobytes(),
+                                                                         mode="MEM")
+                   for i in range(200))
+        res["records_identical_to_oracle"] = bool(same and (per[:200] == counts[:200]).all())
+        if not args.no_cpu_baseline:
+            threads, note = host_cores()
+            t3 = time.perf_counter()
+            O.mem_batch(oix, sample[:64 * threads], threads=threads)
+            dt0 = time.perf_counter() - t3
+            m = int(min(n, max(64 * threads, 64 * threads * args.cpu_seconds / max(dt0, 1e-3))))
+            h = d_reads[:m].cpu().numpy()
+            t3 = time.perf_counter()
+            O.mem_batch(oix, h, threads=threads)
+            dt = time.perf_counter() - t3
+            res["cpu_baseline"] = {"value": m / dt, "unit": "reads/s", "cores": threads,
+                                   "kind": "port",
+                                   "sample": "%d reads of the same reads, longSA::findMEM "
+                                             "restated (oracle orc_mem, %d threads), %.1f s"
+                                             % (m, threads, dt),
+                                   "cores_note": note}
+            log("MEM cpu baseline: %.3e reads/s on %d threads" % (m / dt, threads))
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def fit_batch(B, P, L, free, min_len=20, headroom=12 << 30, nbins=50_000, max_batch=None):
     """the largest batch ceil(P / k) <= B (k = 1, 2, ...) whose pipeline
     buffers leave `headroom` of the free HBM: two search sets' match rows and
@@ -537,6 +653,8 @@ def main():
     torch.cuda.set_device(dev)
     if args.config == "c5":
         return bench_c5(args, cfg, world, rank, local, dist)
+    if args.config == "c3mem":
+        return bench_mem(args, cfg, world, rank, local, dist)
 
     t0 = time.time()
     contigs = synth.make_genome(cfg["genome"])

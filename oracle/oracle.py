@@ -102,6 +102,13 @@ def lib():
             getattr(L, fn).argtypes = [C.POINTER(OrcIndex), u8p, C.c_uint32,
                                        C.c_uint32, C.POINTER(OrcMatch),
                                        C.c_uint32, C.POINTER(OrcCounters)]
+        L.orc_mem_dev.argtypes = [C.POINTER(OrcIndex), C.POINTER(OrcAccel), u8p, C.c_uint32,
+                                  C.c_uint32, C.POINTER(OrcMatch), C.c_uint32,
+                                  C.POINTER(OrcCounters)]
+        L.orc_mem_batch.argtypes = [C.POINTER(OrcIndex), C.POINTER(OrcAccel), u8p, C.c_uint32,
+                                    C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, u32p,
+                                    C.POINTER(OrcCounters)]
+        L.orc_mem_batch.restype = C.c_uint64
         L.orc_resolve.argtypes = [C.POINTER(OrcIndex), u8p, C.c_uint32,
                                   C.POINTER(OrcMatch), C.c_uint32,
                                   C.POINTER(OrcHit), C.c_uint32, u32p, i64p]
@@ -261,11 +268,13 @@ class Index:
 
     def search(self, read: bytes, mode="MAM", min_len=20, counters=None):
         P = np.frombuffer(read, np.uint8)
-        fn = {"MAM": lib().orc_mam, "MEM": lib().orc_mem, "MUM": lib().orc_mum}[mode]
+        fn = {"MAM": lib().orc_mam, "MEM": lib().orc_mem, "MUM": lib().orc_mum,
+              "MEM_DEV": lib().orc_mem_dev}[mode]
         cap = 512
         while True:
             out = (OrcMatch * cap)()
-            n = fn(C.byref(self.c), _p(P, u8p), len(P), min_len, out, cap,
+            extra = (C.byref(self.acc),) if mode == "MEM_DEV" else ()
+            n = fn(C.byref(self.c), *extra, _p(P, u8p), len(P), min_len, out, cap,
                    C.byref(counters) if counters is not None else None)
             if n <= cap:
                 break
@@ -447,6 +456,23 @@ def map_only(ix: Index, reads: np.ndarray, min_len=20, threads=1):
     reads = np.ascontiguousarray(reads, np.uint8)
     return int(lib().orc_map_only(C.byref(ix.c), _p(reads, u8p), reads.shape[1],
                                   reads.shape[1], reads.shape[0], min_len, threads, None))
+
+
+def mem_batch(ix: Index, reads: np.ndarray, min_len=20, threads=1, device_probes=False,
+              count=False):
+    """longSA::findMEM (-maxmatch) over every read on `threads` host threads:
+    the reference's probe sequence, or (device_probes) smash-paper_amd/csrc/
+    mem.hip's (k-mer table from the root, 8-byte singleton compares; needs
+    ix.accel()) -- the same matches.  Returns (total, per-read counts,
+    counters or None)."""
+    reads = np.ascontiguousarray(reads, np.uint8)
+    n, L = reads.shape
+    ctr = OrcCounters() if count else None
+    per = np.zeros(n, np.uint32)
+    tot = lib().orc_mem_batch(C.byref(ix.c), C.byref(ix.acc) if device_probes else None,
+                              _p(reads, u8p), L, L, n, min_len, threads, _p(per, u32p),
+                              C.byref(ctr) if ctr is not None else None)
+    return int(tot), per, ctr
 
 
 def map_only_fast(ix: Index, reads: np.ndarray, min_len=20, threads=1, count=False):

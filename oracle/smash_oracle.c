@@ -445,16 +445,92 @@ static void collect_mems(const ctx_t *x, sink_t *s, const uint8_t *P,
   }
 }
 
+static int acgt(uint8_t c);
+
+/* traverse as smash-paper_amd/csrc/mem.hip's traverse_x runs it (same
+ * outcome, fewer probes): (C) a descent from the root with K ACGT bases
+ * available starts at depth K from the k-mer table (one 16-byte entry);
+ * (A) a singleton extends by comparing the read with the text 8 bytes per
+ * load (load8: the aligned 8-byte word(s) holding them).  Counted like the
+ * device loads them: one k-mer-table line, text lines per aligned word. */
+static void traverse_dev(const ctx_t *x, const orc_accel *acc, const uint8_t *P, uint64_t L,
+                         uint64_t prefix, ival_t *cur, uint64_t limit) {
+  const uint64_t N = x->ix->N;
+  const uint32_t K = acc->K;
+  if (cur->depth >= limit) return;
+  if (cur->depth == 0 && cur->start == 0 && cur->end == N - 1 && K > 0 && K <= limit &&
+      prefix + K <= L) {
+    uint64_t w = 0;
+    int ok = 1;
+    for (uint32_t k = 0; k < K; ++k) {
+      const int v = acgt(P[prefix + k]);
+      ok = ok && v >= 0;
+      w = (w << 2) | (uint64_t)(v & 3);
+    }
+    if (ok) {
+      if (x->c) tick(&x->c->sa_loads, &x->c->kt_lines, &x->c->last_kt, 16 * w);
+      const uint64_t lo = acc->KT[2 * w] & ((1ull << 40) - 1);
+      const uint64_t hi = acc->KT[2 * w + 1] & ((1ull << 40) - 1);
+      if (lo <= hi) {
+        cur->depth = K; cur->start = lo; cur->end = hi;
+        if (cur->depth == limit) return;
+      }
+    }
+  }
+  while (prefix + cur->depth < L) {
+    if (cur->start == cur->end) {                                  /* (A) */
+      const uint64_t pos = SAat(x, cur->start);
+      while (prefix + cur->depth < L && cur->depth < limit) {
+        const uint64_t rr = L - prefix - cur->depth, rl = limit - cur->depth;
+        const uint64_t rem = rr < rl ? rr : rl;
+        const uint32_t lim = rem < 8 ? (uint32_t)rem : 8u;
+        const uint64_t a = pos + cur->depth;
+        if (x->c) {
+          tick(&x->c->ref_loads, &x->c->ref_lines, &x->c->last_ref, a & ~7ull);
+          if (a & 7) tick(&x->c->ref_loads, &x->c->ref_lines, &x->c->last_ref, (a & ~7ull) + 8);
+        }
+        uint32_t k = 0;
+        while (k < lim && x->ix->T[a + k] == P[prefix + cur->depth + k]) ++k;
+        cur->depth += k;
+        if (k < lim) break;
+      }
+      return;
+    }
+    uint64_t s = cur->start, e = cur->end;
+    if (!td_faster(x, (int64_t)(int8_t)P[prefix + cur->depth], cur->depth, &s, &e)) return;
+    cur->depth += 1;
+    cur->start = s;
+    cur->end = e;
+    if (cur->depth == limit) return;
+  }
+}
+
+static int mem_core(const orc_index *ix, const orc_accel *acc, const uint8_t *P, uint32_t L,
+                    uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr);
+
 int orc_mem(const orc_index *ix, const uint8_t *P, uint32_t L,
             uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr) {
+  return mem_core(ix, NULL, P, L, min_len, out, cap, ctr);
+}
+
+int orc_mem_dev(const orc_index *ix, const orc_accel *acc, const uint8_t *P, uint32_t L,
+                uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr) {
+  return mem_core(ix, acc, P, L, min_len, out, cap, ctr);
+}
+
+/* findMEM (longSA.cpp:395-431); acc: mem.hip's traverse (traverse_dev) */
+static int mem_core(const orc_index *ix, const orc_accel *acc, const uint8_t *P, uint32_t L,
+                    uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr) {
   if (min_len < 1) return 0;                           /* longSA.cpp:588 */
   ctx_t x = mkctx(ix, ctr);
   sink_t s = {out, cap, 0};
   const uint64_t N = ix->N;
   uint64_t prefix = 1;                                 /* longSA.cpp:398 */
   ival_t mli = {0, 0, N - 1}, xmi = {0, 0, N - 1};
+#define TRAV(cur, lim) (acc ? traverse_dev(&x, acc, P, L, prefix, cur, lim) \
+                            : traverse(&x, P, L, prefix, cur, lim))
   while (prefix <= L) {
-    traverse(&x, P, L, prefix, &mli, min_len);
+    TRAV(&mli, min_len);
     if (mli.depth > xmi.depth) xmi = mli;
     if (mli.depth <= 1) {
       mli.depth = 0; mli.start = 0; mli.end = N - 1;
@@ -463,7 +539,7 @@ int orc_mem(const orc_index *ix, const uint8_t *P, uint32_t L,
       continue;
     }
     if (mli.depth >= min_len) {
-      traverse(&x, P, L, prefix, &xmi, L);
+      TRAV(&xmi, L);
       collect_mems(&x, &s, P, min_len, prefix, mli, xmi);
       ++prefix;
       if (!suffixlink(&x, &mli)) {
@@ -482,7 +558,69 @@ int orc_mem(const orc_index *ix, const uint8_t *P, uint32_t L,
       xmi = mli;
     }
   }
+#undef TRAV
   return (int)s.n;
+}
+
+/* MEM (-maxmatch) over n reads on `threads` host threads: the reference's
+ * probe sequence (acc == NULL, orc_mem) or mem.hip's (orc_mem_dev); per-read
+ * match counts into n_out (or NULL); returns the matches found */
+typedef struct {
+  const orc_index *ix;
+  const orc_accel *acc;
+  const uint8_t *reads;
+  uint32_t L, min_len;
+  uint64_t stride, begin, end, total;
+  uint32_t *n_out;
+  orc_counters ctr;
+  int count;
+} memjob_t;
+
+static void *mem_worker(void *arg) {
+  memjob_t *j = (memjob_t *)arg;
+  orc_match m[64];
+  memset(&j->ctr, 0, sizeof(j->ctr));
+  j->ctr.last_sa = j->ctr.last_isa = j->ctr.last_ref = j->ctr.last_lcp = ~0ull;
+  j->ctr.last_kt = j->ctr.last_u = j->ctr.last_bm = ~0ull;
+  for (uint64_t q = j->begin; q < j->end; ++q) {
+    const int n = mem_core(j->ix, j->acc, j->reads + q * j->stride, j->L, j->min_len, m, 64,
+                           j->count ? &j->ctr : NULL);
+    if (j->n_out) j->n_out[q] = (uint32_t)n;
+    j->total += (uint64_t)n;
+  }
+  return NULL;
+}
+
+uint64_t orc_mem_batch(const orc_index *ix, const orc_accel *acc, const uint8_t *reads,
+                       uint32_t L, uint64_t stride, uint64_t n, uint32_t min_len, int threads,
+                       uint32_t *n_out, orc_counters *ctr) {
+  if (threads < 1) threads = 1;
+  if (threads > 1024) threads = 1024;
+  pthread_t th[1024];
+  memjob_t *jobs = (memjob_t *)calloc((size_t)threads, sizeof(memjob_t));
+  for (int t = 0; t < threads; ++t) {
+    jobs[t].ix = ix; jobs[t].acc = acc; jobs[t].reads = reads; jobs[t].L = L;
+    jobs[t].min_len = min_len; jobs[t].stride = stride; jobs[t].n_out = n_out;
+    jobs[t].begin = n * (uint64_t)t / (uint64_t)threads;
+    jobs[t].end = n * (uint64_t)(t + 1) / (uint64_t)threads;
+    jobs[t].count = ctr != NULL;
+    pthread_create(&th[t], NULL, mem_worker, &jobs[t]);
+  }
+  uint64_t total = 0;
+  if (ctr) memset(ctr, 0, sizeof(*ctr));
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    total += jobs[t].total;
+    if (ctr) {
+      ctr->sa_loads += jobs[t].ctr.sa_loads; ctr->sa_lines += jobs[t].ctr.sa_lines;
+      ctr->isa_loads += jobs[t].ctr.isa_loads; ctr->isa_lines += jobs[t].ctr.isa_lines;
+      ctr->ref_loads += jobs[t].ctr.ref_loads; ctr->ref_lines += jobs[t].ctr.ref_lines;
+      ctr->lcp_loads += jobs[t].ctr.lcp_loads; ctr->lcp_lines += jobs[t].ctr.lcp_lines;
+      ctr->ovf_lookups += jobs[t].ctr.ovf_lookups; ctr->kt_lines += jobs[t].ctr.kt_lines;
+    }
+  }
+  free(jobs);
+  return total;
 }
 
 static int by_ref_cmp(const void *a, const void *b) {   /* longSA.cpp:492-499 */

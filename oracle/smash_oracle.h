@@ -137,6 +137,15 @@ int orc_mam(const orc_index *ix, const uint8_t *P, uint32_t L,
  * (starts at prefix 1). */
 int orc_mem(const orc_index *ix, const uint8_t *P, uint32_t L,
             uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr);
+/* mem.hip's probe sequence for the same matches (k-mer table from the root,
+ * 8-byte singleton compares): the device MEM path's algorithmic lines */
+int orc_mem_dev(const orc_index *ix, const orc_accel *acc, const uint8_t *P, uint32_t L,
+                uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr);
+/* MEM over n reads on `threads` threads (acc NULL: orc_mem, else orc_mem_dev);
+ * per-read counts into n_out (or NULL); returns the total */
+uint64_t orc_mem_batch(const orc_index *ix, const orc_accel *acc, const uint8_t *reads,
+                       uint32_t L, uint64_t stride, uint64_t n, uint32_t min_len, int threads,
+                       uint32_t *n_out, orc_counters *ctr);
 /* longSA::MUM (longSA.cpp:549-585). */
 int orc_mum(const orc_index *ix, const uint8_t *P, uint32_t L,
             uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr);

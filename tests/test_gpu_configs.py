@@ -429,6 +429,31 @@ def test_c5_prepare_rebuilds_u_full_genome(hg19, hg19_oracle, monkeypatch):
         torch.cuda.synchronize()
 
 
+def test_c3_mem_hg19_equals_oracle(hg19, hg19_oracle):
+    """-maxmatch (memsam's MEM mode, csrc/mem.hip, smash_match_batch) at hg19
+    on 20 k of C3's 150 bp SMASH reads: every read's MEM count equals the
+    oracle's restatement of longSA::findMEM (longSA.cpp:395-490), and the
+    records of the first 4 000 reads equal it in emission order."""
+    import readgen
+    contigs, _, dix = hg19
+    oix, _ = hg19_oracle
+    P, L, cap = 10_000, 150, 1024
+    n = 2 * P
+    d = readgen.Generator(dix, contigs, L, seed=77).generate(P)
+    out = torch.zeros(n * cap * 2, dtype=torch.int64, device="cuda")
+    nn = torch.zeros(n, dtype=torch.int32, device="cuda")
+    S.match_batch(dix, d, n, L, out, cap, nn, mode="MEM")
+    torch.cuda.synchronize()
+    h = d.cpu().numpy()
+    got_n = nn.cpu().numpy()
+    tot, per, _ = O.mem_batch(oix, h, threads=THREADS)
+    assert got_n.tolist() == per.tolist()
+    assert got_n.max() <= cap and tot > n          # several MEMs per SMASH read
+    o = out.view(n, 2 * cap)[:4000].cpu().numpy().view(np.uint64)
+    for i in range(4000):
+        assert S.unpack_records(o[i], got_n[i], cap) == oix.search(h[i].tobytes(), mode="MEM"), i
+
+
 # ---------------------------------------------------------------------------
 # idx8 on the mid genome: the 64-bit search and chain vs an independent oracle
 # ---------------------------------------------------------------------------

@@ -61,3 +61,40 @@ def test_fast_search_equals_plain_on_mid_genome():
     n3, k3 = O.map_only_v3(ix, reads, threads=4, count=True)
     assert n1 == n2 == n3
     assert k3.lines() < k2.lines() < k1.lines()     # the point of the accelerators
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_device_mem_probes_match_reference_goldens(tiny_ix, s):
+    """orc_mem_dev (csrc/mem.hip's probe sequence: the k-mer table from the
+    root, 8-byte singleton compares) emits the compiled reference's -maxmatch
+    triples in order, like orc_mem; the threaded batch agrees read by read
+    and counts fewer probe lines than the reference's sequence."""
+    tiny_ix.accel()
+    exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+           for l in read_gz_lines("%s_MEM.txt.gz" % s)]
+    reads = interleaved_reads(s)[:len(exp)]
+    for i, e in enumerate(exp):
+        assert tiny_ix.search(reads[i].tobytes(), mode="MEM_DEV") == e, i
+    t0, p0, c0 = O.mem_batch(tiny_ix, reads, threads=3, count=True)
+    t1, p1, c1 = O.mem_batch(tiny_ix, reads, threads=3, device_probes=True, count=True)
+    assert t0 == t1 == sum(len(e) for e in exp)
+    assert p0.tolist() == p1.tolist() == [len(e) for e in exp]
+    lines = lambda c: c.sa_lines + c.isa_lines + c.ref_lines + c.lcp_lines + c.kt_lines
+    assert lines(c1) < lines(c0)
+
+
+def test_device_mem_probes_on_edge_reads(tiny_ix):
+    tiny_ix.accel()
+    T = tiny_ix.T[:tiny_ix.N]
+    rng = np.random.default_rng(6)
+    cases = [b"z" * 100, b"n" * 100, b"a" * 100, b"acgt" * 30]
+    for _ in range(200):
+        p = int(rng.integers(0, tiny_ix.N - 200))
+        r = bytearray(T[p:p + 120].tobytes())
+        for _k in range(int(rng.integers(0, 4))):
+            r[int(rng.integers(0, 120))] = int(rng.choice(list(b"acgtnz`$N")))
+        cases.append(bytes(r))
+    for P in cases:
+        for ml in (20, 12, 30):
+            assert tiny_ix.search(P, mode="MEM_DEV", min_len=ml) == \
+                tiny_ix.search(P, mode="MEM", min_len=ml)
