@@ -249,6 +249,7 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
     prep_ms = sum(ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(reps)) / reps
     scan_ms = sum(ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(reps)) / reps
     kms = prep_ms + scan_ms
+    S.mappability_release(dix)
     # the scan reproduces the index build's map.bin (compared on the device)
     dmap = S.device_view(dix.info.d_map, dix.info.map_bytes, torch.uint8)
     same_map = bool(torch.equal(out, dmap[2 + 2 * g0:2 + 2 * g1]))

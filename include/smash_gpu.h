@@ -210,10 +210,14 @@ int smash_mappability_scan(const smash_index *ix, uint64_t begin, uint64_t end,
 /* unique lengths U -- and their directory -- that smash_mappability_scan of  */
 /* the same [begin, end) reads, in place in the index (the values are the     */
 /* index build's).  Three streaming partition passes (csrc/uniq_build.hip);   */
-/* ~4 B per position of scratch HBM.  Asynchronous on `stream`; no search or  */
-/* scan may run on the index concurrently.                                    */
+/* ~4 B per window position of scratch HBM, kept until                        */
+/* smash_mappability_release.  Asynchronous on `stream`; no search or scan    */
+/* may run on the index concurrently.                                         */
 int smash_mappability_prepare(const smash_index *ix, uint64_t begin, uint64_t end,
                               void *stream);
+/* smash_mappability_prepare keeps its scratch HBM (4 B per window position +
+ * 2 GB) in the index for the next call; this frees it (synchronous). */
+int smash_mappability_release(const smash_index *ix);
 /* The text window [*lo, *hi) that smash_mappability_prepare(begin, end)     */
 /* rebuilds (the forward and reverse-complement positions of those bases).    */
 int smash_mappability_window(const smash_index *ix, uint64_t begin, uint64_t end,

@@ -116,6 +116,7 @@ void build_aux_t(smash_index *ix, hipStream_t s) {
   if (!ix->d_uniq) ix->d_uniq = dalloc<uint8_t>(N + 64);
   SMASH_HIPX(hipMemsetAsync(ix->d_uniq + N, 0, 64, s));
   build_uniq_range(ix, 0, N, s);   // from SA + L8 (uniq_build.hip)
+  release_uniq_scratch(ix);        // (the index build's HBM is the pipelines' after it)
   // k: floor(log4 N) characters, <= 16 (about one suffix per k-mer: a root
   // descent lands on a singleton or a short run; hg19: 4^16 x 16 B = 69 GB)
   int K = 4;

@@ -137,6 +137,8 @@ struct smash_index {
   uint64_t pos_mask = ~0ull;     // kPkPosMask when SA / ISA carry packed hints (pack_index.hip)
   uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
   mutable uint64_t *d_nsdir = nullptr;   // first U < 255 per 4096 positions (mappability.hip)
+  uint8_t *d_uscratch = nullptr; // U's partition passes (uniq_build.hip), kept between
+  uint64_t uscratch_bytes = 0;   // smash_mappability_prepare calls until released
   uint64_t *d_kmer = nullptr;    // per k-mer: {lo,hi} + (k+2)-mer presence bits (kt_filter)
   uint32_t kmer_k = 0;
   uint64_t *d_bitmap = nullptr;  // (none since round 3: the presence bits live in d_kmer)
@@ -168,6 +170,7 @@ void build_aux(smash_index *ix, hipStream_t s);   // U + k-mer table (aux_build.
 void pack_index(smash_index *ix, bool pack, hipStream_t s);
 // U for text positions [lo, hi) from SA + L8 (uniq_build.hip; lo rounded down to 64)
 void build_uniq_range(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s);
+void release_uniq_scratch(smash_index *ix);   // the passes' scratch HBM
 // mam.hip: smash_map_batch without the per-launch synchronisation of the
 // probe check (sync_check = false: the caller runs probe_check later)
 // caller-owned search workspace (the pipeline's double-buffered sets): the

@@ -76,7 +76,13 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   // CHECK: every probe is checked against the span of the index arrays and
   // the records: a wild address retires its lane and fails the call instead
   // of faulting the GPU.
-  auto kern = sm::k_mam_sm<IdxT, B, CHECK, STATS>;
+  // the packed-word instantiation for an index whose 8-byte SA / ISA words
+  // carry the search's hints (pack_index.hip; SMASH_SM_PK=0: the plain
+  // kernel over them, for A/B -- it reads the elements through the same mask)
+  const char *pke = std::getenv("SMASH_SM_PK");
+  const bool pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask && !(pke && pke[0] == '0');
+  auto kern = pk ? sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8>
+                 : sm::k_mam_sm<IdxT, B, CHECK, STATS, false>;
   int per_cu = 0, cus = 0;
   SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu, reinterpret_cast<const void *>(kern), B, lds));
@@ -209,10 +215,6 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   sm::Ctx<IdxT> c;
   const DevIndex<IdxT> x = make_dev_index<IdxT>(ix);
   c.T = x.T; c.SA = x.SA.p; c.ISA = x.ISA.p; c.L8 = x.L8; c.U = x.U; c.KT = x.KT;
-  // packed SA / ISA words (pack_index.hip): the search reads their hints
-  c.pm = ix->pos_mask;
-  c.pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask ? 1u : 0u;
-  if (const char *e = std::getenv("SMASH_SM_PK")) c.pk = c.pk && std::atoi(e) != 0;
   c.N = x.N; c.logN = uint32_t(x.logN); c.K = uint32_t(x.K); c.B = uint32_t(x.B);
   c.min_len = min_len;
   c.rec = reinterpret_cast<const uint4 *>(rec);

@@ -334,8 +334,8 @@ enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
 // S_CMP ops (16-32 text bytes compared with the read)
 enum : uint32_t { O_EXT = 0, O_BS };
 // ALU continuations, in the order the decide chain runs them
-enum : uint32_t { A_NONE = 0, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE, A_EXPAND,
-                  A_AFTER, A_TOP, A_TRAV, A_DONE };
+enum : uint32_t { A_NONE = 0, A_BSP, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE,
+                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE };
 // binary-search modes: 0 where P' sorts (traverse); 1 / 2 the left / right
 // end of a run of suffixes sharing `cap` characters (from `cbase`) with P
 enum : uint32_t { BS_INSERT = 0, BS_LEFT, BS_RIGHT };
@@ -486,8 +486,6 @@ struct Ctx {
   // the index (DevIndex fields, flattened: every field is a live SGPR)
   const uint8_t *T;
   const IdxT *SA, *ISA;
-  uint64_t pm;            // position bits of an SA / ISA word (common.hpp kPkPosMask, or ~0)
-  uint32_t pk;            // the words carry the packed hints (common.hpp): 0 / 1
   const uint8_t *L8, *U;
   const uint64_t *KT;     // k-mer table: {lo, hi} + (k+2)-mer presence bits (common.hpp)
   uint64_t N;
@@ -551,6 +549,14 @@ __device__ __forceinline__ bool pk_above(uint64_t w, uint32_t b, uint32_t xd) {
 }
 // the lowercase base of 2-bit code q (a0 c1 g2 t3)
 __device__ __forceinline__ uint32_t pk_char(uint32_t q) { return (0x74676361u >> (8 * q)) & 0xFFu; }
+// the window's 7 bases as bytes 0..6 of a u64 (byte 7 zero): each 2-bit code
+// spread to a byte selector, one permute of the a c g t table per 4 bytes
+__device__ __forceinline__ uint64_t pk_window(uint64_t w) {
+  const uint32_t c = uint32_t(w >> 50);   // 14 bits: base i at bits 2i
+  const uint32_t s0 = (c & 3u) | ((c << 6) & 0x300u) | ((c << 12) & 0x30000u) | ((c << 18) & 0x3000000u);
+  const uint32_t s1 = ((c >> 8) & 3u) | ((c >> 2) & 0x300u) | ((c << 4) & 0x30000u) | 0x0c000000u;
+  return uint64_t(SM_PERM(0u, 0x74676361u, s0)) | (uint64_t(SM_PERM(0u, 0x74676361u, s1)) << 32);
+}
 
 // Direct rows: the bad-mask nibble of the 4 bytes of w (bit j: byte j is not
 // a base that occurs in the text), bases at or past `live` (0..4) masked.
@@ -607,8 +613,13 @@ inline void bad_table(const uint64_t in_text[4], uint32_t *lo, uint32_t *hi) {
 // scanner, bounded by [start, end]).  Same final (depth, interval) as the
 // reference's traverse; ~2.5 log2(interval) probes instead of 4 log2 per
 // character.
-template <class IdxT, int BLOCK, bool CHECK, bool STATS>
+template <class IdxT, int BLOCK, bool CHECK, bool STATS, bool PK = false>
 __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
+  // PK: the SA / ISA words carry the packed hints (common.hpp; 8-byte
+  // elements only): their position bits are PM, and the hint paths below
+  // exist only in this instantiation
+  static_assert(!PK || sizeof(IdxT) == 8, "packed words are 8-byte elements");
+  constexpr uint64_t PM = PK ? kPkPosMask : ~0ull;
   extern __shared__ uint32_t ldsw[];
   // (the 256-bit in-text set stays in scalar registers: dynamic LDS is
   // exactly 16 blocks x 64 rows x 160 B = the CU's 160 KB at 150 bp)
@@ -660,6 +671,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // SA[(m+1+hi)/2] (v3, when pfr), so the next probe's text compare issues
   // one iteration later instead of two
   FlagRef pf{fl, 9}, pfr{fl, 10};
+  // PK: what the ISA words of an expand_link's ends told (set where they are
+  // consumed, read by A_EXPAND in the same iteration): the left end stops at
+  // start (- 1 with xl1), the right end at end (+ 1 with xr1)
+  FlagRef xls{fl, 12}, xl1{fl, 13}, xrs{fl, 14}, xr1{fl, 15};
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
@@ -698,25 +713,21 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   auto bs_probe = [&]() -> bool {
     SM_HOOK_CMPBS(true, sp, cbase + lc);
     const uint32_t o = cbase + lc;
-    if (c.pk && ((sp >> kPkPosBits) & 7u) != 5u && o >= c.K && o < c.K + kPkWindow) {
+    if (PK && ((sp >> kPkPosBits) & 7u) != 5u && o - c.K < kPkWindow) {
       const uint32_t rem = cap - lc, nav = c.K + kPkWindow - o;
       const uint32_t lim = rem < nav ? rem : nav;
-      const uint32_t w = uint32_t(sp >> (50 + 2 * (o - c.K)));
-      const uint32_t off = prefix + o;
-      uint32_t k = 0, tb = 0;
-      for (; k < lim; ++k) {
-        tb = pk_char((w >> (2 * k)) & 3u);
-        if (P[off + k] != tb) break;
-      }
+      const uint64_t win = pk_window(sp) >> (8 * (o - c.K));
+      const uint32_t k = agree8(win, lds_load8(P, prefix + o), lim);
       lc += k;
       if (k < lim || k == rem) {
         SM_HOOK_CMPBS(false, sp, cbase + lc);
-        bs_decide(k == rem, k == rem ? 0u : uint32_t(P[off + k]), tb);
+        bs_decide(k == rem, k == rem ? 0u : uint32_t(P[prefix + o + k]),
+                  uint32_t(win >> (8 * (k & 7))) & 0xFFu);
         pf = false; pfr = false; need2 = false;
         return true;
       }
     }
-    addr = reinterpret_cast<uint64_t>(c.T + (sp & c.pm) + cbase + lc);
+    addr = reinterpret_cast<uint64_t>(c.T + (sp & PM) + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
     need2 = c.pf && lo < m;
     pfr = c.pf && m + 1 < hi;
@@ -735,6 +746,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     need2 = l && r;
     st = l && r ? S_EXB : l ? S_EXL : S_EXR;
     return l || r;
+  };
+
+  // PK: expand_link's run around [start, end] at depth xd = the current
+  // depth (both are set when the ISA words arrive): from the ISA word of
+  // start, L8[start] and L8[start - 1]; from end's, L8[end + 1] and L8[end + 2]
+  auto isa_hints = [&](uint64_t wl, uint64_t wr) {
+    const uint32_t d = depth;
+    xls = pk_below(wl, 40, d) || (pk_above(wl, 40, d) && pk_below(wl, 33, d));
+    xl1 = !pk_below(wl, 40, d);
+    xrs = pk_below(wr, 47, d) || (pk_above(wr, 47, d) && pk_below(wr, 54, d));
+    xr1 = !pk_below(wr, 47, d);
   };
 
   for (;;) {
@@ -860,10 +882,6 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
 #endif
     const uint32_t ao = st >= S_BYTE ? 0u : uint32_t(addr) & 15;   // element offset in v
     uint32_t a = A_NONE;
-    // the ISA words of an expand_link's two ends (this iteration only: the
-    // decide chain runs A_EXPAND right after the consume that loads them)
-    uint64_t xwl = 0, xwr = 0;
-    bool xw = false;
     SM_REGION(0);
     // the scan states' byte masks, one computation shared by all four (their
     // bodies would otherwise each pay for it): bit i of mv / mv2 is byte i of
@@ -994,17 +1012,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
           sp = iv;
           // 16 bytes first: a binary-search probe usually decides early
-          if (bs_probe()) a = A_BS;
+          a = A_BSP;
         } else if (op == O_ISAJ) {
-          start = end = iv & c.pm; have_pos = false;
-          xwl = xwr = iv; xw = c.pk != 0;
+          start = end = iv & PM; have_pos = false;
+          if (PK) isa_hints(iv, iv);
           a = A_EXPAND;
         } else if (op == O_NS_SA2) {                  // suffix link, both ends
-          addr = ia(c.ISA, (iv & c.pm) + 1); addr2 = ia(c.ISA, (iv2 & c.pm) + 1);
+          addr = ia(c.ISA, (iv & PM) + 1); addr2 = ia(c.ISA, (iv2 & PM) + 1);
           op = O_NS_ISA2;
         } else {                                      // O_NS_ISA2
-          start = iv & c.pm; end = iv2 & c.pm; need2 = false;
-          xwl = iv; xwr = iv2; xw = c.pk != 0;
+          start = iv & PM; end = iv2 & PM; need2 = false;
+          if (PK) isa_hints(iv, iv2);
           ++prefix; have_pos = false;
           if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
           else a = A_EXPAND;
@@ -1013,12 +1031,12 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_BYTE: {                                 // is_leftmaximal: T[pos-1]
         SM_REGION(6);
-        SM_HOOK_BYTE(pos & c.pm);
+        SM_HOOK_BYTE(pos & PM);
         if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
-          if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & c.pm, prefix, depth);
+          if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & PM, prefix, depth);
           ++nem;
         }
-        uscan_start(pos & c.pm, depth);
+        uscan_start(pos & PM, depth);
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
@@ -1059,7 +1077,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             SM_HOOK_PF(ia(c.SA, m));
             sp = left ? idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15) : v3;
             lc = lL < lR ? lL : lR;
-            if (bs_probe()) a = A_BS;
+            a = A_BSP;
           } else {
             a = A_BS;
           }
@@ -1155,6 +1173,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
 
     // ---------------- decide ----------------
+    if (a == A_BSP) {                                 // probe m's SA word is in sp
+      a = bs_probe() ? A_BS : A_NONE;
+    }
     if (a == A_BS) {                                  // next probe of a binary search
       SM_REGION(10);
       if (lo < hi) {
@@ -1185,7 +1206,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         SM_HOOK_RUN(true, 1, 0, 0);
         // packed: the SA word of rank bi holds L8[bi] and L8[bi + 1], the
         // run's first stop on either side when it ends at bi
-        const bool ls = c.pk && pk_below(bpos, 36, xd), rs = c.pk && pk_below(bpos, 43, xd);
+        const bool ls = PK && pk_below(bpos, 36, xd), rs = PK && pk_below(bpos, 43, xd);
         a = ex_start(start, end, ls, rs) ? A_NONE : A_RUN_DONE;
       }
     }
@@ -1227,7 +1248,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_TOP;
       } else {
         depth = dch - j;
-        addr = ia(c.ISA, (pos & c.pm) + j);
+        addr = ia(c.ISA, (pos & PM) + j);
         st = S_IDX; op = O_ISAJ;
         a = A_NONE;
       }
@@ -1245,11 +1266,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       // and L8[end + 1 .. end + 2]: a run that ends within one more suffix
       // on a side needs no L8 probe there
       bool ls = false, rs = false;
-      if (xw) {
-        if (pk_below(xwl, 40, xd)) ls = true;                      // L8[start] < xd
-        else if (pk_above(xwl, 40, xd) && pk_below(xwl, 33, xd)) { es = start - 1; ls = true; }
-        if (pk_below(xwr, 47, xd)) rs = true;                      // L8[end + 1] < xd
-        else if (pk_above(xwr, 47, xd) && pk_below(xwr, 54, xd)) { ee = end + 1; rs = true; }
+      if (PK) {
+        ls = xls; rs = xrs;
+        if (ls && xl1) es = start - 1;
+        if (rs && xr1) ee = end + 1;
       }
       a = ex_start(0, N - 1, ls, rs) ? A_NONE : A_RUN_DONE;
     }
@@ -1267,19 +1287,19 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (!have_pos) {
           addr = ia(c.SA, start);
           st = S_IDX; op = O_SAPOS2;
-        } else if (depth >= c.min_len && prefix != 0 && (pos & c.pm) != 0 &&
-                   (!c.pk || ((pos >> kPkPosBits) & 7u) >= 4u)) {
-          addr = reinterpret_cast<uint64_t>(c.T + (pos & c.pm) - 1);
+        } else if (depth >= c.min_len && prefix != 0 && (pos & PM) != 0 &&
+                   (!PK || ((pos >> kPkPosBits) & 7u) >= 4u)) {
+          addr = reinterpret_cast<uint64_t>(c.T + (pos & PM) - 1);
           st = S_BYTE;
         } else {
-          // (packed: is_leftmaximal from the BWT character in pos's SA word)
+          // (PK: is_leftmaximal from the BWT character in pos's SA word)
           if (depth >= c.min_len &&
-              (prefix == 0 || (pos & c.pm) == 0 ||
+              (!PK || prefix == 0 || (pos & PM) == 0 ||
                P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
-            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & c.pm, prefix, depth);
+            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & PM, prefix, depth);
             ++nem;
           }
-          uscan_start(pos & c.pm, depth);
+          uscan_start(pos & PM, depth);
         }
       }
     }
@@ -1443,7 +1463,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             addr = ia(c.SA, start);
             st = S_IDX; op = O_SAPOS;
           } else {
-            addr = reinterpret_cast<uint64_t>(c.T + (pos & c.pm) + depth);
+            addr = reinterpret_cast<uint64_t>(c.T + (pos & PM) + depth);
             addr2 = addr + 16;
             need2 = L - prefix - depth > 16;
             st = S_CMP; op = O_EXT; lc = 0;

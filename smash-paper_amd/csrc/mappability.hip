@@ -117,70 +117,6 @@ __device__ __forceinline__ uint32_t byte_of(const uint4 &v, uint32_t q) {
   return (w >> (8 * (q & 3))) & 0xFF;
 }
 
-// dir[t] = the first text position p in [t << 12, (t + 1) << 12) with
-// U[p] < 255, else kNone
-__global__ __launch_bounds__(kMB) void k_nsdir(const uint8_t *__restrict__ U, uint64_t N,
-                                               uint64_t *__restrict__ dir, uint64_t t0,
-                                               uint64_t t1) {
-  __shared__ unsigned long long s_first;
-  for (uint64_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
-    if (threadIdx.x == 0) s_first = kNone;
-    __syncthreads();
-    const uint64_t p0 = (t << kDirShift) + uint64_t(threadIdx.x) * kMPer;
-    uint64_t f = kNone;
-    if (p0 < N) {
-      const uint4 v = load16u(U + p0);
-      for (uint32_t q = 0; q < uint32_t(kMPer) && f == kNone; ++q)
-        if (p0 + q < N && byte_of(v, q) < 255) f = p0 + q;
-    }
-    if (f != kNone) atomicMin(&s_first, (unsigned long long)f);
-    __syncthreads();
-    if (threadIdx.x == 0) dir[t] = s_first;
-    __syncthreads();
-  }
-}
-
-// dir[t] = min(dir[t], dir[t + 1], ...): the first unsaturated position at or
-// after tile t, from each tile's own first (a min scan of the reversed
-// directory on the device; entries already propagated are fixed points)
-hipError_t dir_suffix_min(uint64_t *dir, uint64_t ndir, hipStream_t s) {
-  uint64_t *tmp = nullptr;
-  void *tb = nullptr;
-  size_t nb = 0;
-  auto in = std::make_reverse_iterator(dir + ndir);
-  auto out = std::make_reverse_iterator(static_cast<uint64_t *>(nullptr) + ndir);
-  hipError_t e = hipcub::DeviceScan::InclusiveScan(nullptr, nb, in, out, hipcub::Min(), ndir, s);
-  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void **>(&tmp), 8 * ndir, s);
-  if (e == hipSuccess) e = hipMallocAsync(&tb, nb, s);
-  if (e == hipSuccess)
-    e = hipcub::DeviceScan::InclusiveScan(tb, nb, in, std::make_reverse_iterator(tmp + ndir),
-                                          hipcub::Min(), ndir, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(dir, tmp, 8 * ndir, hipMemcpyDeviceToDevice, s);
-  if (tmp) (void)hipFreeAsync(tmp, s);
-  if (tb) (void)hipFreeAsync(tb, s);
-  return e;
-}
-
-// the directory entries of text positions [lo, hi) from U, then propagated
-hipError_t build_nsdir(const smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
-  const uint64_t ndir = (ix->N + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
-  if (!ix->d_nsdir) {
-    hipError_t e = hipMalloc(&ix->d_nsdir, 8 * ndir);
-    if (e != hipSuccess) return e;
-    lo = 0;
-    hi = ix->N;
-  }
-  const uint64_t t0 = lo >> kDirShift;
-  const uint64_t t1 = std::min(ndir, (hi + (uint64_t(1) << kDirShift) - 1) >> kDirShift);
-  if (t0 < t1)
-    k_nsdir<<<unsigned(std::min<uint64_t>(t1 - t0, 65536)), kMB, 0, s>>>(ix->d_uniq, ix->N,
-                                                                      ix->d_nsdir, t0, t1);
-  hipError_t e = hipGetLastError();
-  // (the scan covers entry t1 too: a window tile without an unsaturated
-  // position takes the propagated entry after the window)
-  return e == hipSuccess ? dir_suffix_min(ix->d_nsdir, std::min(ndir, t1 + 1), s) : e;
-}
-
 // an unsaturated text position >= p (kNone: none before N): the first one
 // at or after the next multiple of 4096 (exact when p is a multiple; a later,
 // looser bound otherwise, which the callers accept).  dir is the suffix-min
@@ -226,6 +162,119 @@ __device__ __forceinline__ uint32_t sat_mask16(const uint4 &v) {
 }
 // the 16-bit mask reversed (byte 15 - q of the rc block is base q)
 __device__ __forceinline__ uint32_t rev16(uint32_t m) { return __brev(m) >> 16; }
+
+// dir[t] = the first text position p in [t << 12, (t + 1) << 12) with
+// U[p] < 255, else kNone: one wave per tile, 64 bytes per lane, the first
+// lane holding an unsaturated byte found by a ballot (no LDS, no barrier)
+__global__ __launch_bounds__(kMB) void k_nsdir(const uint8_t *__restrict__ U, uint64_t N,
+                                               uint64_t *__restrict__ dir, uint64_t t0,
+                                               uint64_t t1) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = uint64_t(gridDim.x) * (blockDim.x >> 6);
+  for (uint64_t t = t0 + uint64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); t < t1;
+       t += waves) {
+    const uint64_t p0 = (t << kDirShift) + uint64_t(lane) * 64;
+    uint32_t q = 64;   // this lane's first unsaturated byte (64: none)
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      if (p0 + 16 * k < N && q == 64) {
+        uint32_t m = ~sat_mask16(load16u(U + p0 + 16 * k)) & 0xFFFFu;
+        if (p0 + 16 * k + 16 > N) m &= (1u << uint32_t(N - p0 - 16 * k)) - 1u;
+        if (m) q = 16 * k + uint32_t(__builtin_ctz(m));
+      }
+    }
+    const uint64_t b = __ballot(q < 64);
+    const uint64_t mine = p0 + q;   // (every lane takes part in the shuffle)
+    const uint64_t f = __shfl(mine, b ? int(__builtin_ctzll(b)) : 0, 64);
+    if (lane == 0) dir[t] = b ? f : kNone;
+  }
+}
+
+// dir[t] = min(dir[t], dir[t + 1], ...): the first unsaturated position at or
+// after tile t, from each tile's own first (entries already propagated are
+// fixed points of it).  Three small kernels: the minimum of each segment of
+// kSegDir entries, a suffix minimum over the segments (one block), then each
+// segment's own suffix minimum with the carry from the segments after it.
+constexpr uint32_t kSegDir = 4096;
+__global__ __launch_bounds__(kMB) void k_dir_segmin(const uint64_t *__restrict__ dir, uint64_t n,
+                                                    uint64_t *__restrict__ segmin) {
+  __shared__ unsigned long long s_m;
+  if (threadIdx.x == 0) s_m = kNone;
+  __syncthreads();
+  const uint64_t a = uint64_t(blockIdx.x) * kSegDir;
+  unsigned long long m = kNone;
+  for (uint64_t t = a + threadIdx.x; t < a + kSegDir && t < n; t += blockDim.x)
+    m = dir[t] < m ? dir[t] : m;
+  atomicMin(&s_m, m);
+  __syncthreads();
+  if (threadIdx.x == 0) segmin[blockIdx.x] = s_m;
+}
+__global__ void k_dir_carry(uint64_t *segmin, uint32_t nseg) {   // one thread: nseg ~ 400
+  if (threadIdx.x) return;
+  uint64_t m = kNone;
+  for (uint32_t k = nseg; k-- > 0;) {
+    const uint64_t v = segmin[k];
+    segmin[k] = m;   // the carry into segment k: the minimum after it
+    m = v < m ? v : m;
+  }
+}
+__global__ __launch_bounds__(kMB) void k_dir_apply(uint64_t *__restrict__ dir, uint64_t n,
+                                                   const uint64_t *__restrict__ carry) {
+  // kSegDir entries per block, 16 per thread: each thread's suffix minimum,
+  // then the block's suffix scan of the thread minima (LDS), then apply
+  __shared__ uint64_t s_t[kMB];
+  constexpr uint32_t per = kSegDir / kMB;
+  const uint64_t a = uint64_t(blockIdx.x) * kSegDir + uint64_t(threadIdx.x) * per;
+  uint64_t v[per];
+  uint64_t m = kNone;
+#pragma unroll
+  for (int k = int(per) - 1; k >= 0; --k) {
+    v[k] = a + k < n ? dir[a + k] : kNone;
+    m = v[k] < m ? v[k] : m;
+    v[k] = m;
+  }
+  s_t[threadIdx.x] = m;
+  __syncthreads();
+  uint64_t after = carry[blockIdx.x];
+  for (uint32_t u = threadIdx.x + 1; u < kMB; ++u) after = s_t[u] < after ? s_t[u] : after;
+#pragma unroll
+  for (uint32_t k = 0; k < per; ++k)
+    if (a + k < n) dir[a + k] = v[k] < after ? v[k] : after;
+}
+
+hipError_t dir_suffix_min(uint64_t *dir, uint64_t ndir, hipStream_t s) {
+  const uint32_t nseg = uint32_t((ndir + kSegDir - 1) / kSegDir);
+  uint64_t *seg = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void **>(&seg), 8 * (nseg + 1), s);
+  if (e != hipSuccess) return e;
+  k_dir_segmin<<<nseg, kMB, 0, s>>>(dir, ndir, seg);
+  k_dir_carry<<<1, 64, 0, s>>>(seg, nseg);
+  k_dir_apply<<<nseg, kMB, 0, s>>>(dir, ndir, seg);
+  e = hipGetLastError();
+  (void)hipFreeAsync(seg, s);
+  return e;
+}
+
+// the directory entries of text positions [lo, hi) from U, then propagated
+hipError_t build_nsdir(const smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
+  const uint64_t ndir = (ix->N + (uint64_t(1) << kDirShift) - 1) >> kDirShift;
+  if (!ix->d_nsdir) {
+    hipError_t e = hipMalloc(&ix->d_nsdir, 8 * ndir);
+    if (e != hipSuccess) return e;
+    lo = 0;
+    hi = ix->N;
+  }
+  const uint64_t t0 = lo >> kDirShift;
+  const uint64_t t1 = std::min(ndir, (hi + (uint64_t(1) << kDirShift) - 1) >> kDirShift);
+  if (t0 < t1)   // (one wave per tile)
+    k_nsdir<<<unsigned(std::min<uint64_t>((t1 - t0 + 3) / 4, 65536)), kMB, 0, s>>>(
+        ix->d_uniq, ix->N, ix->d_nsdir, t0, t1);
+  hipError_t e = hipGetLastError();
+  // (the scan covers entry t1 too: a window tile without an unsaturated
+  // position takes the propagated entry after the window)
+  return e == hipSuccess ? dir_suffix_min(ix->d_nsdir, std::min(ndir, t1 + 1), s) : e;
+}
+
 
 // bin ordinal (bisect_right of abs0 + the tile's first base) per tile
 __global__ void k_tilebins(MapCtx c, const Seg *segs, uint32_t nseg, uint64_t ntiles,
@@ -784,6 +833,14 @@ extern "C" int smash_mappability_prepare(const smash_index *ix, uint64_t begin, 
     return f.what.find("hipMalloc") != std::string::npos ? SMASH_ERR_NOMEM : SMASH_ERR_HIP;
   }
   SMASH_HIP(build_nsdir(ix, lo & ~uint64_t(63), hi, s));
+  return SMASH_OK;
+}
+
+extern "C" int smash_mappability_release(const smash_index *ix) {
+  if (!ix) return SMASH_ERR_ARG;
+  SMASH_HIP(hipSetDevice(ix->device));
+  SMASH_HIP(hipDeviceSynchronize());
+  release_uniq_scratch(const_cast<smash_index *>(ix));
   return SMASH_OK;
 }
 

@@ -13,7 +13,7 @@
 // known in advance -- SA is a permutation, so every aligned window of 2^k
 // positions receives exactly 2^k entries:
 //
-//   pass 1 (k_upart1): ranks in tiles of 16 384; each entry {x mod 2^24, v}
+//   pass 1 (k_upart1): ranks in tiles of 8 192; each entry {x mod 2^24, v}
 //     (one u32) goes to the level-1 bucket of x >> 24; a tile is sorted by
 //     bucket in LDS and each bucket's run is stored contiguously at an
 //     atomically claimed offset inside the bucket's fixed slice of E1 (u32
@@ -37,9 +37,10 @@
 namespace smash {
 namespace {
 
-constexpr int kUT = 1024;                        // threads per block
+constexpr int kUT = 512;                         // threads per block (passes 1, 2)
 constexpr int kUPer = 16;                        // entries per thread per tile
-constexpr uint32_t kUTile = uint32_t(kUT) * kUPer;   // 16 384
+constexpr uint32_t kUTile = uint32_t(kUT) * kUPer;   // 8 192: 54 KB of LDS, 2 blocks per CU
+constexpr int kU3 = 1024;                        // threads per block (pass 3)
 constexpr int kS1 = 24;                          // level-1 bucket: 2^24 positions
 constexpr int kS2 = 16;                          // window: 2^16 positions
 constexpr uint32_t kNB1Max = 512;                // level-1 buckets (2^33 positions)
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(kUT) void k_upart2(const uint32_t *__restrict__ E1,
                                                 uint32_t c0, uint32_t nc, unsigned int *cur,
                                                 uint32_t *E2) {
   __shared__ TileLds t;
-  const uint64_t tiles_per_bucket = (uint64_t(1) << kS1) / kUTile;   // 1024
+  const uint64_t tiles_per_bucket = (uint64_t(1) << kS1) / kUTile;   // 2048
   const uint64_t ntiles = uint64_t(nc) * tiles_per_bucket;
   for (uint32_t b = threadIdx.x; b < kNB2; b += kUT) t.cnt[b] = 0;
   __syncthreads();
@@ -187,7 +188,7 @@ __global__ __launch_bounds__(kUT) void k_upart2(const uint32_t *__restrict__ E1,
 }
 
 // pass 3: one block per window of 2^16 positions: entries -> LDS bytes -> U
-__global__ __launch_bounds__(kUT) void k_upart3(const uint32_t *__restrict__ E2, uint64_t n,
+__global__ __launch_bounds__(kU3) void k_upart3(const uint32_t *__restrict__ E2, uint64_t n,
                                                 uint32_t c0, uint32_t nc, uint64_t lo,
                                                 uint8_t *U) {
   __shared__ uint32_t s_u[(1u << kS2) / 4];
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(kUT) void k_upart3(const uint32_t *__restrict__ E2,
     if (wbeg >= n) continue;                                     // (block-uniform)
     const uint32_t wsize = uint32_t(umin64(uint64_t(1) << kS2, n - wbeg));
     const uint32_t *src = E2 + (w << kS2);
-    for (uint32_t j = threadIdx.x * 4; j < wsize; j += kUT * 4) {
+    for (uint32_t j = threadIdx.x * 4; j < wsize; j += kU3 * 4) {
       if (j + 4 <= wsize) {
         const uint4 v = *reinterpret_cast<const uint4 *>(src + j);
         sb[v.x & 0xFFFF] = uint8_t(v.x >> 24);
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(kUT) void k_upart3(const uint32_t *__restrict__ E2,
     }
     __syncthreads();
     uint8_t *dst = U + lo + wbeg;   // lo is a multiple of 64: 16-byte aligned stores
-    for (uint32_t j = threadIdx.x * 16; j < wsize; j += kUT * 16) {
+    for (uint32_t j = threadIdx.x * 16; j < wsize; j += kU3 * 16) {
       if (j + 16 <= wsize) {
         *reinterpret_cast<uint4 *>(dst + j) = *reinterpret_cast<const uint4 *>(sb + j);
       } else {
@@ -236,32 +237,44 @@ void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   }
   int cus = 0;
   SMASH_HIPX(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
-  uint32_t *E1 = nullptr, *E2 = nullptr;
-  unsigned int *cur = nullptr;
+  // scratch: E1 (4 B per window position), E2 (one chunk), the cursors --
+  // kept in the index between calls (release_uniq_scratch)
   const uint32_t chunk = std::min(kChunk, nb1);
-  SMASH_HIPX(hipMallocAsync(reinterpret_cast<void **>(&E1), 4 * n, s));
-  SMASH_HIPX(hipMallocAsync(reinterpret_cast<void **>(&E2), 4 * (uint64_t(chunk) << kS1), s));
-  SMASH_HIPX(hipMallocAsync(reinterpret_cast<void **>(&cur), 4 * uint64_t(kChunk) * kNB2, s));
+  const uint64_t b_e1 = (4 * n + 255) & ~uint64_t(255);
+  const uint64_t b_e2 = 4 * (uint64_t(chunk) << kS1);
+  const uint64_t need = b_e1 + b_e2 + 4 * uint64_t(kChunk) * kNB2;
+  if (ix->uscratch_bytes < need) {
+    release_uniq_scratch(ix);
+    ix->d_uscratch = dalloc<uint8_t>(need);
+    ix->uscratch_bytes = need;
+  }
+  uint32_t *E1 = reinterpret_cast<uint32_t *>(ix->d_uscratch);
+  uint32_t *E2 = reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1);
+  unsigned int *cur = reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + b_e2);
   SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * nb1, s));
   const uint64_t t1 = (N + kUTile - 1) / kUTile;
-  k_upart1<IdxT><<<unsigned(std::min<uint64_t>(t1, uint64_t(cus))), kUT, 0, s>>>(
+  k_upart1<IdxT><<<unsigned(std::min<uint64_t>(t1, 2 * uint64_t(cus))), kUT, 0, s>>>(
       static_cast<const IdxT *>(ix->d_sa), ix->pos_mask, ix->d_lcp8, N, lo, hi, nb1, cur, E1);
   SMASH_HIPX(hipGetLastError());
   for (uint32_t c0 = 0; c0 < nb1; c0 += kChunk) {
     const uint32_t nc = std::min(kChunk, nb1 - c0);
     SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * uint64_t(nc) * kNB2, s));
     const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << kS1) / kUTile);
-    k_upart2<<<unsigned(std::min<uint64_t>(t2, uint64_t(cus))), kUT, 0, s>>>(E1, n, c0, nc, cur, E2);
-    k_upart3<<<unsigned(std::min<uint64_t>(uint64_t(nc) * kNB2, uint64_t(cus) * 2)), kUT, 0, s>>>(
+    k_upart2<<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, s>>>(E1, n, c0, nc,
+                                                                               cur, E2);
+    k_upart3<<<unsigned(std::min<uint64_t>(uint64_t(nc) * kNB2, uint64_t(cus) * 2)), kU3, 0, s>>>(
         E2, n, c0, nc, lo, ix->d_uniq);
     SMASH_HIPX(hipGetLastError());
   }
-  SMASH_HIPX(hipFreeAsync(E1, s));
-  SMASH_HIPX(hipFreeAsync(E2, s));
-  SMASH_HIPX(hipFreeAsync(cur, s));
 }
 
 }  // namespace
+
+void release_uniq_scratch(smash_index *ix) {
+  if (ix->d_uscratch) (void)hipFree(ix->d_uscratch);
+  ix->d_uscratch = nullptr;
+  ix->uscratch_bytes = 0;
+}
 
 // U for the text positions [lo, hi) (lo rounded down to a multiple of 64),
 // in ix->d_uniq; the rest of U is left as it is

@@ -63,6 +63,7 @@ EXPORTS = [
     "smash_read_stride", "smash_pipeline_max_batch",
     "smash_mappability_prepare", "smash_mappability_window", "smash_index_pack",
     "smash_pipeline_reserve_keys", "smash_pipeline_key_capacity", "smash_pipeline_error",
+    "smash_mappability_release",
 ]
 
 
@@ -225,6 +226,7 @@ def lib():
     L.smash_read_stride.restype = C.c_uint32
     L.smash_mappability_prepare.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
     L.smash_index_pack.argtypes = [vp, C.c_int, vp]
+    L.smash_mappability_release.argtypes = [vp]
     L.smash_pipeline_reserve_keys.argtypes = [vp, C.c_uint64, vp]
     L.smash_pipeline_key_capacity.argtypes = [vp]
     L.smash_pipeline_key_capacity.restype = C.c_uint64
@@ -766,6 +768,11 @@ def mappability_prepare(index: Index, begin, end, stream=None):
     from SA + the LCP bytes, in place."""
     check(lib().smash_mappability_prepare(index.h, begin, end, vp(_stream(stream))),
           "smash_mappability_prepare")
+
+
+def mappability_release(index: Index):
+    """free mappability_prepare's scratch HBM (smash_mappability_release)"""
+    check(lib().smash_mappability_release(index.h), "smash_mappability_release")
 
 
 def mappability_window(index: Index, begin, end):

@@ -427,6 +427,7 @@ def test_c5_prepare_rebuilds_u_full_genome(hg19, hg19_oracle, monkeypatch):
         U[:N].copy_(keep)
         S.mappability_prepare(dix, 0, total)
         torch.cuda.synchronize()
+        S.mappability_release(dix)   # (the scratch HBM: the later tests' pipelines need it)
 
 
 def test_c3_mem_hg19_equals_oracle(hg19, hg19_oracle):

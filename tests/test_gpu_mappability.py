@@ -178,3 +178,4 @@ def test_prepare_per_partition(mid, parts):
         U[:N].copy_(want)
         S.mappability_prepare(dix, 0, total)   # (the directory too)
         torch.cuda.synchronize()
+        S.mappability_release(dix)

@@ -258,9 +258,6 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   emu_T = T;
   c.T = T; c.SA = static_cast<const IdxT *>(SA); c.ISA = static_cast<const IdxT *>(ISA);
   c.L8 = L8; c.U = U; c.KT = KT;
-  // packed index words (common.hpp): the SA / ISA arrays given carry them
-  c.pk = packed && sizeof(IdxT) == 8 ? 1u : 0u;
-  c.pm = c.pk ? kPkPosMask : ~0ull;
   (void)BM;   // (round 3: the filter's presence bits live in KT)
   c.N = N; c.logN = uint32_t(logN); c.K = uint32_t(K); c.B = uint32_t(B); c.min_len = min_len;
   c.rec = rec.data(); c.chunks = g.chunks; c.c_bad = g.c_bad; c.w_row = g.w_row; c.w_raw = g.w_raw;
@@ -292,7 +289,9 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   emu_bad = 0;
   for (int k = 0; k < 8; ++k) { emu_probes[k] = emu_lines[k] = 0; emu_last[k] = ~0ull; }
   emu_req[0] = emu_req[1] = 0;
-  sm::k_mam_sm<IdxT, 1, true, true>(c);
+  // packed index words (common.hpp): the SA / ISA arrays given carry them
+  if (packed && sizeof(IdxT) == 8) sm::k_mam_sm<IdxT, 1, true, true, sizeof(IdxT) == 8>(c);
+  else sm::k_mam_sm<IdxT, 1, true, true, false>(c);
   for (int k = 0; k < 10; ++k) viol[k] = v[k];
   viol[0] += emu_bad;
   for (int k = 0; k < 8; ++k) { counters[k] = emu_probes[k]; counters[8 + k] = emu_lines[k]; }
