@@ -436,11 +436,14 @@ def bench_mem(args, cfg, world, rank, local, dist):
             "bytes_method": "64 B x line transitions of mem.hip's probe sequence (oracle "
                             "orc_mem_dev on the downloaded index, %d reads)" % ns}
         # the device's records == the oracle's, in emission order
+        # (reads whose MEMs exceed cap -- a repeat family's millions -- keep
+        # exact counts and cut records: their counts are compared)
         o = out.view(n, 2 * cap)[:200].cpu().numpy().view(np.uint64)
         same = all(S.unpack_records(o[i], counts[i], cap) == oix.search(sample[i].tobytes(),
                                                                          mode="MEM")
-                   for i in range(200))
-        res["records_identical_to_oracle"] = bool(same and (per[:200] == counts[:200]).all())
+                   for i in range(200) if counts[i] <= cap)
+        res["records_identical_to_oracle"] = bool(same)
+        res["counts_identical_to_oracle"] = bool((per == counts[:ns]).all())
         if not args.no_cpu_baseline:
             threads, note = host_cores()
             t3 = time.perf_counter()

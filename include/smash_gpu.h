@@ -309,20 +309,21 @@ int smash_count_batches_ready(smash_pipeline *p, const uint8_t *d_reads, uint64_
                               uint64_t batch_pairs, uint64_t *d_counts, void *stream,
                               void *ready);
 
-#define SMASH_EXPORT_HDR_WORDS 3   /* u64 words per key in smash_phase_export's d_send */
+#define SMASH_EXPORT_HDR_WORDS 1   /* u64 words per key in smash_phase_export's d_send */
 
 /* Multi-GPU phases (one rank per GPU; the caller runs the collectives):
  *  1. smash_phase_map      -- map/resolve/tag/filter/hash + in-batch first-wins
  *  2. smash_phase_export   -- the keyed pairs grouped by owner rank
  *                             ((hash >> 1) % world), each owner's segment in
  *                             pair order: per key a SMASH_EXPORT_HDR_WORDS-word
- *                             header {hash hi, hash lo, nk << 40 | word offset
- *                             in its owner segment} in *d_send and the key's nk
+ *                             header {nk << 40 | word offset in its owner
+ *                             segment} in *d_send (the owner recomputes the
+ *                             key's hashes from its words) and the key's nk
  *                             canonical hit words (tid << 48 | pos0) in
  *                             *d_send_words (both pipeline-owned, valid until
  *                             the next export); h_send_counts[world] /
  *                             h_send_words[world] filled (synchronises)
- *     caller: all_to_all of the counts, then of d_send (3 words per key) and
+ *     caller: all_to_all of the counts, then of d_send (1 word per key) and
  *             of d_send_words -> d_recv, d_recv_words (source-rank order)
  *  3. smash_dedup_owner    -- owner side: first-wins in receive order (source
  *                             ranks in rank order = the global pair order)

@@ -153,7 +153,26 @@ template <class IdxT>
 __device__ void collect_mems(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
                              uint64_t prefix, const Ival &mli, Ival xmi, MemSink &s) {
   const uint64_t N = m.x.N;
-  for (uint64_t i = xmi.start; i <= xmi.end; ++i)
+  // the interval's suffixes in rank order, 8 at a time: their SA elements
+  // and text bytes are independent loads, all in flight before the first
+  // emission (an interval of a repeat family holds millions of suffixes,
+  // and one lane walks it); emissions stay in rank order
+  uint64_t i = xmi.start;
+  if (xmi.depth >= min_len) {
+    const uint8_t pb = prefix ? P[prefix - 1] : 0;
+    for (; i + 8 <= xmi.end + 1; i += 8) {
+      uint64_t x[8];
+      uint8_t b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = uint64_t(m.x.SA[i + k]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = x[k] ? m.x.T[x[k] - 1] : 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (prefix == 0 || x[k] == 0 || pb != b[k]) s.emit(x[k], prefix, xmi.depth);
+    }
+  }
+  for (; i <= xmi.end; ++i)
     find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[i]), xmi.depth, s);
   if (mli.start == xmi.start && mli.end == xmi.end) return;
   while (xmi.depth >= mli.depth) {

