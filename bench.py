@@ -379,9 +379,12 @@ def bench_mem(args, cfg, world, rank, local, dist):
     def launch():
         S.match_batch(dix, d_reads, n, L, out, cap, nn, mode="MEM")
 
+    log("MEM: %d reads, cap %d; warm-up launch" % (n, cap))
     for _ in range(max(1, args.warmup)):
+        t0 = time.perf_counter()
         launch()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        log("MEM: warm-up launch %.3f s" % (time.perf_counter() - t0))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
     if world > 1:
         dist.barrier()
@@ -390,6 +393,8 @@ def bench_mem(args, cfg, world, rank, local, dist):
         ev[2 * i].record()
         launch()
         ev[2 * i + 1].record()
+        ev[2 * i + 1].synchronize()   # (a progress line per launch; the next is queued after)
+        log("MEM: launch %d done" % i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -421,8 +426,10 @@ def bench_mem(args, cfg, world, rank, local, dist):
         sample = d_reads[:ns].cpu().numpy()
         oix, _ = host_index(S, O, dix, T, sp, sz, names, sample_reads=sample)
         log("host copy of the index: %.1f s" % (time.time() - t2))
+        t2 = time.time()
         _, per, ctr = O.mem_batch(oix, sample, threads=host_cores()[0], device_probes=True,
                                   count=True)
+        log("MEM: oracle probe sequence over %d reads: %.1f s" % (ns, time.time() - t2))
         lines = {"text": ctr.ref_lines / ns, "sa": ctr.sa_lines / ns, "isa": ctr.isa_lines / ns,
                  "lcp": ctr.lcp_lines / ns, "kmer": ctr.kt_lines / ns}
         b_read = 64.0 * sum(lines.values())

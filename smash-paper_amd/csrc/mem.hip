@@ -51,10 +51,61 @@ struct Ival {
   uint64_t depth, start, end;
 };
 
-// expand_link (longSA.h:158-174) over the exact LCP
+// LCP runs for a depth d <= 255, where the u8 byte decides LCP >= d exactly
+// (L8 = min(LCP, 255)): no overflow-table bisection, 16 bytes per load.  A
+// repeat family's suffixes share more than 255 characters, so the exact
+// lcp_at of every step of its run cost a ~30-load bisection each.
+//   run_down: the j = s, s - 1, ... (at most `lim`) with L8[j] >= d, counted
+//   run_up:   the j = s, s + 1, ... < N (at most `lim`) with L8[j] >= d
+// (d >= 1 and L8[0] = 0 stop run_down at 0; the array has 64 pad bytes)
+__host__ __device__ __forceinline__ uint32_t dword_sel(const uint4 &v, uint32_t i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+__host__ __device__ __forceinline__ uint64_t run_down(const uint8_t *L8, uint64_t s, uint32_t d,
+                                             uint64_t lim) {
+  uint64_t n = 0;
+  while (n < lim) {
+    const uint64_t j = s - n, base = j & ~15ull;
+    const uint4 v = *reinterpret_cast<const uint4 *>(L8 + base);
+    for (int o = int(j - base); o >= 0; --o) {
+      if (((dword_sel(v, uint32_t(o) >> 2) >> (8 * (o & 3))) & 0xFF) < d || n >= lim) return n;
+      ++n;
+    }
+  }
+  return n;
+}
+__host__ __device__ __forceinline__ uint64_t run_up(const uint8_t *L8, uint64_t s, uint64_t N, uint32_t d,
+                                           uint64_t lim) {
+  uint64_t n = 0;
+  if (s >= N) return 0;
+  if (lim > N - s) lim = N - s;
+  while (n < lim) {
+    const uint64_t j = s + n, base = j & ~15ull;
+    const uint4 v = *reinterpret_cast<const uint4 *>(L8 + base);
+    for (uint32_t o = uint32_t(j - base); o < 16; ++o) {
+      if (((dword_sel(v, o >> 2) >> (8 * (o & 3))) & 0xFF) < d || n >= lim) return n;
+      ++n;
+    }
+  }
+  return n;
+}
+
+// expand_link (longSA.h:158-174) over the exact LCP.  It fails iff the two
+// runs together reach thresh (each step counts, left run first): for
+// depth <= 255 both runs come from run_down / run_up, capped there
 template <class IdxT>
 __device__ bool expand_link_x(const MemIx<IdxT> &m, Ival &l) {
   const uint64_t thresh = 2 * l.depth * m.x.logN;
+  if (l.depth <= 255) {
+    const uint32_t d = uint32_t(l.depth);
+    const uint64_t a = run_down(m.x.L8, l.start, d, thresh < l.start + 1 ? thresh : l.start + 1);
+    if (a >= thresh) return false;
+    const uint64_t b = run_up(m.x.L8, l.end + 1, m.x.N, d, thresh - a);
+    if (a + b >= thresh) return false;
+    l.start -= a;
+    l.end += b;
+    return true;
+  }
   uint64_t exp = 0, s = l.start, e = l.end;
   while (lcp_at(m, s) >= l.depth) {
     if (++exp >= thresh) return false;
@@ -148,32 +199,40 @@ __device__ __forceinline__ void find_lmax(const MemIx<IdxT> &m, const uint8_t *P
   }
 }
 
+// find_Lmaximal of `count` ranks in order (first, first - 1, ... when down,
+// else first, first + 1, ...) at one length, 8 at a time: their SA elements
+// and text bytes are independent loads, all in flight before the first
+// emission (an interval of a repeat family holds millions of suffixes, and
+// one lane walks it); emissions stay in the given order
+template <class IdxT>
+__device__ void lmax_ranks(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
+                           uint64_t prefix, uint64_t first, bool down, uint64_t count,
+                           uint64_t len, MemSink &s) {
+  if (len < min_len) return;                 // find_lmax emits nothing
+  const uint8_t pb = prefix ? P[prefix - 1] : 0;
+  uint64_t k0 = 0;
+  for (; k0 + 8 <= count; k0 += 8) {
+    uint64_t x[8];
+    uint8_t b[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = uint64_t(m.x.SA[down ? first - k0 - k : first + k0 + k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = x[k] ? m.x.T[x[k] - 1] : 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (prefix == 0 || x[k] == 0 || pb != b[k]) s.emit(x[k], prefix, len);
+  }
+  for (; k0 < count; ++k0)
+    find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[down ? first - k0 : first + k0]), len, s);
+}
+
 // collectMEMs (longSA.cpp:461-490); xmi by value as in the reference
 template <class IdxT>
 __device__ void collect_mems(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
                              uint64_t prefix, const Ival &mli, Ival xmi, MemSink &s) {
   const uint64_t N = m.x.N;
-  // the interval's suffixes in rank order, 8 at a time: their SA elements
-  // and text bytes are independent loads, all in flight before the first
-  // emission (an interval of a repeat family holds millions of suffixes,
-  // and one lane walks it); emissions stay in rank order
-  uint64_t i = xmi.start;
-  if (xmi.depth >= min_len) {
-    const uint8_t pb = prefix ? P[prefix - 1] : 0;
-    for (; i + 8 <= xmi.end + 1; i += 8) {
-      uint64_t x[8];
-      uint8_t b[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) x[k] = uint64_t(m.x.SA[i + k]);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) b[k] = x[k] ? m.x.T[x[k] - 1] : 0;
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (prefix == 0 || x[k] == 0 || pb != b[k]) s.emit(x[k], prefix, xmi.depth);
-    }
-  }
-  for (; i <= xmi.end; ++i)
-    find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[i]), xmi.depth, s);
+  lmax_ranks(m, P, min_len, prefix, xmi.start, false,
+             xmi.end >= xmi.start ? xmi.end - xmi.start + 1 : 0, xmi.depth, s);
   if (mli.start == xmi.start && mli.end == xmi.end) return;
   while (xmi.depth >= mli.depth) {
     if (xmi.end + 1 < N) {
@@ -182,7 +241,17 @@ __device__ void collect_mems(const MemIx<IdxT> &m, const uint8_t *P, uint32_t mi
     } else {
       xmi.depth = lcp_at(m, xmi.start);
     }
-    if (xmi.depth >= mli.depth) {
+    if (xmi.depth >= mli.depth && xmi.depth <= 255) {
+      // the two loops below as runs of the u8 LCP (run_down / run_up), the
+      // left run's ranks emitted downwards, then the right run's upwards
+      const uint32_t d = uint32_t(xmi.depth);
+      const uint64_t nl = run_down(m.x.L8, xmi.start, d, xmi.start + 1);
+      lmax_ranks(m, P, min_len, prefix, xmi.start - 1, true, nl, xmi.depth, s);
+      xmi.start -= nl;
+      const uint64_t nr = run_up(m.x.L8, xmi.end + 1, N, d, N);
+      lmax_ranks(m, P, min_len, prefix, xmi.end + 1, false, nr, xmi.depth, s);
+      xmi.end += nr;
+    } else if (xmi.depth >= mli.depth) {
       while (lcp_at(m, xmi.start) >= xmi.depth) {
         --xmi.start;
         find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[xmi.start]), xmi.depth, s);

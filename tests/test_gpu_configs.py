@@ -451,14 +451,18 @@ def test_c3_mem_hg19_equals_oracle(hg19, hg19_oracle):
     tot, per, _ = O.mem_batch(oix, h, threads=THREADS)
     assert got_n.tolist() == per.tolist()
     assert tot > n                                  # several MEMs per SMASH read
-    # (a read inside a repeat family has millions: its records are cut at
-    # cap, its count is still exact -- compare the records of the others)
-    assert (got_n <= cap).mean() > 0.99
+    # (a read inside a repeat family has thousands to millions: its records
+    # are cut at cap, its count is still exact -- compare the records of the
+    # others; 91% of these reads have <= 1 024 MEMs, profiles/r05/ab3)
+    assert (got_n <= cap).mean() > 0.8
     o = out.view(n, 2 * cap)[:4000].cpu().numpy().view(np.uint64)
+    compared = 0
     for i in range(4000):
         if got_n[i] <= cap:
             assert S.unpack_records(o[i], got_n[i], cap) == oix.search(h[i].tobytes(),
                                                                        mode="MEM"), i
+            compared += 1
+    assert compared > 3000
 
 
 # ---------------------------------------------------------------------------
