@@ -227,7 +227,7 @@ class Index:
         self.N = N
         if SA is None:
             SA, ISA, LCP = build_index(self.T[:N])
-        it = np.uint32 if N <= 0xFFFFFFFF else np.uint64
+        it = np.uint32 if N <= 0xFFFFFFFF and not pos_mask else np.uint64   # (packed: u64 words)
         self.SA = np.ascontiguousarray(SA, dtype=it)
         self.ISA = np.ascontiguousarray(ISA, dtype=it)
         if L8 is None:

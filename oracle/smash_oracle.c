@@ -225,6 +225,7 @@ typedef struct {
   const orc_index *ix;
   orc_counters *c;
   uint32_t isz;      /* element bytes of SA/ISA */
+  int dev;           /* mem.hip's probe sequence (orc_mem_dev) */
 } ctx_t;
 
 static inline uint64_t idx_at(const orc_index *ix, const void *a, uint32_t isz, uint64_t k) {
@@ -366,6 +367,7 @@ static ctx_t mkctx(const orc_index *ix, orc_counters *c) {
   ctx_t x;
   x.ix = ix; x.c = c;
   x.isz = ix->idx_bytes == 4 ? 4 : 8;
+  x.dev = 0;
   return x;
 }
 
@@ -417,13 +419,30 @@ static void find_lmax(const ctx_t *x, sink_t *s, const uint8_t *P,
   }
 }
 
+/* find_Lmaximal of the suffix at SA rank `rank`.  mem.hip over packed
+ * words (pos_mask, 8-byte elements): a word whose tag (bits 33-35) is 0..3
+ * names T[i - 1] as a c g t, so the device compares with it instead of
+ * loading the text byte (csrc/mem.hip left_max); the outcome is the same */
+static void find_lmax_rank(const ctx_t *x, sink_t *s, const uint8_t *P, uint32_t min_len,
+                           uint64_t prefix, uint64_t rank, uint64_t len) {
+  const uint64_t i = SAat(x, rank);
+  if (x->dev && x->ix->pos_mask && x->isz == 8 && prefix != 0 && i != 0) {
+    const unsigned tag = (unsigned)((((const uint64_t *)x->ix->SA)[rank] >> 33) & 7);
+    if (tag < 4) {
+      if (P[prefix - 1] != (uint8_t)"acgt"[tag] && len >= min_len) emit(s, i, prefix, len);
+      return;
+    }
+  }
+  find_lmax(x, s, P, min_len, prefix, i, len);
+}
+
 /* collectMEMs (longSA.cpp:461-490) */
 static void collect_mems(const ctx_t *x, sink_t *s, const uint8_t *P,
                          uint32_t min_len, uint64_t prefix, ival_t mli,
                          ival_t xmi) {
   const uint64_t N = x->ix->N;
   for (uint64_t i = xmi.start; i <= xmi.end; ++i)
-    find_lmax(x, s, P, min_len, prefix, SAat(x, i), xmi.depth);
+    find_lmax_rank(x, s, P, min_len, prefix, i, xmi.depth);
   if (mli.start == xmi.start && mli.end == xmi.end) return;
   while (xmi.depth >= mli.depth) {
     if (xmi.end + 1 < N) {
@@ -435,11 +454,11 @@ static void collect_mems(const ctx_t *x, sink_t *s, const uint8_t *P,
     if (xmi.depth >= mli.depth) {
       while (LCPat(x, xmi.start) >= xmi.depth) {
         --xmi.start;
-        find_lmax(x, s, P, min_len, prefix, SAat(x, xmi.start), xmi.depth);
+        find_lmax_rank(x, s, P, min_len, prefix, xmi.start, xmi.depth);
       }
       while (xmi.end + 1 < N && LCPat(x, xmi.end + 1) >= xmi.depth) {
         ++xmi.end;
-        find_lmax(x, s, P, min_len, prefix, SAat(x, xmi.end), xmi.depth);
+        find_lmax_rank(x, s, P, min_len, prefix, xmi.end, xmi.depth);
       }
     }
   }
@@ -523,6 +542,7 @@ static int mem_core(const orc_index *ix, const orc_accel *acc, const uint8_t *P,
                     uint32_t min_len, orc_match *out, uint32_t cap, orc_counters *ctr) {
   if (min_len < 1) return 0;                           /* longSA.cpp:588 */
   ctx_t x = mkctx(ix, ctr);
+  x.dev = acc != NULL;
   sink_t s = {out, cap, 0};
   const uint64_t N = ix->N;
   uint64_t prefix = 1;                                 /* longSA.cpp:398 */

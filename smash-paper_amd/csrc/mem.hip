@@ -22,6 +22,9 @@
 #include "common.hpp"
 #include "mam_device.hpp"
 
+#include <hipcub/hipcub.hpp>
+
+#include <cstdlib>
 #include <cstring>
 
 namespace smash {
@@ -32,6 +35,7 @@ struct MemIx {
   DevIndex<IdxT> x;
   const uint64_t *ovf;   // {idx, val} for LCP >= 255, sorted by idx
   uint64_t n_ovf;
+  bool pk;               // packed SA words: the BWT character in bits 33-35
 };
 
 template <class IdxT>
@@ -180,9 +184,28 @@ __device__ void traverse_x(const MemIx<IdxT> &m, const uint8_t *P, uint64_t L, u
   }
 }
 
+// A collectMEMs call over a large interval, left to k_mem_jobs (a wave per
+// call, its runs and left-maximality checks 64 ranks at a time): in SIMT a
+// lane walking a repeat family's million suffixes holds its whole wave, the
+// other 63 lanes' next reads included, for the walk.  The lane leaves a hole
+// in its read's records: `inl` records of its own came before it, hole h of
+// the read (k_mem_fix places the records around the holes afterwards).
+struct MemJob {
+  uint64_t r;                 // read
+  uint32_t prefix, inl, h;
+  uint32_t pb;                // P[prefix - 1] (prefix > 0)
+  uint64_t md, ms, me;        // mli {depth, start, end}
+  uint64_t xd, xs, xe;        // xmi
+};
+
 struct MemSink {
   uint4 *out;
   uint32_t cap, n;
+  // deferral (jobs == nullptr: every collectMEMs inline)
+  MemJob *jobs;
+  unsigned long long *n_jobs;
+  uint64_t job_cap, defer, r;
+  uint32_t holes;
   __device__ void emit(uint64_t ref, uint64_t q, uint64_t len) {
     if (n < cap)
       out[n] = make_uint4(uint32_t(ref), uint32_t(ref >> 32), uint32_t(q), uint32_t(len));
@@ -190,13 +213,26 @@ struct MemSink {
   }
 };
 
-// find_Lmaximal (longSA.cpp:438-457)
+// find_Lmaximal's test (longSA.cpp:438-457) for the suffix at x whose SA
+// word is `raw`: a packed word with tag 0..3 names T[x - 1] (a c g t), so
+// no text byte is loaded for it (oracle orc_mem_dev counts the same)
+template <class IdxT>
+__device__ __forceinline__ bool left_max(const MemIx<IdxT> &m, uint64_t prefix, uint32_t pb,
+                                         uint64_t raw, uint64_t x) {
+  if (prefix == 0 || x == 0) return true;
+  if (m.pk) {
+    const uint32_t tag = uint32_t(raw >> kPkPosBits) & 7u;
+    if (tag < 4) return pb != ((0x74676361u >> (8 * tag)) & 0xFFu);
+  }
+  return pb != m.x.T[x - 1];
+}
+
+// find_Lmaximal (longSA.cpp:438-457) of the suffix at SA rank `rank`
 template <class IdxT>
 __device__ __forceinline__ void find_lmax(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
-                                          uint64_t prefix, uint64_t i, uint64_t len, MemSink &s) {
-  if (prefix == 0 || i == 0 || P[prefix - 1] != m.x.T[i - 1]) {
-    if (len >= min_len) s.emit(i, prefix, len);
-  }
+                                          uint64_t prefix, uint64_t rank, uint64_t len, MemSink &s) {
+  const uint64_t raw = uint64_t(m.x.SA.p[rank]), x = raw & m.x.SA.mask;
+  if (left_max(m, prefix, prefix ? P[prefix - 1] : 0u, raw, x) && len >= min_len) s.emit(x, prefix, len);
 }
 
 // find_Lmaximal of `count` ranks in order (first, first - 1, ... when down,
@@ -209,21 +245,20 @@ __device__ void lmax_ranks(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_
                            uint64_t prefix, uint64_t first, bool down, uint64_t count,
                            uint64_t len, MemSink &s) {
   if (len < min_len) return;                 // find_lmax emits nothing
-  const uint8_t pb = prefix ? P[prefix - 1] : 0;
+  const uint32_t pb = prefix ? P[prefix - 1] : 0u;
   uint64_t k0 = 0;
   for (; k0 + 8 <= count; k0 += 8) {
-    uint64_t x[8];
-    uint8_t b[8];
+    uint64_t w[8];
+    bool e[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = uint64_t(m.x.SA[down ? first - k0 - k : first + k0 + k]);
+    for (int k = 0; k < 8; ++k) w[k] = uint64_t(m.x.SA.p[down ? first - k0 - k : first + k0 + k]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) b[k] = x[k] ? m.x.T[x[k] - 1] : 0;
+    for (int k = 0; k < 8; ++k) e[k] = left_max(m, prefix, pb, w[k], w[k] & m.x.SA.mask);
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if (prefix == 0 || x[k] == 0 || pb != b[k]) s.emit(x[k], prefix, len);
+      if (e[k]) s.emit(w[k] & m.x.SA.mask, prefix, len);
   }
-  for (; k0 < count; ++k0)
-    find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[down ? first - k0 : first + k0]), len, s);
+  for (; k0 < count; ++k0) find_lmax(m, P, min_len, prefix, down ? first - k0 : first + k0, len, s);
 }
 
 // collectMEMs (longSA.cpp:461-490); xmi by value as in the reference
@@ -231,6 +266,20 @@ template <class IdxT>
 __device__ void collect_mems(const MemIx<IdxT> &m, const uint8_t *P, uint32_t min_len,
                              uint64_t prefix, const Ival &mli, Ival xmi, MemSink &s) {
   const uint64_t N = m.x.N;
+  // every rank of mli is visited (xmi grows to mli): a large one goes to a job
+  if (s.jobs && mli.end >= mli.start && mli.end - mli.start + 1 >= s.defer && s.holes < 0xFFFFu) {
+    const unsigned long long j = atomicAdd(s.n_jobs, 1ull);
+    if (j < s.job_cap) {
+      MemJob &J = s.jobs[j];
+      J.r = s.r; J.prefix = uint32_t(prefix); J.inl = s.n; J.h = s.holes;
+      J.pb = prefix ? P[prefix - 1] : 0u;
+      J.md = mli.depth; J.ms = mli.start; J.me = mli.end;
+      J.xd = xmi.depth; J.xs = xmi.start; J.xe = xmi.end;
+      ++s.holes;
+      return;
+    }
+    // (the job list is full: inline, as without deferral)
+  }
   lmax_ranks(m, P, min_len, prefix, xmi.start, false,
              xmi.end >= xmi.start ? xmi.end - xmi.start + 1 : 0, xmi.depth, s);
   if (mli.start == xmi.start && mli.end == xmi.end) return;
@@ -254,11 +303,11 @@ __device__ void collect_mems(const MemIx<IdxT> &m, const uint8_t *P, uint32_t mi
     } else if (xmi.depth >= mli.depth) {
       while (lcp_at(m, xmi.start) >= xmi.depth) {
         --xmi.start;
-        find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[xmi.start]), xmi.depth, s);
+        find_lmax(m, P, min_len, prefix, xmi.start, xmi.depth, s);
       }
       while (xmi.end + 1 < N && lcp_at(m, xmi.end + 1) >= xmi.depth) {
         ++xmi.end;
-        find_lmax(m, P, min_len, prefix, uint64_t(m.x.SA[xmi.end]), xmi.depth, s);
+        find_lmax(m, P, min_len, prefix, xmi.end, xmi.depth, s);
       }
     }
   }
@@ -311,7 +360,9 @@ __global__ __launch_bounds__(BLOCK) void k_mem(MemIx<IdxT> m, const uint8_t *__r
                                                uint32_t len0, uint64_t n_reads, uint32_t min_len,
                                                uint4 *__restrict__ out, uint32_t cap,
                                                uint32_t *__restrict__ n_out, uint32_t row,
-                                               unsigned long long *work) {
+                                               unsigned long long *work, MemJob *jobs,
+                                               unsigned long long *n_jobs, uint64_t job_cap,
+                                               uint64_t defer, uint32_t *__restrict__ n_holes) {
   extern __shared__ uint8_t lds[];
   uint8_t *P = lds + threadIdx.x * row;
   for (;;) {
@@ -320,9 +371,159 @@ __global__ __launch_bounds__(BLOCK) void k_mem(MemIx<IdxT> m, const uint8_t *__r
     const uint32_t L = lens ? lens[r] : len0;
     const uint8_t *src = seqs + r * stride;
     for (uint32_t k = 0; k < row; ++k) P[k] = k < L ? src[k] : 0;
-    MemSink s{out + r * cap, cap, 0};
+    MemSink s{out + r * cap, cap, 0, jobs, n_jobs, job_cap, defer, r, 0};
     mem_read(m, P, L, min_len, s);
-    n_out[r] = s.n;
+    n_out[r] = s.n;                 // (the holes' records are added by k_mem_fix)
+    if (n_holes) n_holes[r] = s.holes;
+  }
+}
+
+// ---- deferred collectMEMs (MemJob): one wave per job ----------------------
+// the lane's 64-bit mask of the lanes below it
+__device__ __forceinline__ uint64_t lanes_below() {
+  const uint32_t lane = threadIdx.x & 63;
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// positions s, s - 1, ... with L8 >= d (d in 1..255), counted by the wave:
+// lane l tests positions s - n - 16 l - t, t = 0..15 (below 0: a stop)
+__device__ uint64_t wave_run_down(const uint8_t *L8, uint64_t s, uint32_t d) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t n = 0;; n += 1024) {
+    uint32_t stop = 16;
+    for (uint32_t t = 0; t < 16; ++t) {
+      const uint64_t k = n + 16ull * lane + t;
+      if (k > s || L8[s - k] < d) { stop = t; break; }
+    }
+    const uint64_t b = __ballot(stop < 16);
+    if (b) {
+      const int fl = __builtin_ctzll(b);
+      return n + 16ull * uint64_t(fl) + uint64_t(__shfl(int(stop), fl, 64));
+    }
+  }
+}
+// positions s, s + 1, ... < N with L8 >= d, counted by the wave
+__device__ uint64_t wave_run_up(const uint8_t *L8, uint64_t s, uint64_t N, uint32_t d) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t n = 0;; n += 1024) {
+    uint32_t stop = 16;
+    for (uint32_t t = 0; t < 16; ++t) {
+      const uint64_t q = s + n + 16ull * lane + t;
+      if (q >= N || L8[q] < d) { stop = t; break; }
+    }
+    const uint64_t b = __ballot(stop < 16);
+    if (b) {
+      const int fl = __builtin_ctzll(b);
+      return n + 16ull * uint64_t(fl) + uint64_t(__shfl(int(stop), fl, 64));
+    }
+  }
+}
+
+// COUNT (WRITE = false): the records each job emits -> E[j].  WRITE: a job
+// whose first record lands below cap (base[j], k_mem_fix) writes them, in
+// the order collectMEMs emits them, until cap.  Control flow is wave-uniform.
+template <class IdxT, bool WRITE>
+__global__ __launch_bounds__(256) void k_mem_jobs(MemIx<IdxT> m, const MemJob *__restrict__ jobs,
+                                                  const unsigned long long *n_jobs, uint64_t job_cap,
+                                                  uint32_t min_len, uint4 *__restrict__ out,
+                                                  uint32_t cap, uint32_t *__restrict__ E,
+                                                  const uint32_t *__restrict__ base) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nj = *n_jobs < job_cap ? *n_jobs : job_cap;
+  const uint64_t waves = uint64_t(gridDim.x) * (blockDim.x / 64);
+  const uint64_t N = m.x.N;
+  const uint64_t below = lanes_below();
+  for (uint64_t j = uint64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64; j < nj; j += waves) {
+    const MemJob J = jobs[j];
+    uint64_t pos = WRITE ? base[j] : 0;
+    if (WRITE && pos >= cap) continue;
+    uint4 *o = out + J.r * cap;
+    uint64_t emitted = 0;
+    bool full = false;
+    // find_Lmaximal of `count` ranks (first, first -/+ 1, ...) at length len
+    auto ranks = [&](uint64_t first, bool down, uint64_t count, uint64_t len) {
+      if (len < min_len || full) return;
+      for (uint64_t k0 = 0; k0 < count; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        bool e = false;
+        uint64_t x = 0;
+        if (k < count) {
+          const uint64_t w = uint64_t(m.x.SA.p[down ? first - k : first + k]);
+          x = w & m.x.SA.mask;
+          e = left_max(m, J.prefix, J.pb, w, x);
+        }
+        const uint64_t b = __ballot(e);
+        if (WRITE) {
+          const uint64_t p = pos + uint64_t(__popcll(b & below));
+          if (e && p < cap)
+            o[p] = make_uint4(uint32_t(x), uint32_t(x >> 32), J.prefix, uint32_t(len));
+        }
+        pos += uint64_t(__popcll(b));
+        emitted += uint64_t(__popcll(b));
+        if (WRITE && pos >= cap) { full = true; return; }
+      }
+    };
+    uint64_t xd = J.xd, xs = J.xs, xe = J.xe;
+    ranks(xs, false, xe >= xs ? xe - xs + 1 : 0, xd);
+    if (!(J.ms == xs && J.me == xe)) {
+      while (xd >= J.md && !full) {
+        if (xe + 1 < N) {
+          const uint64_t a = lcp_at(m, xs), b = lcp_at(m, xe + 1);
+          xd = a > b ? a : b;
+        } else {
+          xd = lcp_at(m, xs);
+        }
+        if (xd < J.md) break;
+        if (xd <= 255) {
+          const uint64_t nl = wave_run_down(m.x.L8, xs, uint32_t(xd));
+          ranks(xs - 1, true, nl, xd);
+          xs -= nl;
+          const uint64_t nr = wave_run_up(m.x.L8, xe + 1, N, uint32_t(xd));
+          ranks(xe + 1, false, nr, xd);
+          xe += nr;
+        } else {
+          while (!full && lcp_at(m, xs) >= xd) { --xs; ranks(xs, false, 1, xd); }
+          while (!full && xe + 1 < N && lcp_at(m, xe + 1) >= xd) { ++xe; ranks(xe, false, 1, xd); }
+        }
+      }
+    }
+    if (!WRITE && lane == 0) E[j] = uint32_t(emitted < 0xFFFFFFFFull ? emitted : 0xFFFFFFFFull);
+  }
+}
+
+// job j -> slot off[r] + h: the read's jobs in hole order
+__global__ void k_job_slots(const MemJob *__restrict__ jobs, const unsigned long long *n_jobs,
+                            uint64_t job_cap, const uint32_t *__restrict__ off,
+                            uint32_t *__restrict__ slot) {
+  const uint64_t nj = *n_jobs < job_cap ? *n_jobs : job_cap;
+  for (uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < nj;
+       j += uint64_t(gridDim.x) * blockDim.x)
+    slot[off[jobs[j].r] + jobs[j].h] = uint32_t(j);
+}
+
+// a read with holes: each job's first record index (its own records before
+// it + the earlier holes' records), the read's total, and its own records
+// moved up past the holes (from the last: a record only moves up)
+__global__ void k_mem_fix(const MemJob *__restrict__ jobs, const uint32_t *__restrict__ E,
+                          const uint32_t *__restrict__ n_holes, const uint32_t *__restrict__ off,
+                          const uint32_t *__restrict__ slot, uint64_t n_reads, uint4 *__restrict__ out,
+                          uint32_t cap, uint32_t *__restrict__ n_out, uint32_t *__restrict__ base) {
+  const uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_reads || n_holes[r] == 0) return;
+  const uint32_t nh = n_holes[r], o = off[r], own = n_out[r];
+  uint64_t acc = 0;
+  for (uint32_t h = 0; h < nh; ++h) {
+    const uint32_t j = slot[o + h];
+    base[j] = uint32_t(jobs[j].inl + acc < 0xFFFFFFFFull ? jobs[j].inl + acc : 0xFFFFFFFFull);
+    acc += E[j];
+  }
+  n_out[r] = uint32_t(own + acc < 0xFFFFFFFFull ? own + acc : 0xFFFFFFFFull);
+  uint4 *row = out + r * cap;
+  uint64_t sh = acc;
+  int64_t hh = int64_t(nh) - 1;
+  for (uint32_t k = own < cap ? own : cap; k-- > 0;) {
+    while (hh >= 0 && jobs[slot[o + hh]].inl > k) { sh -= E[slot[o + hh]]; --hh; }
+    if (sh && k + sh < cap) row[k + sh] = row[k];
   }
 }
 
@@ -423,11 +624,54 @@ int launch_mem(const smash_index *ix, uint32_t min_len, const uint8_t *seqs, uin
   m.x = make_dev_index<IdxT>(ix);
   m.ovf = ix->d_ovf;
   m.n_ovf = ix->n_ovf;
+  m.pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask;
+  // deferral: collectMEMs calls over >= SMASH_MEM_DEFER ranks (default 64;
+  // 0: none) become jobs, up to 4 per read on average (a full list: inline)
+  uint64_t defer = 64;
+  if (const char *e = std::getenv("SMASH_MEM_DEFER")) defer = uint64_t(std::strtoull(e, nullptr, 10));
+  const uint64_t job_cap = defer ? std::min<uint64_t>(std::max<uint64_t>(4 * n_reads, 1 << 16),
+                                                      (1ull << 31)) : 0;
+  MemJob *jobs = nullptr;
+  unsigned long long *n_jobs = nullptr;
+  uint32_t *E = nullptr, *base = nullptr, *slot = nullptr, *holes = nullptr, *off = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_bytes = 0;
+  if (job_cap) {
+    SMASH_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, holes, off, n_reads + 1, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&jobs), job_cap * sizeof(MemJob), s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&n_jobs), 8, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&E), job_cap * 4, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&base), job_cap * 4, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&slot), job_cap * 4, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&holes), (n_reads + 1) * 4, s));
+    SMASH_HIP(hipMallocAsync(reinterpret_cast<void **>(&off), (n_reads + 1) * 4, s));
+    SMASH_HIP(hipMallocAsync(&tmp, tmp_bytes + 16, s));
+    SMASH_HIP(hipMemsetAsync(n_jobs, 0, 8, s));
+    SMASH_HIP(hipMemsetAsync(holes + n_reads, 0, 4, s));
+  }
   SMASH_HIP(hipMemsetAsync(ix->d_work, 0, 8, s));
   if (ix->kev[0]) SMASH_HIP(hipEventRecord(ix->kev[0], s));
   kern<<<unsigned(blocks), B, lds, s>>>(m, seqs, stride, lens, len, n_reads, min_len, out, cap,
-                                        n_out, row, reinterpret_cast<unsigned long long *>(ix->d_work));
+                                        n_out, row, reinterpret_cast<unsigned long long *>(ix->d_work),
+                                        jobs, n_jobs, job_cap, defer ? defer : ~0ull, holes);
   SMASH_HIP(hipGetLastError());
+  if (job_cap) {
+    // the jobs' record counts; each read's jobs in hole order; the reads'
+    // totals and first job records; the records that land below cap
+    const unsigned gj = unsigned(std::min<uint64_t>(std::max<uint64_t>(1, uint64_t(cus) * 8),
+                                                    (job_cap + 3) / 4));
+    k_mem_jobs<IdxT, false><<<gj, 256, 0, s>>>(m, jobs, n_jobs, job_cap, min_len, out, cap, E, base);
+    SMASH_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, holes, off, n_reads + 1, s));
+    k_job_slots<<<unsigned(std::min<uint64_t>(65535, (job_cap + 255) / 256)), 256, 0, s>>>(
+        jobs, n_jobs, job_cap, off, slot);
+    k_mem_fix<<<unsigned((n_reads + 255) / 256), 256, 0, s>>>(jobs, E, holes, off, slot, n_reads, out,
+                                                            cap, n_out, base);
+    k_mem_jobs<IdxT, true><<<gj, 256, 0, s>>>(m, jobs, n_jobs, job_cap, min_len, out, cap, E, base);
+    SMASH_HIP(hipGetLastError());
+    for (void *q : {(void *)jobs, (void *)n_jobs, (void *)E, (void *)base, (void *)slot, (void *)holes,
+                    (void *)off, tmp})
+      (void)hipFreeAsync(q, s);
+  }
   if (ix->kev[1]) SMASH_HIP(hipEventRecord(ix->kev[1], s));
   return SMASH_OK;
 }

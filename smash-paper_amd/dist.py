@@ -116,6 +116,9 @@ class ShardedCounter:
         self.key_slack = int(key_slack)
         self.batch = 0          # batches stepped since the last reset
         self.key_need = 0       # the first batch's projection (plan_pairs > 0)
+        # exported since construction: keys / words to every owner, and to
+        # the other ranks only (the bytes that cross the links)
+        self.sent = {"keys": 0, "words": 0, "remote_keys": 0, "remote_words": 0}
         self.timing = {}
         self._t = None
 
@@ -215,6 +218,10 @@ class ShardedCounter:
             self._size_keys(sum(int(x) for x in cnt), sum(rcv))
         self._mark("counts")
         snd, sndw = [int(x) for x in cnt], [int(x) for x in wcnt]
+        self.sent["keys"] += sum(snd)
+        self.sent["words"] += sum(sndw)
+        self.sent["remote_keys"] += sum(snd) - snd[r]
+        self.sent["remote_words"] += sum(sndw) - sndw[r]
         n_recv, n_words = sum(rcv), sum(rcw)
         recv = torch.empty((max(n_recv, 1), hdr.shape[1]), dtype=torch.int64, device=dev)
         self.comm.all_to_all(recv[:n_recv], hdr[:sum(snd)], rcv, snd)

@@ -132,3 +132,34 @@ def test_modes_equal_oracle_mid_genome(mid, mode, L):
         exp = oix.search(reads[i].tobytes(), mode)
         assert n[i] == len(exp), (i, mode)
         assert got[i] == exp[:cap], (i, mode, reads[i].tobytes()[:40])
+
+
+@pytest.mark.parametrize("defer", ["0", "2", "64"])
+@pytest.mark.parametrize("cap", [37, 4096])
+def test_mem_deferred_collect_equal_oracle(mid, defer, cap, monkeypatch):
+    """collectMEMs calls over >= SMASH_MEM_DEFER ranks run as wave jobs
+    (csrc/mem.hip k_mem_jobs) and their records are placed around the lane's
+    own (k_mem_fix): the records, cut at cap, and the counts equal the
+    oracle's for every threshold (0: none deferred; 2: nearly every call)."""
+    T, oix, dix = mid
+    monkeypatch.setenv("SMASH_MEM_DEFER", defer)
+    rng = np.random.default_rng(7)
+    reads = _edge_reads(T[:-1], 150, 300, rng)
+    got, n = run_match(dix, reads, "MEM", cap=cap)
+    for i in range(len(reads)):
+        exp = oix.search(reads[i].tobytes(), "MEM")
+        assert n[i] == len(exp), (i, defer, cap)
+        assert got[i] == exp[:cap], (i, defer, cap)
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_mem_deferred_matches_reference_triples(gix, s, monkeypatch):
+    """the reference's own MEM triples with nearly every collectMEMs call
+    deferred to the wave jobs (SMASH_MEM_DEFER=2)"""
+    monkeypatch.setenv("SMASH_MEM_DEFER", "2")
+    reads = interleaved_reads(s)
+    exp = [[tuple(map(int, x.split(","))) for x in l.split()[2:]]
+           for l in read_gz_lines("%s_MEM.txt.gz" % s)]
+    got, n = run_match(gix, reads[:len(exp)], "MEM", cap=16384)
+    bad = [i for i in range(len(exp)) if got[i] != exp[i]]
+    assert not bad, (bad[:5], got[bad[0]] if bad else None, exp[bad[0]] if bad else None)

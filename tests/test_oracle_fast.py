@@ -1,11 +1,16 @@
 """The accelerated search (device SMASH_MODE_MAM, restated in the oracle as
 orc_mam_fast) must emit exactly the reference's MAM triples: checked against
 the golden vectors and against orc_mam on a larger synthetic genome (CPU)."""
+import os
+import sys
+
 import numpy as np
 import pytest
 
 import oracle as O
 from conftest import interleaved_reads, read_gz_lines
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.parametrize("s", ["s100", "s150"])
@@ -98,3 +103,38 @@ def test_device_mem_probes_on_edge_reads(tiny_ix):
         for ml in (20, 12, 30):
             assert tiny_ix.search(P, mode="MEM_DEV", min_len=ml) == \
                 tiny_ix.search(P, mode="MEM", min_len=ml)
+
+
+def test_device_mem_probes_packed_words():
+    """mem.hip over packed 8-byte SA words decides find_Lmaximal from the
+    word's BWT tag instead of a text byte (csrc/mem.hip left_max); the
+    oracle's restatement of that probe sequence (orc_mem_dev over an index
+    with pos_mask) gives the reference's MEMs with fewer text lines."""
+    import synth
+    sys.path.insert(0, os.path.join(ROOT, "tools", "sm_emu"))
+    import sm_emu
+    g = synth.make_genome("mid")
+    T, sp, sz, names = O.text_from_contigs(g)
+    ix = O.Index(T, sp, sz, names)
+    ix.accel()
+    sa, isa = sm_emu.pack_words(ix.T, ix.SA, ix.ISA, ix.L8, ix.acc.K)
+    pix = O.Index(ix.T, sp, sz, names, SA=sa, ISA=isa, L8=ix.L8, ovf=ix.ovf, padded_text=True,
+                  pos_mask=sm_emu.POS_MASK)
+    assert pix.SA.dtype == np.uint64
+    pix.accel()
+    rng = np.random.default_rng(11)
+    N = ix.N
+    reads = []
+    for i in range(120):                      # genome slices: repeat copies give many MEMs
+        p = int(rng.integers(0, N - 151))
+        r = bytearray(ix.T[p:p + 150].tobytes())
+        if i % 3 == 0:
+            r[int(rng.integers(0, 150))] = ord("g")
+        reads.append(bytes(r))
+    R = np.frombuffer(b"".join(reads), np.uint8).reshape(len(reads), 150)
+    for r in reads:
+        assert pix.search(r, mode="MEM_DEV") == ix.search(r, mode="MEM")
+    _, per_a, ca = O.mem_batch(ix, R, device_probes=True, count=True)
+    _, per_b, cb = O.mem_batch(pix, R, device_probes=True, count=True)
+    assert (per_a == per_b).all() and per_a.sum() > len(reads)
+    assert cb.ref_lines < ca.ref_lines
