@@ -77,10 +77,10 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   // the records: a wild address retires its lane and fails the call instead
   // of faulting the GPU.
   // the packed-word instantiation for an index whose 8-byte SA / ISA words
-  // carry the search's hints (pack_index.hip; SMASH_SM_PK=0: the plain
-  // kernel over them, for A/B -- it reads the elements through the same mask)
-  const char *pke = std::getenv("SMASH_SM_PK");
-  const bool pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask && !(pke && pke[0] == '0');
+  // carry the search's hints (pack_index.hip); the plain kernel reads whole
+  // elements, so an A/B of the two runs over an unpacked index
+  // (SMASH_PACK_IDX=0 or smash_index_pack) instead
+  const bool pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask;
   auto kern = pk ? sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8>
                  : sm::k_mam_sm<IdxT, B, CHECK, STATS, false>;
   int per_cu = 0, cus = 0;
