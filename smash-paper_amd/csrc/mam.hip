@@ -228,12 +228,10 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.bm_dual = 3;
   c.pf = 1;
   c.u32 = 1;
-  if (const char *e = std::getenv("SMASH_SM_PF")) c.pf = uint32_t(std::atoi(e));
-  if (const char *e = std::getenv("SMASH_SM_U32")) c.u32 = uint32_t(std::atoi(e));
-  if (const char *e = std::getenv("SMASH_SM_BM_DUAL")) c.bm_dual = uint32_t(std::atoi(e));
-  if (const char *e = std::getenv("SMASH_SM_GRAB")) c.grab = uint32_t(std::max(1, std::atoi(e)));
+  // (pf, u32, bm_dual, grab and lin_blocks are the kernel's compile-time
+  // defaults on the device, SM_KNOB in mam_sm.hpp: the fields above only
+  // document them; tools/sm_emu varies them)
   if (const char *e = std::getenv("SMASH_SM_PAD")) c.pad = uint32_t(std::atoi(e));
-  if (const char *e = std::getenv("SMASH_SM_LIN")) c.lin_blocks = uint32_t(std::max(1, std::atoi(e)));
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
   c.out = out; c.n_out = n_out;
   c.work = ws ? ws->work : reinterpret_cast<unsigned long long *>(ix->d_work);

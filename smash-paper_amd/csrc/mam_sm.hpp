@@ -31,6 +31,15 @@
 #ifndef PAD_KEEP
 #define PAD_KEEP(x) asm volatile("" : "+v"(x))
 #endif
+// The search's policy knobs (binary-search prefetch, 32-byte U scans, linear
+// L8 blocks before bisecting a run, the (F) filter policy, reads claimed per
+// wave): compile-time defaults on the device, where their alternatives are
+// dead code that still shapes the loop's registers and schedule; the host
+// emulator (tools/sm_emu, SM_KNOB defined there) keeps them as runtime Ctx
+// fields for its A/B tests of the policies.
+#ifndef SM_KNOB
+#define SM_KNOB(field, dflt) (dflt)
+#endif
 #ifndef SM_HOOK_BM
 #define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes (policies 0-2)
 #endif
@@ -684,7 +693,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     dch = d; j = 1;
     addr = reinterpret_cast<uint64_t>(c.U + p + 1);
     addr2 = addr + 16;
-    need2 = c.u32 && d - 1 > 16;
+    need2 = SM_KNOB(u32, 1u) && d - 1 > 16;
     st = S_USCAN;
   };
   // a run [es, ee] grows within [lb, hb] while L8 >= xd: both sides' first
@@ -729,9 +738,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     addr = reinterpret_cast<uint64_t>(c.T + (sp & PM) + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
-    need2 = c.pf && lo < m;
-    pfr = c.pf && m + 1 < hi;
-    pf = c.pf != 0;
+    need2 = SM_KNOB(pf, 1u) && lo < m;
+    pfr = SM_KNOB(pf, 1u) && m + 1 < hi;
+    pf = SM_KNOB(pf, 1u) != 0;
     st = S_CMP; op = O_BS;
     return false;
   };
@@ -771,7 +780,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     unsigned long long base = 0;
     uint32_t take = 0;
     if (newm && avail < need) {
-      take = need > c.grab ? need : c.grab;
+      take = need > SM_KNOB(grab, 16u) ? need : SM_KNOB(grab, 16u);
       if (lane == uint32_t(__builtin_ctzll(newm)))
         base = atomicAdd(c.work, (unsigned long long)take);
     }
@@ -919,7 +928,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       case S_BM: {                                   // (F) a k-mer table entry arrived
         SM_REGION(3);
         need2 = false;
-        if (c.bm_dual == 3) {
+        if (SM_KNOB(bm_dual, 3u) == 3) {
           // the entry of the k-mer at x = kp + fj + 2; c0 = the 2-bit codes of
           // the k + 4 read bases [x - 2, x + k + 2), first most significant:
           // its presence bits give the B-mers at x - 2, x - 1, x (common.hpp)
@@ -946,8 +955,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         // A B-mer's presence is bit (code & 15) of its first k-mer's entry.
         const uint64_t cc = bm2 ? c0 : c1;
         const bool pa = (lo64(v) >> (40 + (cc & 15))) & 1ull;
-        const bool pb = !c.bm_dual || ((lo64(v2) >> (40 + (c0 & 15))) & 1ull);
-        if (c.bm_dual == 2) {
+        const bool pb = !SM_KNOB(bm_dual, 3u) || ((lo64(v2) >> (40 + (c0 & 15))) & 1ull);
+        if (SM_KNOB(bm_dual, 3u) == 2) {
           // cover policy (bm_dual 2): the pair probed depends on the mode fm
           // (A_TOP); an absent B-mer at s rules out the windows [s-D, s]
           // (D = min_len - B), so the window advances past every window an
@@ -986,7 +995,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           a = A_TOP;
         } else if (!pa || !pb) {
           depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
-        } else if (!bm2 && !c.bm_dual) {
+        } else if (!bm2 && !SM_KNOB(bm_dual, 3u)) {
           bm2 = true;
           addr = reinterpret_cast<uint64_t>(c.KT + 2 * (c0 >> 4));
         } else {
@@ -1108,7 +1117,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else {
           addr += need2 ? 32 : 16;
           addr2 = addr + 16;
-          need2 = c.u32 && dch - j > 16;
+          need2 = SM_KNOB(u32, 1u) && dch - j > 16;
         }
         break;
       }
@@ -1147,7 +1156,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         const bool more = left ? moreL : moreR;
         if (!more) {
           a = left ? A_XL_DONE : A_RUN_DONE;
-        } else if (++nblk < c.lin_blocks) {
+        } else if (++nblk < SM_KNOB(lin_blocks, 8u)) {
           addr = left ? lblock(es) : reinterpret_cast<uint64_t>(c.L8 + ee + 1);
           st = left ? S_EXL : S_EXR;
         } else {                                      // long run: bisect for its end
@@ -1328,7 +1337,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           depth = 0; start = 0; end = N - 1; have_pos = false;
           prefix = uint32_t(kb) + 1;                  // (A_TOP again: parks in S_ALU)
           fm = 0;
-        } else if (c.bm_dual == 3) {
+        } else if (SM_KNOB(bm_dual, 3u) == 3) {
           // (F) policy 3.  Window [p, p + min_len) can start a match only if
           // its D + 1 B-mers (offsets 0..D from p) all occur; an absent
           // B-mer at offset s rules out the windows s - D .. s.  One k-mer
@@ -1399,9 +1408,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           // {last, first} of this window, 1 and 2 (bm_dual 2) see S_BM
           uint32_t s1 = prefix + D, s2 = prefix;
           bool ok = okQ && okP;
-          if (c.bm_dual == 2 && fm == 1 && okQ && okM) {
+          if (SM_KNOB(bm_dual, 3u) == 2 && fm == 1 && okQ && okM) {
             s2 = sM; ok = true;
-          } else if (c.bm_dual == 2 && fm == 2 && okP && okP1) {
+          } else if (SM_KNOB(bm_dual, 3u) == 2 && fm == 2 && okP && okP1) {
             s1 = prefix; s2 = prefix + 1; ok = true;
           } else {
             fm = 0;
@@ -1424,7 +1433,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             // a B-mer's presence: its first k-mer's entry (B = k + 2)
             addr = reinterpret_cast<uint64_t>(c.KT + 2 * (c1 >> 4));
             st = S_BM; bm2 = false;
-            if (c.bm_dual) { addr2 = reinterpret_cast<uint64_t>(c.KT + 2 * (c0 >> 4)); need2 = true; }
+            if (SM_KNOB(bm_dual, 3u)) { addr2 = reinterpret_cast<uint64_t>(c.KT + 2 * (c0 >> 4)); need2 = true; }
             a = A_NONE;
           } else {
             proceed = true;                             // no bitmap verdict

@@ -108,6 +108,8 @@ static void emu_dma_row(uint32_t *dst, const uint4 *src, uint32_t n, const uint4
 // with the whole wave)
 #define SM_HOST_LANE
 #define SM_DMA_ROW_HOST
+// the policy knobs stay runtime here (the device compiles their defaults)
+#define SM_KNOB(field, dflt) (c.field)
 #define PAD_KEEP(x) ((void)(x))
 // v_perm_b32 on the host: byte i of the result from selector byte i (0-7 a
 // byte of {s0:s1}, 8-11 the sign of byte 1/3/5/7 spread, 12 zero, 13+ 0xFF)
