@@ -278,6 +278,12 @@ int smash_pipeline_reserve_keys(smash_pipeline *p, uint64_t keys, void *stream);
 /* The keys the set takes for sure (a full set is SMASH_ERR_NOMEM in the
  * pipeline's statistics, never a silent cut). */
 uint64_t smash_pipeline_key_capacity(const smash_pipeline *p);
+/* 1 when the pipeline's searches hand the post stage each forward match's
+ * right map.bin byte with the match (from the packed SA word of its row,
+ * DESIGN.md section 3), so that byte is not loaded: the index is packed, its
+ * map.bin was computed from it (not read from a file), and the tag offsets
+ * are its contig offsets.  SMASH_MAP_HINT=0 at creation turns it off. */
+int smash_pipeline_map_hints(const smash_pipeline *p);
 /* The data error recorded so far (0: none; the error of smash_stats), as of
  * the work queued on `stream`: waits for that stream only (not for a search
  * running on the pipeline's own streams). */

@@ -134,6 +134,9 @@ struct smash_index {
   uint64_t n_ovf = 0;
   uint8_t *d_map = nullptr;
   uint64_t map_bytes = 0;
+  // map.bin was computed here from this index (build_map), not read from a
+  // file: the search's map hints (SearchWs::mhint) may stand in for its bytes
+  bool map_own = false;
   uint64_t pos_mask = ~0ull;     // kPkPosMask when SA / ISA carry packed hints (pack_index.hip)
   uint8_t *d_uniq = nullptr;     // U[x] (aux_build.hip), N + 64
   mutable uint64_t *d_nsdir = nullptr;   // first U < 255 per 4096 positions (mappability.hip)
@@ -184,6 +187,9 @@ struct SearchWs {
   // buffers' previous reader, so the records of the next batch are built
   // while that reader still runs
   hipEvent_t gate = nullptr;
+  // the pipeline's packed-index searches: match words carry the map hint
+  // (sm::Ctx::mhint; bits 40..47, the post stage masks the reference to 40)
+  bool mhint = false;
 };
 int map_batch_impl(const smash_index *ix, int mode, uint32_t min_len, const uint8_t *d_seqs,
                    uint64_t stride, const uint16_t *d_lens, uint32_t len, uint64_t n_reads,

@@ -232,6 +232,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   // defaults on the device, SM_KNOB in mam_sm.hpp: the fields above only
   // document them; tools/sm_emu varies them)
   if (const char *e = std::getenv("SMASH_SM_PAD")) c.pad = uint32_t(std::atoi(e));
+  c.mhint = ws && ws->mhint ? 1u : 0u;
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;
   c.out = out; c.n_out = n_out;
   c.work = ws ? ws->work : reinterpret_cast<unsigned long long *>(ix->d_work);

@@ -512,6 +512,11 @@ struct Ctx {
   uint32_t bad_tab_lo, bad_tab_hi;
   uint32_t lin_blocks;    // L8 blocks scanned per side of a run before bisecting (>= 1)
   uint32_t pad;           // experiment: dependent ALU ops added per iteration (0 = none)
+  // (PK, the read -> bin-count pipeline) each emitted match word carries in
+  // bits 40..47 the map.bin right byte m = max(LCP[r], LCP[r + 1]) + 1 of
+  // its own SA row r when the word's L8 hints give it exactly (both < 127),
+  // else 0 (csrc/pipeline.hip mate_fast)
+  uint32_t mhint;
   uint32_t grab;          // reads a wave claims per atomic on `work` (>= 1)
   uint32_t bm_dual;       // (F) policy: 0 one B-mer per iteration, 1 last + first in one,
                           // 2 the cover policy (two B-mers per iteration chosen by mode),
@@ -558,6 +563,12 @@ __device__ __forceinline__ bool pk_above(uint64_t w, uint32_t b, uint32_t xd) {
 }
 // the lowercase base of 2-bit code q (a0 c1 g2 t3)
 __device__ __forceinline__ uint32_t pk_char(uint32_t q) { return (0x74676361u >> (8 * q)) & 0xFFu; }
+// the match word's map hint (Ctx::mhint) from its packed SA word w: m of the
+// row from its two L8 bytes when both are below the 127 cap, else 0
+__device__ __forceinline__ uint64_t pk_map_hint(uint64_t w) {
+  const uint32_t a = uint32_t(w >> 36) & 127u, b = uint32_t(w >> 43) & 127u;
+  return (a < 127u && b < 127u) ? uint64_t((a > b ? a : b) + 1u) << 40 : 0ull;
+}
 // the window's 7 bases as bytes 0..6 of a u64 (byte 7 zero): each 2-bit code
 // spread to a byte selector, one permute of the a c g t table per 4 bytes
 __device__ __forceinline__ uint64_t pk_window(uint64_t w) {
@@ -1042,7 +1053,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         SM_REGION(6);
         SM_HOOK_BYTE(pos & PM);
         if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
-          if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & PM, prefix, depth);
+          if (nem < c.cap)
+            c.out[rd * c.cap + nem] =
+                pack_match(pos & PM, prefix, depth) | (PK && c.mhint ? pk_map_hint(pos) : 0ull);
           ++nem;
         }
         uscan_start(pos & PM, depth);
@@ -1305,7 +1318,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           if (depth >= c.min_len &&
               (!PK || prefix == 0 || (pos & PM) == 0 ||
                P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
-            if (nem < c.cap) c.out[rd * c.cap + nem] = pack_match(pos & PM, prefix, depth);
+            if (nem < c.cap)
+              c.out[rd * c.cap + nem] =
+                  pack_match(pos & PM, prefix, depth) | (PK && c.mhint ? pk_map_hint(pos) : 0ull);
             ++nem;
           }
           uscan_start(pos & PM, depth);

@@ -146,6 +146,10 @@ struct smash_pipeline {
   uint8_t *d_post_ws = nullptr;   // k_post workspace: kPostThreads slices
   uint64_t hash_mask = ~0ull;
   bool post_fast = false;
+  // the searches' match words carry map hints (SearchWs::mhint, PostCfg):
+  // packed index words, map.bin built from this index, tag offsets equal to
+  // its contig offsets (SMASH_MAP_HINT=0: off, A/B)
+  bool mhint = false;
   uint32_t post_cap = 0;
   uint32_t *d_send_q = nullptr;   // exported slot -> pair
   unsigned long long *d_owner = nullptr;  // per owner: [0,64) keys [64,128) words (k_export_totals)
@@ -193,7 +197,14 @@ struct PostCfg {
   // [sp_cell[c], sp_cell[c + 1]] only
   const uint32_t *sp_cell;
   uint32_t sp_shift, sp_ncell;
+  // the search's map hints (SearchWs::mhint): a forward match word carries
+  // its right map.bin byte before the edge rule in bits 40..47 (0: none)
+  bool mhint;
 };
+
+// the reference position of a match word: 48 bits (smash_gpu.h), 40 when
+// the word may carry a map hint (N < 2^33 then)
+constexpr uint64_t kRefMask = 0xFFFFFFFFFFull;
 
 struct Aln {
   int64_t pos, qpos;
@@ -228,7 +239,7 @@ __device__ int mate_hits(const PostCfg &c, const uint64_t *m, uint32_t n,
   const uint32_t L = c.L;
   for (uint32_t k = 0; k < n; ++k) {
     const uint64_t w = m[k];
-    const uint64_t ref = w & 0xFFFFFFFFFFFFull;
+    const uint64_t ref = w & (c.mhint ? kRefMask : 0xFFFFFFFFFFFFull);
     const uint32_t q = uint32_t((w >> 48) & 0xFF), len = uint32_t(w >> 56);
     uint32_t lo = 0, hi = c.n_seq;          // upper_bound(startpos, ref)
     while (lo < hi) {
@@ -471,6 +482,26 @@ __device__ __forceinline__ void wave_push(uint32_t *list, uint32_t *n, bool pred
   if (pred) list[base + uint32_t(__popcll(b & ((1ull << lane) - 1)))] = v;
 }
 
+// the same network over (key, payload) pairs, ordered by key
+template <int N>
+__device__ __forceinline__ void sort_net2(uint64_t (&v)[N], uint32_t (&r)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+      for (int j = k % p; j <= N - 1 - k; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i < k; ++i)
+          if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const bool sw = v[i + j + k] < v[i + j];
+            const uint64_t a = v[i + j], b = v[i + j + k];
+            const uint32_t ra = r[i + j], rb = r[i + j + k];
+            v[i + j] = sw ? b : a; v[i + j + k] = sw ? a : b;
+            r[i + j] = sw ? rb : ra; r[i + j + k] = sw ? ra : rb;
+          }
+}
+
 // Batcher odd-even merge sort, N a power of two (fully unrolled)
 template <int N>
 __device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
@@ -492,12 +523,13 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *__re
                                           int32_t &err) {
   const uint32_t L = c.L;
   uint64_t A[CAP];
+  uint32_t R[CAP];   // 0x100 | the alignment's right map byte, from the match's hint; 0: load it
   uint64_t w[CAP];
 #pragma unroll
   for (int k = 0; k < CAP; ++k) w[k] = uint32_t(k) < n ? m[k] : 0;
 #pragma unroll
   for (int k = 0; k < CAP; ++k) {
-    const uint64_t ref = w[k] & 0xFFFFFFFFFFFFull;
+    const uint64_t ref = w[k] & (c.mhint ? kRefMask : 0xFFFFFFFFFFFFull);
     const uint32_t q = uint32_t((w[k] >> 48) & 0xFF), len = uint32_t(w[k] >> 56);
     // upper_bound(startpos, ref) over the directory's cell range (global
     // memory: no LDS, see d_stats); slots past n skip it (not ok below)
@@ -522,8 +554,14 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *__re
     A[k] = ok ? (uint64_t(rc) << 63) | (uint64_t(si >> 1) << 48) | (uint64_t(pos) << 16) |
                     (prefix << 8) | len
               : ~0ull;
+    // a forward match starts at forward base b = ref - startpos: its right
+    // byte is m of its own SA row, zeroed when m + b >= the contig's size
+    // (longSA.cpp:666), at map entry tag_off + b (the pipeline enables the
+    // hints only when tag_off is the index's own contig offsets)
+    const uint32_t h = c.mhint && !rc ? uint32_t(w[k] >> 40) & 0xFFu : 0u;
+    R[k] = h ? 0x100u | (ref - sp[si] + h >= c.sizes[si] ? 0u : h) : 0u;
   }
-  sort_net(A);
+  sort_net2(A, R);
   // merge runs on one diagonal (rc, tid, pos) into hits; tag every block
   uint32_t g_prefix = 0, g_qmin = 0;
   int32_t g_l0 = 0, g_r0 = 0;
@@ -539,7 +577,7 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *__re
     const uint32_t abspos = c.tag_off[tid] + pos + 1;
     const uint32_t li = abspos + prefix + len - 1, ri = abspos + prefix - 1;
     const unsigned lm = valid ? mapb(c, 2 + uint64_t(li) * 2) : 0u;
-    const unsigned rm = valid ? mapb(c, 2 + uint64_t(ri) * 2 + 1) : 0u;
+    const unsigned rm = !valid ? 0u : (R[i] & 0x100u) ? (R[i] & 0xFFu) : mapb(c, 2 + uint64_t(ri) * 2 + 1);
     const int32_t left = lm ? int32_t(lm) - 1 : 255, right = rm ? int32_t(rm) : 255;
     if (start) {
       g_prefix = prefix; g_qmin = qpos; g_l0 = left; g_r0 = right;
@@ -1420,6 +1458,7 @@ PostCfg post_cfg(const smash_pipeline *p) {
   c.sp_cell = p->d_sp_cell;
   c.sp_shift = p->sp_shift;
   c.sp_ncell = p->sp_ncell;
+  c.mhint = p->mhint;
   return c;
 }
 
@@ -1491,6 +1530,17 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_chrom_off = dalloc<int64_t>(p->n_contig);
     p->d_bins = dalloc<int64_t>(p->nbins);
     SMASH_HIPX(hipMemcpy(p->d_tag_off, cfg->h_tag_offsets, 4 * p->n_contig, hipMemcpyHostToDevice));
+    {
+      const char *mh = getenv("SMASH_MAP_HINT");
+      bool ok = !(mh && mh[0] == '0') && ix->pos_mask == kPkPosMask && ix->rcref && ix->d_map &&
+                ix->map_own;
+      uint64_t off = 0;
+      for (uint32_t t = 0; ok && t < p->n_contig; ++t) {
+        ok = cfg->h_tag_offsets[t] == off;
+        off += ix->sizes[2 * t];
+      }
+      p->mhint = ok;
+    }
     SMASH_HIPX(hipMemcpy(p->d_small, cfg->h_small_chr, p->n_contig, hipMemcpyHostToDevice));
     SMASH_HIPX(hipMemcpy(p->d_chrom_off, cfg->h_chrom_off, 8 * p->n_contig, hipMemcpyHostToDevice));
     SMASH_HIPX(hipMemcpy(p->d_bins, cfg->h_bin_starts, 8 * p->nbins, hipMemcpyHostToDevice));
@@ -1732,7 +1782,7 @@ static int search_into(smash_pipeline *p, int k, const uint8_t *d_reads, uint64_
     SMASH_HIP(hipMalloc(reinterpret_cast<void **>(&p->d_rec_s[k]), p->rec_bytes));
   }
   const SearchWs ws{p->d_rec_s[k], p->d_rec_s[k] ? p->rec_bytes : 0, p->d_work_s[k],
-                    p->set_used[k] && !p->gate_prep ? p->ev_free[k] : nullptr};
+                    p->set_used[k] && !p->gate_prep ? p->ev_free[k] : nullptr, p->mhint};
   const int rc = map_batch_impl(p->ix, SMASH_MODE_MAM, p->min_len, d_reads, p->stride, nullptr,
                                 p->read_len, 2 * n_pairs, p->d_match_s[k], p->slots,
                                 p->d_nmatch_s[k], xs, false, &ws);   // probe check at stats time
@@ -2581,6 +2631,8 @@ extern "C" uint64_t smash_pipeline_key_capacity(const smash_pipeline *p) {
   // keys the set takes for sure: half its slots, and 16 words of arena each
   return p ? std::min<uint64_t>((p->table_mask + 1) / 2, p->arena_cap / 16) : 0;
 }
+
+extern "C" int smash_pipeline_map_hints(const smash_pipeline *p) { return p && p->mhint ? 1 : 0; }
 
 extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   if (!p) return SMASH_ERR_ARG;

@@ -558,6 +558,7 @@ void finish_lcp(smash_index *ix, const uint32_t *lcp, hipStream_t s) {
 void build_map(smash_index *ix, const uint32_t *lcp, hipStream_t s) {
   if (ix->idx_bytes == 4) build_map_t<uint32_t>(ix, lcp, s);
   else build_map_t<uint64_t>(ix, lcp, s);
+  ix->map_own = true;
 }
 
 }  // namespace smash

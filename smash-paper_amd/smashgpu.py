@@ -63,7 +63,7 @@ EXPORTS = [
     "smash_read_stride", "smash_pipeline_max_batch",
     "smash_mappability_prepare", "smash_mappability_window", "smash_index_pack",
     "smash_pipeline_reserve_keys", "smash_pipeline_key_capacity", "smash_pipeline_error",
-    "smash_mappability_release",
+    "smash_mappability_release", "smash_pipeline_map_hints",
 ]
 
 
@@ -230,6 +230,8 @@ def lib():
     L.smash_pipeline_reserve_keys.argtypes = [vp, C.c_uint64, vp]
     L.smash_pipeline_key_capacity.argtypes = [vp]
     L.smash_pipeline_key_capacity.restype = C.c_uint64
+    L.smash_pipeline_map_hints.argtypes = [vp]
+    L.smash_pipeline_map_hints.restype = C.c_int
     L.smash_pipeline_error.argtypes = [vp, vp, C.POINTER(C.c_int32)]
     L.smash_mappability_window.argtypes = [vp, C.c_uint64, C.c_uint64, u64p, u64p]
     L.smash_pipeline_max_batch.argtypes = [C.c_uint32, C.c_uint32]
@@ -608,6 +610,12 @@ class Pipeline:
 
     def reset(self, stream=None):
         check(lib().smash_pipeline_reset(self.h, vp(_stream(stream))), "smash_pipeline_reset")
+
+    @property
+    def map_hints(self):
+        """the searches hand forward matches' right map.bin bytes to the post
+        stage (smash_pipeline_map_hints)"""
+        return bool(lib().smash_pipeline_map_hints(self.h))
 
     @property
     def key_capacity(self):

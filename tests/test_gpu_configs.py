@@ -505,13 +505,30 @@ def test_idx8_pipeline_equals_independent_oracle(monkeypatch, tmp_path):
     synth.write_index_side_files(str(tmp_path), g)
     cs = {l.split("\t")[0]: int(l.split("\t")[2]) for l in open(tmp_path / "chrom_sizes.txt")}
     starts = np.array([int(l.split("\t")[2]) for l in open(bins_path)], np.int64)
-    counts, st, _ = _device_counts(dix, cs, starts, reads, 2500)
+    counts, st, pipe = _device_counts(dix, cs, starts, reads, 2500)
+    # the device-built map and the index's own tag offsets: the searches
+    # hand the post stage each forward match's right map.bin byte
+    assert pipe.map_hints
     assert st.error == 0
     op, err = _oracle_counts(oix, oix.mappability(), cs, starts, reads)
     assert err == 0
     assert np.array_equal(counts, op.counts)
     assert (st.positions, st.dups, st.kept) == (op.state.total, op.state.dups, op.state.kept)
     assert st.dupe_pairs == op.n_dupe.value
+    # the same per-pair hit lists (one batch, all pairs) with the hints off
+    n = reads.shape[0] // 2
+    peek = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("SMASH_MAP_HINT", env)
+        c2, st2, p2 = _device_counts(dix, cs, starts, reads, n)
+        assert p2.map_hints == (env == "1")
+        assert np.array_equal(c2, counts) and st2.as_dict() == st.as_dict()
+        peek.append(p2.peek(n))
+    monkeypatch.delenv("SMASH_MAP_HINT")
+    (nk1, keep1, h1), (nk2, keep2, h2) = peek
+    assert np.array_equal(nk1, nk2) and np.array_equal(keep1, keep2)
+    for q in np.nonzero(nk1 > 0)[0]:
+        assert np.array_equal(h1[q, :nk1[q]], h2[q, :nk1[q]]), q
 
 
 # ---------------------------------------------------------------------------

@@ -268,6 +268,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   sm::bad_table(in_text, &c.bad_tab_lo, &c.bad_tab_hi);
   c.lin_blocks = lin_blocks;
   c.pad = 0;
+  c.mhint = 0;
   c.grab = 1;
   c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 3;   // = the device default (mam.hip)
   c.pf = std::getenv("SMASH_SM_PF") ? uint32_t(std::atoi(std::getenv("SMASH_SM_PF"))) : 1;
