@@ -103,7 +103,8 @@ struct smash_pipeline {
   int set = 1;
   int32_t *d_nk = nullptr;
   uint32_t *d_nmajor = nullptr;
-  uint64_t *d_hits = nullptr;
+  uint64_t *d_hits = nullptr;     // [max_pairs][2 * slots]: full hit rows (HitRows)
+  uint64_t *d_hhead = nullptr;    // [max_pairs][kHitHead]: dense head rows
   uint64_t *d_hash = nullptr;   // [2*max_pairs] hi, lo
   uint8_t *d_keep = nullptr;
   uint64_t *d_slot = nullptr;     // [max_pairs] k_dedup_claim -> k_dedup_decide
@@ -205,6 +206,21 @@ struct PostCfg {
 // the reference position of a match word: 48 bits (smash_gpu.h), 40 when
 // the word may carry a map hint (N < 2^33 then)
 constexpr uint64_t kRefMask = 0xFFFFFFFFFFull;
+
+// A pair's kept hit words (its key, smashMEM.py:122-131): in a dense head row
+// of kHitHead words when it has at most that many (C3: all but a few; 6.7 on
+// average), else in its full row of 2 * slots words.  Every reader knows nk,
+// so it picks the row without a flag.  Dense rows put 64 consecutive pairs in
+// 8 KB: the post stage, the de-dup and the binning read them as streams
+// instead of one random line 2 * slots words apart per pair.
+constexpr uint32_t kHitHead = 16;
+struct HitRows {
+  uint64_t *head, *full;
+  uint32_t slots;
+  __device__ __forceinline__ uint64_t *row(uint64_t q, int32_t nk) const {
+    return nk <= int32_t(kHitHead) ? head + q * kHitHead : full + q * 2 * uint64_t(slots);
+  }
+};
 
 struct Aln {
   int64_t pos, qpos;
@@ -337,7 +353,7 @@ __host__ __device__ inline uint64_t post_ws_bytes(uint32_t slots) {
 __device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restrict__ match,
                                        const uint32_t *__restrict__ nmatch, uint64_t q,
                                        int32_t *nk_out, uint32_t *nmajor_out,
-                                       uint64_t *hits_out, uint64_t *hash_out, int32_t &err,
+                                       HitRows hits_out, uint64_t *hash_out, int32_t &err,
                                        unsigned long long &nm, uint8_t *ws) {
   {
     Aln *a = reinterpret_cast<Aln *>(ws);
@@ -358,7 +374,7 @@ __device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restr
       const int mx = h2[i].L0 > h2[i].R0 ? h2[i].L0 : h2[i].R0;
       if (int(h2[i].qend) - int(h2[i].qstart) - mx >= c.min_excess) h2[m2++] = h2[i];
     }
-    uint64_t *ho = hits_out + q * (2 * uint64_t(c.slots));
+    uint64_t *ho = hits_out.full + q * (2 * uint64_t(c.slots));
     int32_t nk = -1;
     uint32_t nmaj = 0;
     uint64_t hh = 0x9E3779B97F4A7C15ull, hl = 0xD1B54A32D192ED03ull;
@@ -383,6 +399,8 @@ __device__ __noinline__ void post_pair(const PostCfg &c, const uint64_t *__restr
       }
       hh = (mix64(hh ^ uint64_t(nk)) & c.hash_mask) | 1;
       hl = (mix64(hl + uint64_t(nk)) & c.hash_mask) | 1;
+      if (nk <= int32_t(kHitHead))           // (the readers look for it there)
+        for (int32_t i = 0; i < nk; ++i) hits_out.head[q * kHitHead + i] = ho[i];
     }
     nk_out[q] = nk;
     nmajor_out[q] = nmaj;
@@ -431,7 +449,7 @@ __global__ __launch_bounds__(kB) void k_post(PostCfg c, const uint64_t *__restri
                                              const uint32_t *__restrict__ nmatch,
                                              uint64_t n_pairs, const uint32_t *list,
                                              const uint32_t *n_list, int32_t *nk_out,
-                                             uint32_t *nmajor_out, uint64_t *hits_out,
+                                             uint32_t *nmajor_out, HitRows hits_out,
                                              uint64_t *hash_out, unsigned long long *stats,
                                              uint8_t *ws) {
   SMASH_BESIDE_SEARCH();
@@ -609,7 +627,7 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
                                                   const uint32_t *n_list, uint32_t lim,
                                                   uint32_t *up_list, uint32_t *up_n,
                                                   int32_t *nk_out, uint32_t *nmajor_out,
-                                                  uint64_t *hits_out, uint64_t *hash_out,
+                                                  HitRows hits_out, uint64_t *hash_out,
                                                   unsigned long long *stats) {
   SMASH_BESIDE_SEARCH();
   const uint64_t *sp = c.startpos;
@@ -632,7 +650,10 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
       uint64_t H1[CAP], H2[CAP];
       mate_fast<CAP>(c, sp, match + (2 * q) * c.slots, n1, H1, err);
       mate_fast<CAP>(c, sp, match + (2 * q + 1) * c.slots, n2, H2, err);
-      uint64_t *ho = hits_out + q * (2 * uint64_t(c.slots));
+      // (8 words per mate: at most 16 kept hits, the head row; 16 per mate:
+      // the full row, copied to the head row below when they fit)
+      uint64_t *ho = CAP <= 8 ? hits_out.head + q * kHitHead
+                              : hits_out.full + q * (2 * uint64_t(c.slots));
       int32_t nk = -1;
       uint32_t nmaj = 0;
       uint64_t hh = 0x9E3779B97F4A7C15ull, hl = 0xD1B54A32D192ED03ull;
@@ -668,6 +689,8 @@ __global__ __launch_bounds__(kB) void k_post_fast(PostCfg c, const uint64_t *__r
         }
         hh = (mix64(hh ^ uint64_t(nk)) & c.hash_mask) | 1;
         hl = (mix64(hl + uint64_t(nk)) & c.hash_mask) | 1;
+        if (CAP > 8 && nk <= int32_t(kHitHead))
+          for (int32_t i = 0; i < nk; ++i) hits_out.head[q * kHitHead + i] = ho[i];
       }
       nk_out[q] = nk;
       nmajor_out[q] = nmaj;
@@ -809,13 +832,14 @@ __device__ __forceinline__ void wave_fill_records(uint64_t *arena, uint64_t off,
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSlotOld = ~0ull, kSlotNone = ~0ull - 1;
 
-__device__ __forceinline__ KeyRef pair_key(const uint64_t *hits, uint32_t slots, const int32_t *nk,
+__device__ __forceinline__ KeyRef pair_key(const HitRows &hits, const int32_t *nk,
                                            const uint64_t *hash, uint64_t q) {
-  return KeyRef{hits + q * 2 * uint64_t(slots), uint32_t(nk[q]), hash[2 * q + 1]};
+  const int32_t k = nk[q];
+  return KeyRef{hits.row(q, k), uint32_t(k), hash[2 * q + 1]};
 }
 
 __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__restrict__ hash,
-                              const uint64_t *__restrict__ hits, uint32_t slots, uint64_t n,
+                              HitRows hits, uint64_t n,
                               uint64_t *table, uint64_t mask, const uint64_t *arena,
                               uint64_t epoch, uint64_t *slot_of, unsigned long long *stats) {
   SMASH_BESIDE_SEARCH();
@@ -823,7 +847,7 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
   int32_t err = 0;
   for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += stride) {
     if (nk[q] < 0) continue;
-    const KeyRef me = pair_key(hits, slots, nk, hash, q);
+    const KeyRef me = pair_key(hits, nk, hash, q);
     const uint64_t hi = hash[2 * q];
     const unsigned long long mine = (epoch << kRefShift) | (q + 1);
     uint64_t res = kSlotNone;
@@ -863,7 +887,7 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
           }
         } else if ((ref >> kRefShift) == epoch) {
           const uint64_t q2 = (ref & (kRefPub - 1)) - 1;
-          if (same_key(me, pair_key(hits, slots, nk, hash, q2))) {
+          if (same_key(me, pair_key(hits, nk, hash, q2))) {
             atomicMin(sr, mine);
             res = i;
             break;
@@ -883,7 +907,7 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
 
 // one wave per kDecGroups x 64 consecutive pairs per trip (wave-wide scans)
 __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *__restrict__ hash,
-                               const uint64_t *__restrict__ hits, uint32_t slots,
+                               HitRows hits,
                                const uint32_t *__restrict__ nmajor,
                                const int64_t *__restrict__ chrom_off, uint64_t n,
                                uint64_t *table, uint64_t *arena, uint64_t arena_cap,
@@ -935,7 +959,7 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
       wbase += total;
       const bool ok = win && off + need <= arena_cap;
       wave_fill_records(arena, off, incl, total, ok, win ? hash[2 * q + 1] : 0ull,
-                        win ? uint32_t(m) : 0u, hits + (in ? q : 0) * 2 * uint64_t(slots), coop);
+                        win ? uint32_t(m) : 0u, hits.row(in ? q : 0, m), coop);
       if (win) {
         if (!ok) {
           full = true;   // the slot stays a claim: never matched (no kRefPub)
@@ -951,7 +975,7 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
         cnt[q] = c;
         int64_t last = -1;
         if (c) {
-          const uint64_t *h = hits + q * 2 * uint64_t(slots);
+          const uint64_t *h = hits.row(q, m);
           for (int32_t j = m - 1; j >= 0; --j)
             if (chrom_off[uint32_t(h[j] >> 48)] >= 0) {
               last = int64_t(h[j] & 0xFFFFFFFFFFFFull);
@@ -1131,12 +1155,11 @@ __global__ void k_count(const uint8_t *keep, const uint32_t *nmajor, uint64_t n,
 }
 
 __global__ void k_emit(const uint8_t *keep, const int32_t *nk,
-                       const uint64_t *hits, const uint32_t *off, uint64_t n,
-                       uint32_t slots, const int64_t *chrom_off, int64_t *pos0,
-                       int64_t *absp) {
+                       HitRows hits, const uint32_t *off, uint64_t n,
+                       const int64_t *chrom_off, int64_t *pos0, int64_t *absp) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= n || !keep[q]) return;
-  const uint64_t *h = hits + q * 2 * uint64_t(slots);
+  const uint64_t *h = hits.row(q, nk[q]);
   uint64_t o = off[q];
   for (int32_t i = 0; i < nk[q]; ++i) {
     const uint32_t tid = uint32_t(h[i] >> 48);
@@ -1209,7 +1232,7 @@ __global__ __launch_bounds__(kB) void k_bin(const int64_t *__restrict__ pos0,
 // per pair: the count of positions it emits (kept pairs: their major hits)
 // and the pos0 of the last one (-1: none), read from the end of its hit row
 __global__ void k_count_last(const uint8_t *keep, const uint32_t *nmajor, const int32_t *nk,
-                             const uint64_t *hits, uint32_t slots, const int64_t *chrom_off,
+                             HitRows hits, const int64_t *chrom_off,
                              uint64_t n, uint32_t *cnt, int64_t *lp) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= n) return;
@@ -1217,7 +1240,7 @@ __global__ void k_count_last(const uint8_t *keep, const uint32_t *nmajor, const 
   cnt[q] = c;
   int64_t last = -1;
   if (c) {
-    const uint64_t *h = hits + q * 2 * uint64_t(slots);
+    const uint64_t *h = hits.row(q, nk[q]);
     for (int32_t i = nk[q] - 1; i >= 0; --i)
       if (chrom_off[uint32_t(h[i] >> 48)] >= 0) {
         last = int64_t(h[i] & 0xFFFFFFFFFFFFull);
@@ -1235,7 +1258,7 @@ __global__ void k_count_last(const uint8_t *keep, const uint32_t *nmajor, const 
 // writing and re-reading the positions.
 __global__ __launch_bounds__(kB) void k_emit_bin(
     const uint8_t *__restrict__ keep, const int32_t *__restrict__ nk,
-    const uint64_t *__restrict__ hits, uint32_t slots, const int64_t *__restrict__ chrom_off,
+    HitRows hits, const int64_t *__restrict__ chrom_off,
     const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
     const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
     uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats) {
@@ -1249,7 +1272,7 @@ __global__ __launch_bounds__(kB) void k_emit_bin(
     if (m <= 0) continue;
     int64_t prev = q ? lps[q - 1] : -1;
     if (prev < 0) prev = prev0;
-    const uint64_t *h = hits + q * 2 * uint64_t(slots);
+    const uint64_t *h = hits.row(q, m);
     for (int32_t i = 0; i < m; ++i) {
       const uint64_t w = h[i];
       const int64_t co = chrom_off[uint32_t(w >> 48)];
@@ -1297,7 +1320,7 @@ inline uint32_t bin_part_size(uint32_t nbins) {
 }
 __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     const uint8_t *__restrict__ keep, const int32_t *__restrict__ nk,
-    const uint64_t *__restrict__ hits, uint32_t slots, const int64_t *__restrict__ chrom_off,
+    HitRows hits, const int64_t *__restrict__ chrom_off,
     const int64_t *__restrict__ lps, uint64_t n, const int64_t *prev_p,
     const int64_t *__restrict__ bins, uint32_t nbins, const uint32_t *__restrict__ cell,
     uint32_t ncell, uint32_t cshift, unsigned long long *counts, unsigned long long *stats,
@@ -1326,9 +1349,11 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
       a.kp = keep[x];
       a.m = nk[x];
       a.lp = x ? lps[x - 1] : -1;
-      const uint4 *r = reinterpret_cast<const uint4 *>(hits + x * 2 * uint64_t(slots));
+      // (the head row's first 4 words, fetched before nk is known: a pair
+      // with more than kHitHead hits reads its full row below instead)
+      const uint4 *r = reinterpret_cast<const uint4 *>(hits.head + x * kHitHead);
       a.h0 = r[0];
-      if (slots > 1) a.h1 = r[1];   // (a one-slot row is 16 B: r[1] is the next pair's)
+      a.h1 = r[1];
     }
     return a;
   };
@@ -1338,10 +1363,11 @@ __global__ __launch_bounds__(1024) void k_emit_bin_lds(
     const Ahead nxt = fetch(q + stride);
     const int32_t m = cur.kp ? cur.m : 0;
     int64_t prev = cur.lp < 0 ? prev0 : cur.lp;
-    const uint64_t *h = hits + q * 2 * uint64_t(slots);
+    const uint64_t *h = hits.row(q, cur.m);
+    const int32_t pre = cur.m <= int32_t(kHitHead) ? 4 : 0;   // words from the prefetch
     for (int32_t i = 0; i < m; ++i) {
       const uint4 &hv = i < 2 ? cur.h0 : cur.h1;
-      const uint64_t w = i >= 4 ? h[i]
+      const uint64_t w = i >= pre ? h[i]
                                 : (i & 1) ? (uint64_t(hv.w) << 32 | hv.z) : (uint64_t(hv.y) << 32 | hv.x);
       const int64_t co = chrom_off[uint32_t(w >> 48)];
       if (co < 0) continue;
@@ -1461,6 +1487,8 @@ PostCfg post_cfg(const smash_pipeline *p) {
   c.mhint = p->mhint;
   return c;
 }
+
+HitRows hit_rows(const smash_pipeline *p) { return HitRows{p->d_hhead, p->d_hits, p->slots}; }
 
 }  // namespace
 }  // namespace smash
@@ -1603,6 +1631,7 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_nk = dalloc<int32_t>(P);
     p->d_nmajor = dalloc<uint32_t>(P);
     p->d_hits = dalloc<uint64_t>(P * 2 * p->slots);
+    p->d_hhead = dalloc<uint64_t>(P * smash::kHitHead);
     p->d_hash = dalloc<uint64_t>(2 * P);
     p->d_keep = dalloc<uint8_t>(P);
     {   // the multi-GPU export's per-(owner, block) counts, up to 64 owners
@@ -1740,7 +1769,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
   if (p->h_recv_base) (void)hipHostFree(p->h_recv_base);
   for (void *q : {(void *)p->d_tag_off, (void *)p->d_small, (void *)p->d_chrom_off,
                   (void *)p->d_bins, (void *)p->d_cell, (void *)p->d_sp_cell,
-                  (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits,
+                  (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits, (void *)p->d_hhead,
                   (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_bcnt, (void *)p->d_boff,
                   p->d_scan_temp, (void *)p->d_oslot,
                   (void *)p->d_slot, (void *)p->d_tsum, (void *)p->d_tlast,
@@ -1841,18 +1870,18 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
     const PostCfg pc = post_cfg(p);
     k_post_fast<8><<<grid_for(n_pairs, kB, 1u << 30), kB, 0, s>>>(
         pc, p->d_match, p->d_nmatch, n_pairs, nullptr, nullptr, std::min(8u, p->post_cap),
-        p->d_l16 + 1, p->d_l16, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+        p->d_l16 + 1, p->d_l16, p->d_nk, p->d_nmajor, hit_rows(p), p->d_hash, p->d_stats);
     SMASH_HIP(hipGetLastError());
     k_post_fast<FCAP><<<grid_for(n_pairs, kB, 1024), kB, 0, s>>>(
         pc, p->d_match, p->d_nmatch, n_pairs, p->d_l16 + 1, p->d_l16, p->post_cap,
-        p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash, p->d_stats);
+        p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, hit_rows(p), p->d_hash, p->d_stats);
     SMASH_HIP(hipGetLastError());
     k_post<<<kPostBlocks, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs,
-                                      p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, p->d_hits,
+                                      p->d_fb + 1, p->d_fb, p->d_nk, p->d_nmajor, hit_rows(p),
                                       p->d_hash, p->d_stats, p->d_post_ws);
   } else {
     k_post<<<kPostBlocks, kB, 0, s>>>(post_cfg(p), p->d_match, p->d_nmatch, n_pairs, nullptr,
-                                      nullptr, p->d_nk, p->d_nmajor, p->d_hits, p->d_hash,
+                                      nullptr, p->d_nk, p->d_nmajor, hit_rows(p), p->d_hash,
                                       p->d_stats, p->d_post_ws);
   }
   SMASH_HIP(hipGetLastError());
@@ -1908,12 +1937,12 @@ static int dedup_local(smash_pipeline *p, hipStream_t s) {
   const uint64_t n = p->n_pairs;
   if (!n) return SMASH_OK;
   const uint64_t epoch = next_epoch(p);
-  k_dedup_claim<<<grid_for(n, kB, 8192), kB, 0, s>>>(p->d_nk, p->d_hash, p->d_hits, p->slots, n,
+  k_dedup_claim<<<grid_for(n, kB, 8192), kB, 0, s>>>(p->d_nk, p->d_hash, hit_rows(p), n,
                                                      p->d_table, p->table_mask, p->d_arena, epoch,
                                                      p->d_slot, p->d_stats);
   SMASH_HIP(hipGetLastError());
   k_dedup_decide<<<grid_for((n + kDecGroups - 1) / kDecGroups, kB, 8192), kB, 0, s>>>(
-      p->d_nk, p->d_hash, p->d_hits, p->slots, p->d_nmajor, p->d_chrom_off, n, p->d_table,
+      p->d_nk, p->d_hash, hit_rows(p), p->d_nmajor, p->d_chrom_off, n, p->d_table,
       p->d_arena, p->arena_cap, p->d_arena_top, epoch, p->d_slot, p->d_keep, p->d_cnt, p->d_lp,
       p->d_stats, (p->coop_copy & 2u) != 0);
   SMASH_HIP(hipGetLastError());
@@ -1932,7 +1961,7 @@ extern "C" int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *s
     if (n) {
       if (!p->cnt_ready)   // (the multi-GPU path: keep came from the owners)
         k_count_last<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, p->d_nk,
-                                                             p->d_hits, p->slots, p->d_chrom_off,
+                                                             hit_rows(p), p->d_chrom_off,
                                                              n, p->d_cnt, p->d_lp);
       // posoff (offsets) and lps ("last valid" position), no LDS
       const uint64_t ntile = (n + kScanTile - 1) / kScanTile;
@@ -1952,8 +1981,8 @@ extern "C" int smash_phase_positions(smash_pipeline *p, int64_t *d_tail, void *s
     k_count<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nmajor, n, p->d_cnt);
     size_t tb = p->temp_bytes;
     SMASH_HIP(hipcub::DeviceScan::InclusiveSum(p->d_temp, tb, p->d_cnt, p->d_posoff + 1, n, s));
-    k_emit<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nk, p->d_hits,
-                                                    p->d_posoff, n, p->slots,
+    k_emit<<<grid_for(n, kB, 1u << 30), kB, 0, s>>>(p->d_keep, p->d_nk, hit_rows(p),
+                                                    p->d_posoff, n,
                                                     p->d_chrom_off, p->d_pos0, p->d_abs);
   }
   p->pos_dirty = false;
@@ -1976,14 +2005,14 @@ extern "C" int smash_phase_bin(smash_pipeline *p, const int64_t *d_prev,
       const unsigned gx = unsigned(std::min<uint64_t>(kBinBlocks, (n + 1023) / 1024));
       const dim3 grid(gx, parts);
       k_emit_bin_lds<<<grid, 1024, 0, s>>>(
-          p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
+          p->d_keep, p->d_nk, hit_rows(p), p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
           p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
           p->d_stats, part, p->bin_flush, p->d_binpart);
       k_bin_reduce<<<grid_for(p->nbins, kB, 1024), kB, 0, s>>>(
           p->d_binpart, gx, p->nbins, reinterpret_cast<unsigned long long *>(d_counts));
     } else if (n) {
       k_emit_bin<<<grid_for(n, kB, 8192), kB, 0, s>>>(
-          p->d_keep, p->d_nk, p->d_hits, p->slots, p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
+          p->d_keep, p->d_nk, hit_rows(p), p->d_chrom_off, p->d_lps, n, prev, p->d_bins,
           p->nbins, p->d_cell, p->ncell, p->cshift, reinterpret_cast<unsigned long long *>(d_counts),
           p->d_stats);
     }
@@ -2184,7 +2213,7 @@ __global__ void k_export_totals(const uint64_t *bc, const uint64_t *boff, int wo
 }
 
 __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uint64_t *hash,
-                                                    const uint64_t *hits, uint32_t slots,
+                                                    HitRows hits,
                                                     uint64_t n, int world, uint32_t nblk,
                                                     uint64_t gbase, const uint64_t *boff,
                                                     uint64_t *hdr, uint64_t *words,
@@ -2220,7 +2249,7 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
     hdr[kHdrWords * e] = uint64_t(k) << 40 | (w - seg_w);   // offset in the owner's words
     send_q[e] = uint32_t(q);
     if (!coop) {   // (SMASH_COOP_COPY=0: one key per lane, the round-3 form)
-      const uint64_t *src = hits + q * 2 * uint64_t(slots);
+      const uint64_t *src = hits.row(q, int32_t(k));
       for (uint32_t i = 0; i < k; ++i) words[w + i] = src[i];
     }
   }
@@ -2237,7 +2266,7 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
     if (lane >= uint32_t(d)) incl += y;
   }
   const uint32_t total = __shfl(incl, 63, 64);
-  const uint64_t row = q * 2 * uint64_t(slots);
+  const uint64_t row = act ? reinterpret_cast<uint64_t>(hits.row(q, int32_t(k))) : 0ull;
   for (uint32_t t0 = 0; t0 < total; t0 += 64) {   // (wave-uniform: every shuffle has all lanes)
     const uint32_t t = t0 + lane;
     // the lane whose key holds word t: the first l with incl(l) > t
@@ -2251,7 +2280,7 @@ __global__ __launch_bounds__(kB) void k_export_fill(const int32_t *nk, const uin
     const uint32_t prev = uint32_t(__shfl(int(incl), int((l + 63u) & 63u), 64));
     const uint32_t before = l ? prev : 0u;
     const uint64_t wl = __shfl(w, int(l), 64), rl = __shfl(row, int(l), 64);
-    if (t < total) words[wl + (t - before)] = hits[rl + (t - before)];
+    if (t < total) words[wl + (t - before)] = reinterpret_cast<const uint64_t *>(rl)[t - before];
   }
 }
 
@@ -2473,7 +2502,7 @@ extern "C" int smash_phase_export(smash_pipeline *p, int world, uint64_t global_
     SMASH_HIP(hipMalloc(&p->d_send_words, 8 * p->send_words_cap));
   }
   if (n)
-    k_export_fill<<<nblk, kB, 0, s>>>(p->d_nk, p->d_hash, p->d_hits, p->slots, n, world, nblk,
+    k_export_fill<<<nblk, kB, 0, s>>>(p->d_nk, p->d_hash, hit_rows(p), n, world, nblk,
                                       global_base, p->d_boff, p->d_send_hdr, p->d_send_words,
                                       p->d_send_q, (p->coop_copy & 1u) != 0);
   SMASH_HIP(hipGetLastError());
@@ -2589,7 +2618,19 @@ extern "C" int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_
   if (!n) return SMASH_OK;
   if (h_nk) SMASH_HIP(hipMemcpy(h_nk, p->d_nk, 4 * n, hipMemcpyDeviceToHost));
   if (h_keep) SMASH_HIP(hipMemcpy(h_keep, p->d_keep, n, hipMemcpyDeviceToHost));
-  if (h_hits) SMASH_HIP(hipMemcpy(h_hits, p->d_hits, 8 * n * 2 * p->slots, hipMemcpyDeviceToHost));
+  if (h_hits) {
+    // the ABI's layout, [n][2 * slots] words: the full rows, with the pairs
+    // whose hits live in their dense head rows (HitRows) copied in
+    const uint64_t W = 2 * uint64_t(p->slots);
+    SMASH_HIP(hipMemcpy(h_hits, p->d_hits, 8 * n * W, hipMemcpyDeviceToHost));
+    std::vector<int32_t> nk(n);
+    std::vector<uint64_t> head(n * smash::kHitHead);
+    SMASH_HIP(hipMemcpy(nk.data(), p->d_nk, 4 * n, hipMemcpyDeviceToHost));
+    SMASH_HIP(hipMemcpy(head.data(), p->d_hhead, 8 * n * smash::kHitHead, hipMemcpyDeviceToHost));
+    for (uint64_t q = 0; q < n; ++q)
+      if (nk[q] > 0 && nk[q] <= int32_t(smash::kHitHead))
+        std::memcpy(h_hits + q * W, head.data() + q * smash::kHitHead, 8 * size_t(nk[q]));
+  }
   if (h_hash) SMASH_HIP(hipMemcpy(h_hash, p->d_hash, 16 * n, hipMemcpyDeviceToHost));
   return SMASH_OK;
 }
@@ -2734,7 +2775,7 @@ extern "C" int smash_pipeline_positions(smash_pipeline *p, int64_t *h_pos0, int6
   if (p->pos_dirty && p->n_pairs) {   // fused path: write the last batch's positions now
     SMASH_HIP(ensure_positions(p));
     k_emit<<<grid_for(p->n_pairs, kB, 1u << 30), kB, 0, p->last>>>(
-        p->d_keep, p->d_nk, p->d_hits, p->d_posoff, p->n_pairs, p->slots, p->d_chrom_off,
+        p->d_keep, p->d_nk, hit_rows(p), p->d_posoff, p->n_pairs, p->d_chrom_off,
         p->d_pos0, p->d_abs);
     SMASH_HIP(hipGetLastError());
     p->pos_dirty = false;
