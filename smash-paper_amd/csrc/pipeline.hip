@@ -108,6 +108,8 @@ struct smash_pipeline {
   uint64_t *d_hash = nullptr;   // [2*max_pairs] hi, lo
   uint8_t *d_keep = nullptr;
   uint64_t *d_slot = nullptr;     // [max_pairs] k_dedup_claim -> k_dedup_decide
+  uint8_t *d_contest = nullptr;   // [max_pairs] claims of an already-claimed key mark it
+                                  // (kSlotIns; null: SMASH_CLAIM_FLAG=0, every decide reads)
   uint64_t *d_tsum = nullptr;     // [tiles] the LDS-free scans' tile aggregates / prefixes
   int64_t *d_tlast = nullptr;
   bool cnt_ready = false;         // k_dedup_decide wrote d_cnt / d_lp for this batch
@@ -831,6 +833,13 @@ __device__ __forceinline__ void wave_fill_records(uint64_t *arena, uint64_t off,
 // kSlotNone (no key, or the set is full: the error is raised).
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSlotOld = ~0ull, kSlotNone = ~0ull - 1;
+// (single GPU) slot_of flag: the pair's claim filled an empty slot.  Unless
+// a later claim of the same key marked it (contest[q]), nobody else claimed
+// that slot this batch, so the pair wins and k_dedup_decide skips re-reading
+// the slot (one random table line per key).  Every later claimant marks the
+// claim it finds (the slot's current minimum), and the first of them finds
+// the filler, so a filler that lost is always marked.
+constexpr uint64_t kSlotIns = 1ull << 62;
 
 __device__ __forceinline__ KeyRef pair_key(const HitRows &hits, const int32_t *nk,
                                            const uint64_t *hash, uint64_t q) {
@@ -841,7 +850,8 @@ __device__ __forceinline__ KeyRef pair_key(const HitRows &hits, const int32_t *n
 __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__restrict__ hash,
                               HitRows hits, uint64_t n,
                               uint64_t *table, uint64_t mask, const uint64_t *arena,
-                              uint64_t epoch, uint64_t *slot_of, unsigned long long *stats) {
+                              uint64_t epoch, uint64_t *slot_of, uint8_t *contest,
+                              unsigned long long *stats) {
   SMASH_BESIDE_SEARCH();
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   int32_t err = 0;
@@ -861,7 +871,7 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
         const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
         if (prev == 0) {
           __hip_atomic_store(sr, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          res = i;
+          res = i | (contest ? kSlotIns : 0ull);
           break;
         }
         cur = prev;
@@ -888,6 +898,7 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
         } else if ((ref >> kRefShift) == epoch) {
           const uint64_t q2 = (ref & (kRefPub - 1)) - 1;
           if (same_key(me, pair_key(hits, nk, hash, q2))) {
+            if (contest) contest[q2] = 1;   // (see kSlotIns)
             atomicMin(sr, mine);
             res = i;
             break;
@@ -912,7 +923,8 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
                                const int64_t *__restrict__ chrom_off, uint64_t n,
                                uint64_t *table, uint64_t *arena, uint64_t arena_cap,
                                unsigned long long *arena_top, uint64_t epoch,
-                               const uint64_t *__restrict__ slot_of, uint8_t *keep,
+                               const uint64_t *__restrict__ slot_of,
+                               const uint8_t *__restrict__ contest, uint8_t *keep,
                                uint32_t *cnt, int64_t *lp, unsigned long long *stats, bool coop) {
   SMASH_BESIDE_SEARCH();
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
@@ -931,10 +943,12 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
       bool win = false;
       if (m >= 0) {
         const uint64_t sl = slot_of[q];
-        if (sl < kSlotNone) {
+        if (sl < kSlotNone && (sl & kSlotIns) && !contest[q]) {
+          win = true;                       // the slot's only claimant this batch
+        } else if (sl < kSlotNone) {
           const unsigned long long ref = __hip_atomic_load(
-              reinterpret_cast<unsigned long long *>(&table[2 * sl + 1]), __ATOMIC_RELAXED,
-              __HIP_MEMORY_SCOPE_AGENT);
+              reinterpret_cast<unsigned long long *>(&table[2 * (sl & ~kSlotIns) + 1]),
+              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           win = ref == ((epoch << kRefShift) | (q + 1));
         }
         ++kp;
@@ -964,9 +978,10 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
         if (!ok) {
           full = true;   // the slot stays a claim: never matched (no kRefPub)
         } else {
-          __hip_atomic_store(reinterpret_cast<unsigned long long *>(&table[2 * slot_of[q] + 1]),
-                             (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(
+              reinterpret_cast<unsigned long long *>(&table[2 * (slot_of[q] & ~kSlotIns) + 1]),
+              (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)), __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (in) {
@@ -1698,6 +1713,10 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
     p->d_stats = dalloc<unsigned long long>(kStatWords);
     SMASH_HIPX(hipMemset(p->d_stats, 0, 8 * kStatWords));
     p->d_slot = dalloc<uint64_t>(P);
+    {
+      const char *cf = getenv("SMASH_CLAIM_FLAG");   // (A/B: 0 = every decide reads its slot)
+      if (!(cf && cf[0] == '0')) p->d_contest = dalloc<uint8_t>(P);
+    }
     p->d_tsum = dalloc<uint64_t>(P / kScanTile + 1);
     p->d_tlast = dalloc<int64_t>(P / kScanTile + 1);
     p->d_send_q = dalloc<uint32_t>(P);
@@ -1772,7 +1791,7 @@ extern "C" void smash_pipeline_free(smash_pipeline *p) {
                   (void *)p->d_nk, (void *)p->d_nmajor, (void *)p->d_hits, (void *)p->d_hhead,
                   (void *)p->d_hash, (void *)p->d_keep, (void *)p->d_bcnt, (void *)p->d_boff,
                   p->d_scan_temp, (void *)p->d_oslot,
-                  (void *)p->d_slot, (void *)p->d_tsum, (void *)p->d_tlast,
+                  (void *)p->d_slot, (void *)p->d_contest, (void *)p->d_tsum, (void *)p->d_tlast,
                   p->d_temp, (void *)p->d_table,
                   (void *)p->d_posoff, (void *)p->d_cnt, (void *)p->d_pos0,
                   (void *)p->d_abs, (void *)p->d_prev, (void *)p->d_stats,
@@ -1937,14 +1956,15 @@ static int dedup_local(smash_pipeline *p, hipStream_t s) {
   const uint64_t n = p->n_pairs;
   if (!n) return SMASH_OK;
   const uint64_t epoch = next_epoch(p);
+  if (p->d_contest) SMASH_HIP(hipMemsetAsync(p->d_contest, 0, n, s));
   k_dedup_claim<<<grid_for(n, kB, 8192), kB, 0, s>>>(p->d_nk, p->d_hash, hit_rows(p), n,
                                                      p->d_table, p->table_mask, p->d_arena, epoch,
-                                                     p->d_slot, p->d_stats);
+                                                     p->d_slot, p->d_contest, p->d_stats);
   SMASH_HIP(hipGetLastError());
   k_dedup_decide<<<grid_for((n + kDecGroups - 1) / kDecGroups, kB, 8192), kB, 0, s>>>(
       p->d_nk, p->d_hash, hit_rows(p), p->d_nmajor, p->d_chrom_off, n, p->d_table,
-      p->d_arena, p->arena_cap, p->d_arena_top, epoch, p->d_slot, p->d_keep, p->d_cnt, p->d_lp,
-      p->d_stats, (p->coop_copy & 2u) != 0);
+      p->d_arena, p->arena_cap, p->d_arena_top, epoch, p->d_slot, p->d_contest, p->d_keep,
+      p->d_cnt, p->d_lp, p->d_stats, (p->coop_copy & 2u) != 0);
   SMASH_HIP(hipGetLastError());
   p->cnt_ready = true;
   return SMASH_OK;
