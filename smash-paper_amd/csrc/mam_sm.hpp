@@ -633,8 +633,14 @@ inline void bad_table(const uint64_t in_text[4], uint32_t *lo, uint32_t *hi) {
 // scanner, bounded by [start, end]).  Same final (depth, interval) as the
 // reference's traverse; ~2.5 log2(interval) probes instead of 4 log2 per
 // character.
-template <class IdxT, int BLOCK, bool CHECK, bool STATS, bool PK = false>
+template <class IdxT, int BLOCK, bool CHECK, bool STATS, bool PK = false, int GEO = 0>
 __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
+  // GEO 1: the launch geometry of 150-base reads on an index with a 16-mer
+  // table (K 16, min_len 20, B 18, 40-word rows), as constants: the shifts,
+  // masks and row offsets built from them fold, and the loop keeps fewer
+  // SGPRs live (run_sm picks it only when the Ctx holds exactly these)
+  const uint32_t gK = GEO ? 16u : c.K, gMin = GEO ? 20u : c.min_len, gB = GEO ? 18u : c.B;
+  const uint32_t gRow = GEO ? 40u : c.w_row, gLen0 = GEO ? 150u : c.len0;
   // PK: the SA / ISA words carry the packed hints (common.hpp; 8-byte
   // elements only): their position bits are PM, and the hint paths below
   // exist only in this instantiation
@@ -649,11 +655,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     return ((w >> (b & 63)) & 1ull) != 0;
   };
   const uint64_t N = c.N;
-  uint32_t *row = ldsw + threadIdx.x * c.w_row;
+  uint32_t *row = ldsw + threadIdx.x * gRow;
   const uint8_t *P = reinterpret_cast<const uint8_t *>(row);
   const uint32_t lane = threadIdx.x & 63;
   // direct rows: the bytes of row word `lane` inside the read (0..4)
-  const uint32_t row_live = 4 * lane < c.len0 ? (c.len0 - 4 * lane < 4 ? c.len0 - 4 * lane : 4u) : 0u;
+  const uint32_t row_live = 4 * lane < gLen0 ? (gLen0 - 4 * lane < 4 ? gLen0 - 4 * lane : 4u) : 0u;
 
   uint64_t q_next = 0, q_end = 0;   // this wave's claimed, unassigned reads
   uint32_t st = S_NEW, op = 0, pend = A_NONE;
@@ -733,10 +739,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   auto bs_probe = [&]() -> bool {
     SM_HOOK_CMPBS(true, sp, cbase + lc);
     const uint32_t o = cbase + lc;
-    if (PK && ((sp >> kPkPosBits) & 7u) != 5u && o - c.K < kPkWindow) {
-      const uint32_t rem = cap - lc, nav = c.K + kPkWindow - o;
+    if (PK && ((sp >> kPkPosBits) & 7u) != 5u && o - gK < kPkWindow) {
+      const uint32_t rem = cap - lc, nav = gK + kPkWindow - o;
       const uint32_t lim = rem < nav ? rem : nav;
-      const uint64_t win = pk_window(sp) >> (8 * (o - c.K));
+      const uint64_t win = pk_window(sp) >> (8 * (o - gK));
       const uint32_t k = agree8(win, lds_load8(P, prefix + o), lim);
       lc += k;
       if (k < lim || k == rem) {
@@ -813,9 +819,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         while (cm) {
           const uint32_t ln = uint32_t(__builtin_ctzll(cm));
           cm &= cm - 1;
-          // (direct rows have one length, c.len0: row_live is this lane's
+          // (direct rows have one length, gLen0: row_live is this lane's
           // live bytes of word `lane`, 0 past the read)
-          const uint32_t w = row_live ? ldsw[ln * c.w_row + lane] : 0u;
+          const uint32_t w = row_live ? ldsw[ln * gRow + lane] : 0u;
           const uint32_t nib = row_live ? bad_nibble(w, c.bad_tab_lo, c.bad_tab_hi, row_live) : 0u;
           if (__ballot(nib != 0)) {   // rare: a read with a bad base
             uint32_t x = nib << (4 * (lane & 7));
@@ -860,7 +866,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         if (rd >= c.n_reads) {
           st = S_EXIT;
         } else {
-          L = c.lens ? c.lens[rd] : c.len0;
+          L = c.lens ? c.lens[rd] : gLen0;
           // records: the lane loads the bad-mask chunks, the read's bytes go
           // to its LDS row by DMA (below); direct rows: the row is DMA'd
           // from the read and the wave computes the mask next iteration
@@ -884,9 +890,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         fm_ &= fm_ - 1;
         const uint64_t rl = __shfl(rd, int(ln), 64);
         if (c.direct)
-          SM_DMA_ROW(ldsw + ln * c.w_row, c.rows + rl * (c.w_row >> 2), c.w_row >> 2, lane);
+          SM_DMA_ROW(ldsw + ln * gRow, c.rows + rl * (gRow >> 2), gRow >> 2, lane);
         else
-          SM_DMA_ROW(ldsw + ln * c.w_row, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
+          SM_DMA_ROW(ldsw + ln * gRow, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
       }
     }
     if (st < S_ALU || fresh) continue;
@@ -944,7 +950,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           // the k + 4 read bases [x - 2, x + k + 2), first most significant:
           // its presence bits give the B-mers at x - 2, x - 1, x (common.hpp)
           const uint64_t f48 = kt_filter(lo64(v), hi64(v));
-          const uint32_t nb = 2 * (c.K + 4);
+          const uint32_t nb = 2 * (gK + 4);
           const uint32_t l1 = uint32_t(c0 >> (nb - 2)) & 3, l0 = uint32_t(c0 >> (nb - 4)) & 3;
           const uint32_t r1 = uint32_t(c0 >> 2) & 3, r2 = uint32_t(c0) & 3;
           const uint32_t bits = (uint32_t(f48 >> (32 + 4 * l1 + l0)) & 1u) |
@@ -973,7 +979,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           // (D = min_len - B), so the window advances past every window an
           // absent probe covers.  Modes: 0 {L(p), F(p)}, 1 {L(p), L(p+D+1)},
           // 2 {F(p), F(p+1)} with L(p) known present.
-          const uint32_t D = c.min_len - c.B;
+          const uint32_t D = gMin - gB;
           const uint32_t fm0 = fm;
           SM_HOOK_BM(fm, pa, pb);
           uint32_t adv = 0, nfm = 0;
@@ -993,7 +999,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           }
           if (pass) {
             skip_f = true; fm = 1;                      // window passed: go on at (C)
-            m = (fm0 == 0 ? c0 : c1) >> (2 * (c.B - c.K));   // F(p) -> the k-mer code
+            m = (fm0 == 0 ? c0 : c1) >> (2 * (gB - gK));   // F(p) -> the k-mer code
             ktr_set = true;
           } else {
             fm = nfm;
@@ -1002,7 +1008,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           a = A_TOP;
         } else if (!pa && !bm2) {
           depth = 0; start = 0; end = N - 1; have_pos = false;
-          prefix += c.min_len - c.B + 1;
+          prefix += gMin - gB + 1;
           a = A_TOP;
         } else if (!pa || !pb) {
           depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix; a = A_TOP;
@@ -1018,7 +1024,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       case S_KT: {                                   // (C)
         SM_REGION(4);
         const uint64_t l0 = lo64(v) & kKtMask, h0 = hi64(v) & kKtMask;
-        if (l0 <= h0) { depth = c.K; start = l0; end = h0; have_pos = false; }
+        if (l0 <= h0) { depth = gK; start = l0; end = h0; have_pos = false; }
         a = A_TRAV;
         break;
       }
@@ -1309,13 +1315,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         } else if (!have_pos) {
           addr = ia(c.SA, start);
           st = S_IDX; op = O_SAPOS2;
-        } else if (depth >= c.min_len && prefix != 0 && (pos & PM) != 0 &&
+        } else if (depth >= gMin && prefix != 0 && (pos & PM) != 0 &&
                    (!PK || ((pos >> kPkPosBits) & 7u) >= 4u)) {
           addr = reinterpret_cast<uint64_t>(c.T + (pos & PM) - 1);
           st = S_BYTE;
         } else {
           // (PK: is_leftmaximal from the BWT character in pos's SA word)
-          if (depth >= c.min_len &&
+          if (depth >= gMin &&
               (!PK || prefix == 0 || (pos & PM) == 0 ||
                P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
             if (nem < c.cap)
@@ -1331,20 +1337,20 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       SM_REGION(17);
       // (F) runs while the state is shallow, once per prefix (skip_f: this
       // prefix's window already passed the bitmap)
-      bool proceed = skip_f || depth >= c.min_len;
+      bool proceed = skip_f || depth >= gMin;
       const bool ktr = skip_f && ktr_set;             // k-mer code of this window in m
       skip_f = false; ktr_set = false;
-      if (prefix >= L || (!proceed && prefix + c.min_len > L)) {
+      if (prefix >= L || (!proceed && prefix + gMin > L)) {
         a = A_DONE;
       } else if (!proceed) {
         SM_REGION(24);
         // bad-mask work only for reads holding a bad base (clean: none)
         int32_t kb = -1;
-        const uint32_t B = c.B;
-        const uint32_t D = c.min_len - B;
+        const uint32_t B = gB;
+        const uint32_t D = gMin - B;
         if (!clean) {
           SM_REGION(20);
-          kb = bad.last(prefix, c.min_len);
+          kb = bad.last(prefix, gMin);
           while (kb >= 0 && in_text(P[kb]))
             kb = bad.last(prefix, uint32_t(kb) - prefix);
         }
@@ -1360,7 +1366,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           // D + 1 = 3 (B = k + 2 = min_len - 2) take one probe, and inside a
           // run of absent B-mers the entry D + 2 bases in rules out D + 3
           // windows at once.  What is known is kept per read position (fk).
-          if (B != c.K + 2 || B > c.min_len || D + 3 > 16) {
+          if (B != gK + 2 || B > gMin || D + 3 > 16) {
             proceed = true;                           // no filter for this geometry
           } else {
             const uint32_t sh = prefix - kp;         // (prefix never decreases)
@@ -1378,12 +1384,12 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
             }
             fk = kn | (pr << 16);
             const uint32_t need = (2u << D) - 1;     // offsets 0..D
-            if (prefix + c.min_len > L) {
+            if (prefix + gMin > L) {
               a = A_DONE;
             } else if ((kn & pr & need) == need) {
               proceed = true;                         // the window passes: (C)
             } else {
-              const uint32_t W = c.K + 4;             // read bases one entry needs
+              const uint32_t W = gK + 4;             // read bases one entry needs
               const uint32_t u = uint32_t(__builtin_ctz(~kn & need));   // lowest unknown
               auto ok_at = [&](uint32_t jj) {
                 return prefix + jj + W <= L && (clean || bad.bits(prefix + jj, W) == 0);
@@ -1401,8 +1407,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
               } else {
                 SM_REGION(21);
                 fj = jq;
-                c0 = codes_raw(row, c.w_row, prefix + jq, W);
-                addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((c0 >> 4) & ((1ull << (2 * c.K)) - 1)));
+                c0 = codes_raw(row, gRow, prefix + jq, W);
+                addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((c0 >> 4) & ((1ull << (2 * gK)) - 1)));
                 st = S_BM;
                 a = A_NONE;
               }
@@ -1430,20 +1436,20 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           } else {
             fm = 0;
           }
-          if (B > 0 && B <= c.min_len && ok) {
+          if (B > 0 && B <= gMin && ok) {
             // both codes from one pass over the row when the span allows
             const uint32_t lo_s = s1 < s2 ? s1 : s2, hi_s = s1 < s2 ? s2 : s1;
             const uint32_t span = hi_s + B - lo_s;
             if (span <= 21) {
               SM_REGION(21);
-              const uint64_t X = codes_raw(row, c.w_row, lo_s, span);
+              const uint64_t X = codes_raw(row, gRow, lo_s, span);
               const uint64_t mk = (1ull << (2 * B)) - 1;
               c1 = (X >> (2 * (lo_s + span - s1 - B))) & mk;
               c0 = (X >> (2 * (lo_s + span - s2 - B))) & mk;
             } else {
               SM_REGION(22);
-              c0 = codes_raw(row, c.w_row, s2, B);
-              c1 = codes_raw(row, c.w_row, s1, B);
+              c0 = codes_raw(row, gRow, s2, B);
+              c1 = codes_raw(row, gRow, s1, B);
             }
             // a B-mer's presence: its first k-mer's entry (B = k + 2)
             addr = reinterpret_cast<uint64_t>(c.KT + 2 * (c1 >> 4));
@@ -1457,16 +1463,16 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         }
       }
       if (a == A_TOP && proceed) {                     // (C) from the root
-        if (depth == 0 && prefix + c.K <= L && (clean || bad.bits(prefix, c.K) == 0)) {
+        if (depth == 0 && prefix + gK <= L && (clean || bad.bits(prefix, gK) == 0)) {
           if (kx == prefix) {
             // the filter loaded this k-mer's entry already (policy 3)
             SM_REGION(25);
-            if (klo <= khi) { depth = c.K; start = klo; end = khi; have_pos = false; }
+            if (klo <= khi) { depth = gK; start = klo; end = khi; have_pos = false; }
             a = A_TRAV;
           } else {
-            // the window's first B-mer code (c.B >= c.K) from the filter pass
+            // the window's first B-mer code (gB >= gK) from the filter pass
             SM_REGION(23);
-            const uint64_t kc = ktr ? m : codes_raw(row, c.w_row, prefix, c.K);
+            const uint64_t kc = ktr ? m : codes_raw(row, gRow, prefix, gK);
             addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
             st = S_KT;
             a = A_NONE;
