@@ -84,13 +84,15 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   auto kern = pk ? sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8>
                  : sm::k_mam_sm<IdxT, B, CHECK, STATS, false>;
   // the production geometry as compile-time constants (k_mam_sm GEO 1):
-  // packed words, 150-base reads, K 16 / B 18 / min_len 20
+  // packed words, 150-base direct rows, K 16 / B 18 / min_len 20, 131 match
+  // slots, map hints, 2^32 < N <= 2^33 (every value the kernel folds)
   static const bool geo_env = [] {
     const char *e = std::getenv("SMASH_SM_GEO");
     return !(e && e[0] == '0');
   }();
   if (pk && !STATS && geo_env && c0.K == 16 && c0.B == 18 && c0.min_len == 20 &&
-      c0.w_row == 40 && c0.len0 == 150)
+      c0.w_row == 40 && c0.len0 == 150 && c0.direct == 1 && c0.pad == 0 && !c0.lens &&
+      c0.mhint && c0.logN == 33 && c0.cap == 131)
     kern = sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8, 1>;
   int per_cu = 0, cus = 0;
   SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(

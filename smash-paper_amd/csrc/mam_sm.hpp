@@ -641,6 +641,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // SGPRs live (run_sm picks it only when the Ctx holds exactly these)
   const uint32_t gK = GEO ? 16u : c.K, gMin = GEO ? 20u : c.min_len, gB = GEO ? 18u : c.B;
   const uint32_t gRow = GEO ? 40u : c.w_row, gLen0 = GEO ? 150u : c.len0;
+  // (and the pipeline's launch: direct rows, no length array, 131 match
+  // slots, map hints on, a text of 2^32..2^33 characters, no SMASH_SM_PAD)
+  const uint32_t gDirect = GEO ? 1u : c.direct, gPad = GEO ? 0u : c.pad, gMh = GEO ? 1u : c.mhint;
+  const uint32_t gLogN = GEO ? 33u : c.logN, gCap = GEO ? 131u : c.cap;
+  const uint16_t *const gLens = GEO ? nullptr : c.lens;
   // PK: the SA / ISA words carry the packed hints (common.hpp; 8-byte
   // elements only): their position bits are PM, and the hint paths below
   // exist only in this instantiation
@@ -808,7 +813,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     // have landed -- waited for here, before this iteration's loads are
     // issued, where nothing else is outstanding; the bad mask of each, one
     // row word per lane, assembled only when a base is bad
-    if (c.direct) {
+    if (gDirect) {
       uint64_t cm = __ballot(st == S_COPY);
       if (cm) {
         SM_REGION(27);
@@ -837,7 +842,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
 #endif
       }
     }
-    const uint32_t st_ld = S_COPY + c.direct;   // the lowest state that loads
+    const uint32_t st_ld = S_COPY + gDirect;   // the lowest state that loads
     if (CHECK && st >= st_ld &&
         (addr < c.lo || addr >= c.hi || (need2 && (addr2 < c.lo || addr2 >= c.hi)))) {
       if (atomicAdd(c.viol, 1ull) == 0) {
@@ -866,13 +871,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         if (rd >= c.n_reads) {
           st = S_EXIT;
         } else {
-          L = c.lens ? c.lens[rd] : gLen0;
+          L = gLens ? gLens[rd] : gLen0;
           // records: the lane loads the bad-mask chunks, the read's bytes go
           // to its LDS row by DMA (below); direct rows: the row is DMA'd
           // from the read and the wave computes the mask next iteration
           addr = reinterpret_cast<uint64_t>(c.rec + rd * c.chunks);
           addr2 = addr + 16;
-          need2 = !c.direct && c.c_bad > 1;
+          need2 = !gDirect && c.c_bad > 1;
           pf = false; pfr = false;
           bad = Bad{0, 0, 0, 0, 0, 0, 0, 0};
           st = S_COPY;
@@ -889,7 +894,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         const uint32_t ln = uint32_t(__builtin_ctzll(fm_));
         fm_ &= fm_ - 1;
         const uint64_t rl = __shfl(rd, int(ln), 64);
-        if (c.direct)
+        if (gDirect)
           SM_DMA_ROW(ldsw + ln * gRow, c.rows + rl * (gRow >> 2), gRow >> 2, lane);
         else
           SM_DMA_ROW(ldsw + ln * gRow, c.rec + rl * c.chunks + c.c_bad, c.chunks - c.c_bad, lane);
@@ -930,7 +935,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
       case S_COPY: {                                 // bad-mask chunks 0 (v), 1 (v2)
         SM_REGION(2);
-        if (!c.direct) {   // (direct rows: the wave set the mask above)
+        if (!gDirect) {   // (direct rows: the wave set the mask above)
           bad.w0 = v.x; bad.w1 = v.y; bad.w2 = v.z; bad.w3 = v.w;
           bad.w4 = v2.x; bad.w5 = v2.y; bad.w6 = v2.z; bad.w7 = v2.w;   // (zero: c_bad 1)
         }
@@ -1059,9 +1064,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         SM_REGION(6);
         SM_HOOK_BYTE(pos & PM);
         if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
-          if (nem < c.cap)
-            c.out[rd * c.cap + nem] =
-                pack_match(pos & PM, prefix, depth) | (PK && c.mhint ? pk_map_hint(pos) : 0ull);
+          if (nem < gCap)
+            c.out[rd * gCap + nem] =
+                pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
           ++nem;
         }
         uscan_start(pos & PM, depth);
@@ -1190,11 +1195,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         break;
     }
 
-    if (c.pad) {                                    // issue-bound experiment (SMASH_SM_PAD)
-      // c.pad dependent v_add per lane; the empty asm keeps every one of them
+    if (gPad) {                                    // issue-bound experiment (SMASH_SM_PAD)
+      // gPad dependent v_add per lane; the empty asm keeps every one of them
       // (an earlier form let the compiler sink the chain under a rare branch)
       uint32_t x = uint32_t(addr);
-      for (uint32_t k = 0; k < c.pad; ++k) {
+      for (uint32_t k = 0; k < gPad; ++k) {
         x += k;
         PAD_KEEP(x);
       }
@@ -1285,7 +1290,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       SM_REGION(15);
       // the run around [start, end] with L8 >= depth = the suffixes sharing
       // P[prefix, prefix+depth); it fails iff it holds >= thresh more
-      thresh = 2u * depth * c.logN;
+      thresh = 2u * depth * gLogN;
       xd = depth; xrun = false;
       cbase = 0; cap = depth;
       es = start; ee = end;
@@ -1324,9 +1329,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           if (depth >= gMin &&
               (!PK || prefix == 0 || (pos & PM) == 0 ||
                P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
-            if (nem < c.cap)
-              c.out[rd * c.cap + nem] =
-                  pack_match(pos & PM, prefix, depth) | (PK && c.mhint ? pk_map_hint(pos) : 0ull);
+            if (nem < gCap)
+              c.out[rd * gCap + nem] =
+                  pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
             ++nem;
           }
           uscan_start(pos & PM, depth);
@@ -1335,6 +1340,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     if (a == A_TOP) {
       SM_REGION(17);
+      uint32_t kpos = ~0u;                            // a k-mer table probe's read window
       // (F) runs while the state is shallow, once per prefix (skip_f: this
       // prefix's window already passed the bitmap)
       bool proceed = skip_f || depth >= gMin;
@@ -1407,8 +1413,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
               } else {
                 SM_REGION(21);
                 fj = jq;
-                c0 = codes_raw(row, gRow, prefix + jq, W);
-                addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((c0 >> 4) & ((1ull << (2 * gK)) - 1)));
+                kpos = prefix + jq;                   // the entry's window: below
                 st = S_BM;
                 a = A_NONE;
               }
@@ -1472,14 +1477,23 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           } else {
             // the window's first B-mer code (gB >= gK) from the filter pass
             SM_REGION(23);
-            const uint64_t kc = ktr ? m : codes_raw(row, gRow, prefix, gK);
-            addr = reinterpret_cast<uint64_t>(c.KT + 2 * kc);
+            if (ktr) addr = reinterpret_cast<uint64_t>(c.KT + 2 * m);
+            else kpos = prefix;
             st = S_KT;
             a = A_NONE;
           }
         } else {
           a = A_TRAV;
         }
+      }
+      // one row read for both k-mer table probes: the filter's entry (S_BM,
+      // the 20 bases from kpos: its k-mer is bases 2..K+1, c0 keeps them all)
+      // and the root's k-mer (S_KT, bases 0..K-1 of the same span)
+      if (kpos != ~0u) {
+        const uint64_t cw = codes_raw(row, gRow, kpos, gK + 4);
+        const bool fb = st == S_BM;
+        if (fb) c0 = cw;
+        addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((cw >> (fb ? 4 : 8)) & ((1ull << (2 * gK)) - 1)));
       }
     }
     if (a == A_TRAV) {
