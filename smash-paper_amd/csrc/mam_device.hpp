@@ -321,18 +321,28 @@ constexpr int kScan = 32;
 
 // 8 read bytes at byte offset `off` of an LDS row (row 4-byte aligned and
 // padded; bytes past the read are masked by the callers)
+// (v_alignbyte_b32: the low dword of {hi, lo} >> 8 * (s & 3); the host
+// emulation substitutes its own)
+#ifndef SM_ALIGNBYTE
+#define SM_ALIGNBYTE(hi, lo, s) __builtin_amdgcn_alignbyte(hi, lo, s)
+#endif
 __device__ __forceinline__ uint64_t lds_load8(const uint8_t *P, uint64_t off) {
+  // three aligned words, two byte-aligns (no 64-bit shifts, no select on the
+  // offset): the rows carry the third word's over-read
   const uint32_t *w = reinterpret_cast<const uint32_t *>(P);
-  const uint64_t q = off >> 2, sh = (off & 3) * 8;
-  const uint64_t lo = uint64_t(w[q]) | (uint64_t(w[q + 1]) << 32);
-  if (sh == 0) return lo;
-  return (lo >> sh) | (uint64_t(w[q + 2]) << (64 - sh));
+  const uint32_t q = uint32_t(off) >> 2, s = uint32_t(off) & 3;
+  const uint32_t w0 = w[q], w1 = w[q + 1], w2 = w[q + 2];
+  return uint64_t(SM_ALIGNBYTE(w1, w0, s)) | (uint64_t(SM_ALIGNBYTE(w2, w1, s)) << 32);
 }
 
 // bytes of agreement of two 8-byte words, capped at lim (<= 8)
+// (ctz with 64 for zero: v_ffbl pairs with no compare-and-select on the
+// 64-bit difference; the host emulation substitutes its own)
+#ifndef SM_CTZ64
+#define SM_CTZ64(x) __builtin_ctzg(x, 64)
+#endif
 __device__ __forceinline__ uint32_t agree8(uint64_t a, uint64_t b, uint32_t lim) {
-  const uint64_t d = a ^ b;
-  const uint32_t k = d ? uint32_t(__builtin_ctzll(d) >> 3) : 8u;
+  const uint32_t k = uint32_t(SM_CTZ64(a ^ b)) >> 3;
   return k < lim ? k : lim;
 }
 

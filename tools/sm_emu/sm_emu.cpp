@@ -132,6 +132,12 @@ static uint32_t emu_pk_sub16(uint32_t a, uint32_t b) {
   return ((a - b) & 0xFFFFu) | (((a >> 16) - (b >> 16)) << 16);
 }
 #define SM_PK_SUB16(a, b) emu_pk_sub16(a, b)
+// v_alignbyte_b32 on the host
+static uint32_t emu_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+  return uint32_t(((uint64_t(hi) << 32) | lo) >> (8 * (s & 3)));
+}
+#define SM_ALIGNBYTE(hi, lo, s) emu_alignbyte(hi, lo, s)
+#define SM_CTZ64(x) ((x) ? __builtin_ctzll(x) : 64)
 // traverse binary searches by interval size (1..63, 64 = larger) and start depth
 static uint64_t emu_bs_size[65], emu_bs_depth[256], emu_bm[16], emu_f[16 * 8];
 #define SM_HOOK_BM(mode, a1, a2) (++emu_bm[4 * (mode) + 2 * (a1) + (a2)])
