@@ -2,6 +2,7 @@
 # tools/r05_upart.sh TAG -- U rebuild partition passes with 1024-thread tiles
 # (16 384 entries) vs 512 (SMASH_UPART_THREADS=512): the C5 and index parity
 # tests, then the C5 line alternating, on one box.
+# (the 1024-thread tiles were reverted after this run: the record of profiles/r05/upart1/)
 set -euo pipefail
 TAG=${1:?tag}
 R=$(cd "$(dirname "$0")/.." && pwd)
