@@ -490,6 +490,23 @@ __device__ __forceinline__ uint64_t codes_raw(const uint32_t *R, uint32_t w_row,
   return (x >> (48 - 2 * (sh + n))) & ((1ull << (2 * n)) - 1);
 }
 
+// the same over 7 words (28 bases): n <= 25 (the filter's pair of 20-base
+// entry windows 3 bases apart), q clamped to w_row - 7 (p + n <= 4 w_row)
+__device__ __forceinline__ uint64_t codes_raw7(const uint32_t *R, uint32_t w_row, uint32_t p,
+                                               uint32_t n) {
+  const uint32_t q0 = p >> 2, qm = w_row - 7;
+  const uint32_t q = q0 < qm ? q0 : qm, sh = p - 4 * q;
+  uint32_t hi = byte4_codes(R[q]);
+  hi = (hi << 8) | byte4_codes(R[q + 1]);
+  hi = (hi << 8) | byte4_codes(R[q + 2]);
+  uint32_t lo = byte4_codes(R[q + 3]);
+  lo = (lo << 8) | byte4_codes(R[q + 4]);
+  lo = (lo << 8) | byte4_codes(R[q + 5]);
+  lo = (lo << 8) | byte4_codes(R[q + 6]);
+  const uint64_t x = (uint64_t(hi) << 32) | lo;   // 28 bases, the first most significant
+  return (x >> (56 - 2 * (sh + n))) & ((1ull << (2 * n)) - 1);
+}
+
 template <class IdxT>
 struct Ctx {
   // the index (DevIndex fields, flattened: every field is a live SGPR)
@@ -523,6 +540,8 @@ struct Ctx {
                           // 3 (default) one k-mer entry = the window's B + 2 B-mers
   uint32_t pf;            // binary-search compares also load the children's SA elements
   uint32_t u32;           // (B) U scans load 32 bytes per iteration (else 16)
+  uint32_t f2;            // (F) policy 3: a second k-mer entry (the next three B-mers)
+                          // rides along with the first when they are unknown
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -949,21 +968,32 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_BM: {                                   // (F) a k-mer table entry arrived
         SM_REGION(3);
+        const bool two = need2;   // (policy 3: v2 holds the entry 3 bases on)
         need2 = false;
         if (SM_KNOB(bm_dual, 3u) == 3) {
           // the entry of the k-mer at x = kp + fj + 2; c0 = the 2-bit codes of
           // the k + 4 read bases [x - 2, x + k + 2), first most significant:
-          // its presence bits give the B-mers at x - 2, x - 1, x (common.hpp)
-          const uint64_t f48 = kt_filter(lo64(v), hi64(v));
+          // its presence bits give the B-mers at x - 2, x - 1, x (common.hpp).
+          // two: v2 / c1 are the same for the k-mer at x + 3
           const uint32_t nb = 2 * (gK + 4);
-          const uint32_t l1 = uint32_t(c0 >> (nb - 2)) & 3, l0 = uint32_t(c0 >> (nb - 4)) & 3;
-          const uint32_t r1 = uint32_t(c0 >> 2) & 3, r2 = uint32_t(c0) & 3;
-          const uint32_t bits = (uint32_t(f48 >> (32 + 4 * l1 + l0)) & 1u) |
-                                ((uint32_t(f48 >> (16 + 4 * l0 + r1)) & 1u) << 1) |
-                                ((uint32_t(f48 >> (4 * r1 + r2)) & 1u) << 2);
+          auto entry_bits = [&](const uint4 &e, uint64_t cc) {
+            const uint64_t f48 = kt_filter(lo64(e), hi64(e));
+            const uint32_t l1 = uint32_t(cc >> (nb - 2)) & 3, l0 = uint32_t(cc >> (nb - 4)) & 3;
+            const uint32_t r1 = uint32_t(cc >> 2) & 3, r2 = uint32_t(cc) & 3;
+            return (uint32_t(f48 >> (32 + 4 * l1 + l0)) & 1u) |
+                   ((uint32_t(f48 >> (16 + 4 * l0 + r1)) & 1u) << 1) |
+                   ((uint32_t(f48 >> (4 * r1 + r2)) & 1u) << 2);
+          };
+          const uint32_t bits = entry_bits(v, c0);
           SM_HOOK_F(fj, bits);
           fk |= (7u << fj) | (bits << (16 + fj));
           fdead = bits != 7u;
+          if (two) {
+            const uint32_t bits2 = entry_bits(v2, c1);
+            SM_HOOK_F(fj + 3, bits2);
+            fk |= (7u << (fj + 3)) | (bits2 << (19 + fj));
+            fdead = fdead || bits2 != 7u;
+          }
           kx = kp + fj + 2;
           klo = lo64(v) & kKtMask;
           khi = hi64(v) & kKtMask;
@@ -1306,38 +1336,6 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       a = ex_start(0, N - 1, ls, rs) ? A_NONE : A_RUN_DONE;
     }
-    if (a == A_AFTER) {
-      SM_REGION(16);
-      if (depth <= 1) {
-        depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
-        a = A_TOP;
-      } else {
-        a = A_NONE;
-        if (start != end) {                          // non-singleton suffix link
-          --depth;
-          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
-          st = S_IDX; op = O_NS_SA2;
-        } else if (!have_pos) {
-          addr = ia(c.SA, start);
-          st = S_IDX; op = O_SAPOS2;
-        } else if (depth >= gMin && prefix != 0 && (pos & PM) != 0 &&
-                   (!PK || ((pos >> kPkPosBits) & 7u) >= 4u)) {
-          addr = reinterpret_cast<uint64_t>(c.T + (pos & PM) - 1);
-          st = S_BYTE;
-        } else {
-          // (PK: is_leftmaximal from the BWT character in pos's SA word)
-          if (depth >= gMin &&
-              (!PK || prefix == 0 || (pos & PM) == 0 ||
-               P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
-            if (nem < gCap)
-              c.out[rd * gCap + nem] =
-                  pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
-            ++nem;
-          }
-          uscan_start(pos & PM, depth);
-        }
-      }
-    }
     if (a == A_TOP) {
       SM_REGION(17);
       uint32_t kpos = ~0u;                            // a k-mer table probe's read window
@@ -1414,6 +1412,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
                 SM_REGION(21);
                 fj = jq;
                 kpos = prefix + jq;                   // the entry's window: below
+                // the next three B-mers' entry too, when some of them are
+                // unknown and its window lies in the read: a run of absent
+                // B-mers (a segment junction) is crossed twice as fast
+                need2 = SM_KNOB(f2, 1u) && ((kn >> (jq + 3)) & 7u) != 7u && ok_at(jq + 3);
                 st = S_BM;
                 a = A_NONE;
               }
@@ -1490,10 +1492,16 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       // the 20 bases from kpos: its k-mer is bases 2..K+1, c0 keeps them all)
       // and the root's k-mer (S_KT, bases 0..K-1 of the same span)
       if (kpos != ~0u) {
-        const uint64_t cw = codes_raw(row, gRow, kpos, gK + 4);
+        // (23 bases: the second filter entry's window is the last 20)
+        const uint64_t kmask = (1ull << (2 * gK)) - 1;
+        const uint64_t cw = codes_raw7(row, gRow, kpos, gK + 7);
         const bool fb = st == S_BM;
-        if (fb) c0 = cw;
-        addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((cw >> (fb ? 4 : 8)) & ((1ull << (2 * gK)) - 1)));
+        if (fb) {
+          c0 = cw >> 6;
+          c1 = cw & ((1ull << (2 * (gK + 4))) - 1);
+          addr2 = reinterpret_cast<uint64_t>(c.KT + 2 * ((c1 >> 4) & kmask));
+        }
+        addr = reinterpret_cast<uint64_t>(c.KT + 2 * ((cw >> (fb ? 10 : 14)) & kmask));
       }
     }
     if (a == A_TRAV) {
@@ -1520,6 +1528,38 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           lc = 0;
           addr = ia(c.SA, m);
           st = S_IDX; op = O_BS_SA;
+        }
+      }
+    }
+    if (a == A_AFTER) {
+      SM_REGION(16);
+      if (depth <= 1) {
+        depth = 0; start = 0; end = N - 1; have_pos = false; ++prefix;
+        a = A_TOP;
+      } else {
+        a = A_NONE;
+        if (start != end) {                          // non-singleton suffix link
+          --depth;
+          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
+          st = S_IDX; op = O_NS_SA2;
+        } else if (!have_pos) {
+          addr = ia(c.SA, start);
+          st = S_IDX; op = O_SAPOS2;
+        } else if (depth >= gMin && prefix != 0 && (pos & PM) != 0 &&
+                   (!PK || ((pos >> kPkPosBits) & 7u) >= 4u)) {
+          addr = reinterpret_cast<uint64_t>(c.T + (pos & PM) - 1);
+          st = S_BYTE;
+        } else {
+          // (PK: is_leftmaximal from the BWT character in pos's SA word)
+          if (depth >= gMin &&
+              (!PK || prefix == 0 || (pos & PM) == 0 ||
+               P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
+            if (nem < gCap)
+              c.out[rd * gCap + nem] =
+                  pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
+            ++nem;
+          }
+          uscan_start(pos & PM, depth);
         }
       }
     }
