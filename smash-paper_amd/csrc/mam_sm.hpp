@@ -61,6 +61,9 @@
 #ifndef SM_HOOK_BYTE
 #define SM_HOOK_BYTE(pos)
 #endif
+#ifndef SM_HOOK_PARK
+#define SM_HOOK_PARK(a)           // host emulation: decide chains that park in S_ALU, by action
+#endif
 #ifndef SM_LOAD16
 #define SM_LOAD16(a) ::smash::sm::load16u(a)
 #endif
@@ -1273,6 +1276,26 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = ex_start(start, end, ls, rs) ? A_NONE : A_RUN_DONE;
       }
     }
+    if (a == A_EXPAND) {                              // expand_link (longSA.h:158-174)
+      SM_REGION(15);
+      // the run around [start, end] with L8 >= depth = the suffixes sharing
+      // P[prefix, prefix+depth); it fails iff it holds >= thresh more
+      thresh = 2u * depth * gLogN;
+      xd = depth; xrun = false;
+      cbase = 0; cap = depth;
+      es = start; ee = end;
+      SM_HOOK_RUN(true, 0, 0, 0);
+      // packed: the ISA words of start and end hold L8[start - 1 .. start]
+      // and L8[end + 1 .. end + 2]: a run that ends within one more suffix
+      // on a side needs no L8 probe there
+      bool ls = false, rs = false;
+      if (PK) {
+        ls = xls; rs = xrs;
+        if (ls && xl1) es = start - 1;
+        if (rs && xr1) ee = end + 1;
+      }
+      a = ex_start(0, N - 1, ls, rs) ? A_NONE : A_RUN_DONE;
+    }
     if (a == A_XL_DONE) {                             // left end known: right side
       SM_REGION(12);
       const uint64_t hb = xrun ? end : N - 1;
@@ -1315,26 +1338,6 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         st = S_IDX; op = O_ISAJ;
         a = A_NONE;
       }
-    }
-    if (a == A_EXPAND) {                              // expand_link (longSA.h:158-174)
-      SM_REGION(15);
-      // the run around [start, end] with L8 >= depth = the suffixes sharing
-      // P[prefix, prefix+depth); it fails iff it holds >= thresh more
-      thresh = 2u * depth * gLogN;
-      xd = depth; xrun = false;
-      cbase = 0; cap = depth;
-      es = start; ee = end;
-      SM_HOOK_RUN(true, 0, 0, 0);
-      // packed: the ISA words of start and end hold L8[start - 1 .. start]
-      // and L8[end + 1 .. end + 2]: a run that ends within one more suffix
-      // on a side needs no L8 probe there
-      bool ls = false, rs = false;
-      if (PK) {
-        ls = xls; rs = xrs;
-        if (ls && xl1) es = start - 1;
-        if (rs && xr1) ee = end + 1;
-      }
-      a = ex_start(0, N - 1, ls, rs) ? A_NONE : A_RUN_DONE;
     }
     if (a == A_TOP) {
       SM_REGION(17);
@@ -1570,6 +1573,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       it = 0;
       st = S_NEW;
     } else if (a != A_NONE) {
+      SM_HOOK_PARK(a);
       pend = a;
       st = S_ALU;
     }

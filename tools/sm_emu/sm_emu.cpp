@@ -178,6 +178,8 @@ static void emu_hook_byte(uint64_t pos) {
 #define SM_HOOK_CMPBS(begin, sp, off) emu_hook_cmpbs(begin, sp, off)
 #define SM_HOOK_RUN(begin, kind, el, er) emu_hook_run(begin, kind, el, er)
 #define SM_HOOK_BYTE(pos) emu_hook_byte(pos)
+static uint64_t emu_park[16];
+#define SM_HOOK_PARK(a) (++emu_park[(a) & 15])
 #include "../../smash-paper_amd/csrc/mam_sm.hpp"
 
 thread_local dim3 threadIdx, blockIdx, blockDim;
@@ -358,4 +360,9 @@ extern "C" int sm_emu_map(const uint8_t *T, const void *SA, const void *ISA, int
                          min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters, 0);
   return run<uint64_t>(T, SA, ISA, L8, U, KT, K, BM, B, in_text, N, logN, reads, stride, L, n,
                        min_len, out, cap, n_out, iters, spans, viol, lin_blocks, counters, packed);
+}
+
+// decide chains parked in S_ALU since the last reset, by pending action
+extern "C" void sm_emu_park_hist(uint64_t *out, int reset) {
+  for (int k = 0; k < 16; ++k) { out[k] = emu_park[k]; if (reset) emu_park[k] = 0; }
 }
