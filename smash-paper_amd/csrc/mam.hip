@@ -239,7 +239,7 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.bm_dual = 3;
   c.pf = 1;
   c.u32 = 1;
-  c.f2 = 1;
+  c.f2 = 2;
   // (pf, u32, bm_dual, grab and lin_blocks are the kernel's compile-time
   // defaults on the device, SM_KNOB in mam_sm.hpp: the fields above only
   // document them; tools/sm_emu varies them)

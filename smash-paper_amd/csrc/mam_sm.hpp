@@ -544,7 +544,8 @@ struct Ctx {
   uint32_t pf;            // binary-search compares also load the children's SA elements
   uint32_t u32;           // (B) U scans load 32 bytes per iteration (else 16)
   uint32_t f2;            // (F) policy 3: a second k-mer entry (the next three B-mers)
-                          // rides along with the first when they are unknown
+                          // rides along with the first when they are unknown (1: always,
+                          // 2: only after an entry showed an absent B-mer)
   const uint16_t *lens;
   uint32_t len0, cap;
   uint64_t n_reads;
@@ -1418,7 +1419,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
                 // the next three B-mers' entry too, when some of them are
                 // unknown and its window lies in the read: a run of absent
                 // B-mers (a segment junction) is crossed twice as fast
-                need2 = SM_KNOB(f2, 1u) && ((kn >> (jq + 3)) & 7u) != 7u && ok_at(jq + 3);
+                // (f2 2: only inside a run of absent B-mers, where it pays)
+                need2 = SM_KNOB(f2, 2u) && (SM_KNOB(f2, 2u) == 1 || fdead) &&
+                        ((kn >> (jq + 3)) & 7u) != 7u && ok_at(jq + 3);
                 st = S_BM;
                 a = A_NONE;
               }

@@ -281,7 +281,7 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   c.bm_dual = std::getenv("SMASH_SM_BM_DUAL") ? uint32_t(std::atoi(std::getenv("SMASH_SM_BM_DUAL"))) : 3;   // = the device default (mam.hip)
   c.pf = std::getenv("SMASH_SM_PF") ? uint32_t(std::atoi(std::getenv("SMASH_SM_PF"))) : 1;
   c.u32 = std::getenv("SMASH_SM_U32") ? uint32_t(std::atoi(std::getenv("SMASH_SM_U32"))) : 1;
-  c.f2 = std::getenv("SMASH_SM_F2") ? uint32_t(std::atoi(std::getenv("SMASH_SM_F2"))) : 1;
+  c.f2 = std::getenv("SMASH_SM_F2") ? uint32_t(std::atoi(std::getenv("SMASH_SM_F2"))) : 2;
   c.lens = nullptr; c.len0 = L; c.cap = cap; c.n_reads = n;
   c.out = out; c.n_out = n_out;
   unsigned long long work = 0;
