@@ -186,6 +186,123 @@ def host_index(S, O, dix, T, sp, sz, names, sample_reads=None):
     return oix, mp
 
 
+def add_sample_kmers(S, dix, oix, reads):
+    """copy the device k-mer entries of `reads`' k-mers into the host table
+    host_index left lazily committed (oix holds that array, not a copy), so
+    the host emulation and the oracle's k-mer descents can run on them"""
+    import torch
+    K = dix.info.kmer_k
+    codes = kmer_codes(reads, K)
+    if len(codes):
+        kt_dev = S.device_view(dix.info.d_kmer, 16 << (2 * K), torch.int64).view(-1, 2)
+        idx = torch.from_numpy(codes.astype(np.int64)).to(kt_dev.device)
+        oix._KT.reshape(-1, 2)[codes.astype(np.int64)] = \
+            kt_dev.index_select(0, idx).cpu().numpy().view(np.uint64)
+
+
+def search_lines(S, dix, oix, sample):
+    """k_mam_sm's probe sequence over `sample` on the host (tools/sm_emu, the
+    kernel's own source, one lane): (emulator, iterations per read, lines)"""
+    import sm_emu
+    add_sample_kmers(S, dix, oix, sample)
+    emu = sm_emu.Emu(oix, copy=False, packed=bool(dix.info.pos_bits))
+    _, emu_it = emu.map(sample)
+    return emu, emu_it, sum(v[1] for v in emu.counters.values())
+
+
+def c2_line(args, dix, contigs, dev, oix, mp, steps=20, warmup=3):
+    """BASELINE configs[1] (C2) on the resident hg19 index: 1 M x 100 bp SMASH
+    reads (500 k pairs, one batch) through the whole chain into
+    sample_bins/100000; the GEO 100 search kernel (mam.hip run_sm).  Roofline
+    from the emulated probe sequence of a sample of its reads; the oracle runs
+    the whole C2 workload on the host's cores (cpu_baseline) and its counts
+    must equal the device's."""
+    import torch
+    import smashgpu as S
+    import readgen
+    cfg = CONFIGS["c2"]
+    starts = bin_starts_for(cfg, contigs, tempfile.mkdtemp())
+    cs = chrom_sizes_for(cfg, contigs)
+    P, L = cfg["pairs"], cfg["read_len"]
+    d_reads = S.to_rows(readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000).generate(P), L)
+    pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P + P // 8 + (1 << 20),
+                      read_stride=d_reads.shape[1])
+    counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
+
+    def step():
+        counts.zero_()
+        pipe.reset()
+        pipe.count_batches(d_reads, P, P, counts, resident=True)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ref = counts.cpu().numpy().copy()
+    pipe.profile(True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    mam_ms, launches, mam_reads = pipe.profile_read()
+    pipe.profile(False)
+    st = pipe.stats()
+    dev_counts = counts.cpu().numpy()
+    value = 2 * P * steps / el
+    avg_ms = mam_ms / max(launches, 1)
+    res = {"metric": "reads/sec mapped+binned (hg19, 100 bp, C2)", "value": value,
+           "unit": "reads/s", "ms_per_step": 1000.0 * el / steps, "steps": steps,
+           "warmup": warmup, "workload": cfg["workload"], "pairs": P, "read_len": L,
+           "bins": int(len(starts)), "batch_pairs": P,
+           "search_kernel": "k_mam_sm GEO 100" if dix.info.pos_bits else "k_mam_sm",
+           "deterministic_counts": bool(np.array_equal(dev_counts, ref)),
+           "stats": st.as_dict(), "roofline": None, "cpu_baseline": None}
+    log("C2: %d steps %.3f s -> %.3e reads/s, %.3f ms per step, k_mam %.3f ms per launch"
+        % (steps, el, value, 1000.0 * el / steps, avg_ms))
+    if oix is not None:
+        import oracle as O
+        ns = min(4000, 2 * P)
+        sample = d_reads[:ns, :L].contiguous().cpu().numpy()
+        emu, emu_it, lines = search_lines(S, dix, oix, sample)
+        b_read = 64.0 * lines / ns
+        rpl = mam_reads / max(launches, 1)
+        achieved = rpl * b_read / (avg_ms / 1e3) / 1e9
+        res["roofline"] = {
+            "bound": "hbm", "kernel": "k_mam_sm", "achieved": round(achieved, 2), "peak": 8000.0,
+            "unit": "GB/s", "frac": round(achieved / 8000.0, 5), "traffic": None,
+            "bytes_per_read": round(b_read, 1), "avg_kernel_ms": round(avg_ms, 3),
+            "reads_per_launch": int(rpl),
+            "lines_per_read": {k: round(v[1] / ns, 3) for k, v in emu.counters.items()},
+            "loop_iterations_per_read": round(float(emu_it.mean()), 1),
+            "requests_per_read": round(emu.requests[0] / ns, 2),
+            "bytes_method": "64 B x line transitions of the kernel's probe sequence (tools/sm_emu "
+                            "on the downloaded index, %d reads)" % ns}
+        if not args.no_cpu_baseline:
+            # the whole C2 workload through the oracle's chain (~8 s on 16
+            # threads): its counts against the device's
+            threads, note = host_cores()
+            h = d_reads[:2 * P, :L].contiguous().cpu().numpy()
+            op = O.Pipeline(oix, mp, cs, starts)
+            t3 = time.perf_counter()
+            err = op.run(h, threads=threads)
+            dt = time.perf_counter() - t3
+            exact = bool(err == 0 and np.array_equal(dev_counts.astype(np.uint64), op.counts))
+            res["cpu_baseline"] = {
+                "value": 2 * P / dt, "unit": "reads/s", "cores": threads, "kind": "port",
+                "sample": "the whole C2 workload, %d pairs (%d reads), whole chain "
+                          "(oracle/smash_oracle.c orc_run_pairs, %d threads), %.1f s"
+                          % (P, 2 * P, threads, dt),
+                "cores_note": note}
+            res["bin_counts_identical_to_oracle"] = exact
+            log("C2 cpu baseline: %.3e reads/s on %d threads; counts == oracle: %s"
+                % (2 * P / dt, threads, exact))
+    pipe.close()
+    del d_reads
+    torch.cuda.empty_cache()
+    return res
+
+
 def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps=3):
     """C5 on the resident index: map.bin bytes of every forward base (longSA::
     show) + unique 36-mer counts per contig and per bin, bases split into
@@ -352,27 +469,24 @@ def bench_c5(args, cfg, world, rank, local, dist):
         dist.destroy_process_group()
 
 
-def bench_mem(args, cfg, world, rank, local, dist):
-    """--config c3mem: MEM (-maxmatch) of C3-style reads (csrc/mem.hip,
-    smash_match_batch SMASH_MODE_MEM), every launch over all the rank's reads;
-    roofline from the line transitions of mem.hip's own probe sequence
-    (oracle orc_mem_dev: the k-mer table from the root, 8-byte singleton
-    compares, counted) on a sample; CPU baseline the reference's probe
+def mem_line(args, cfg, dix, d_reads, n, dev, oix, world=1, rank=0, dist=None, steps=None,
+             warmup=None, cpu_seconds=None):
+    """MEM (-maxmatch) of n C3-style reads (d_reads: dense [n, L] on the
+    device; csrc/mem.hip, smash_match_batch SMASH_MODE_MEM), every launch over
+    all of them; roofline from the line transitions of mem.hip's own probe
+    sequence (oracle orc_mem_dev: the k-mer table from the root, 8-byte
+    singleton compares, counted) on a sample, `traffic` from the FETCH_SIZE
+    pass in profiles/pmc_c3mem.json; CPU baseline the reference's probe
     sequence (orc_mem, the oracle) on the host's cores; the device's records
-    of a sample equal the oracle's, in emission order."""
+    of a sample equal the oracle's, in emission order.  oix: the host copy
+    of the index (rank 0), or None."""
     import torch
     import smashgpu as S
-    import synth
-    import readgen
     import oracle as O
-    dev = torch.device("cuda", local)
-    contigs = synth.make_genome(cfg["genome"])
-    T, sp, sz, names = S.text_from_contigs(contigs)
-    dix = S.Index.create(T, sp, sz, names, device=local)
-    log("device index: %.1f s" % dix.info.build_seconds)
-    P, L, cap = cfg["pairs"], cfg["read_len"], cfg["cap"]
-    n = 2 * P
-    d_reads = readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000 + rank).generate(P)
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
+    L, cap = cfg["read_len"], cfg["cap"]
     out = torch.zeros(n * cap * 2, dtype=torch.int64, device=dev)
     nn = torch.zeros(n, dtype=torch.int32, device=dev)
 
@@ -380,16 +494,16 @@ def bench_mem(args, cfg, world, rank, local, dist):
         S.match_batch(dix, d_reads, n, L, out, cap, nn, mode="MEM")
 
     log("MEM: %d reads, cap %d; warm-up launch" % (n, cap))
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         t0 = time.perf_counter()
         launch()
         torch.cuda.synchronize()
         log("MEM: warm-up launch %.3f s" % (time.perf_counter() - t0))
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * steps)]
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         ev[2 * i].record()
         launch()
         ev[2 * i + 1].record()
@@ -403,30 +517,28 @@ def bench_mem(args, cfg, world, rank, local, dist):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.steps)) / args.steps
+    kms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(steps)) / steps
     counts = nn.cpu().numpy()
-    value = n * world * args.steps / el
+    value = n * world * steps / el
     log("MEM: %d reads x %d launches in %.3f s -> %.3e reads/s; %.1f ms per launch; %.1f MEMs "
-        "per read (max %d, cap %d)" % (n, args.steps, el, value, kms, counts.mean(), counts.max(),
-                                       cap))
+        "per read (max %d, cap %d)" % (n, steps, el, value, kms, counts.mean(), counts.max(), cap))
     res = {"metric": "reads/sec MEM search (memsam -maxmatch, hg19, 150 bp)", "value": value,
-           "unit": "reads/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": 1000.0 * el / args.steps, "higher_is_better": True,
+           "unit": "reads/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+           "ms_per_step": 1000.0 * el / steps, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "u8/u64 (integer)",
            "data": "synthetic (tools/synth.py hg19-shaped genome; SMASH reads generated on the "
                    "device, tools/readgen.hip, seeded)",
            "config": {"workload": cfg["workload"], "genome": cfg["genome"], "reads": n,
-                      "read_len": L, "cap_per_read": cap, "kernel": "k_mem (csrc/mem.hip)",
+                      "read_len": L, "cap_per_read": cap,
+                      "kernel": "k_mem + k_mem_jobs (csrc/mem.hip)",
                       "parallelism": "dp%d: read shards" % world},
            "mems_per_read": round(float(counts.mean()), 2), "mems_max": int(counts.max()),
            "records_cut": int((counts > cap).sum()), "roofline": None, "cpu_baseline": None}
-    if rank == 0:
+    if oix is not None:
         t2 = time.time()
         ns = 2000
         sample = d_reads[:ns].cpu().numpy()
-        oix, _ = host_index(S, O, dix, T, sp, sz, names, sample_reads=sample)
-        log("host copy of the index: %.1f s" % (time.time() - t2))
-        t2 = time.time()
+        add_sample_kmers(S, dix, oix, sample)
         _, per, ctr = O.mem_batch(oix, sample, threads=host_cores()[0], device_probes=True,
                                   count=True)
         log("MEM: oracle probe sequence over %d reads: %.1f s" % (ns, time.time() - t2))
@@ -435,13 +547,22 @@ def bench_mem(args, cfg, world, rank, local, dist):
         b_read = 64.0 * sum(lines.values())
         achieved = n * b_read / (kms / 1e3) / 1e9
         res["roofline"] = {
-            "bound": "hbm", "kernel": "k_mem", "achieved": round(achieved, 2), "peak": 8000.0,
-            "unit": "GB/s", "frac": round(achieved / 8000.0, 5), "traffic": None,
+            "bound": "hbm", "kernel": "k_mem + k_mem_jobs", "achieved": round(achieved, 2),
+            "peak": 8000.0, "unit": "GB/s", "frac": round(achieved / 8000.0, 5), "traffic": None,
             "bytes_per_read": round(b_read, 1), "avg_kernel_ms": round(kms, 3),
             "lines_per_read": {k: round(v, 2) for k, v in lines.items()},
             "lines_G_per_s": round(n * sum(lines.values()) / (kms / 1e3) / 1e9, 2),
             "bytes_method": "64 B x line transitions of mem.hip's probe sequence (oracle "
                             "orc_mem_dev on the downloaded index, %d reads)" % ns}
+        pmc = os.path.join(ROOT, "profiles", "pmc_c3mem.json")
+        if os.path.exists(pmc):
+            try:
+                j = json.load(open(pmc))
+                res["roofline"]["traffic"] = j["mem_bytes_per_read"] * n
+                res["roofline"]["traffic_bytes_per_read"] = j["mem_bytes_per_read"]
+                res["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
+            except Exception:   # noqa: BLE001
+                pass
         # the device's records == the oracle's, in emission order
         # (reads whose MEMs exceed cap -- a repeat family's millions -- keep
         # exact counts and cut records: their counts are compared)
@@ -456,7 +577,7 @@ def bench_mem(args, cfg, world, rank, local, dist):
             t3 = time.perf_counter()
             O.mem_batch(oix, sample[:64 * threads], threads=threads)
             dt0 = time.perf_counter() - t3
-            m = int(min(n, max(64 * threads, 64 * threads * args.cpu_seconds / max(dt0, 1e-3))))
+            m = int(min(n, max(64 * threads, 64 * threads * cpu_seconds / max(dt0, 1e-3))))
             h = d_reads[:m].cpu().numpy()
             t3 = time.perf_counter()
             O.mem_batch(oix, h, threads=threads)
@@ -468,6 +589,35 @@ def bench_mem(args, cfg, world, rank, local, dist):
                                              % (m, threads, dt),
                                    "cores_note": note}
             log("MEM cpu baseline: %.3e reads/s on %d threads" % (m / dt, threads))
+    del out, nn
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_mem(args, cfg, world, rank, local, dist):
+    """--config c3mem: the MEM line (mem_line) as the headline, on reads of
+    its own (cfg pairs, seeded as C3's)."""
+    import torch
+    import smashgpu as S
+    import synth
+    import readgen
+    import oracle as O
+    dev = torch.device("cuda", local)
+    contigs = synth.make_genome(cfg["genome"])
+    T, sp, sz, names = S.text_from_contigs(contigs)
+    dix = S.Index.create(T, sp, sz, names, device=local)
+    log("device index: %.1f s" % dix.info.build_seconds)
+    P = cfg["pairs"]
+    d_reads = readgen.Generator(dix, contigs, cfg["read_len"],
+                                seed=cfg["seed"] * 1000 + rank).generate(P)
+    oix = None
+    if rank == 0:
+        t2 = time.time()
+        oix, _ = host_index(S, O, dix, T, sp, sz, names,
+                            sample_reads=d_reads[:2000].cpu().numpy())
+        log("host copy of the index: %.1f s" % (time.time() - t2))
+    res = mem_line(args, cfg, dix, d_reads, 2 * P, dev, oix, world, rank, dist)
+    if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -635,6 +785,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 scan on the same index")
     ap.add_argument("--no-feed", action="store_true", help="skip the file-fed measurement")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="skip the C2 and MEM lines on the same index (c3, one GPU)")
     ap.add_argument("--feed-pairs", type=int, default=0,
                     help="pairs of the file-fed run (0: all the rank's pairs, the C3 run)")
     args = ap.parse_args()
@@ -833,10 +985,7 @@ def main():
         # k_mam_sm's own probe sequence, counted by running the kernel's code
         # on the host (tools/sm_emu: the same source, one lane) over this
         # index and a sample of the same reads
-        import sm_emu
-        emu = sm_emu.Emu(oix, copy=False, packed=bool(dix.info.pos_bits))
-        _, emu_it = emu.map(sample)
-        lines = sum(v[1] for v in emu.counters.values())
+        emu, emu_it, lines = search_lines(S, dix, oix, sample)
         b_read = 64.0 * lines / ns
         # achieved = the bytes of one launch / the average launch duration
         # (HIP events around each k_mam_sm on its own stream; rocprofv3's
@@ -948,9 +1097,32 @@ def main():
             out["host_boundary"] = {"error": repr(e)}
     out["deterministic_counts"] = same
     out["stats_last_step"] = st.as_dict()
+    # the other hg19 lines on the same resident index (BASELINE configs[1]
+    # C2, the MEM mode north_star names, configs[4] C5): each needs HBM of
+    # its own, so the C3 pipeline and its file-fed buffers go first
+    subs = cfg["genome"] == "hg19" and args.config == "c3"
+    if subs and world == 1 and not args.no_sub:
+        pipe.close()
+        torch.cuda.empty_cache()
+        try:
+            out["c2"] = c2_line(args, dix, contigs, dev, oix, mp if oix is not None else None)
+        except Exception as e:   # noqa: BLE001
+            log("C2 line failed: %r" % (e,))
+            out["c2"] = {"error": repr(e)}
+        try:
+            mcfg = CONFIGS["c3mem"]
+            nm = 2 * mcfg["pairs"]
+            # the first 2 M of C3's own reads, dense (k_mem reads [n, L])
+            dm = d_reads[:nm, :L].contiguous()
+            out["c3mem"] = mem_line(args, mcfg, dix, dm, nm, dev, oix, steps=2, warmup=1,
+                                    cpu_seconds=min(10.0, args.cpu_seconds))
+            del dm
+        except Exception as e:   # noqa: BLE001
+            log("MEM line failed: %r" % (e,))
+            out["c3mem"] = {"error": repr(e)}
     if cfg["genome"] == "hg19" and not args.no_c5:
         # the scan needs ~12 GB of its own (its map.bin output and the
-        # comparison): the C3 pipeline and its file-fed buffers go first
+        # comparison)
         pipe.close()
         torch.cuda.empty_cache()
         out["c5"] = c5_scan(args, dix, contigs, "50000", world, rank, dev, dist, oix)

@@ -83,17 +83,20 @@ int run_sm(const smash_index *ix, const sm::Ctx<IdxT> &c0, uint64_t n_reads, siz
   const bool pk = sizeof(IdxT) == 8 && ix->pos_mask == kPkPosMask;
   auto kern = pk ? sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8>
                  : sm::k_mam_sm<IdxT, B, CHECK, STATS, false>;
-  // the production geometry as compile-time constants (k_mam_sm GEO 1):
-  // packed words, 150-base direct rows, K 16 / B 18 / min_len 20, 131 match
-  // slots, map hints, 2^32 < N <= 2^33 (every value the kernel folds)
+  // the production geometries as compile-time constants (k_mam_sm GEO = L):
+  // packed words, L-base direct rows (L = 150: C3 / C4; L = 100: C2), K 16 /
+  // B 18 / min_len 20, L - 19 match slots, map hints, 2^32 < N <= 2^33
+  // (every value the kernel folds)
   static const bool geo_env = [] {
     const char *e = std::getenv("SMASH_SM_GEO");
     return !(e && e[0] == '0');
   }();
   if (pk && !STATS && geo_env && c0.K == 16 && c0.B == 18 && c0.min_len == 20 &&
-      c0.w_row == 40 && c0.len0 == 150 && c0.direct == 1 && c0.pad == 0 && !c0.lens &&
-      c0.mhint && c0.logN == 33 && c0.cap == 131)
-    kern = sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8, 1>;
+      c0.direct == 1 && c0.pad == 0 && !c0.lens && c0.mhint && c0.logN == 33 &&
+      c0.cap == c0.len0 - 19 && c0.w_row == sm::geo_row(c0.len0)) {
+    if (c0.len0 == 150) kern = sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8, 150>;
+    else if (c0.len0 == 100) kern = sm::k_mam_sm<IdxT, B, CHECK, STATS, sizeof(IdxT) == 8, 100>;
+  }
   int per_cu = 0, cus = 0;
   SMASH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &per_cu, reinterpret_cast<const void *>(kern), B, lds));
@@ -242,7 +245,18 @@ int launch_sm(const smash_index *ix, uint32_t min_len, const uint8_t *seqs,
   c.f2 = 2;
   // (pf, u32, bm_dual, grab and lin_blocks are the kernel's compile-time
   // defaults on the device, SM_KNOB in mam_sm.hpp: the fields above only
-  // document them; tools/sm_emu varies them)
+  // document them; tools/sm_emu varies them.  The environment variables that
+  // set them in the emulator do nothing here: say so once.)
+  static const bool knob_warned = [] {
+    const char *names[] = {"SMASH_SM_BM_DUAL", "SMASH_SM_PF", "SMASH_SM_U32", "SMASH_SM_GRAB",
+                           "SMASH_SM_LIN", "SMASH_SM_F2"};
+    for (const char *n : names)
+      if (std::getenv(n))
+        std::fprintf(stderr, "smash: %s is an emulator knob (tools/sm_emu); the device kernel "
+                             "uses its compile-time default\n", n);
+    return true;
+  }();
+  (void)knob_warned;
   if (const char *e = std::getenv("SMASH_SM_PAD")) c.pad = uint32_t(std::atoi(e));
   c.mhint = ws && ws->mhint ? 1u : 0u;
   c.lens = lens; c.len0 = len; c.cap = cap; c.n_reads = n_reads;

@@ -137,6 +137,11 @@ struct Geom {
   uint32_t chunks;   // 16-byte record chunks per read
 };
 
+// the LDS row words of make_geom(L), as a constant expression (GEO kernels)
+__host__ __device__ constexpr uint32_t geo_row(uint32_t L) {
+  return ((L + 11) / 4 + 3) / 4 * 4 < 8 ? 8u : ((L + 11) / 4 + 3) / 4 * 4;
+}
+
 inline Geom make_geom(uint32_t max_len) {
   Geom g;
   g.w_raw = (max_len + 11) / 4;      // lds_load8 at offset <= L-1 reads 3 words
@@ -658,16 +663,18 @@ inline void bad_table(const uint64_t in_text[4], uint32_t *lo, uint32_t *hi) {
 // character.
 template <class IdxT, int BLOCK, bool CHECK, bool STATS, bool PK = false, int GEO = 0>
 __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
-  // GEO 1: the launch geometry of 150-base reads on an index with a 16-mer
-  // table (K 16, min_len 20, B 18, 40-word rows), as constants: the shifts,
-  // masks and row offsets built from them fold, and the loop keeps fewer
-  // SGPRs live (run_sm picks it only when the Ctx holds exactly these)
+  // GEO = L (150 or 100): the launch geometry of L-base reads on an index
+  // with a 16-mer table (K 16, min_len 20, B 18, geo_row(L)-word rows), as
+  // constants: the shifts, masks and row offsets built from them fold, and
+  // the loop keeps fewer SGPRs live (run_sm picks it only when the Ctx holds
+  // exactly these)
+  static_assert(GEO == 0 || (GEO >= 21 && GEO <= 255), "GEO is 0 or the read length");
   const uint32_t gK = GEO ? 16u : c.K, gMin = GEO ? 20u : c.min_len, gB = GEO ? 18u : c.B;
-  const uint32_t gRow = GEO ? 40u : c.w_row, gLen0 = GEO ? 150u : c.len0;
-  // (and the pipeline's launch: direct rows, no length array, 131 match
+  const uint32_t gRow = GEO ? geo_row(GEO) : c.w_row, gLen0 = GEO ? uint32_t(GEO) : c.len0;
+  // (and the pipeline's launch: direct rows, no length array, L - 19 match
   // slots, map hints on, a text of 2^32..2^33 characters, no SMASH_SM_PAD)
   const uint32_t gDirect = GEO ? 1u : c.direct, gPad = GEO ? 0u : c.pad, gMh = GEO ? 1u : c.mhint;
-  const uint32_t gLogN = GEO ? 33u : c.logN, gCap = GEO ? 131u : c.cap;
+  const uint32_t gLogN = GEO ? 33u : c.logN, gCap = GEO ? uint32_t(GEO) - 19u : c.cap;
   const uint16_t *const gLens = GEO ? nullptr : c.lens;
   // PK: the SA / ISA words carry the packed hints (common.hpp; 8-byte
   // elements only): their position bits are PM, and the hint paths below
@@ -1419,8 +1426,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
                 // the next three B-mers' entry too, when some of them are
                 // unknown and its window lies in the read: a run of absent
                 // B-mers (a segment junction) is crossed twice as fast
-                // (f2 2: only inside a run of absent B-mers, where it pays)
-                need2 = SM_KNOB(f2, 2u) && (SM_KNOB(f2, 2u) == 1 || fdead) &&
+                // (f2 2: only inside a run of absent B-mers, where it pays).
+                // Its bits land at offsets jq + 3 .. jq + 5 of fk's 16-bit
+                // halves, so only when jq + 6 <= 16 (D <= 10; min_len >= 29
+                // at B 18 takes one entry per probe)
+                need2 = SM_KNOB(f2, 2u) && (SM_KNOB(f2, 2u) == 1 || fdead) && jq + 6 <= 16 &&
                         ((kn >> (jq + 3)) & 7u) != 7u && ok_at(jq + 3);
                 st = S_BM;
                 a = A_NONE;

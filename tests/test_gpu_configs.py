@@ -55,14 +55,21 @@ def _reads(contigs, n_pairs, L, seed):
     return S.prepare_reads(reads)
 
 
-def _device_counts(dix, cs, starts, reads, batch):
+def _device_counts(dix, cs, starts, reads, batch, rows=False):
+    """rows: the mates in the device's native rows (S.to_rows), the layout
+    the bench's batches use -- the search DMAs them straight into LDS, and on
+    the packed hg19 index at 150 / 100 bp runs the GEO kernels (mam.hip
+    run_sm); dense mates go through k_prep's records and the generic kernel"""
     n = reads.shape[0] // 2
-    pipe = S.Pipeline(dix, cs, starts, reads.shape[1], min(batch, n), dedup_capacity=n)
+    L = reads.shape[1]
+    pipe = S.Pipeline(dix, cs, starts, L, min(batch, n), dedup_capacity=n,
+                      read_stride=S.read_stride(L) if rows else 0)
     counts = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
     pipe.reset()
     for b0 in range(0, n, batch):
         b1 = min(n, b0 + batch)
-        pipe.count_batch(torch.from_numpy(reads[2 * b0:2 * b1]).cuda(), b1 - b0, counts)
+        d = torch.from_numpy(reads[2 * b0:2 * b1]).cuda()
+        pipe.count_batch(S.to_rows(d, L) if rows else d, b1 - b0, counts)
     st = pipe.stats()
     return counts.cpu().numpy().astype(np.uint64), st, pipe
 
@@ -253,8 +260,10 @@ def _chrom_sizes(contigs):
     return out
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c3"])
-def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, tmp_path):
+@pytest.mark.parametrize("cfg,rows", [("c2", False), ("c2", True), ("c3", False), ("c3", True)])
+def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, rows, tmp_path):
+    """C2 whole / a C3 sample against the oracle, from dense mates (generic
+    search kernel) and from native rows (the GEO 100 / GEO 150 kernels)"""
     contigs, _, dix = hg19
     oix, mp = hg19_oracle
     src = os.path.join(ROOT, "data", "bins", "50000", "bins.txt")
@@ -267,8 +276,9 @@ def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, tmp_path):
     starts = np.array([int(l.split("\t")[2]) for l in open(path)], np.int64)
     reads = _reads(contigs, n, L, seed)
     cs = _chrom_sizes(contigs)
-    counts, st, _ = _device_counts(dix, cs, starts, reads, 40_000)
+    counts, st, pipe = _device_counts(dix, cs, starts, reads, 40_000, rows=rows)
     assert st.error == 0
+    assert pipe.map_hints() == bool(dix.info.pos_bits)
     op, err = _oracle_counts(oix, mp, cs, starts, reads)
     assert err == 0
     assert np.array_equal(counts, op.counts)

@@ -66,7 +66,9 @@ def test_state_machine_edge_reads(emu, tiny_ix, L, direct, monkeypatch):
     extra = [b"z" * L, b"n" * L, b"a" * L, (b"acgt" * 64)[:L], (b"c" * (L // 2) + b"z" + b"c" * L)[:L]]
     reads = np.concatenate([reads, np.array([np.frombuffer(x, np.uint8) for x in extra])])
     for e in (emu[0], emu[2]):
-        for ml, lin in ((20, 2), (12, 2), (30, 2), (20, 1), (12, 1)):
+        # (tiny index: K 9, B 11, so min_len 22 / 24 put the filter's window
+        # spread D at 11 / 13, where its second entry no longer fits fk)
+        for ml, lin in ((20, 2), (12, 2), (30, 2), (20, 1), (12, 1), (22, 2), (24, 2)):
             got, _ = e.map(reads, min_len=ml, lin_blocks=lin)
             for i in range(len(reads)):
                 assert got[i] == tiny_ix.search(reads[i].tobytes(), min_len=ml), (e.packed, ml, lin, i)
