@@ -278,7 +278,7 @@ def test_hg19_counts_equal_oracle(hg19, hg19_oracle, cfg, rows, tmp_path):
     cs = _chrom_sizes(contigs)
     counts, st, pipe = _device_counts(dix, cs, starts, reads, 40_000, rows=rows)
     assert st.error == 0
-    assert pipe.map_hints() == bool(dix.info.pos_bits)
+    assert pipe.map_hints == bool(dix.info.pos_bits)
     op, err = _oracle_counts(oix, mp, cs, starts, reads)
     assert err == 0
     assert np.array_equal(counts, op.counts)
