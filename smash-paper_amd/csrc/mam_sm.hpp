@@ -43,6 +43,19 @@
 #ifndef SM_HOOK_BM
 #define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes (policies 0-2)
 #endif
+// round-6 request cuts, each a compile-time switch for A/B builds (1: on):
+// SM_PAIR the pair loads of adjacent SA words, SM_BSL2 the second probe of a
+// window-decided binary-search step from the pair, SM_TSH line-clamped text
+// compare blocks
+#ifndef SM_PAIR
+#define SM_PAIR 1
+#endif
+#ifndef SM_BSL2
+#define SM_BSL2 1
+#endif
+#ifndef SM_TSH
+#define SM_TSH 1
+#endif
 #ifndef SM_HOOK_F
 #define SM_HOOK_F(j, bits)         // host emulation: filter outcomes (policy 3)
 #endif
@@ -352,7 +365,7 @@ enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
 enum : uint32_t { O_EXT = 0, O_BS };
 // ALU continuations, in the order the decide chain runs them
 enum : uint32_t { A_NONE = 0, A_BSP, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE,
-                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE };
+                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE, A_BSL };
 // binary-search modes: 0 where P' sorts (traverse); 1 / 2 the left / right
 // end of a run of suffixes sharing `cap` characters (from `cbase`) with P
 enum : uint32_t { BS_INSERT = 0, BS_LEFT, BS_RIGHT };
@@ -736,6 +749,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // consumed, read by A_EXPAND in the same iteration): the left end stops at
   // start (- 1 with xl1), the right end at end (+ 1 with xr1)
   FlagRef xls{fl, 12}, xl1{fl, 13}, xrs{fl, 14}, xr1{fl, 15};
+  // pair loads (8-byte elements): one 16-byte load at the exact address of
+  // SA[e] brings SA[e] and SA[e + 1], where the search wants both -- the two
+  // ends of a 2-suffix interval's suffix link (O_NS_SA2), and a binary-search
+  // probe m whose left child is m - 1 (O_BS_SA: ee then holds SA[m - 1] until
+  // m moves, so the probe's compare needs no prefetch of that child).  Set
+  // while such a load is in flight (it is issued unaligned) and, for the
+  // binary search, while ee holds the left child
+  FlagRef pl{fl, 16};
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
@@ -752,6 +773,17 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // blocks in one iteration (S_EXB), or the one side with room; false: none
   // left blocks are the 16 bytes ENDING at es (from 0 when es < 15), right
   // blocks start at ee + 1
+  // the SA word of binary-search probe m = (lo + hi) / 2; with 8-byte
+  // elements and a left child m - 1 (intervals of up to ~5 suffixes), as the
+  // pair SA[m - 1], SA[m] (pl)
+  auto bs_load = [&]() {
+    m = (lo + hi) >> 1;
+    // (m - lo is 1 or 2 <=> the interval holds 2..5 suffixes)
+    const bool p = SM_PAIR && sizeof(IdxT) == 8 && bsm == BS_INSERT && hi - lo - 2 < 4;
+    pl = p;
+    addr = ia(c.SA, p ? m - 1 : m);
+    st = S_IDX; op = O_BS_SA;
+  };
   // probe m decided: P' agrees with S_m on lc characters past cbase; ranout:
   // P' ran out (it is a prefix of S_m), else its next byte pb differs from
   // the text's tb (signed chars, like the reference)
@@ -790,7 +822,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     addr = reinterpret_cast<uint64_t>(c.T + (sp & PM) + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
-    need2 = SM_KNOB(pf, 1u) && lo < m;
+    need2 = SM_KNOB(pf, 1u) && lo < m && !pl;
     pfr = SM_KNOB(pf, 1u) && m + 1 < hi;
     pf = SM_KNOB(pf, 1u) != 0;
     st = S_CMP; op = O_BS;
@@ -884,11 +916,21 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
     uint64_t v3 = 0;
-    const uint64_t amask = st >= S_BYTE ? ~uint64_t(0) : ~uint64_t(15);
-    if (st >= st_ld) v = SM_LOAD16ST(addr & amask, st);
+    const uint64_t amask = st >= S_BYTE || (st == S_IDX && pl) ? ~uint64_t(0) : ~uint64_t(15);
+    // a text compare block that would cross a 64-byte line (two requests)
+    // starts up to tsh bytes earlier instead, to end at the line's end: the
+    // bytes before the compare position are ones the suffix is known to share
+    // with the read (the interval's depth and the agreed lc), so they agree
+    uint32_t tsh = 0;
+    if (SM_TSH && st == S_CMP) {
+      const uint32_t o6 = uint32_t(addr) & 63u, known = (op == O_BS ? cbase : depth) + lc;
+      tsh = o6 > 48u ? o6 - 48u : 0u;
+      tsh = tsh < known ? tsh : known;
+    }
+    if (st >= st_ld) v = SM_LOAD16ST((addr - tsh) & amask, st);
     if (need2) {
       if (pf) v2 = SM_LOADPF16(addr2 & ~uint64_t(15));
-      else v2 = SM_LOAD16ST(addr2 & amask, st);
+      else v2 = SM_LOAD16ST((addr2 - tsh) & amask, st);
     }
     if (pfr) v3 = SM_LOADIDX(c.SA, (m + 1 + hi) >> 1);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
@@ -1076,13 +1118,15 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_IDX: {
         SM_REGION(5);
-        const uint64_t iv = idx_val<IdxT>(v, ao);
-        const uint64_t iv2 = idx_val<IdxT>(v2, uint32_t(addr2) & 15);
+        // (pl: the pair SA[e], SA[e + 1] from the exact address)
+        const uint64_t iv = pl ? (op == O_BS_SA ? hi64(v) : lo64(v)) : idx_val<IdxT>(v, ao);
+        const uint64_t iv2 = pl ? hi64(v) : idx_val<IdxT>(v2, uint32_t(addr2) & 15);
         if (op == O_SAPOS || op == O_SAPOS2) {
           pos = iv; have_pos = true;
           a = op == O_SAPOS ? A_TRAV : A_AFTER;
         } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
           sp = iv;
+          if (pl) ee = lo64(v);                       // its left child's word
           // 16 bytes first: a binary-search probe usually decides early
           a = A_BSP;
         } else if (op == O_ISAJ) {
@@ -1091,7 +1135,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           a = A_EXPAND;
         } else if (op == O_NS_SA2) {                  // suffix link, both ends
           addr = ia(c.ISA, (iv & PM) + 1); addr2 = ia(c.ISA, (iv2 & PM) + 1);
-          op = O_NS_ISA2;
+          op = O_NS_ISA2; need2 = true; pl = false;
         } else {                                      // O_NS_ISA2
           start = iv & PM; end = iv2 & PM; need2 = false;
           if (PK) isa_hints(iv, iv2);
@@ -1120,13 +1164,15 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         const bool tn2 = need2 && !pf;
         const uint32_t off = prefix + (op == O_BS ? cbase : depth) + lc;
         const uint32_t rem = op == O_BS ? cap - lc : L - off;
-        const uint32_t lim = rem < 16 ? rem : 16u;
-        uint32_t k = agree_block(v, 0, P, off, lim);
+        // (v starts tsh bytes before the compare position; those agree)
+        const uint32_t w1 = 16u - tsh;
+        const uint32_t lim = rem < w1 ? rem : w1;
+        uint32_t k = agree_block(v, 0, P, off - tsh, lim + tsh) - tsh;
         if (tn2 && k == lim && k < rem) {
           const uint32_t lim2 = rem - k < 16 ? rem - k : 16u;
           k += agree_block(v2, 0, P, off + k, lim2);
         }
-        const uint32_t got = tn2 ? (rem < 32 ? rem : 32u) : lim;   // bytes available
+        const uint32_t got = tn2 ? (rem < w1 + 16 ? rem : w1 + 16) : lim;   // bytes available
         const bool had_pf = pf;
         pf = false; pfr = false;
         lc += k;
@@ -1143,13 +1189,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           need2 = false;
           // P' < S_m iff P' ran out (prefix of S_m) or the first differing
           // byte of P' is smaller
-          const uint32_t tbyte = k < 16 ? byte_at(v, k) : byte_at(v2, k - 16);
+          const uint32_t tbyte = k < w1 ? byte_at(v, k + tsh) : byte_at(v2, k - w1);
           bs_decide(k == rem, k == rem ? 0u : uint32_t(P[off + k]), tbyte);
           const bool left = hi == m;
           if (had_pf && lo < hi) {                    // the next probe's SA element is here
             m = (lo + hi) >> 1;
-            SM_HOOK_PF(ia(c.SA, m));
-            sp = left ? idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15) : v3;
+            if (!(left && pl)) SM_HOOK_PF(ia(c.SA, m));   // (pl: loaded with m's word)
+            sp = left ? (pl ? ee : idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15)) : v3;
+            pl = false;
             lc = lL < lR ? lL : lR;
             a = A_BSP;
           } else {
@@ -1247,18 +1294,26 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
 
     // ---------------- decide ----------------
-    if (a == A_BSP) {                                 // probe m's SA word is in sp
+    // probe m's SA word is in sp (A_BSP).  A probe decided by its packed
+    // word's window that goes left to m - 1 while ee holds that child's word
+    // (pl) probes it at once instead of loading it: at most two probes here
+#pragma unroll 1
+    for (uint32_t t = 0; t < (SM_BSL2 ? 2u : 1u) && a == A_BSP; ++t) {
       a = bs_probe() ? A_BS : A_NONE;
+      if (SM_BSL2 && a == A_BS && pl && hi == m) {               // (then m - 1 = (lo + hi) / 2)
+        --m; sp = ee; pl = false;
+        lc = lL < lR ? lL : lR;
+        a = A_BSP;
+      }
     }
+    if (a == A_BSP) a = A_BS;                         // (not reached: ee is used once)
     if (a == A_BS) {                                  // next probe of a binary search
       SM_REGION(10);
       if (lo < hi) {
-        m = (lo + hi) >> 1;
         lc = lL < lR ? lL : lR;
-        addr = ia(c.SA, m);
-        st = S_IDX; op = O_BS_SA;
-        a = A_NONE;
+        a = A_BSL;
       } else {
+        pl = false;
         a = A_BS_DONE;
       }
     }
@@ -1540,10 +1595,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           SM_HOOK_BS(end - start + 1, depth);
           lo = start; hi = end + 1; lL = 0; lR = 0; best = 0;
           bsm = BS_INSERT; cbase = depth; cap = L - prefix - depth;
-          m = (lo + hi) >> 1;
           lc = 0;
-          addr = ia(c.SA, m);
-          st = S_IDX; op = O_BS_SA;
+          a = A_BSL;
         }
       }
     }
@@ -1556,7 +1609,9 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_NONE;
         if (start != end) {                          // non-singleton suffix link
           --depth;
-          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
+          // (adjacent ends, 8-byte elements: one pair load)
+          pl = SM_PAIR && sizeof(IdxT) == 8 && end == start + 1;
+          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = !pl;
           st = S_IDX; op = O_NS_SA2;
         } else if (!have_pos) {
           addr = ia(c.SA, start);
@@ -1578,6 +1633,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           uscan_start(pos & PM, depth);
         }
       }
+    }
+    if (a == A_BSL) {                                 // (one site for A_BS and A_TRAV)
+      bs_load();
+      a = A_NONE;
     }
     if (a == A_DONE) {
       SM_REGION(19);

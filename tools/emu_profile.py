@@ -70,6 +70,18 @@ def main():
     print("  probes/read %.1f: " % sum(pr.values()) + " ".join("%s %.2f" % kv for kv in pr.items()))
     print("  lines/read  %.1f: " % sum(ln.values()) + " ".join("%s %.2f" % kv for kv in ln.items()))
     print("  matches/read %.2f" % (sum(len(g) for g in got) / n))
+    print("  requests/read %.2f (speculative %.2f)" % (emu.requests[0] / n, emu.requests[1] / n))
+    import ctypes as C
+    rq = np.zeros((128, 4), np.uint64)
+    sm_emu.lib().sm_emu_req_by_state(rq.ctypes.data_as(C.c_void_p))
+    stn = ["EXIT", "NEW", "ALU", "COPY", "BM", "KT", "IDX", "BYTE", "CMP", "USCAN", "EXL", "EXR", "EXB"]
+    idxop = ["SAPOS", "SAPOS2", "BS_SA", "ISAJ", "NS_SA2", "NS_ISA2"]
+    print("  requests/read by state.op: all / re-probe (line among the lane's last 8) / speculative / crossing")
+    for k in range(128):
+        if rq[k, 0]:
+            st, op = k >> 3, k & 7
+            nm = stn[st] + ("." + (idxop[op] if st == 6 else ("EXT" if op == 0 else "BS")) if st in (6, 8) else "")
+            print("    %-14s %6.2f %6.2f %6.2f %6.2f" % ((nm,) + tuple(rq[k] / n)))
     import ctypes as C
     hs, hd = np.zeros(65, np.uint64), np.zeros(256, np.uint64)
     sm_emu.lib().sm_emu_bs_hist(hs.ctypes.data_as(C.c_void_p), hd.ctypes.data_as(C.c_void_p), 1)

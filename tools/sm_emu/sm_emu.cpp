@@ -20,10 +20,28 @@ static unsigned long long emu_ws[64];   // the kernel's STATS counters of the la
 // touches), speculative ones included ([1] counts those), the row DMA one per
 // line of its chunks
 static uint64_t emu_req[2];
+// requests by the issuing lane state and op (8 * st + op, set at each
+// iteration's first load): [0] all, [1] to a line among the lane's last 8
+// requested lines (a re-probe), [2] speculative, [3] the second line of a
+// block that crosses a 64-byte line
+static uint32_t emu_st;
+static uint64_t emu_rq[128][4];
+static uint64_t emu_ring[8];
+static uint32_t emu_ring_i;
 static void emu_reqs(uint64_t a, uint64_t n, bool spec) {
   const uint64_t k = ((a + n - 1) >> 6) - (a >> 6) + 1;
   emu_req[0] += k;
   if (spec) emu_req[1] += k;
+  for (uint64_t line = a >> 6; line <= (a + n - 1) >> 6; ++line) {
+    uint64_t *r = emu_rq[emu_st & 127];
+    ++r[0];
+    bool rep = false;
+    for (uint32_t q = 0; q < 8; ++q) rep = rep || emu_ring[q] == line;
+    r[1] += rep;
+    r[2] += spec;
+    r[3] += line != (a >> 6);
+    emu_ring[emu_ring_i++ & 7] = line;
+  }
 }
 // the 16 bytes at address a, exactly (the kernel aligns the blocks it wants
 // aligned); a block crossing a 64-byte line is two requests and touches two
@@ -71,7 +89,7 @@ static uint4 emu_load16st(uint64_t a, bool filter) {
   std::memcpy(&r, reinterpret_cast<const void *>(a), 16);
   return r;
 }
-#define SM_LOAD16ST(a, st) emu_load16st(a, (st) == 4u /* S_BM */)
+#define SM_LOAD16ST(a, st) (emu_st = 8u * (st) + ((st) == 6u || (st) == 8u ? op : 0u), emu_load16st(a, (st) == 4u /* S_BM */))
 // speculative SA prefetches: checked, not counted; the element the search
 // goes on with is counted (one 8- or 4-byte probe) by SM_HOOK_PF
 #define SM_LOADPF16(a) emu_load16(a, false)
@@ -301,6 +319,8 @@ static int run(const uint8_t *T, const void *SA, const void *ISA, const uint8_t 
   emu_bad = 0;
   for (int k = 0; k < 8; ++k) { emu_probes[k] = emu_lines[k] = 0; emu_last[k] = ~0ull; }
   emu_req[0] = emu_req[1] = 0;
+  std::memset(emu_rq, 0, sizeof(emu_rq));
+  std::memset(emu_ring, 0xFF, sizeof(emu_ring));
   // packed index words (common.hpp): the SA / ISA arrays given carry them
   if (packed && sizeof(IdxT) == 8) sm::k_mam_sm<IdxT, 1, true, true, sizeof(IdxT) == 8>(c);
   else sm::k_mam_sm<IdxT, 1, true, true, false>(c);
@@ -319,6 +339,7 @@ extern "C" void sm_emu_ws(uint64_t *out) {
 
 // device requests of the last sm_emu_map: [0] all, [1] speculative
 extern "C" void sm_emu_requests(uint64_t *out) { out[0] = emu_req[0]; out[1] = emu_req[1]; }
+extern "C" void sm_emu_req_by_state(uint64_t *out) { std::memcpy(out, emu_rq, sizeof(emu_rq)); }
 
 // (F) policy-3 probe outcomes since the last reset: [8 * j + bits]
 extern "C" void sm_emu_filter_hist(uint64_t *out, int reset) {
