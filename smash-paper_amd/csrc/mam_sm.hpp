@@ -43,19 +43,6 @@
 #ifndef SM_HOOK_BM
 #define SM_HOOK_BM(mode, a1, a2)   // host emulation: filter outcomes (policies 0-2)
 #endif
-// round-6 request cuts, each a compile-time switch for A/B builds (1: on):
-// SM_PAIR the pair loads of adjacent SA words, SM_BSL2 the second probe of a
-// window-decided binary-search step from the pair, SM_TSH line-clamped text
-// compare blocks
-#ifndef SM_PAIR
-#define SM_PAIR 1
-#endif
-#ifndef SM_BSL2
-#define SM_BSL2 1
-#endif
-#ifndef SM_TSH
-#define SM_TSH 1
-#endif
 #ifndef SM_HOOK_F
 #define SM_HOOK_F(j, bits)         // host emulation: filter outcomes (policy 3)
 #endif
@@ -365,7 +352,7 @@ enum : uint32_t { O_SAPOS, O_SAPOS2, O_BS_SA, O_ISAJ, O_NS_SA2, O_NS_ISA2 };
 enum : uint32_t { O_EXT = 0, O_BS };
 // ALU continuations, in the order the decide chain runs them
 enum : uint32_t { A_NONE = 0, A_BSP, A_BS, A_BS_DONE, A_XL_DONE, A_RUN_DONE, A_CHAIN_DONE,
-                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE, A_BSL };
+                  A_EXPAND, A_AFTER, A_TOP, A_TRAV, A_DONE, A_EMIT, A_EXS };
 // binary-search modes: 0 where P' sorts (traverse); 1 / 2 the left / right
 // end of a run of suffixes sharing `cap` characters (from `cbase`) with P
 enum : uint32_t { BS_INSERT = 0, BS_LEFT, BS_RIGHT };
@@ -468,6 +455,13 @@ struct Bad {   // the read's bad mask (registers; named, never an array)
     const uint64_t x = (uint64_t(word(q + 1)) << 32) | word(q);
     const uint32_t y = uint32_t(x >> s);
     return n >= 32 ? y : (y & ((1u << n) - 1));
+  }
+  // bits [a, a+64) as a 64-bit word (past the mask: zero)
+  __device__ __forceinline__ uint64_t bits64(uint32_t a) const {
+    const uint32_t q = a >> 5, s = a & 31;
+    const uint64_t x = (uint64_t(word(q + 1)) << 32) | word(q);
+    const uint64_t z = uint64_t(word(q + 2)) << 32;
+    return (x >> s) | (s ? z << (32 - s) : 0ull);
   }
   // highest set bit in [a, a+n), or -1
   __device__ __forceinline__ int32_t last(uint32_t a, uint32_t n) const {
@@ -749,14 +743,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // consumed, read by A_EXPAND in the same iteration): the left end stops at
   // start (- 1 with xl1), the right end at end (+ 1 with xr1)
   FlagRef xls{fl, 12}, xl1{fl, 13}, xrs{fl, 14}, xr1{fl, 15};
-  // pair loads (8-byte elements): one 16-byte load at the exact address of
-  // SA[e] brings SA[e] and SA[e + 1], where the search wants both -- the two
-  // ends of a 2-suffix interval's suffix link (O_NS_SA2), and a binary-search
-  // probe m whose left child is m - 1 (O_BS_SA: ee then holds SA[m - 1] until
-  // m moves, so the probe's compare needs no prefetch of that child).  Set
-  // while such a load is in flight (it is issued unaligned) and, for the
-  // binary search, while ee holds the left child
-  FlagRef pl{fl, 16};
+  FlagRef em{fl, 16};   // A_EMIT: the singleton at pos is a match to emit
   uint32_t dch = 0, j = 0, thresh = 0, xd = 0;
   uint32_t it = 0;
   uint64_t w_iters = 0, w_active = 0;
@@ -773,17 +760,6 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
   // blocks in one iteration (S_EXB), or the one side with room; false: none
   // left blocks are the 16 bytes ENDING at es (from 0 when es < 15), right
   // blocks start at ee + 1
-  // the SA word of binary-search probe m = (lo + hi) / 2; with 8-byte
-  // elements and a left child m - 1 (intervals of up to ~5 suffixes), as the
-  // pair SA[m - 1], SA[m] (pl)
-  auto bs_load = [&]() {
-    m = (lo + hi) >> 1;
-    // (m - lo is 1 or 2 <=> the interval holds 2..5 suffixes)
-    const bool p = SM_PAIR && sizeof(IdxT) == 8 && bsm == BS_INSERT && hi - lo - 2 < 4;
-    pl = p;
-    addr = ia(c.SA, p ? m - 1 : m);
-    st = S_IDX; op = O_BS_SA;
-  };
   // probe m decided: P' agrees with S_m on lc characters past cbase; ranout:
   // P' ran out (it is a prefix of S_m), else its next byte pb differs from
   // the text's tb (signed chars, like the reference)
@@ -822,7 +798,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     addr = reinterpret_cast<uint64_t>(c.T + (sp & PM) + cbase + lc);
     addr2 = ia(c.SA, (lo + m) >> 1);
-    need2 = SM_KNOB(pf, 1u) && lo < m && !pl;
+    need2 = SM_KNOB(pf, 1u) && lo < m;
     pfr = SM_KNOB(pf, 1u) && m + 1 < hi;
     pf = SM_KNOB(pf, 1u) != 0;
     st = S_CMP; op = O_BS;
@@ -916,21 +892,11 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
     uint4 v = make_uint4(0, 0, 0, 0), v2 = make_uint4(0, 0, 0, 0);
     uint64_t v3 = 0;
-    const uint64_t amask = st >= S_BYTE || (st == S_IDX && pl) ? ~uint64_t(0) : ~uint64_t(15);
-    // a text compare block that would cross a 64-byte line (two requests)
-    // starts up to tsh bytes earlier instead, to end at the line's end: the
-    // bytes before the compare position are ones the suffix is known to share
-    // with the read (the interval's depth and the agreed lc), so they agree
-    uint32_t tsh = 0;
-    if (SM_TSH && st == S_CMP) {
-      const uint32_t o6 = uint32_t(addr) & 63u, known = (op == O_BS ? cbase : depth) + lc;
-      tsh = o6 > 48u ? o6 - 48u : 0u;
-      tsh = tsh < known ? tsh : known;
-    }
-    if (st >= st_ld) v = SM_LOAD16ST((addr - tsh) & amask, st);
+    const uint64_t amask = st >= S_BYTE ? ~uint64_t(0) : ~uint64_t(15);
+    if (st >= st_ld) v = SM_LOAD16ST(addr & amask, st);
     if (need2) {
       if (pf) v2 = SM_LOADPF16(addr2 & ~uint64_t(15));
-      else v2 = SM_LOAD16ST((addr2 - tsh) & amask, st);
+      else v2 = SM_LOAD16ST(addr2 & amask, st);
     }
     if (pfr) v3 = SM_LOADIDX(c.SA, (m + 1 + hi) >> 1);
     bool fresh = false;   // assigned a read this iteration: its first chunk loads next
@@ -1118,27 +1084,26 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       }
       case S_IDX: {
         SM_REGION(5);
-        // (pl: the pair SA[e], SA[e + 1] from the exact address)
-        const uint64_t iv = pl ? (op == O_BS_SA ? hi64(v) : lo64(v)) : idx_val<IdxT>(v, ao);
-        const uint64_t iv2 = pl ? hi64(v) : idx_val<IdxT>(v2, uint32_t(addr2) & 15);
+        const uint64_t iv = idx_val<IdxT>(v, ao);
+        const uint64_t iv2 = idx_val<IdxT>(v2, uint32_t(addr2) & 15);
+        // (PK: the ISA words of an expand_link's ends -- one word for a
+        // suffix link's target (O_ISAJ), two for a non-singleton's; one site)
+        if (PK && (op == O_ISAJ || op == O_NS_ISA2)) isa_hints(iv, op == O_ISAJ ? iv : iv2);
         if (op == O_SAPOS || op == O_SAPOS2) {
           pos = iv; have_pos = true;
           a = op == O_SAPOS ? A_TRAV : A_AFTER;
         } else if (op == O_BS_SA) {                   // probe m: compare from lcp lc
           sp = iv;
-          if (pl) ee = lo64(v);                       // its left child's word
           // 16 bytes first: a binary-search probe usually decides early
           a = A_BSP;
         } else if (op == O_ISAJ) {
           start = end = iv & PM; have_pos = false;
-          if (PK) isa_hints(iv, iv);
           a = A_EXPAND;
         } else if (op == O_NS_SA2) {                  // suffix link, both ends
           addr = ia(c.ISA, (iv & PM) + 1); addr2 = ia(c.ISA, (iv2 & PM) + 1);
-          op = O_NS_ISA2; need2 = true; pl = false;
+          op = O_NS_ISA2;
         } else {                                      // O_NS_ISA2
           start = iv & PM; end = iv2 & PM; need2 = false;
-          if (PK) isa_hints(iv, iv2);
           ++prefix; have_pos = false;
           if (depth == 0) { start = 0; end = N - 1; a = A_TOP; }
           else a = A_EXPAND;
@@ -1148,13 +1113,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       case S_BYTE: {                                 // is_leftmaximal: T[pos-1]
         SM_REGION(6);
         SM_HOOK_BYTE(pos & PM);
-        if (P[prefix - 1] != uint8_t(byte_at(v, ao))) {
-          if (nem < gCap)
-            c.out[rd * gCap + nem] =
-                pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
-          ++nem;
-        }
-        uscan_start(pos & PM, depth);
+        em = P[prefix - 1] != uint8_t(byte_at(v, ao));
+        a = A_EMIT;
         break;
       }
       case S_CMP: {                                  // (A) extension / traverse probe
@@ -1164,15 +1124,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         const bool tn2 = need2 && !pf;
         const uint32_t off = prefix + (op == O_BS ? cbase : depth) + lc;
         const uint32_t rem = op == O_BS ? cap - lc : L - off;
-        // (v starts tsh bytes before the compare position; those agree)
-        const uint32_t w1 = 16u - tsh;
-        const uint32_t lim = rem < w1 ? rem : w1;
-        uint32_t k = agree_block(v, 0, P, off - tsh, lim + tsh) - tsh;
+        const uint32_t lim = rem < 16 ? rem : 16u;
+        uint32_t k = agree_block(v, 0, P, off, lim);
         if (tn2 && k == lim && k < rem) {
           const uint32_t lim2 = rem - k < 16 ? rem - k : 16u;
           k += agree_block(v2, 0, P, off + k, lim2);
         }
-        const uint32_t got = tn2 ? (rem < w1 + 16 ? rem : w1 + 16) : lim;   // bytes available
+        const uint32_t got = tn2 ? (rem < 32 ? rem : 32u) : lim;   // bytes available
         const bool had_pf = pf;
         pf = false; pfr = false;
         lc += k;
@@ -1189,14 +1147,13 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           need2 = false;
           // P' < S_m iff P' ran out (prefix of S_m) or the first differing
           // byte of P' is smaller
-          const uint32_t tbyte = k < w1 ? byte_at(v, k + tsh) : byte_at(v2, k - w1);
+          const uint32_t tbyte = k < 16 ? byte_at(v, k) : byte_at(v2, k - 16);
           bs_decide(k == rem, k == rem ? 0u : uint32_t(P[off + k]), tbyte);
           const bool left = hi == m;
           if (had_pf && lo < hi) {                    // the next probe's SA element is here
             m = (lo + hi) >> 1;
-            if (!(left && pl)) SM_HOOK_PF(ia(c.SA, m));   // (pl: loaded with m's word)
-            sp = left ? (pl ? ee : idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15)) : v3;
-            pl = false;
+            SM_HOOK_PF(ia(c.SA, m));
+            sp = left ? idx_val<IdxT>(v2, uint32_t(m * sizeof(IdxT)) & 15) : v3;
             lc = lL < lR ? lL : lR;
             a = A_BSP;
           } else {
@@ -1294,26 +1251,18 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     }
 
     // ---------------- decide ----------------
-    // probe m's SA word is in sp (A_BSP).  A probe decided by its packed
-    // word's window that goes left to m - 1 while ee holds that child's word
-    // (pl) probes it at once instead of loading it: at most two probes here
-#pragma unroll 1
-    for (uint32_t t = 0; t < (SM_BSL2 ? 2u : 1u) && a == A_BSP; ++t) {
+    if (a == A_BSP) {                                 // probe m's SA word is in sp
       a = bs_probe() ? A_BS : A_NONE;
-      if (SM_BSL2 && a == A_BS && pl && hi == m) {               // (then m - 1 = (lo + hi) / 2)
-        --m; sp = ee; pl = false;
-        lc = lL < lR ? lL : lR;
-        a = A_BSP;
-      }
     }
-    if (a == A_BSP) a = A_BS;                         // (not reached: ee is used once)
     if (a == A_BS) {                                  // next probe of a binary search
       SM_REGION(10);
       if (lo < hi) {
+        m = (lo + hi) >> 1;
         lc = lL < lR ? lL : lR;
-        a = A_BSL;
+        addr = ia(c.SA, m);
+        st = S_IDX; op = O_BS_SA;
+        a = A_NONE;
       } else {
-        pl = false;
         a = A_BS_DONE;
       }
     }
@@ -1335,8 +1284,8 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         SM_HOOK_RUN(true, 1, 0, 0);
         // packed: the SA word of rank bi holds L8[bi] and L8[bi + 1], the
         // run's first stop on either side when it ends at bi
-        const bool ls = PK && pk_below(bpos, 36, xd), rs = PK && pk_below(bpos, 43, xd);
-        a = ex_start(start, end, ls, rs) ? A_NONE : A_RUN_DONE;
+        xls = PK && pk_below(bpos, 36, xd); xrs = PK && pk_below(bpos, 43, xd);
+        a = A_EXS;
       }
     }
     if (a == A_EXPAND) {                              // expand_link (longSA.h:158-174)
@@ -1351,13 +1300,14 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
       // packed: the ISA words of start and end hold L8[start - 1 .. start]
       // and L8[end + 1 .. end + 2]: a run that ends within one more suffix
       // on a side needs no L8 probe there
-      bool ls = false, rs = false;
       if (PK) {
-        ls = xls; rs = xrs;
-        if (ls && xl1) es = start - 1;
-        if (rs && xr1) ee = end + 1;
+        if (xls && xl1) es = start - 1;
+        if (xrs && xr1) ee = end + 1;
       }
-      a = ex_start(0, N - 1, ls, rs) ? A_NONE : A_RUN_DONE;
+      a = A_EXS;
+    }
+    if (a == A_EXS) {                                 // (one site: the two runs above)
+      a = ex_start(xrun ? start : 0, xrun ? end : N - 1, xls, xrs) ? A_NONE : A_RUN_DONE;
     }
     if (a == A_XL_DONE) {                             // left end known: right side
       SM_REGION(12);
@@ -1405,6 +1355,16 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
     if (a == A_TOP) {
       SM_REGION(17);
       uint32_t kpos = ~0u;                            // a k-mer table probe's read window
+      // the read's bad bits [prefix, prefix + 64) as this A_TOP starts: the
+      // window tests below are shifts of them (prefix only grows here, by at
+      // most 16, and a test spans at most 36 bits past that); clean reads
+      // (almost all) skip the extraction
+      const uint32_t bp0 = prefix;
+      uint64_t bwin = 0;
+      if (!clean) bwin = bad.bits64(prefix);
+      auto badw = [&](uint32_t p, uint32_t n) {
+        return uint32_t(bwin >> (p - bp0)) & ((1u << n) - 1u);
+      };
       // (F) runs while the state is shallow, once per prefix (skip_f: this
       // prefix's window already passed the bitmap)
       bool proceed = skip_f || depth >= gMin;
@@ -1462,7 +1422,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
               const uint32_t W = gK + 4;             // read bases one entry needs
               const uint32_t u = uint32_t(__builtin_ctz(~kn & need));   // lowest unknown
               auto ok_at = [&](uint32_t jj) {
-                return prefix + jj + W <= L && (clean || bad.bits(prefix + jj, W) == 0);
+                return prefix + jj + W <= L && badw(prefix + jj, W) == 0;
               };
               // after an absent B-mer, bet on a run of them: offsets D..D+2;
               // else the entry whose three B-mers start at the lowest
@@ -1541,7 +1501,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         }
       }
       if (a == A_TOP && proceed) {                     // (C) from the root
-        if (depth == 0 && prefix + gK <= L && (clean || bad.bits(prefix, gK) == 0)) {
+        if (depth == 0 && prefix + gK <= L && badw(prefix, gK) == 0) {
           if (kx == prefix) {
             // the filter loaded this k-mer's entry already (policy 3)
             SM_REGION(25);
@@ -1595,8 +1555,10 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           SM_HOOK_BS(end - start + 1, depth);
           lo = start; hi = end + 1; lL = 0; lR = 0; best = 0;
           bsm = BS_INSERT; cbase = depth; cap = L - prefix - depth;
+          m = (lo + hi) >> 1;
           lc = 0;
-          a = A_BSL;
+          addr = ia(c.SA, m);
+          st = S_IDX; op = O_BS_SA;
         }
       }
     }
@@ -1609,9 +1571,7 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
         a = A_NONE;
         if (start != end) {                          // non-singleton suffix link
           --depth;
-          // (adjacent ends, 8-byte elements: one pair load)
-          pl = SM_PAIR && sizeof(IdxT) == 8 && end == start + 1;
-          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = !pl;
+          addr = ia(c.SA, start); addr2 = ia(c.SA, end); need2 = true;
           st = S_IDX; op = O_NS_SA2;
         } else if (!have_pos) {
           addr = ia(c.SA, start);
@@ -1622,20 +1582,21 @@ __global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
           st = S_BYTE;
         } else {
           // (PK: is_leftmaximal from the BWT character in pos's SA word)
-          if (depth >= gMin &&
-              (!PK || prefix == 0 || (pos & PM) == 0 ||
-               P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u))) {
-            if (nem < gCap)
-              c.out[rd * gCap + nem] =
-                  pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
-            ++nem;
-          }
-          uscan_start(pos & PM, depth);
+          em = depth >= gMin &&
+               (!PK || prefix == 0 || (pos & PM) == 0 ||
+                P[prefix - 1] != pk_char(uint32_t(pos >> kPkPosBits) & 3u));
+          a = A_EMIT;
         }
       }
     }
-    if (a == A_BSL) {                                 // (one site for A_BS and A_TRAV)
-      bs_load();
+    if (a == A_EMIT) {                                // (one site: S_BYTE and A_AFTER)
+      if (em) {
+        if (nem < gCap)
+          c.out[rd * gCap + nem] =
+              pack_match(pos & PM, prefix, depth) | (PK && gMh ? pk_map_hint(pos) : 0ull);
+        ++nem;
+      }
+      uscan_start(pos & PM, depth);
       a = A_NONE;
     }
     if (a == A_DONE) {
