@@ -668,8 +668,12 @@ inline void bad_table(const uint64_t in_text[4], uint32_t *lo, uint32_t *hi) {
 // scanner, bounded by [start, end]).  Same final (depth, interval) as the
 // reference's traverse; ~2.5 log2(interval) probes instead of 4 log2 per
 // character.
+// (occupancy experiments: the GEO kernels' minimum waves per SIMD)
+#ifndef SM_GEO_WPS
+#define SM_GEO_WPS 1
+#endif
 template <class IdxT, int BLOCK, bool CHECK, bool STATS, bool PK = false, int GEO = 0>
-__global__ __launch_bounds__(BLOCK) void k_mam_sm(const Ctx<IdxT> c) {
+__global__ __launch_bounds__(BLOCK, GEO ? SM_GEO_WPS : 1) void k_mam_sm(const Ctx<IdxT> c) {
   // GEO = L (150 or 100): the launch geometry of L-base reads on an index
   // with a 16-mer table (K 16, min_len 20, B 18, geo_row(L)-word rows), as
   // constants: the shifts, masks and row offsets built from them fold, and
