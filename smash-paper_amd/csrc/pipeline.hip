@@ -537,49 +537,108 @@ __device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
             cx(v[i + j], v[i + j + k]);
 }
 
+// One mate's matches -> its tagged, merged, to_print-ordered hits (H).  The
+// loads are issued slot-parallel in five rounds: the match words, the contig
+// directory cells, two contig starts per cell, the contig's start / sizes /
+// tag offset / small flag, and the two map.bin bytes of every alignment.  A
+// slot without a load to make (past n, invalid, or a map byte the search's
+// hint already gave) reads a fixed address instead (c.map: one hot line), so
+// no load waits on a branch and the rounds overlap their slots' latencies
+// (each slot was a chain of ~4 dependent loads, one slot after the other).
 template <int CAP>
 __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *__restrict__ sp,
                                           const uint64_t *m, uint32_t n, uint64_t (&H)[CAP],
                                           int32_t &err) {
   const uint32_t L = c.L;
   uint64_t A[CAP];
-  uint32_t R[CAP];   // 0x100 | the alignment's right map byte, from the match's hint; 0: load it
+  uint32_t R[CAP];   // payload through the sort: left byte | right byte << 8 | small << 16
   uint64_t w[CAP];
 #pragma unroll
   for (int k = 0; k < CAP; ++k) w[k] = uint32_t(k) < n ? m[k] : 0;
+  const uint64_t rmask = c.mhint ? kRefMask : 0xFFFFFFFFFFFFull;
+  // round 2: the directory cell of every slot (slots past n: ref 0, cell 0)
+  uint32_t c0[CAP], c1[CAP];
 #pragma unroll
   for (int k = 0; k < CAP; ++k) {
-    const uint64_t ref = w[k] & (c.mhint ? kRefMask : 0xFFFFFFFFFFFFull);
+    uint64_t cl = (w[k] & rmask) >> c.sp_shift;
+    cl = cl < c.sp_ncell ? cl : c.sp_ncell - 1;
+    c0[k] = c.sp_cell[cl];
+    c1[k] = c.sp_cell[cl + 1];
+  }
+  // round 3: upper_bound(startpos, ref) over [c0, c1): the range's first
+  // start decides it when the range holds at most one (almost every cell;
+  // the bisection otherwise, rare: several small contigs in one cell)
+  uint32_t lo[CAP];
+  {
+    uint64_t s0[CAP];
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) s0[k] = sp[c0[k] < c.n_seq ? c0[k] : c.n_seq - 1];
+#pragma unroll
+    for (int k = 0; k < CAP; ++k) {
+      const uint64_t ref = w[k] & rmask;
+      uint32_t l = c0[k], h = c1[k];
+      if (h - l <= 1) {
+        l += uint32_t(l < h && s0[k] <= ref);
+      } else {
+        while (l < h) {
+          const uint32_t mid = (l + h) >> 1;
+          if (sp[mid] <= ref) l = mid + 1; else h = mid;
+        }
+      }
+      lo[k] = uint32_t(k) < n ? l : 0u;
+    }
+  }
+  // round 4: the contig's start, its size (forward: the hint's edge rule) or
+  // its mate's (reverse strand: the position), its tag offset and small flag
+  uint64_t spi[CAP], sz[CAP];
+  uint32_t toff[CAP], sml = 0;
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    const uint32_t si = lo[k] ? lo[k] - 1 : 0;
+    spi[k] = sp[si];
+    sz[k] = c.sizes[(si & 1) ? si - 1 : si];
+    toff[k] = c.tag_off[si >> 1];
+    sml |= uint32_t(c.small[si >> 1] != 0) << k;
+  }
+  // the alignments (Alignment::resolve) and the addresses of their two map
+  // bytes: left at the base after the block's end, right at its first base
+  // (mappability_tag.cpp:98-101), the right one from the search's hint for a
+  // forward match (its own SA row's m, zeroed when m + b >= the contig size,
+  // longSA.cpp:666)
+  // (xl / xr: the bytes' map entries minus 2, halved; 0 = none to load)
+  uint32_t hint[CAP], xl[CAP], xr[CAP];
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    const uint64_t ref = w[k] & rmask;
     const uint32_t q = uint32_t((w[k] >> 48) & 0xFF), len = uint32_t(w[k] >> 56);
-    // upper_bound(startpos, ref) over the directory's cell range (global
-    // memory: no LDS, see d_stats); slots past n skip it (not ok below)
-    uint32_t lo = 0, hi = 0;
-    if (uint32_t(k) < n) {
-      uint64_t cl = ref >> c.sp_shift;
-      cl = cl < c.sp_ncell ? cl : c.sp_ncell - 1;
-      lo = c.sp_cell[cl];
-      hi = c.sp_cell[cl + 1];
-    }
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (sp[mid] <= ref) lo = mid + 1; else hi = mid;
-    }
-    const uint32_t si = lo ? lo - 1 : 0;
-    int64_t pos = int64_t(ref - q - sp[si]);
+    const uint32_t si = lo[k] ? lo[k] - 1 : 0;
+    int64_t pos = int64_t(ref - q - spi[k]);
     const uint32_t extra = L - len - q;
     const uint32_t rc = si & 1;
-    if (rc) pos = int64_t(c.sizes[si - 1] - uint64_t(pos)) - int64_t(L);
+    if (rc) pos = int64_t(sz[k] - uint64_t(pos)) - int64_t(L);
     const uint64_t prefix = rc ? extra : q;
-    const bool ok = uint32_t(k) < n && lo != 0 && pos >= 0;   // erase pos < 0
+    const bool ok = uint32_t(k) < n && lo[k] != 0 && pos >= 0;   // erase pos < 0
     A[k] = ok ? (uint64_t(rc) << 63) | (uint64_t(si >> 1) << 48) | (uint64_t(pos) << 16) |
                     (prefix << 8) | len
               : ~0ull;
-    // a forward match starts at forward base b = ref - startpos: its right
-    // byte is m of its own SA row, zeroed when m + b >= the contig's size
-    // (longSA.cpp:666), at map entry tag_off + b (the pipeline enables the
-    // hints only when tag_off is the index's own contig offsets)
     const uint32_t h = c.mhint && !rc ? uint32_t(w[k] >> 40) & 0xFFu : 0u;
-    R[k] = h ? 0x100u | (ref - sp[si] + h >= c.sizes[si] ? 0u : h) : 0u;
+    hint[k] = h ? 0x100u | (ref - spi[k] + h >= sz[k] ? 0u : h) : 0u;
+    // (mapb: an entry past the map reads 0)
+    const uint32_t abspos = toff[k] + uint32_t(pos) + 1;
+    const uint32_t bl = abspos + uint32_t(prefix) + len - 1, br = abspos + uint32_t(prefix) - 1;
+    xl[k] = ok && 2 + uint64_t(bl) * 2 < c.map_bytes ? bl + 1 : 0u;
+    xr[k] = ok && !hint[k] && 2 + uint64_t(br) * 2 + 1 < c.map_bytes ? br + 1 : 0u;
+  }
+  // round 5: every map byte at once (entry 2 + 2 b (+ 1), b = x - 1; x = 0
+  // reads the map's first byte, a hot line, and is dropped)
+#pragma unroll
+  for (int k = 0; k < CAP; ++k) {
+    const uint32_t lb = c.map[xl[k] ? uint64_t(xl[k]) * 2 : 0];
+    const uint32_t rb = c.map[xr[k] ? uint64_t(xr[k]) * 2 + 1 : 0];
+    const bool ok = A[k] != ~0ull;
+    const uint32_t lm = xl[k] ? lb : 0u;
+    const uint32_t rm = !ok ? 0u : (hint[k] & 0x100u) ? (hint[k] & 0xFFu) : xr[k] ? rb : 0u;
+    R[k] = lm | (rm << 8) | (((sml >> k) & 1u) << 16);
   }
   sort_net2(A, R);
   // merge runs on one diagonal (rc, tid, pos) into hits; tag every block
@@ -594,17 +653,14 @@ __device__ __forceinline__ void mate_fast(const PostCfg &c, const uint64_t *__re
     const uint32_t qpos = rc ? L - len - prefix : prefix;
     const bool start = i == 0 || (A[i - 1] >> 16) != (a >> 16);
     const bool endg = i + 1 == CAP || (A[i + 1 < CAP ? i + 1 : i] >> 16) != (a >> 16);
-    const uint32_t abspos = c.tag_off[tid] + pos + 1;
-    const uint32_t li = abspos + prefix + len - 1, ri = abspos + prefix - 1;
-    const unsigned lm = valid ? mapb(c, 2 + uint64_t(li) * 2) : 0u;
-    const unsigned rm = !valid ? 0u : (R[i] & 0x100u) ? (R[i] & 0xFFu) : mapb(c, 2 + uint64_t(ri) * 2 + 1);
+    const uint32_t lm = R[i] & 0xFFu, rm = (R[i] >> 8) & 0xFFu;
     const int32_t left = lm ? int32_t(lm) - 1 : 255, right = rm ? int32_t(rm) : 255;
     if (start) {
       g_prefix = prefix; g_qmin = qpos; g_l0 = left; g_r0 = right;
     } else {
       g_qmin = qpos < g_qmin ? qpos : g_qmin;
     }
-    if (valid && err == 0 && !c.small[tid]) {
+    if (valid && err == 0 && !((R[i] >> 16) & 1u)) {
       if (uint32_t(left) > len) err = SMASH_ERR_TAG_LEFT;
       else if (uint32_t(right) > len) err = SMASH_ERR_TAG_RIGHT;
     }
