@@ -269,11 +269,14 @@ int smash_pipeline_create(const smash_index *ix, const smash_pipeline_cfg *cfg,
                           smash_pipeline **out);
 void smash_pipeline_free(smash_pipeline *p);
 /* Grow the persistent pair-key set (smashMEM.py:217-228's `seen`) to hold
- * `keys` keys: a no-op when it does already; else only while it is empty
- * (after create / reset, before the first de-dup), SMASH_ERR_ARG when it
- * holds keys, SMASH_ERR_NOMEM when HBM cannot hold it.  Synchronous.  The
+ * `keys` keys: a no-op when it does already; else a larger set, into which
+ * the keys it holds move (their records copied, their slots rehashed), so it
+ * may be called between batches; SMASH_ERR_NOMEM when HBM cannot hold it
+ * (the old set is kept then).  Synchronous: it waits for the device.  The
  * multi-GPU driver sizes each owner's set from the run's pair count and the
- * owner skew of its first batch (dist.py). */
+ * owner skew of its first batch (dist.py); smash_count_fastq grows the
+ * single-GPU set as its batches arrive (a gzip input's pair count is not
+ * known before it is inflated). */
 int smash_pipeline_reserve_keys(smash_pipeline *p, uint64_t keys, void *stream);
 /* The keys the set takes for sure (a full set is SMASH_ERR_NOMEM in the
  * pipeline's statistics, never a silent cut). */

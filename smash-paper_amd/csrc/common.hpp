@@ -200,6 +200,9 @@ uint64_t search_rec_bytes(uint64_t n_reads, uint32_t max_len);
 // the search takes these reads as direct rows (no records): native stride,
 // 16-byte aligned (mam.hip; SMASH_DIRECT_ROWS=0 turns it off for A/B)
 bool search_direct(const uint8_t *seqs, uint64_t stride, uint32_t len);
+// grow the single-GPU key set before a batch of n_next pairs could overflow
+// it (pipeline.hip; synchronous when it grows)
+int ensure_keys(smash_pipeline *p, uint64_t n_next, hipStream_t s);
 // one pipeline batch whose search waits for in_ev (null: for all earlier
 // work on s) instead of for everything on s (pipeline.hip)
 int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,

@@ -785,6 +785,9 @@ extern "C" int smash_count_fastq(smash_pipeline *p, const char *const *r1, uint3
           rc = SMASH_ERR_HIP;
           break;
         }
+        // the key set grows (doubling) before a batch could overflow it: the
+        // pairs of a gzip input are not counted before it is inflated
+        if ((rc = smash::ensure_keys(p, s.n, cs)) != SMASH_OK) break;
         // the batch's search waits for its copy only (not for the previous
         // batch's post stage on cs): it can start under that batch's search
         if ((rc = smash::count_batch_ev(p, dbuf[d], s.n, d_counts, cs, copied[d])) != SMASH_OK)

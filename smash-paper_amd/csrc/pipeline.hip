@@ -127,6 +127,9 @@ struct smash_pipeline {
   uint64_t *d_arena = nullptr;   // canonical keys: [lo, nk, hit words...] per key
   uint64_t arena_cap = 0;        // words
   unsigned long long *d_arena_top = nullptr;
+  // pairs de-duplicated since the last reset (single GPU): a bound on the
+  // keys the set holds, on the host, for the file feed's growth (ensure_keys)
+  uint64_t keys_bound = 0;
   uint64_t epoch = 0;             // launches of the set's insert kernels (ref tags)
   uint32_t *d_posoff = nullptr;   // [max_pairs + 1]
   uint32_t *d_cnt = nullptr;      // [max_pairs]
@@ -2112,6 +2115,7 @@ namespace smash {
 int count_batch_ev(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_pairs,
                    uint64_t *d_counts, hipStream_t s, hipEvent_t in_ev) {
   p->defer_free = p->gate_post;
+  p->keys_bound += n_pairs;
   int rc = phase_map_impl(p, d_reads, n_pairs, s, in_ev);
   p->defer_free = false;
   if (rc) return rc;
@@ -2711,19 +2715,40 @@ extern "C" int smash_pipeline_peek(smash_pipeline *p, int32_t *h_nk, uint8_t *h_
   return SMASH_OK;
 }
 
+// Growth of a set that holds keys: every occupied slot {hash hi, ref} of the
+// old table moves to the first empty slot of its probe sequence in the new
+// one (the claim kernels' (hi ^ hi >> 31) & mask, linear).  Between batches
+// every ref is published (an arena offset, copied with the arena), so the
+// keys, their records and the first-wins decisions stay as they were; two
+// keys with one hi take two slots, as they did.
+__global__ void k_rehash(const uint64_t *__restrict__ old, uint64_t old_slots, uint64_t *nt,
+                         uint64_t mask) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < old_slots; i += stride) {
+    const uint64_t hi = old[2 * i];
+    if (!hi) continue;
+    uint64_t j = (hi ^ (hi >> 31)) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe, j = (j + 1) & mask) {
+      unsigned long long *sh = reinterpret_cast<unsigned long long *>(&nt[2 * j]);
+      if (atomicCAS(sh, 0ull, (unsigned long long)hi) == 0ull) {
+        nt[2 * j + 1] = old[2 * i + 1];
+        break;
+      }
+    }
+  }
+}
+
 extern "C" int smash_pipeline_reserve_keys(smash_pipeline *p, uint64_t keys, void *stream) {
   if (!p) return SMASH_ERR_ARG;
   uint64_t slots = 0, words = 0;
   key_set_geometry(keys, p->max_pairs, &slots, &words);
+  slots = std::max<uint64_t>(slots, p->table_mask + 1);
+  words = std::max<uint64_t>(words, p->arena_cap);
   if (slots <= p->table_mask + 1 && words <= p->arena_cap) return SMASH_OK;
   SMASH_HIP(hipSetDevice(p->device));
   SMASH_HIP(hipDeviceSynchronize());   // (no kernel may hold the old set)
   unsigned long long top = 0;
   SMASH_HIP(hipMemcpy(&top, p->d_arena_top, 8, hipMemcpyDeviceToHost));
-  if (top) {
-    set_error("smash_pipeline_reserve_keys: the key set holds keys (reserve before the first batch)");
-    return SMASH_ERR_ARG;
-  }
   uint64_t *t = nullptr, *a = nullptr;
   if (hipMalloc(reinterpret_cast<void **>(&t), 16 * slots) != hipSuccess ||
       hipMalloc(reinterpret_cast<void **>(&a), 8 * words) != hipSuccess) {
@@ -2732,17 +2757,34 @@ extern "C" int smash_pipeline_reserve_keys(smash_pipeline *p, uint64_t keys, voi
               " keys");
     return SMASH_ERR_NOMEM;
   }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  SMASH_HIP(hipMemsetAsync(t, 0, 16 * slots, s));
+  if (top) {   // the keys move: arena words as they are, slots rehashed
+    SMASH_HIP(hipMemcpyAsync(a, p->d_arena, 8 * std::min<uint64_t>(top, p->arena_cap),
+                             hipMemcpyDeviceToDevice, s));
+    const uint64_t old_slots = p->table_mask + 1;
+    k_rehash<<<grid_for(old_slots, 256, 1u << 16), 256, 0, s>>>(p->d_table, old_slots, t, slots - 1);
+    SMASH_HIP(hipGetLastError());
+  }
+  SMASH_HIP(hipStreamSynchronize(s));
   SMASH_HIP(hipFree(p->d_table));
   SMASH_HIP(hipFree(p->d_arena));
   p->d_table = t;
   p->d_arena = a;
   p->table_mask = slots - 1;
   p->arena_cap = words;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * slots, s));
-  SMASH_HIP(hipStreamSynchronize(s));
   return SMASH_OK;
 }
+
+namespace smash {
+// the single-GPU set must take the next n_next pairs' keys: grow it (at
+// least doubling) when the keys so far plus those could overflow it
+int ensure_keys(smash_pipeline *p, uint64_t n_next, hipStream_t s) {
+  const uint64_t need = p->keys_bound + n_next, cap = smash_pipeline_key_capacity(p);
+  if (need <= cap) return SMASH_OK;
+  return smash_pipeline_reserve_keys(p, std::max(need, 2 * cap), s);
+}
+}  // namespace smash
 
 extern "C" uint64_t smash_pipeline_key_capacity(const smash_pipeline *p) {
   // keys the set takes for sure: half its slots, and 16 words of arena each
@@ -2757,6 +2799,7 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   SMASH_HIP(hipSetDevice(p->device));
   SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * (p->table_mask + 1), s));
   SMASH_HIP(hipMemsetAsync(p->d_arena_top, 0, 8, s));
+  p->keys_bound = 0;
   SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * kStatWords, s));
   k_reset_prev<<<1, 1, 0, s>>>(p->d_prev);   // no host source: stays asynchronous
   SMASH_HIP(hipGetLastError());

@@ -296,23 +296,19 @@ def _is_gzip(path):
         return f.read(2) == b"\x1f\x8b"
 
 
-def fastq_pairs_bound(r1, r2, L):
-    """The key-set capacity of a file-fed run: at most the pairs of the lists.
-    Plain files: a record is at least 2 L + 6 bytes ("@x", seq, "+", qual),
-    a safe upper bound from the sizes.  With gzip files the pairs are counted
-    (the rank-local scan at world 1: each gzip file inflated once, in bounded
-    buffers), since no compression ratio bounds them; input that scan cannot
-    take falls back to 8x compression.  A set that is still too small fails
-    the run (SMASH_ERR_NOMEM), never cuts it."""
+def fastq_pairs_bound(r1, r2, L, batch=1 << 20):
+    """The starting key-set capacity of a file-fed run.  Plain files: a
+    record is at least 2 L + 6 bytes ("@x", seq, "+", qual), so the sizes
+    bound the pairs.  Gzip files are not inflated to count them (that would
+    inflate every member twice, once here and once in the feed): the set
+    starts at one batch and smash_count_fastq grows it, doubling, before a
+    batch could overflow it (smash_pipeline_reserve_keys moves the held keys).
+    A set HBM cannot grow fails the run (SMASH_ERR_NOMEM), never cuts it."""
     if any(_is_gzip(p) for p in r1 + r2):
-        try:
-            return max(S.FastqShards(r1, r2, 0, 1, lambda b: [b]).n, 1)
-        except S.SmashError:
-            pass
+        return max(int(batch), 1)
     n = 0
     for p in r1:
-        z = os.path.getsize(p)
-        n += (8 * z if _is_gzip(p) else z) // (2 * L + 6) + 1
+        n += os.path.getsize(p) // (2 * L + 6) + 1
     return max(n, 1)
 
 
@@ -333,7 +329,7 @@ def _count_files(args, bins):
     rows, starts = S.read_bins(bins)
     r1, r2 = args.reads1.split(), args.reads2.split()
     L = S.first_read_length(r1)
-    cap = args.dedup_capacity or fastq_pairs_bound(r1, r2, L)
+    cap = args.dedup_capacity or fastq_pairs_bound(r1, r2, L, args.batch)
     pipe = S.Pipeline(ix, cs, starts, L, args.batch, dedup_capacity=cap)
     counts = torch.zeros(len(starts), dtype=torch.int64, device=torch.device("cuda", args.device))
     pipe.reset()

@@ -623,7 +623,8 @@ class Pipeline:
         return int(lib().smash_pipeline_key_capacity(self.h))
 
     def reserve_keys(self, keys, stream=None):
-        """grow the (empty) key set to `keys` keys (smash_pipeline_reserve_keys)"""
+        """grow the key set to `keys` keys; held keys move into the larger set
+        (smash_pipeline_reserve_keys)"""
         check(lib().smash_pipeline_reserve_keys(self.h, int(keys), vp(_stream(stream))),
               "smash_pipeline_reserve_keys")
 

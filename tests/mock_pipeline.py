@@ -51,7 +51,7 @@ class OraclePhasePipeline:
         self.error = 0
 
     def reserve_keys(self, keys):
-        assert not self.seen, "smash_pipeline_reserve_keys: the set holds keys"
+        # (the library moves held keys into the larger set: smash_gpu.h)
         self.key_capacity = max(self.key_capacity, int(keys))
 
     def data_error(self, stream=None):

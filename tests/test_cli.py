@@ -395,3 +395,20 @@ def test_cli_memsam_fastq_input(tmp_path, tiny_fa):
     exp = sorted("\t".join(x for x in l.split("\t") if not x.startswith("XO:Z:"))
                  for l in gzip.open(gold("s150_mapout_tagged.txt.gz"), "rt").read().splitlines())
     assert got == exp
+
+
+def test_count_key_set_sizing_does_not_inflate_gzip(tmp_path, monkeypatch):
+    """smash_cli count sizes the key set without inflating gzip input (the
+    feed inflates each member once and grows the set itself): no FastqShards
+    scan, the batch size as the start; plain files: the size bound."""
+    import smashgpu as S
+
+    def refuse(*a, **k):
+        raise AssertionError("gzip input inflated to size the key set")
+    monkeypatch.setattr(S, "FastqShards", refuse)
+    monkeypatch.setattr(S, "FastqIndex", refuse)
+    g1, g2 = gold("s150_r1.fq.gz"), gold("s150_r2.fq.gz")
+    assert smash_cli.fastq_pairs_bound([g1], [g2], 150, 4096) == 4096
+    p1, p2 = _fq(tmp_path, "s150", 1), _fq(tmp_path, "s150", 2)
+    n = sum(1 for _ in open(p1)) // 4
+    assert smash_cli.fastq_pairs_bound([p1], [p2], 150, 4096) >= n

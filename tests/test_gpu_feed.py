@@ -203,3 +203,52 @@ def test_feed_gzip_lanes_refuse_disorder_and_bad_length(gix, setup, tmp_path):
     q = _lane_files(tmp_path, srt[:, :-1].copy(), [0, 300], ["gz", "gz"])
     with pytest.raises(S.SmashError, match="read length"):
         pipe.count_fastq(q[0], q[1], c, sort_names=False)
+
+
+@pytest.mark.parametrize("s", ["s100", "s150"])
+def test_feed_grows_key_set_from_one_batch(gix, setup, s):
+    """A gzip input's pair count is unknown before it is inflated, so smash_cli
+    starts the key set at one batch and smash_count_fastq grows it (doubling,
+    the held keys rehashed into the larger set) before a batch could overflow
+    it: counts, duplicates and statistics equal the batch path's with a set
+    sized for every pair, over many small batches (several growths)."""
+    cs, starts = setup
+    r1, r2 = [gold("%s_r1.fq.gz" % s)], [gold("%s_r2.fq.gz" % s)]
+    names, reads = S.read_fastq_pairs(r1, r2)
+    n, batch = len(names), 23
+    exp = _batch_path(gix, cs, starts, names, reads, batch)
+    pipe = S.Pipeline(gix, cs, starts, reads.shape[1], batch, dedup_capacity=1)
+    cap0 = pipe.key_capacity
+    assert cap0 < n
+    pipe.reset()
+    c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    pipe.count_fastq(r1, r2, c, sort_names=True, threads=3)
+    st = pipe.stats()
+    assert st.error == 0
+    got = (c.cpu().numpy().tolist(), (st.pairs, st.key_pairs, st.dupe_pairs, st.positions,
+                                      st.dups, st.kept))
+    assert got == exp
+    assert pipe.key_capacity >= n > cap0
+
+
+def test_reserve_keys_moves_held_keys(gix, setup):
+    """smash_pipeline_reserve_keys on a set that holds keys: a second pass of
+    the same pairs after the growth finds every keyed pair a duplicate (the
+    keys and their records moved), and the counts gain nothing."""
+    cs, starts = setup
+    names, reads = S.read_fastq_pairs([gold("s150_r1.fq.gz")], [gold("s150_r2.fq.gz")])
+    n = len(names)
+    d = torch.from_numpy(np.ascontiguousarray(reads)).cuda()
+    pipe = S.Pipeline(gix, cs, starts, reads.shape[1], n, dedup_capacity=n)
+    pipe.reset()
+    c = torch.zeros(len(starts), dtype=torch.int64, device="cuda")
+    pipe.count_batch(d, n, c)
+    st1 = pipe.stats()
+    first = c.cpu().numpy().copy()
+    pipe.reserve_keys(8 * n)
+    assert pipe.key_capacity >= 8 * n
+    pipe.count_batch(d, n, c)
+    st2 = pipe.stats()
+    assert st2.error == 0
+    assert st2.dupe_pairs - st1.dupe_pairs == st1.key_pairs
+    assert np.array_equal(c.cpu().numpy(), first)
