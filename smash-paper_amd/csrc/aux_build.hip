@@ -41,10 +41,17 @@ __global__ void k_kcode(const IdxT *__restrict__ SA, const uint8_t *__restrict__
     const uint64_t x = SA[r];
     uint32_t c = 0;
     bool ok = x + K <= N;
-    for (int k = 0; ok && k < K; ++k) {
-      const int v = acgt2(T[x + k]);
-      if (v < 0) ok = false;
-      c = (c << 2) | uint32_t(v);
+    // the k bytes as two 8-byte words (the text has 64 zero bytes of pad):
+    // two requests per rank instead of one byte load each
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(T);
+    const uint64_t q = x >> 3, sh = (x & 7) * 8;
+    const uint64_t a0 = w[q], a1 = w[q + 1], a2 = w[q + 2];
+    const uint64_t b0 = sh ? (a0 >> sh) | (a1 << (64 - sh)) : a0;
+    const uint64_t b1 = sh ? (a1 >> sh) | (a2 << (64 - sh)) : a1;
+    for (int k = 0; k < K; ++k) {
+      const int v = acgt2(uint8_t((k < 8 ? b0 : b1) >> (8 * (k & 7))));
+      ok = ok && v >= 0;
+      c = (c << 2) | uint32_t(v & 3);
     }
     code[r] = ok ? c : 0xFFFFFFFFu;
   }

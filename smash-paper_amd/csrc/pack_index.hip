@@ -39,11 +39,20 @@ __global__ void k_pack_sa(uint64_t *SA, const uint8_t *__restrict__ T,
       SA[r] = x;
       continue;
     }
-    const int bc = x ? base_code(T[x - 1]) : -1;
+    // T[x - 1] and T[x + K .. x + K + 7) from 8-byte words (one request per
+    // line instead of a byte load each, one after the other)
+    const uint64_t *tw = reinterpret_cast<const uint64_t *>(T);
+    auto bytes8 = [&](uint64_t a) {   // T[a .. a + 8); T has 64 zero bytes past N
+      const uint64_t q = a >> 3, sh = (a & 7) * 8;
+      const uint64_t lo = tw[q];
+      return sh ? (lo >> sh) | (tw[q + 1] << (64 - sh)) : lo;
+    };
+    const uint64_t prev = x ? bytes8(x - 1) : 0, fw = bytes8(x + K);
+    const int bc = x ? base_code(uint8_t(prev)) : -1;
     uint64_t tag = bc >= 0 ? uint64_t(bc) : 4u;
     uint64_t win = 0;
-    for (uint32_t i = 0; i < kPkWindow; ++i) {   // (T has 64 zero bytes past N)
-      const int c = x + K + i < N ? base_code(T[x + K + i]) : -1;
+    for (uint32_t i = 0; i < kPkWindow; ++i) {
+      const int c = x + K + i < N ? base_code(uint8_t(fw >> (8 * i))) : -1;
       if (c < 0) {
         tag = 5;
         win = 0;

@@ -245,6 +245,52 @@ __global__ void k_kasai(const uint8_t *__restrict__ T, uint64_t N,
   }
 }
 
+// The same carry in text order, written in text order (PLCP, Karkkainen et
+// al.'s permuted LCP): plcp[i] = lcp(suffix i, its SA predecessor).  Kasai's
+// lcp[ISA[i]] store is a random 4-byte write per position (a partial-line
+// read-modify-write at the memory); here every thread stores its chunk's
+// values consecutively and k_lcp_gather puts them in rank order with one
+// random 4-byte READ per rank.  The predecessor of position i + 1 is loaded
+// while position i is compared (its rank one position earlier still).
+template <class IdxT>
+__global__ void k_plcp(const uint8_t *__restrict__ T, uint64_t N, const IdxT *__restrict__ SA,
+                       const IdxT *__restrict__ ISA, uint32_t *plcp, uint64_t chunk) {
+  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t i0 = t * chunk;
+  if (i0 >= N) return;
+  const uint64_t i1 = i0 + chunk < N ? i0 + chunk : N;
+  uint64_t h = 0;
+  uint64_t r0 = ISA[i0];
+  uint64_t r1 = i0 + 1 < i1 ? uint64_t(ISA[i0 + 1]) : 0;
+  uint64_t j0 = r0 ? uint64_t(SA[r0 - 1]) : 0;
+  for (uint64_t i = i0; i < i1; ++i) {
+    // (first block of this compare, then the next positions' loads)
+    uint64_t x = r0 ? load8(T, i + h) ^ load8(T, j0 + h) : 1;
+    const uint64_t r2 = i + 2 < i1 ? uint64_t(ISA[i + 2]) : 0;
+    const uint64_t j1 = r1 ? uint64_t(SA[r1 - 1]) : 0;
+    if (r0 == 0) {
+      plcp[i] = 0;
+    } else {
+      while (!x) {
+        h += 8;
+        x = load8(T, i + h) ^ load8(T, j0 + h);
+      }
+      h += uint64_t(__builtin_ctzll(x) >> 3);
+      plcp[i] = h > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(h);
+    }
+    h = h ? h - 1 : 0;
+    r0 = r1; r1 = r2; j0 = j1;
+  }
+}
+
+template <class IdxT>
+__global__ void k_lcp_gather(const IdxT *__restrict__ SA, uint64_t N,
+                             const uint32_t *__restrict__ plcp, uint32_t *lcp) {
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < N; r += stride)
+    lcp[r] = r ? plcp[SA[r]] : 0u;
+}
+
 __global__ void k_lcp8(const uint32_t *__restrict__ lcp, uint64_t N, uint8_t *l8,
                        uint8_t *ovf_flag) {
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
@@ -470,9 +516,21 @@ uint32_t *build_lcp32_t(smash_index *ix, hipStream_t s) {
   chunk = std::min<uint64_t>(std::max<uint64_t>(chunk, 64), 65536);
   const uint64_t threads = (N + chunk - 1) / chunk;
   const double t0 = wall();
-  k_kasai<IdxT><<<unsigned((threads + 127) / 128), 128, 0, s>>>(
-      ix->d_text, N, static_cast<const IdxT *>(ix->d_sa),
-      static_cast<const IdxT *>(ix->d_isa), lcp, chunk);
+  const char *ke = getenv("SMASH_LCP_KASAI");   // 1: the rank-order Kasai form (A/B)
+  if (ke && ke[0] == '1') {
+    k_kasai<IdxT><<<unsigned((threads + 127) / 128), 128, 0, s>>>(
+        ix->d_text, N, static_cast<const IdxT *>(ix->d_sa),
+        static_cast<const IdxT *>(ix->d_isa), lcp, chunk);
+  } else {
+    uint32_t *plcp = dalloc<uint32_t>(N);
+    k_plcp<IdxT><<<unsigned((threads + 127) / 128), 128, 0, s>>>(
+        ix->d_text, N, static_cast<const IdxT *>(ix->d_sa),
+        static_cast<const IdxT *>(ix->d_isa), plcp, chunk);
+    k_lcp_gather<IdxT><<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
+        static_cast<const IdxT *>(ix->d_sa), N, plcp, lcp);
+    SMASH_HIPX(hipStreamSynchronize(s));
+    dfree(plcp);
+  }
   SMASH_HIPX(hipGetLastError());
   if (getenv("SMASH_VERBOSE")) {
     SMASH_HIPX(hipStreamSynchronize(s));
