@@ -245,6 +245,35 @@ __global__ void k_kasai(const uint8_t *__restrict__ T, uint64_t N,
   }
 }
 
+// The first offset >= h at which T[a ..] and T[b ..] differ (the bytes
+// before h are known equal).  A compare that runs past its first word goes
+// on 64 bytes at a time, eight independent word pairs per trip: a chunk
+// that starts inside a long repeat (an N run: millions of equal bytes)
+// compared one dependent 8-byte word per memory round trip, and those
+// chunks set the kernel's time.  (Blocks stay inside the text's 64-byte pad:
+// the compare ends at or before the last text byte, a unique '$'.)
+__device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, uint64_t b,
+                                    uint64_t h) {
+  uint64_t x = load8(T, a + h) ^ load8(T, b + h);
+  if (x) return h + uint64_t(__builtin_ctzll(x) >> 3);
+  h += 8;
+  const uint64_t hi = (a > b ? a : b);
+  while (hi + h + 72 <= N + 64) {
+    uint64_t xs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xs[k] = load8(T, a + h + 8 * k) ^ load8(T, b + h + 8 * k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (xs[k]) return h + 8 * k + uint64_t(__builtin_ctzll(xs[k]) >> 3);
+    h += 64;
+  }
+  for (;;) {
+    x = load8(T, a + h) ^ load8(T, b + h);
+    if (x) return h + uint64_t(__builtin_ctzll(x) >> 3);
+    h += 8;
+  }
+}
+
 // The same carry in text order, written in text order (PLCP, Karkkainen et
 // al.'s permuted LCP): plcp[i] = lcp(suffix i, its SA predecessor).  Kasai's
 // lcp[ISA[i]] store is a random 4-byte write per position (a partial-line
@@ -264,18 +293,13 @@ __global__ void k_plcp(const uint8_t *__restrict__ T, uint64_t N, const IdxT *__
   uint64_t r1 = i0 + 1 < i1 ? uint64_t(ISA[i0 + 1]) : 0;
   uint64_t j0 = r0 ? uint64_t(SA[r0 - 1]) : 0;
   for (uint64_t i = i0; i < i1; ++i) {
-    // (first block of this compare, then the next positions' loads)
-    uint64_t x = r0 ? load8(T, i + h) ^ load8(T, j0 + h) : 1;
+    // (the next positions' rank and predecessor load during this compare)
     const uint64_t r2 = i + 2 < i1 ? uint64_t(ISA[i + 2]) : 0;
     const uint64_t j1 = r1 ? uint64_t(SA[r1 - 1]) : 0;
     if (r0 == 0) {
       plcp[i] = 0;
     } else {
-      while (!x) {
-        h += 8;
-        x = load8(T, i + h) ^ load8(T, j0 + h);
-      }
-      h += uint64_t(__builtin_ctzll(x) >> 3);
+      h = lcp_from(T, N, i, j0, h);
       plcp[i] = h > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(h);
     }
     h = h ? h - 1 : 0;
