@@ -80,28 +80,49 @@ __global__ void k_kbounds(const uint32_t *__restrict__ code, uint64_t N, uint64_
 // of the three k-mers it contains: b0..b(k-1) (bit b(k)*4 + b(k+1)),
 // b1..b(k) (bit 16 + b0*4 + b(k+1)) and b2..b(k+1) (bit 32 + b0*4 + b1);
 // filter bit f lives at bit 40 + f % 24 of word f / 24 of the entry
-__device__ inline void kt_set(unsigned long long *kt, uint64_t w, uint32_t f) {
-  atomicOr(&kt[2 * w + (f >= 24 ? 1 : 0)], 1ull << (40 + (f >= 24 ? f - 24 : f)));
-}
 __global__ void k_kfilter(const uint8_t *__restrict__ T, uint64_t N, int K,
                           unsigned long long *kt) {
+  // one thread per k-mer position x: the bits its entry gets from the three
+  // (k+2)-mers that contain it (at x, x - 1, x - 2), OR-ed into the entry's
+  // two words with at most two atomics (was three atomics per (k+2)-mer, one
+  // in each of three entries); the bytes T[x - 2 .. x + K + 2) from 8-byte
+  // words (T has 64 zero bytes past N)
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  const uint64_t mask = (1ull << (2 * K)) - 1;
-  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x + K + 2 <= N;
-       x += stride) {
-    uint64_t c = 0;   // the (k+2)-mer, 2k + 4 bits
+  const uint64_t *tw = reinterpret_cast<const uint64_t *>(T);
+  for (uint64_t x = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; x + K <= N; x += stride) {
+    const uint64_t a = x >= 2 ? x - 2 : 0;   // first byte loaded
+    const uint64_t q = a >> 3, sh = (a & 7) * 8;
+    const uint64_t w0 = tw[q], w1 = tw[q + 1], w2 = tw[q + 2], w3 = tw[q + 3];
+    const uint64_t b0 = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+    const uint64_t b1 = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+    const uint64_t b2 = sh ? (w2 >> sh) | (w3 << (64 - sh)) : w2;
+    const uint32_t off = uint32_t(x - a);   // 2 (or 0 / 1 at the text's start)
+    // code of byte t of [x - 2, x + K + 2) (t = 0..K+3), -1 if not ACGT
+    auto code = [&](uint32_t t) -> int {
+      const uint32_t i = t + off - 2;     // index into the loaded bytes
+      const uint64_t wd = i < 8 ? b0 : i < 16 ? b1 : b2;
+      return acgt2(uint8_t(wd >> (8 * (i & 7))));
+    };
+    uint64_t c = 0;
     bool ok = true;
-    for (int k = 0; k < K + 2; ++k) {
-      const int v = acgt2(T[x + k]);
+    for (int k = 0; k < K; ++k) {
+      const int v = code(2 + k);
       ok = ok && v >= 0;
       c = (c << 2) | uint64_t(v & 3);
     }
     if (!ok) continue;
-    const uint32_t b0 = uint32_t(c >> (2 * K + 2)) & 3, b1 = uint32_t(c >> (2 * K)) & 3;
-    const uint32_t r1 = uint32_t(c >> 2) & 3, r2 = uint32_t(c) & 3;
-    kt_set(kt, c >> 4, r1 * 4 + r2);                       // w = b0..b(k-1)
-    kt_set(kt, (c >> 2) & mask, 16 + b0 * 4 + r2);          // w = b1..b(k)
-    kt_set(kt, c & mask, 32 + b0 * 4 + b1);                 // w = b2..b(k+1)
+    const int l2 = x >= 2 ? code(0) : -1, l1 = x >= 1 ? code(1) : -1;
+    const int r1 = x + K < N ? code(2 + K) : -1, r2 = x + K + 1 < N ? code(3 + K) : -1;
+    unsigned long long m0 = 0, m1 = 0;
+    auto put = [&](uint32_t f) {
+      if (f < 24) m0 |= 1ull << (40 + f);
+      else m1 |= 1ull << (40 + f - 24);
+    };
+    if (r1 >= 0 && r2 >= 0) put(uint32_t(r1 * 4 + r2));            // the (k+2)-mer at x
+    if (l1 >= 0 && r1 >= 0) put(16u + uint32_t(l1 * 4 + r1));      // at x - 1
+    if (l2 >= 0 && l1 >= 0) put(32u + uint32_t(l2 * 4 + l1));      // at x - 2
+    if (m0) atomicOr(&kt[2 * c], m0);
+    if (m1) atomicOr(&kt[2 * c + 1], m1);
   }
 }
 
