@@ -258,7 +258,9 @@ __device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, ui
   if (x) return h + uint64_t(__builtin_ctzll(x) >> 3);
   h += 8;
   const uint64_t hi = (a > b ? a : b);
-  while (hi + h + 72 <= N + 64) {
+  // 64 bytes per trip, then (a compare that ran past 1 KB: a long repeat)
+  // 256 bytes per trip, the word pairs OR-ed before the first is located
+  for (uint32_t trips = 0; hi + h + 72 <= N + 64; ++trips) {
     uint64_t xs[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) xs[k] = load8(T, a + h + 8 * k) ^ load8(T, b + h + 8 * k);
@@ -266,6 +268,14 @@ __device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, ui
     for (int k = 0; k < 8; ++k)
       if (xs[k]) return h + 8 * k + uint64_t(__builtin_ctzll(xs[k]) >> 3);
     h += 64;
+    if (trips < 16) continue;
+    while (hi + h + 264 <= N + 64) {
+      uint64_t any = 0;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) any |= load8(T, a + h + 8 * k) ^ load8(T, b + h + 8 * k);
+      if (any) break;   // (the 64-byte trips locate it)
+      h += 256;
+    }
   }
   for (;;) {
     x = load8(T, a + h) ^ load8(T, b + h);
