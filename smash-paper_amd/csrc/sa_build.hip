@@ -258,9 +258,7 @@ __device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, ui
   if (x) return h + uint64_t(__builtin_ctzll(x) >> 3);
   h += 8;
   const uint64_t hi = (a > b ? a : b);
-  // 64 bytes per trip, then (a compare that ran past 1 KB: a long repeat)
-  // 256 bytes per trip, the word pairs OR-ed before the first is located
-  for (uint32_t trips = 0; hi + h + 72 <= N + 64; ++trips) {
+  while (hi + h + 72 <= N + 64) {
     uint64_t xs[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) xs[k] = load8(T, a + h + 8 * k) ^ load8(T, b + h + 8 * k);
@@ -268,14 +266,6 @@ __device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, ui
     for (int k = 0; k < 8; ++k)
       if (xs[k]) return h + 8 * k + uint64_t(__builtin_ctzll(xs[k]) >> 3);
     h += 64;
-    if (trips < 16) continue;
-    while (hi + h + 264 <= N + 64) {
-      uint64_t any = 0;
-#pragma unroll
-      for (int k = 0; k < 32; ++k) any |= load8(T, a + h + 8 * k) ^ load8(T, b + h + 8 * k);
-      if (any) break;   // (the 64-byte trips locate it)
-      h += 256;
-    }
   }
   for (;;) {
     x = load8(T, a + h) ^ load8(T, b + h);
@@ -294,26 +284,46 @@ __device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, ui
 template <class IdxT>
 __global__ void k_plcp(const uint8_t *__restrict__ T, uint64_t N, const IdxT *__restrict__ SA,
                        const IdxT *__restrict__ ISA, uint32_t *plcp, uint64_t chunk) {
+  // chunk: a multiple of kPB.  A lane takes its chunk kPB positions at a
+  // time: their ranks in one 64/128-byte read, their predecessors' text
+  // positions (kPB independent random loads) at once, then the kPB compares
+  // (the carried h chains them), and the kPB values stored as one 64-byte
+  // line -- every line a lane touches is read or written whole (a lane's
+  // element-wise walk left 1 000 partial lines per CU in flight, more than
+  // the caches hold, and each store a partial-line write)
+  constexpr int kPB = 16;
   const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint64_t i0 = t * chunk;
   if (i0 >= N) return;
   const uint64_t i1 = i0 + chunk < N ? i0 + chunk : N;
   uint64_t h = 0;
-  uint64_t r0 = ISA[i0];
-  uint64_t r1 = i0 + 1 < i1 ? uint64_t(ISA[i0 + 1]) : 0;
-  uint64_t j0 = r0 ? uint64_t(SA[r0 - 1]) : 0;
-  for (uint64_t i = i0; i < i1; ++i) {
-    // (the next positions' rank and predecessor load during this compare)
-    const uint64_t r2 = i + 2 < i1 ? uint64_t(ISA[i + 2]) : 0;
-    const uint64_t j1 = r1 ? uint64_t(SA[r1 - 1]) : 0;
-    if (r0 == 0) {
-      plcp[i] = 0;
-    } else {
-      h = lcp_from(T, N, i, j0, h);
-      plcp[i] = h > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(h);
+  for (uint64_t ib = i0; ib < i1; ib += kPB) {
+    const uint32_t nb = i1 - ib < uint64_t(kPB) ? uint32_t(i1 - ib) : uint32_t(kPB);
+    uint64_t r[kPB], j[kPB];
+#pragma unroll
+    for (int k = 0; k < kPB; ++k) r[k] = uint32_t(k) < nb ? uint64_t(ISA[ib + k]) : 0;
+#pragma unroll
+    for (int k = 0; k < kPB; ++k) j[k] = r[k] ? uint64_t(SA[r[k] - 1]) : 0;
+    uint32_t v[kPB];
+#pragma unroll
+    for (int k = 0; k < kPB; ++k) {
+      v[k] = 0;
+      if (uint32_t(k) < nb) {
+        if (r[k]) {
+          h = lcp_from(T, N, ib + k, j[k], h);
+          v[k] = h > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(h);
+        }
+        h = h ? h - 1 : 0;
+      }
     }
-    h = h ? h - 1 : 0;
-    r0 = r1; r1 = r2; j0 = j1;
+    if (nb == uint32_t(kPB)) {
+      uint4 *o = reinterpret_cast<uint4 *>(plcp + ib);
+#pragma unroll
+      for (int k = 0; k < kPB / 4; ++k)
+        o[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    } else {
+      for (uint32_t k = 0; k < nb; ++k) plcp[ib + k] = v[k];
+    }
   }
 }
 
@@ -557,9 +567,11 @@ uint32_t *build_lcp32_t(smash_index *ix, hipStream_t s) {
         static_cast<const IdxT *>(ix->d_isa), lcp, chunk);
   } else {
     uint32_t *plcp = dalloc<uint32_t>(N);
-    k_plcp<IdxT><<<unsigned((threads + 127) / 128), 128, 0, s>>>(
+    const uint64_t pc = (chunk + 15) & ~uint64_t(15);   // (k_plcp: whole 16-position blocks)
+    const uint64_t pt = (N + pc - 1) / pc;
+    k_plcp<IdxT><<<unsigned((pt + 127) / 128), 128, 0, s>>>(
         ix->d_text, N, static_cast<const IdxT *>(ix->d_sa),
-        static_cast<const IdxT *>(ix->d_isa), plcp, chunk);
+        static_cast<const IdxT *>(ix->d_isa), plcp, pc);
     k_lcp_gather<IdxT><<<grid_for(N, 256, 1u << 20), 256, 0, s>>>(
         static_cast<const IdxT *>(ix->d_sa), N, plcp, lcp);
     SMASH_HIPX(hipStreamSynchronize(s));
