@@ -246,55 +246,32 @@ __global__ void k_kasai(const uint8_t *__restrict__ T, uint64_t N,
 }
 
 // The first offset >= h at which T[a ..] and T[b ..] differ (the bytes
-// before h are known equal), for a wave: every lane calls it (act: the lane
-// has a compare).
-// Each lane tries its own compare for 128 bytes; the compares still equal
-// then -- a lane inside a long repeat, an N run of millions of bytes -- are
-// finished one after the other by the whole wave, 512 bytes per trip (lane l
-// compares the 8 bytes at offset 8 l, the first differing lane by ballot).
-// A lane alone in a long compare held its 63 neighbours idle for as long,
-// and a wave's time was the sum of its lanes' long compares.
-__device__ inline uint64_t lcp_wave(const uint8_t *T, uint64_t N, uint64_t a, uint64_t b,
-                                    uint64_t h, bool act) {
-  const uint32_t lane = threadIdx.x & 63;
-  bool open = act;
-  if (act) {
-    const uint64_t hi = a > b ? a : b;
-    for (int t = 0; t < 16 && open; ++t) {
-      if (hi + h + 16 > N + 64) break;   // (near the text's end: the wave's loop)
-      const uint64_t x = load8(T, a + h) ^ load8(T, b + h);
-      if (x) {
-        h += uint64_t(__builtin_ctzll(x) >> 3);
-        open = false;
-      } else {
-        h += 8;
-      }
-    }
+// before h are known equal).  A compare that runs past its first word goes
+// on 64 bytes at a time, eight independent word pairs per trip: a chunk
+// that starts inside a long repeat (an N run: millions of equal bytes)
+// compared one dependent 8-byte word per memory round trip, and those
+// chunks set the kernel's time.  (Blocks stay inside the text's 64-byte pad:
+// the compare ends at or before the last text byte, a unique '$'.)
+__device__ inline uint64_t lcp_from(const uint8_t *T, uint64_t N, uint64_t a, uint64_t b,
+                                    uint64_t h) {
+  uint64_t x = load8(T, a + h) ^ load8(T, b + h);
+  if (x) return h + uint64_t(__builtin_ctzll(x) >> 3);
+  h += 8;
+  const uint64_t hi = (a > b ? a : b);
+  while (hi + h + 72 <= N + 64) {
+    uint64_t xs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xs[k] = load8(T, a + h + 8 * k) ^ load8(T, b + h + 8 * k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (xs[k]) return h + 8 * k + uint64_t(__builtin_ctzll(xs[k]) >> 3);
+    h += 64;
   }
-  uint64_t need = __ballot(open);
-  while (need) {
-    const int l = __builtin_ctzll(need);
-    need &= need - 1;
-    const uint64_t la = __shfl(a, l, 64), lb = __shfl(b, l, 64);
-    uint64_t lh = __shfl(h, l, 64);
-    const uint64_t hi = la > lb ? la : lb;
-    for (;;) {
-      const uint64_t off = lh + 8 * uint64_t(lane);
-      // (a lane past the text's end reports a difference: the compare ends
-      // at or before the last byte, a unique '$', so a lower lane holds it)
-      const uint64_t x = hi + off + 16 <= N + 64 ? load8(T, la + off) ^ load8(T, lb + off) : ~0ull;
-      const uint64_t m = __ballot(x != 0);
-      if (m) {
-        const int f = __builtin_ctzll(m);
-        const uint64_t xf = __shfl(x, f, 64);
-        lh += 8 * uint64_t(f) + uint64_t(__builtin_ctzll(xf) >> 3);
-        break;
-      }
-      lh += 512;
-    }
-    if (int(lane) == l) h = lh;
+  for (;;) {
+    x = load8(T, a + h) ^ load8(T, b + h);
+    if (x) return h + uint64_t(__builtin_ctzll(x) >> 3);
+    h += 8;
   }
-  return h;
 }
 
 // The same carry in text order, written in text order (PLCP, Karkkainen et
@@ -316,14 +293,12 @@ __global__ void k_plcp(const uint8_t *__restrict__ T, uint64_t N, const IdxT *__
   // the caches hold, and each store a partial-line write)
   constexpr int kPB = 16;
   const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  // (lanes past the text stay, with no positions: lcp_wave is wave-wide, so
-  // every lane runs the same trips -- the wave's longest chunk)
-  const uint64_t i0 = t * chunk < N ? t * chunk : N;
+  const uint64_t i0 = t * chunk;
+  if (i0 >= N) return;
   const uint64_t i1 = i0 + chunk < N ? i0 + chunk : N;
   uint64_t h = 0;
-  for (uint64_t q = 0; q < chunk; q += kPB) {
-    const uint64_t ib = i0 + q;
-    const uint32_t nb = ib >= i1 ? 0u : i1 - ib < uint64_t(kPB) ? uint32_t(i1 - ib) : uint32_t(kPB);
+  for (uint64_t ib = i0; ib < i1; ib += kPB) {
+    const uint32_t nb = i1 - ib < uint64_t(kPB) ? uint32_t(i1 - ib) : uint32_t(kPB);
     uint64_t r[kPB], j[kPB];
 #pragma unroll
     for (int k = 0; k < kPB; ++k) r[k] = uint32_t(k) < nb ? uint64_t(ISA[ib + k]) : 0;
@@ -332,12 +307,15 @@ __global__ void k_plcp(const uint8_t *__restrict__ T, uint64_t N, const IdxT *__
     uint32_t v[kPB];
 #pragma unroll
     for (int k = 0; k < kPB; ++k) {
-      const bool act = uint32_t(k) < nb && r[k] != 0;
-      h = lcp_wave(T, N, ib + k, j[k], h, act);   // (every lane: wave-wide)
-      v[k] = act ? (h > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(h)) : 0u;
-      if (uint32_t(k) < nb) h = h ? h - 1 : 0;
+      v[k] = 0;
+      if (uint32_t(k) < nb) {
+        if (r[k]) {
+          h = lcp_from(T, N, ib + k, j[k], h);
+          v[k] = h > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(h);
+        }
+        h = h ? h - 1 : 0;
+      }
     }
-    if (nb == 0) continue;
     if (nb == uint32_t(kPB)) {
       uint4 *o = reinterpret_cast<uint4 *>(plcp + ib);
 #pragma unroll
