@@ -50,4 +50,14 @@ timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$O/calib" -o pmc --output-forma
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/prof_c5" -o run --output-format csv \
     -- python3 "$R/bench.py" --config c5 --steps 5 --warmup 1 --no-cpu-baseline \
     > "$O/prof_c5.json" 2> "$O/prof_c5.log"
+if [ "$PART" = 4 ]; then   # + the C5 and MEM counter passes
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 200 rocprofv3 --pmc $C --kernel-include-regex 'k_upart|k_nsdir|k_mapscan|k_mapfix|k_tilebins' \
+        -d "$O/pmc_c5_$C" -o pmc --output-format csv -- python3 "$R/bench.py" --config c5 --steps 1 \
+        --warmup 0 --no-cpu-baseline > "$O/pmc_c5_$C.json" 2> "$O/pmc_c5_$C.log"
+  done
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex 'k_mem|k_job' -d "$O/pmc_mem" \
+      -o pmc --output-format csv -- python3 "$R/bench.py" --config c3mem --steps 1 --warmup 0 \
+      --no-cpu-baseline > "$O/pmc_mem.json" 2> "$O/pmc_mem.log"
+fi
 exit 0
