@@ -403,6 +403,16 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
                         "avg_kernel_ms": round(kms, 3)},
            "map_identical_to_index_build": same_map, "unique_kmers": n_uniq,
            "cpu_baseline": None}
+    pmc = os.path.join(ROOT, "profiles", "pmc_c5.json")
+    if os.path.exists(pmc) and world == 1:
+        try:
+            j = json.load(open(pmc))
+            res["roofline"]["traffic"] = j["c5_bytes_per_rep"]
+            res["roofline"]["traffic_vs_model"] = round(j["c5_bytes_per_rep"] /
+                                                        max(prep_bytes + scan_bytes, 1), 3)
+            res["roofline"]["traffic_source"] = os.path.relpath(pmc, ROOT)
+        except Exception:   # noqa: BLE001
+            pass
     log("C5: %d reps %.3f s -> %.3e bases/s; prepare %.2f ms + scan %.2f ms; unique %d-mers %d; "
         "map == build: %s" % (reps, el, value, prep_ms, scan_ms, k, n_uniq, same_map))
     if oix is not None and rank == 0 and world == 1 and not args.no_cpu_baseline:
