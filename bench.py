@@ -210,7 +210,7 @@ def search_lines(S, dix, oix, sample):
     return emu, emu_it, sum(v[1] for v in emu.counters.values())
 
 
-def c2_line(args, dix, contigs, dev, oix, mp, steps=20, warmup=3):
+def c2_line(args, dix, contigs, dev, oix, mp, steps=20, warmup=3, batch=None):
     """BASELINE configs[1] (C2) on the resident hg19 index: 1 M x 100 bp SMASH
     reads (500 k pairs, one batch) through the whole chain into
     sample_bins/100000; the GEO 100 search kernel (mam.hip run_sm).  Roofline
@@ -225,14 +225,17 @@ def c2_line(args, dix, contigs, dev, oix, mp, steps=20, warmup=3):
     cs = chrom_sizes_for(cfg, contigs)
     P, L = cfg["pairs"], cfg["read_len"]
     d_reads = S.to_rows(readgen.Generator(dix, contigs, L, seed=cfg["seed"] * 1000).generate(P), L)
-    pipe = S.Pipeline(dix, cs, starts, L, P, dedup_capacity=P + P // 8 + (1 << 20),
+    # (batch: the pairs per search launch; smaller batches let a launch's
+    # tail overlap the next one's start on the other search stream)
+    B = batch or int(os.environ.get("SMASH_C2_BATCH", "0")) or P
+    pipe = S.Pipeline(dix, cs, starts, L, B, dedup_capacity=P + P // 8 + (1 << 20),
                       read_stride=d_reads.shape[1])
     counts = torch.zeros(len(starts), dtype=torch.int64, device=dev)
 
     def step():
         counts.zero_()
         pipe.reset()
-        pipe.count_batches(d_reads, P, P, counts, resident=True)
+        pipe.count_batches(d_reads, P, B, counts, resident=True)
 
     for _ in range(warmup):
         step()
@@ -254,7 +257,7 @@ def c2_line(args, dix, contigs, dev, oix, mp, steps=20, warmup=3):
     res = {"metric": "reads/sec mapped+binned (hg19, 100 bp, C2)", "value": value,
            "unit": "reads/s", "ms_per_step": 1000.0 * el / steps, "steps": steps,
            "warmup": warmup, "workload": cfg["workload"], "pairs": P, "read_len": L,
-           "bins": int(len(starts)), "batch_pairs": P,
+           "bins": int(len(starts)), "batch_pairs": B,
            "search_kernel": "k_mam_sm GEO 100" if dix.info.pos_bits else "k_mam_sm",
            "deterministic_counts": bool(np.array_equal(dev_counts, ref)),
            "stats": st.as_dict(), "roofline": None, "cpu_baseline": None}
