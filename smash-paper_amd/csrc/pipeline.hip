@@ -914,23 +914,10 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
   SMASH_BESIDE_SEARCH();
   const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
   int32_t err = 0;
-  // (the next pair's nk and hash hi are loaded while this pair probes; a
-  // probe is one compare-and-swap of an empty slot to hi -- it claims an
-  // empty slot and reads an occupied one in one round trip, where a load
-  // first took two for the ~99% of keys that are new)
-  uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  int32_t m_cur = q < n ? nk[q] : -1;
-  uint64_t hi_cur = q < n ? hash[2 * q] : 0;
-  for (; q < n; q += stride) {
-    const uint64_t qn = q + stride;
-    const int32_t m_nx = qn < n ? nk[qn] : -1;
-    const uint64_t hi_nx = qn < n ? hash[2 * qn] : 0;
-    const int32_t m_me = m_cur;
-    const uint64_t hi = hi_cur;
-    m_cur = m_nx;
-    hi_cur = hi_nx;
-    if (m_me < 0) continue;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += stride) {
+    if (nk[q] < 0) continue;
     const KeyRef me = pair_key(hits, nk, hash, q);
+    const uint64_t hi = hash[2 * q];
     const unsigned long long mine = (epoch << kRefShift) | (q + 1);
     uint64_t res = kSlotNone;
     uint64_t i = (hi ^ (hi >> 31)) & mask;
@@ -938,11 +925,15 @@ __global__ void k_dedup_claim(const int32_t *__restrict__ nk, const uint64_t *__
     for (uint64_t probe = 0; probe <= mask;) {
       unsigned long long *sh = reinterpret_cast<unsigned long long *>(&table[2 * i]);
       unsigned long long *sr = sh + 1;
-      unsigned long long cur = atomicCAS(sh, 0ull, (unsigned long long)hi);
+      unsigned long long cur = __hip_atomic_load(sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (cur == 0) {
-        __hip_atomic_store(sr, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        res = i | (contest ? kSlotIns : 0ull);
-        break;
+        const unsigned long long prev = atomicCAS(sh, 0ull, (unsigned long long)hi);
+        if (prev == 0) {
+          __hip_atomic_store(sr, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          res = i | (contest ? kSlotIns : 0ull);
+          break;
+        }
+        cur = prev;
       }
       if (cur == hi) {
         const unsigned long long ref =
