@@ -990,57 +990,25 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
   unsigned long long kp = 0, dp = 0;
   bool full = false;
   const uint32_t lane = threadIdx.x & 63;
-  // Every group's loads are issued together, in three rounds (the pair's
-  // nk / slot / contest flag / hash / major count; its slot's ref when the
-  // claim was contested and its row's last hit word; that hit's contig
-  // offset), each from an address valid for every lane (an index clamped to
-  // the batch, a hot line when there is nothing to load): the form that
-  // loaded them one group and one field after the other waited for each
-  // load before issuing the next.
-  const uint64_t nl = n ? n - 1 : 0;
   for (uint64_t b0 = (uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u)) * kDecGroups;
        b0 < n; b0 += stride * kDecGroups) {
-    int32_t mv[kDecGroups];
-    uint64_t slv[kDecGroups], hsv[kDecGroups], lwv[kDecGroups];
-    uint32_t nmv[kDecGroups];
-    bool ctv[kDecGroups];
-#pragma unroll
-    for (uint32_t g = 0; g < kDecGroups; ++g) {
-      const uint64_t q = b0 + 64 * g + lane, qc = q < n ? q : nl;
-      const int32_t m = nk[qc];
-      mv[g] = q < n ? m : -1;
-      slv[g] = slot_of[qc];
-      ctv[g] = contest ? contest[qc] != 0 : false;   // (no claim flags: kSlotIns never set)
-      hsv[g] = hash[2 * qc + 1];
-      nmv[g] = nmajor[qc];
-    }
-    uint64_t refv[kDecGroups];
-#pragma unroll
-    for (uint32_t g = 0; g < kDecGroups; ++g) {
-      const uint64_t q = b0 + 64 * g + lane, qc = q < n ? q : nl;
-      const bool look = mv[g] >= 0 && slv[g] < kSlotNone && !((slv[g] & kSlotIns) && !ctv[g]);
-      refv[g] = __hip_atomic_load(reinterpret_cast<unsigned long long *>(
-                                      &table[look ? 2 * (slv[g] & ~kSlotIns) + 1 : 1]),
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lwv[g] = hits.row(qc, mv[g])[mv[g] > 0 ? mv[g] - 1 : 0];
-    }
-    int64_t cov[kDecGroups];
-#pragma unroll
-    for (uint32_t g = 0; g < kDecGroups; ++g) cov[g] = chrom_off[mv[g] > 0 ? uint32_t(lwv[g] >> 48) : 0u];
     bool wins[kDecGroups];
     uint32_t needs[kDecGroups], incls[kDecGroups], tots[kDecGroups];
     uint32_t sum = 0;
 #pragma unroll
     for (uint32_t g = 0; g < kDecGroups; ++g) {
       const uint64_t q = b0 + 64 * g + lane;
-      const int32_t m = mv[g];
+      const int32_t m = q < n ? nk[q] : -1;
       bool win = false;
       if (m >= 0) {
-        const uint64_t sl = slv[g];
-        if (sl < kSlotNone && (sl & kSlotIns) && !ctv[g]) {
+        const uint64_t sl = slot_of[q];
+        if (sl < kSlotNone && (sl & kSlotIns) && !contest[q]) {
           win = true;                       // the slot's only claimant this batch
         } else if (sl < kSlotNone) {
-          win = refv[g] == ((epoch << kRefShift) | (q + 1));
+          const unsigned long long ref = __hip_atomic_load(
+              reinterpret_cast<unsigned long long *>(&table[2 * (sl & ~kSlotIns) + 1]),
+              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          win = ref == ((epoch << kRefShift) | (q + 1));
         }
         ++kp;
         dp += win ? 0 : 1;
@@ -1057,40 +1025,36 @@ __global__ void k_dedup_decide(const int32_t *__restrict__ nk, const uint64_t *_
     for (uint32_t g = 0; g < kDecGroups; ++g) {
       const uint64_t q = b0 + 64 * g + lane;
       const bool in = q < n;
-      const int32_t m = mv[g];
+      const int32_t m = in ? nk[q] : -1;
       const bool win = wins[g];
       const uint32_t need = needs[g], incl = incls[g], total = tots[g];
       const uint64_t off = uint64_t(wbase) + incl - need;
       wbase += total;
       const bool ok = win && off + need <= arena_cap;
-      wave_fill_records(arena, off, incl, total, ok, win ? hsv[g] : 0ull,
+      wave_fill_records(arena, off, incl, total, ok, win ? hash[2 * q + 1] : 0ull,
                         win ? uint32_t(m) : 0u, hits.row(in ? q : 0, m), coop);
       if (win) {
         if (!ok) {
           full = true;   // the slot stays a claim: never matched (no kRefPub)
         } else {
           __hip_atomic_store(
-              reinterpret_cast<unsigned long long *>(&table[2 * (slv[g] & ~kSlotIns) + 1]),
+              reinterpret_cast<unsigned long long *>(&table[2 * (slot_of[q] & ~kSlotIns) + 1]),
               (unsigned long long)((epoch << kRefShift) | kRefPub | (off + 1)), __ATOMIC_RELAXED,
               __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       if (in) {
         keep[q] = win ? 1 : 0;
-        const uint32_t c = win ? nmv[g] : 0;   // k_count_last
+        const uint32_t c = win ? nmajor[q] : 0;   // k_count_last
         cnt[q] = c;
         int64_t last = -1;
         if (c) {
-          if (cov[g] >= 0) {                   // (the last hit is on a major contig)
-            last = int64_t(lwv[g] & 0xFFFFFFFFFFFFull);
-          } else {
-            const uint64_t *h = hits.row(q, m);
-            for (int32_t j = m - 2; j >= 0; --j)
-              if (chrom_off[uint32_t(h[j] >> 48)] >= 0) {
-                last = int64_t(h[j] & 0xFFFFFFFFFFFFull);
-                break;
-              }
-          }
+          const uint64_t *h = hits.row(q, m);
+          for (int32_t j = m - 1; j >= 0; --j)
+            if (chrom_off[uint32_t(h[j] >> 48)] >= 0) {
+              last = int64_t(h[j] & 0xFFFFFFFFFFFFull);
+              break;
+            }
         }
         lp[q] = last;
       }
