@@ -28,6 +28,14 @@
 // 22 B of HBM traffic per position, all of it streaming, against one random
 // 64-byte line per position for the gather.  Windows past 2^33 positions
 // (the u32 entry holds 24 position bits) fall back to the gather.
+//
+// Round 6: passes 1 and 2 were latency-bound (2.7 and 2.0 TB/s): a tile's
+// loads, its LDS placement and its run stores ran one after the other with
+// two blocks per CU.  Now each lane loads whole vectors (a pair of SA
+// elements + their LCP bytes, four E1 entries) and the next tile's loads
+// are issued before the current tile is placed; a pass-1 variant takes
+// tiles of 16 384 ranks in one block per CU (SMASH_UPART_NT=1024: runs twice
+// as long).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -41,11 +49,8 @@ constexpr int kUT = 512;                         // threads per block (passes 1,
 constexpr int kUPer = 16;                        // entries per thread per tile
 constexpr uint32_t kUTile = uint32_t(kUT) * kUPer;   // 8 192: 54 KB of LDS, 2 blocks per CU
 constexpr int kU3 = 1024;                        // threads per block (pass 3)
-constexpr int kS1 = 24;                          // level-1 bucket: 2^24 positions
-constexpr int kS2 = 16;                          // window: 2^16 positions
-constexpr uint32_t kNB1Max = 512;                // level-1 buckets (2^33 positions)
-constexpr uint32_t kNB2 = 1u << (kS1 - kS2);     // windows per bucket (256)
-constexpr uint32_t kChunk = 32;                  // level-1 buckets per pass-2/3 chunk
+constexpr uint32_t kNB1Max = 512;                // level-1 buckets
+constexpr uint32_t kNB2 = 256;                   // windows per level-1 bucket (S1 - S2 = 8)
 
 __host__ __device__ inline uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
@@ -65,17 +70,19 @@ __global__ void k_uniq_gather(const IdxT *__restrict__ ISA, uint64_t pm,
 // The block's tile sorted by bucket in LDS, then each bucket's run stored at
 // its claimed offset: dst(b) + claimed + rank in run.  nb <= kNB1Max.
 // ent[] / bk[] (bk = 0xFFFF: no entry) are the thread's entries.
+template <int NT>
 struct TileLds {
   uint32_t cnt[kNB1Max];
   uint32_t off[kNB1Max + 1];
   uint32_t gb[kNB1Max];
-  uint32_t ent[kUTile];
-  uint16_t bk[kUTile];
+  uint32_t ent[NT * kUPer];
+  uint16_t bk[NT * kUPer];
 };
 
 // exclusive scan of cnt[0..nb) into off[0..nb] (block-wide, nb <= 1024)
-__device__ __forceinline__ void block_excl_scan(TileLds &t, uint32_t nb) {
-  __shared__ uint32_t s_w[kUT / 64];
+template <int NT>
+__device__ __forceinline__ void block_excl_scan(TileLds<NT> &t, uint32_t nb) {
+  __shared__ uint32_t s_w[NT / 64];
   const uint32_t i = threadIdx.x, lane = i & 63, w = i >> 6;
   uint32_t x = i < nb ? t.cnt[i] : 0u, inc = x;
 #pragma unroll
@@ -93,121 +100,208 @@ __device__ __forceinline__ void block_excl_scan(TileLds &t, uint32_t nb) {
 }
 
 // rank-local part of one tile: claim each bucket's run, place the entries
-// in LDS by bucket, store the runs (dst: slice base of bucket b in elements)
-template <class Dst>
-__device__ __forceinline__ void tile_scatter(TileLds &t, uint32_t nb, const uint32_t (&ent)[kUPer],
-                                             const uint16_t (&bk)[kUPer], unsigned int *cur,
+// in LDS by bucket, store the runs (dst: slice base of bucket b in elements).
+// The runs' global claims are issued before the LDS placement, so their
+// round trip overlaps it.
+template <int NT, class Dst>
+__device__ __forceinline__ void tile_scatter(TileLds<NT> &t, uint32_t nb, const uint32_t (&ent)[kUPer],
+                                             uint32_t (&bk)[kUPer], unsigned int *cur,
                                              Dst dst, uint32_t *out) {
-  uint32_t slot[kUPer];
+  // bk[k] becomes bucket << 16 | rank in the bucket's run (0xFFFF: no entry)
 #pragma unroll
   for (int k = 0; k < kUPer; ++k)
-    slot[k] = bk[k] != 0xFFFF ? atomicAdd(&t.cnt[bk[k]], 1u) : 0u;
+    if (bk[k] != 0xFFFF) bk[k] = (bk[k] << 16) | atomicAdd(&t.cnt[bk[k]], 1u);
   __syncthreads();
   block_excl_scan(t, nb);
-  for (uint32_t b = threadIdx.x; b < nb; b += kUT)
+  for (uint32_t b = threadIdx.x; b < nb; b += NT)
     t.gb[b] = t.cnt[b] ? atomicAdd(&cur[b], t.cnt[b]) : 0u;
 #pragma unroll
   for (int k = 0; k < kUPer; ++k)
     if (bk[k] != 0xFFFF) {
-      const uint32_t j = t.off[bk[k]] + slot[k];
+      const uint32_t b = bk[k] >> 16;
+      const uint32_t j = t.off[b] + (bk[k] & 0xFFFF);
       t.ent[j] = ent[k];
-      t.bk[j] = bk[k];
+      t.bk[j] = uint16_t(b);
     }
   __syncthreads();
   const uint32_t total = t.off[nb];
-  for (uint32_t j = threadIdx.x; j < total; j += kUT) {
+  for (uint32_t j = threadIdx.x; j < total; j += NT) {
     const uint32_t b = t.bk[j];
     out[dst(b) + t.gb[b] + (j - t.off[b])] = t.ent[j];
   }
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += kUT) t.cnt[b] = 0;
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) t.cnt[b] = 0;
   __syncthreads();
 }
 
-// pass 1: ranks -> level-1 buckets of the window [lo, hi)
+// two consecutive SA elements as one load (8 or 16 bytes)
+template <class IdxT> struct Pair2;
+template <> struct Pair2<uint64_t> { using V = ulong2; };
+template <> struct Pair2<uint32_t> { using V = uint2; };
+
+// a thread's share of one pass-1 tile as loaded: rank pairs p = k * kUT +
+// thread (k < kUPer / 2), each instruction reads 64 consecutive pairs
 template <class IdxT>
-__global__ __launch_bounds__(kUT) void k_upart1(const IdxT *__restrict__ SA, uint64_t pm,
+struct P1Raw {
+  typename Pair2<IdxT>::V sa[kUPer / 2];
+  uint16_t l2[kUPer / 2];   // L8[2p], L8[2p + 1]
+  uint8_t l3[kUPer / 2];    // L8[2p + 2] (0 past the end)
+};
+
+template <class IdxT, int NT>
+__device__ __forceinline__ void p1_load(const IdxT *__restrict__ SA, const uint8_t *__restrict__ L8,
+                                        uint64_t N, uint64_t tile, P1Raw<IdxT> &w) {
+  const uint64_t r0 = tile * (NT * kUPer);
+  if (r0 + NT * kUPer < N) {   // (block-uniform) every rank and L8[r + 1] in range
+#pragma unroll
+    for (int k = 0; k < kUPer / 2; ++k) {
+      const uint64_t r = r0 + 2 * (uint64_t(k) * NT + threadIdx.x);
+      w.sa[k] = *reinterpret_cast<const typename Pair2<IdxT>::V *>(SA + r);
+      w.l2[k] = *reinterpret_cast<const uint16_t *>(L8 + r);
+      w.l3[k] = L8[r + 2];
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < kUPer / 2; ++k) {
+    const uint64_t r = r0 + 2 * (uint64_t(k) * NT + threadIdx.x);
+    w.sa[k].x = r < N ? SA[r] : IdxT(0);
+    w.sa[k].y = r + 1 < N ? SA[r + 1] : IdxT(0);
+    w.l2[k] = uint16_t((r < N ? L8[r] : 0) | ((r + 1 < N ? L8[r + 1] : 0) << 8));
+    w.l3[k] = r + 2 < N ? L8[r + 2] : uint8_t(0);
+  }
+}
+
+// pass 1: ranks -> level-1 buckets (2^S1 positions) of the window [lo, hi);
+// the next tile's loads are in flight while this one is placed
+template <class IdxT, int S1, int NT>
+__global__ __launch_bounds__(NT, 2048 / NT) void k_upart1(const IdxT *__restrict__ SA, uint64_t pm,
                                                 const uint8_t *__restrict__ L8, uint64_t N,
                                                 uint64_t lo, uint64_t hi, uint32_t nb,
                                                 unsigned int *cur, uint32_t *E1) {
-  __shared__ TileLds t;
-  for (uint32_t b = threadIdx.x; b < nb; b += kUT) t.cnt[b] = 0;
+  static_assert(S1 <= 24, "an entry holds 24 position bits and the 8-bit value");
+  constexpr uint32_t kTile = NT * kUPer;
+  __shared__ TileLds<NT> t;
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) t.cnt[b] = 0;
   __syncthreads();
-  const uint64_t ntiles = (N + kUTile - 1) / kUTile;
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    // entry k of the thread: rank tile * kUTile + k * kUT + thread (each load
-    // instruction reads 64 consecutive SA elements and LCP bytes)
-    const uint64_t r0 = tile * kUTile + threadIdx.x;
+  const uint64_t ntiles = (N + kTile - 1) / kTile;
+  uint64_t tile = blockIdx.x;
+  P1Raw<IdxT> w;
+  if (tile < ntiles) p1_load<IdxT, NT>(SA, L8, N, tile, w);
+  for (; tile < ntiles; tile += gridDim.x) {
     uint32_t ent[kUPer];
-    uint16_t bk[kUPer];
+    uint32_t bk[kUPer];
 #pragma unroll
-    for (int k = 0; k < kUPer; ++k) {
-      const uint64_t r = r0 + uint64_t(k) * kUT;
-      bk[k] = 0xFFFF;
-      ent[k] = 0;
-      if (r < N) {
-        const uint64_t x = uint64_t(SA[r]) & pm;
-        const uint8_t a = L8[r], c = r + 1 < N ? L8[r + 1] : uint8_t(0);
-        if (x >= lo && x < hi) {
-          bk[k] = uint16_t((x - lo) >> kS1);
-          ent[k] = uint32_t((x - lo) & ((1u << kS1) - 1)) | (uint32_t(a > c ? a : c) << 24);
-        }
+    for (int k = 0; k < kUPer / 2; ++k) {
+      const uint64_t r = tile * kTile + 2 * (uint64_t(k) * NT + threadIdx.x);
+      const uint32_t a = w.l2[k] & 0xFF, b = w.l2[k] >> 8, c = w.l3[k];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint64_t x = uint64_t(h ? w.sa[k].y : w.sa[k].x) & pm;
+        const uint32_t v = h ? (b > c ? b : c) : (a > b ? a : b);
+        const bool in = r + h < N && x >= lo && x < hi;
+        bk[2 * k + h] = in ? uint32_t((x - lo) >> S1) : 0xFFFFu;
+        ent[2 * k + h] = uint32_t((x - lo) & ((1u << S1) - 1)) | (v << 24);
       }
     }
-    tile_scatter(t, nb, ent, bk, cur, [](uint32_t b) { return uint64_t(b) << kS1; }, E1);
+    if (tile + gridDim.x < ntiles) p1_load<IdxT, NT>(SA, L8, N, tile + gridDim.x, w);
+    tile_scatter(t, nb, ent, bk, cur, [](uint32_t b) { return uint64_t(b) << S1; }, E1);
   }
 }
 
-// pass 2: level-1 buckets [c0, c0 + nc) -> their windows (E2 chunk-local)
-__global__ __launch_bounds__(kUT) void k_upart2(const uint32_t *__restrict__ E1, uint64_t n,
+// pass 2: level-1 buckets [c0, c0 + nc) -> their windows of 2^S2 positions
+// (E2 chunk-local); entries read 4 per lane per load, the next tile's in
+// flight while this one is placed
+template <int S1, int S2>
+__global__ __launch_bounds__(kUT, 4) void k_upart2(const uint32_t *__restrict__ E1, uint64_t n,
                                                 uint32_t c0, uint32_t nc, unsigned int *cur,
                                                 uint32_t *E2) {
-  __shared__ TileLds t;
-  const uint64_t tiles_per_bucket = (uint64_t(1) << kS1) / kUTile;   // 2048
-  const uint64_t ntiles = uint64_t(nc) * tiles_per_bucket;
+  static_assert(S1 - S2 == 8, "256 windows per level-1 bucket");
+  __shared__ TileLds<kUT> t;
+  const uint64_t tpb = (uint64_t(1) << S1) / kUTile;   // tiles per bucket
+  const uint64_t ntiles = uint64_t(nc) * tpb;
   for (uint32_t b = threadIdx.x; b < kNB2; b += kUT) t.cnt[b] = 0;
   __syncthreads();
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint32_t bl = uint32_t(tile / tiles_per_bucket);       // chunk-local bucket
-    const uint64_t b = c0 + bl;
-    const uint64_t bbeg = b << kS1;
-    const uint64_t bsize = umin64(uint64_t(1) << kS1, n - bbeg);
-    const uint64_t e0 = (tile % tiles_per_bucket) * kUTile + threadIdx.x;
-    if ((tile % tiles_per_bucket) * kUTile >= bsize) continue;   // (block-uniform)
-    uint32_t ent[kUPer];
-    uint16_t bk[kUPer];
+  // a tile is live when it starts inside its bucket (block-uniform)
+  auto live = [&](uint64_t tile, uint64_t &bbeg, uint64_t &bsize) {
+    const uint64_t b = c0 + tile / tpb;
+    bbeg = b << S1;
+    bsize = umin64(uint64_t(1) << S1, n - bbeg);
+    return (tile % tpb) * kUTile < bsize;
+  };
+  auto load = [&](uint64_t tile, uint4 (&v)[kUPer / 4]) {
+    uint64_t bbeg, bsize;
+    live(tile, bbeg, bsize);
+    const uint64_t e0 = (tile % tpb) * kUTile;
 #pragma unroll
-    for (int k = 0; k < kUPer; ++k) {   // (coalesced: entry k of the thread is e0 + k * kUT)
-      const uint64_t e = e0 + uint64_t(k) * kUT;
-      ent[k] = e < bsize ? E1[bbeg + e] : 0u;
-      bk[k] = e < bsize ? uint16_t((ent[k] >> kS2) & (kNB2 - 1)) : uint16_t(0xFFFF);
+    for (int k = 0; k < kUPer / 4; ++k) {
+      const uint64_t e = e0 + 4 * (uint64_t(k) * kUT + threadIdx.x);
+      if (e + 4 <= bsize) {
+        v[k] = *reinterpret_cast<const uint4 *>(E1 + bbeg + e);
+      } else {
+        v[k].x = e < bsize ? E1[bbeg + e] : 0u;
+        v[k].y = e + 1 < bsize ? E1[bbeg + e + 1] : 0u;
+        v[k].z = e + 2 < bsize ? E1[bbeg + e + 2] : 0u;
+        v[k].w = e + 3 < bsize ? E1[bbeg + e + 3] : 0u;
+      }
     }
+  };
+  auto next_live = [&](uint64_t tile) {
+    uint64_t bbeg, bsize;
+    while (tile < ntiles && !live(tile, bbeg, bsize)) tile += gridDim.x;
+    return tile;
+  };
+  uint4 v[kUPer / 4];
+  uint64_t tile = next_live(blockIdx.x);
+  if (tile < ntiles) load(tile, v);
+  while (tile < ntiles) {
+    uint64_t bbeg, bsize;
+    live(tile, bbeg, bsize);
+    const uint32_t bl = uint32_t(tile / tpb);   // chunk-local bucket
+    const uint64_t e0 = (tile % tpb) * kUTile;
+    uint32_t ent[kUPer];
+    uint32_t bk[kUPer];
+#pragma unroll
+    for (int k = 0; k < kUPer / 4; ++k) {
+      const uint64_t e = e0 + 4 * (uint64_t(k) * kUT + threadIdx.x);
+      const uint32_t q[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        ent[4 * k + h] = q[h];
+        bk[4 * k + h] = e + h < bsize ? (q[h] >> S2) & (kNB2 - 1) : 0xFFFFu;
+      }
+    }
+    const uint64_t nxt = next_live(tile + gridDim.x);
+    if (nxt < ntiles) load(nxt, v);
     tile_scatter(t, kNB2, ent, bk, cur + uint64_t(bl) * kNB2,
-                 [bl](uint32_t w) { return (uint64_t(bl) << kS1) + (uint64_t(w) << kS2); }, E2);
+                 [bl](uint32_t w) { return (uint64_t(bl) << S1) + (uint64_t(w) << S2); }, E2);
+    tile = nxt;
   }
 }
 
-// pass 3: one block per window of 2^16 positions: entries -> LDS bytes -> U
+// pass 3: one block per window of 2^S2 positions: entries -> LDS bytes -> U
+template <int S1, int S2>
 __global__ __launch_bounds__(kU3) void k_upart3(const uint32_t *__restrict__ E2, uint64_t n,
                                                 uint32_t c0, uint32_t nc, uint64_t lo,
                                                 uint8_t *U) {
-  __shared__ uint32_t s_u[(1u << kS2) / 4];
+  __shared__ uint32_t s_u[(1u << S2) / 4];
   uint8_t *sb = reinterpret_cast<uint8_t *>(s_u);
+  constexpr uint32_t kM = (1u << S2) - 1;
   const uint64_t nwin = uint64_t(nc) * kNB2;
   for (uint64_t w = blockIdx.x; w < nwin; w += gridDim.x) {
-    const uint64_t wbeg = (uint64_t(c0) << kS1) + (w << kS2);   // window-relative position
+    const uint64_t wbeg = (uint64_t(c0) << S1) + (w << S2);   // window-relative position
     if (wbeg >= n) continue;                                     // (block-uniform)
-    const uint32_t wsize = uint32_t(umin64(uint64_t(1) << kS2, n - wbeg));
-    const uint32_t *src = E2 + (w << kS2);
+    const uint32_t wsize = uint32_t(umin64(uint64_t(1) << S2, n - wbeg));
+    const uint32_t *src = E2 + (w << S2);
     for (uint32_t j = threadIdx.x * 4; j < wsize; j += kU3 * 4) {
       if (j + 4 <= wsize) {
         const uint4 v = *reinterpret_cast<const uint4 *>(src + j);
-        sb[v.x & 0xFFFF] = uint8_t(v.x >> 24);
-        sb[v.y & 0xFFFF] = uint8_t(v.y >> 24);
-        sb[v.z & 0xFFFF] = uint8_t(v.z >> 24);
-        sb[v.w & 0xFFFF] = uint8_t(v.w >> 24);
+        sb[v.x & kM] = uint8_t(v.x >> 24);
+        sb[v.y & kM] = uint8_t(v.y >> 24);
+        sb[v.z & kM] = uint8_t(v.z >> 24);
+        sb[v.w & kM] = uint8_t(v.w >> 24);
       } else {
-        for (uint32_t q = j; q < wsize; ++q) sb[src[q] & 0xFFFF] = uint8_t(src[q] >> 24);
+        for (uint32_t q = j; q < wsize; ++q) sb[src[q] & kM] = uint8_t(src[q] >> 24);
       }
     }
     __syncthreads();
@@ -223,26 +317,23 @@ __global__ __launch_bounds__(kU3) void k_upart3(const uint32_t *__restrict__ E2,
   }
 }
 
-template <class IdxT>
-void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
+template <class IdxT, int S1, int S2>
+void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   const uint64_t N = ix->N;
   const uint64_t n = hi - lo;
-  const uint32_t nb1 = uint32_t((n + (uint64_t(1) << kS1) - 1) >> kS1);
-  const char *e = getenv("SMASH_UNIQ_GATHER");   // 1: the gather form (A/B)
-  if (nb1 > kNB1Max || (e && e[0] == '1')) {
-    k_uniq_gather<IdxT><<<grid_for(n, 256, 1u << 20), 256, 0, s>>>(
-        static_cast<const IdxT *>(ix->d_isa), ix->pos_mask, ix->d_lcp8, N, lo, hi, ix->d_uniq);
-    SMASH_HIPX(hipGetLastError());
-    return;
-  }
+  const uint32_t nb1 = uint32_t((n + (uint64_t(1) << S1) - 1) >> S1);
   int cus = 0;
   SMASH_HIPX(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->device));
-  // scratch: E1 (4 B per window position), E2 (one chunk), the cursors --
-  // kept in the index between calls (release_uniq_scratch)
-  const uint32_t chunk = std::min(kChunk, nb1);
+  // scratch: E1 (4 B per window position), E2 (one chunk of level-1 buckets,
+  // SMASH_UPART_E2MB, default 2 GB), the cursors -- kept in the index between
+  // calls (release_uniq_scratch)
+  uint64_t e2mb = 2048;
+  if (const char *e = getenv("SMASH_UPART_E2MB")) e2mb = std::max<uint64_t>(1, strtoull(e, 0, 10));
+  const uint32_t kc = uint32_t(std::max<uint64_t>(1, (e2mb << 18) >> S1));   // buckets per chunk
+  const uint32_t chunk = std::min(kc, nb1);
   const uint64_t b_e1 = (4 * n + 255) & ~uint64_t(255);
-  const uint64_t b_e2 = 4 * (uint64_t(chunk) << kS1);
-  const uint64_t need = b_e1 + b_e2 + 4 * uint64_t(kChunk) * kNB2;
+  const uint64_t b_e2 = 4 * (uint64_t(chunk) << S1);
+  const uint64_t need = b_e1 + b_e2 + 4 * uint64_t(std::max(chunk * kNB2, nb1));
   if (ix->uscratch_bytes < need) {
     release_uniq_scratch(ix);
     ix->d_uscratch = dalloc<uint8_t>(need);
@@ -252,20 +343,46 @@ void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   uint32_t *E2 = reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1);
   unsigned int *cur = reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + b_e2);
   SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * nb1, s));
-  const uint64_t t1 = (N + kUTile - 1) / kUTile;
-  k_upart1<IdxT><<<unsigned(std::min<uint64_t>(t1, 2 * uint64_t(cus))), kUT, 0, s>>>(
-      static_cast<const IdxT *>(ix->d_sa), ix->pos_mask, ix->d_lcp8, N, lo, hi, nb1, cur, E1);
+  // SMASH_UPART_NT=1024: pass-1 tiles of 16 384 ranks (one block per CU,
+  // runs twice as long) instead of 8 192 (two blocks per CU)
+  const char *nt = getenv("SMASH_UPART_NT");
+  if (nt && atoi(nt) == 1024) {
+    const uint64_t t1 = (N + 1024 * kUPer - 1) / (1024 * kUPer);
+    k_upart1<IdxT, S1, 1024><<<unsigned(std::min<uint64_t>(t1, uint64_t(cus))), 1024, 0, s>>>(
+        static_cast<const IdxT *>(ix->d_sa), ix->pos_mask, ix->d_lcp8, N, lo, hi, nb1, cur, E1);
+  } else {
+    const uint64_t t1 = (N + kUTile - 1) / kUTile;
+    k_upart1<IdxT, S1, kUT><<<unsigned(std::min<uint64_t>(t1, 2 * uint64_t(cus))), kUT, 0, s>>>(
+        static_cast<const IdxT *>(ix->d_sa), ix->pos_mask, ix->d_lcp8, N, lo, hi, nb1, cur, E1);
+  }
   SMASH_HIPX(hipGetLastError());
-  for (uint32_t c0 = 0; c0 < nb1; c0 += kChunk) {
-    const uint32_t nc = std::min(kChunk, nb1 - c0);
+  const unsigned per_cu3 = (1u << S2) > 65536 ? 1u : 2u;   // LDS: one window per block
+  for (uint32_t c0 = 0; c0 < nb1; c0 += chunk) {
+    const uint32_t nc = std::min(chunk, nb1 - c0);
     SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * uint64_t(nc) * kNB2, s));
-    const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << kS1) / kUTile);
-    k_upart2<<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, s>>>(E1, n, c0, nc,
-                                                                               cur, E2);
-    k_upart3<<<unsigned(std::min<uint64_t>(uint64_t(nc) * kNB2, uint64_t(cus) * 2)), kU3, 0, s>>>(
-        E2, n, c0, nc, lo, ix->d_uniq);
+    const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << S1) / kUTile);
+    k_upart2<S1, S2><<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, s>>>(
+        E1, n, c0, nc, cur, E2);
+    k_upart3<S1, S2><<<unsigned(std::min<uint64_t>(uint64_t(nc) * kNB2, uint64_t(cus) * per_cu3)),
+                       kU3, 0, s>>>(E2, n, c0, nc, lo, ix->d_uniq);
     SMASH_HIPX(hipGetLastError());
   }
+}
+
+// (an entry is one u32: 24 position bits inside the level-1 bucket + the
+// 8-bit value, so level-1 buckets hold 2^24 positions)
+template <class IdxT>
+void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
+  const uint64_t n = hi - lo;
+  const char *g = getenv("SMASH_UNIQ_GATHER");   // 1: the gather form (A/B)
+  const uint32_t nb1 = uint32_t((n + (uint64_t(1) << 24) - 1) >> 24);
+  if (nb1 > kNB1Max || (g && g[0] == '1')) {
+    k_uniq_gather<IdxT><<<grid_for(n, 256, 1u << 20), 256, 0, s>>>(
+        static_cast<const IdxT *>(ix->d_isa), ix->pos_mask, ix->d_lcp8, ix->N, lo, hi, ix->d_uniq);
+    SMASH_HIPX(hipGetLastError());
+    return;
+  }
+  uniq_range_g<IdxT, 24, 16>(ix, lo, hi, s);
 }
 
 }  // namespace

@@ -127,18 +127,19 @@ def host_uniq(oix):
     return np.maximum(L8[isa], Lp[isa]).astype(np.uint8)
 
 
-@pytest.mark.parametrize("form", ["partition", "partition24_chunk1", "gather"])
+@pytest.mark.parametrize("form", ["partition", "partition_chunk1", "partition_nt1024", "gather"])
 def test_prepare_rebuilds_u_from_the_suffix_array(mid, form, monkeypatch):
     """smash_mappability_prepare (C5's preparation from SA + L8,
     csrc/uniq_build.hip): U poisoned on the device, rebuilt for the whole
     genome, equals the host's U from the oracle's ISA + LCP, and the scan over
     it equals the oracle's map.bin (longSA.cpp:612-690); SMASH_UNIQ_GATHER=1
-    runs the gather form for A/B; partition24_chunk1 the round-5 geometry
-    (2^24-position buckets, 2^16 windows) with one bucket per pass-2/3 chunk."""
+    runs the gather form for A/B; partition_chunk1 the partition with one
+    level-1 bucket per pass-2/3 chunk; partition_nt1024 pass 1 in tiles of
+    16 384 ranks."""
     oix, dix, off, starts = mid
     if form == "gather":
         monkeypatch.setenv("SMASH_UNIQ_GATHER", "1")
-    if form == "partition24_chunk1":
+    if form == "partition_chunk1":
         monkeypatch.setenv("SMASH_UPART_S1", "24")
         monkeypatch.setenv("SMASH_UPART_E2MB", "1")
     N = dix.info.N
