@@ -889,14 +889,24 @@ def main():
         # they need no device synchronisation
         sc = ShardedCounter(pipe, rank, world, dev, count_group=dist.new_group(backend="gloo"),
                             plan_pairs=P * world)
+        # the reads are resident and complete: the phase searches wait on no
+        # input event, so a look-ahead search (the next batch's, or the next
+        # run's first ones) starts once its set's post stage is done instead
+        # of behind everything queued for the current batch
+        pipe.reads_resident(True)
 
     resident = os.environ.get("SMASH_BENCH_RESIDENT", "1") != "0"   # (A/B)
     ahead2 = os.environ.get("SMASH_BENCH_AHEAD2", "1") != "0"       # (A/B, sharded step)
 
-    def step(i):
+    # SMASH_BENCH_CROSS=0 (A/B, sharded step): no look-ahead across runs
+    cross = os.environ.get("SMASH_BENCH_CROSS", "1") != "0"
+
+    def step(i, last=0):
         """one run over the rank's P pairs: a fresh key set / adjacent-dup
         state (a new smashMEM.py + varbin.py invocation), carried across
-        the batches"""
+        the batches.  i: the run's index among `last` runs issued back to
+        back (the sharded step searches run i + 1's first batches under run
+        i's last exchange when i + 1 < last)"""
         counts.zero_()
         if not sharded:
             pipe.reset()
@@ -906,11 +916,20 @@ def main():
             # under the previous run's post stage
             pipe.count_batches(d_reads, P, B, counts, resident=resident)
         else:
-            sc.reset()
+            # (cross: the previous run's last batch already issued this run's
+            # first searches -- back-to-back runs over the resident reads, as
+            # the single-GPU chain overlaps them; never across the warm-up /
+            # timed boundary, and the last timed run issues none)
+            sc.reset(keep_search=cross and i > 0)
             for b in range(nb):
                 b0, b1 = b * B, min(P, (b + 1) * B)
                 n0, n1 = b1, min(P, b1 + B)   # the next batch, searched under this one's exchange
                 m0, m1 = n1, min(P, n1 + B)   # and the one after, once this one's export is done
+                if b + 1 == nb and cross and i + 1 < last:
+                    n0, n1 = 0, min(P, B)          # the next run's first batches
+                    m0, m1 = n1, min(P, n1 + B)
+                    if m0 == 0 or nb == 1:
+                        m1 = m0                    # (one batch per run: no second)
                 if not ahead2:
                     m1 = m0
                 sc.step(d_reads[2 * b0:2 * b1], b1 - b0, b0 * world, counts,
@@ -920,7 +939,7 @@ def main():
             dist.all_reduce(counts)
 
     for i in range(args.warmup):
-        step(i)
+        step(i, args.warmup)
     torch.cuda.synchronize()
     ref_counts = counts.cpu().numpy().copy()
     st0 = pipe.stats()
@@ -932,7 +951,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -412,6 +412,19 @@ int smash_pipeline_profile_intervals(smash_pipeline *p, double *h_ms, uint64_t c
 /* Start a new run: clears the pair-key set, the carried adjacent-dup state
  * and the stats (a fresh smashMEM.py + varbin.py invocation). */
 int smash_pipeline_reset(smash_pipeline *p, void *stream);
+/* smash_pipeline_reset with flags.  SMASH_RESET_KEEP_SEARCH: look-ahead
+ * searches already issued (smash_phase_map_ahead / smash_phase_search_ahead)
+ * stay valid for the new run -- a search depends on the reads and the index
+ * only -- so a caller running back-to-back runs over resident reads can
+ * issue the next run's first searches under the last batch's exchange. */
+#define SMASH_RESET_KEEP_SEARCH 1u
+int smash_pipeline_reset_ex(smash_pipeline *p, uint32_t flags, void *stream);
+/* on != 0: every d_reads / d_next later given to the phase calls is resident
+ * in HBM and complete before the call (bench.py's sharded step), so their
+ * searches wait on nothing queued on the caller's stream -- only on the
+ * search set's previous post stage.  Default off: a search waits for the
+ * work already on `stream` (the reads' H2D copy of a file-fed batch). */
+int smash_pipeline_reads_resident(smash_pipeline *p, int on);
 
 /* The positions the last batch emitted, in order: pos0 (0-based, smashMEM.py
  * column 5) and absolute position (pos0 + chrom_sizes.txt col 3) -- the

@@ -113,6 +113,7 @@ struct smash_pipeline {
   uint64_t *d_tsum = nullptr;     // [tiles] the LDS-free scans' tile aggregates / prefixes
   int64_t *d_tlast = nullptr;
   bool cnt_ready = false;         // k_dedup_decide wrote d_cnt / d_lp for this batch
+  bool reads_resident = false;    // smash_pipeline_reads_resident: searches wait on no input event
   // multi-GPU export: per (owner, block) keys << 32 | words and their
   // exclusive scan (k_export_count / k_export_fill); the owner's claim slots
   uint64_t *d_bcnt = nullptr, *d_boff = nullptr;
@@ -1929,6 +1930,7 @@ static int phase_map_impl(smash_pipeline *p, const uint8_t *d_reads, uint64_t n_
   p->d_match = p->d_match_s[k];
   p->d_nmatch = p->d_nmatch_s[k];
   const bool have = p->searched[k] && p->pref_reads[k] == d_reads && p->pref_n[k] == n_pairs;
+  if (!in_ev && p->reads_resident) in_ev = p->ev_done;   // (complete since creation)
   if (!in_ev && (!have || (d_next && n_next))) {
     in_ev = p->ev_in;
     SMASH_HIP(hipEventRecord(in_ev, s));
@@ -1999,6 +2001,7 @@ extern "C" int smash_phase_search_ahead(smash_pipeline *p, const uint8_t *d_read
   }
   SMASH_HIP(hipSetDevice(p->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (p->reads_resident) return search_into(p, k, d_reads, n_pairs, p->ev_done);
   SMASH_HIP(hipEventRecord(p->ev_in, s));   // the reads are ready after the caller's work
   return search_into(p, k, d_reads, n_pairs, p->ev_in);
 }
@@ -2793,8 +2796,8 @@ extern "C" uint64_t smash_pipeline_key_capacity(const smash_pipeline *p) {
 
 extern "C" int smash_pipeline_map_hints(const smash_pipeline *p) { return p && p->mhint ? 1 : 0; }
 
-extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
-  if (!p) return SMASH_ERR_ARG;
+extern "C" int smash_pipeline_reset_ex(smash_pipeline *p, uint32_t flags, void *stream) {
+  if (!p || (flags & ~uint32_t(SMASH_RESET_KEEP_SEARCH))) return SMASH_ERR_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   SMASH_HIP(hipSetDevice(p->device));
   SMASH_HIP(hipMemsetAsync(p->d_table, 0, 16 * (p->table_mask + 1), s));
@@ -2803,13 +2806,26 @@ extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
   SMASH_HIP(hipMemsetAsync(p->d_stats, 0, 8 * kStatWords, s));
   k_reset_prev<<<1, 1, 0, s>>>(p->d_prev);   // no host source: stays asynchronous
   SMASH_HIP(hipGetLastError());
-  // a look-ahead search not consumed before the reset is dropped: the next
-  // phase_map searches its reads again (its set stays busy until ev_found)
-  for (int k = 0; k < 2; ++k) {
-    p->searched[k] = false;
-    p->pref_reads[k] = nullptr;
-    p->pref_n[k] = 0;
-  }
+  // a look-ahead search not consumed before the reset is dropped (the next
+  // phase_map searches its reads again; its set stays busy until ev_found)
+  // unless the caller keeps it: it read only the reads and the index, and
+  // its post stage, which writes the stats and the keys, runs in the new run
+  if (!(flags & SMASH_RESET_KEEP_SEARCH))
+    for (int k = 0; k < 2; ++k) {
+      p->searched[k] = false;
+      p->pref_reads[k] = nullptr;
+      p->pref_n[k] = 0;
+    }
+  return SMASH_OK;
+}
+
+extern "C" int smash_pipeline_reset(smash_pipeline *p, void *stream) {
+  return smash_pipeline_reset_ex(p, 0, stream);
+}
+
+extern "C" int smash_pipeline_reads_resident(smash_pipeline *p, int on) {
+  if (!p) return SMASH_ERR_ARG;
+  p->reads_resident = on != 0;
   return SMASH_OK;
 }
 

@@ -132,8 +132,13 @@ class ShardedCounter:
             self.timing[name] = self.timing.get(name, 0.0) + (t - self._t)
         self._t = t
 
-    def reset(self):
-        self.pipe.reset()
+    def reset(self, keep_search=False):
+        """a new run over this communicator (fresh key sets, adjacent-dup state
+        and stats).  keep_search: the look-ahead searches the previous run's
+        last step issued (its next_reads / next2_reads: this run's first
+        batches, resident and unmodified) stay valid, so back-to-back runs
+        search the next run's first batches under the last batch's exchange"""
+        self.pipe.reset(keep_search=keep_search)
         self.carried.fill_(-1)
         self.batch = 0
 

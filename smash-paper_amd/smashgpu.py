@@ -46,7 +46,7 @@ EXPORTS = [
     "smash_pipeline_create", "smash_pipeline_free", "smash_count_batch",
     "smash_phase_map", "smash_phase_export", "smash_dedup_owner",
     "smash_phase_import", "smash_phase_positions", "smash_phase_bin",
-    "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_peek",
+    "smash_pipeline_stats", "smash_pipeline_reset", "smash_pipeline_reset_ex", "smash_pipeline_reads_resident", "smash_pipeline_peek",
     "smash_pipeline_profile", "smash_pipeline_profile_read",
     "smash_pipeline_positions", "smash_bin_positions", "smash_mappability_scan",
     "smash_sam_records", "smash_sam_format", "smash_sam_free",
@@ -176,6 +176,8 @@ def lib():
     L.smash_phase_bin.argtypes = [vp, vp, vp, vp]
     L.smash_pipeline_stats.argtypes = [vp, C.POINTER(Stats)]
     L.smash_pipeline_reset.argtypes = [vp, vp]
+    L.smash_pipeline_reset_ex.argtypes = [vp, C.c_uint32, vp]
+    L.smash_pipeline_reads_resident.argtypes = [vp, C.c_int]
     L.smash_pipeline_peek.argtypes = [vp, i32p, u8p, u64p, u64p]
     L.smash_pipeline_profile.argtypes = [vp, C.c_int]
     L.smash_pipeline_profile_read.argtypes = [vp, C.POINTER(C.c_double), u64p, u64p]
@@ -608,8 +610,21 @@ class Pipeline:
         check(lib().smash_phase_bin(self.h, _ptr(d_prev), _ptr(d_counts),
                                     vp(_stream(stream))), "smash_phase_bin")
 
-    def reset(self, stream=None):
-        check(lib().smash_pipeline_reset(self.h, vp(_stream(stream))), "smash_pipeline_reset")
+    def reset(self, stream=None, keep_search=False):
+        """a new run (smash_pipeline_reset); keep_search: look-ahead searches
+        already issued stay valid for it (smash_pipeline_reset_ex,
+        SMASH_RESET_KEEP_SEARCH)"""
+        if keep_search:
+            check(lib().smash_pipeline_reset_ex(self.h, 1, vp(_stream(stream))),
+                  "smash_pipeline_reset_ex")
+        else:
+            check(lib().smash_pipeline_reset(self.h, vp(_stream(stream))), "smash_pipeline_reset")
+
+    def reads_resident(self, on=True):
+        """the reads later given to the phase calls are resident and complete:
+        their searches wait on no input event (smash_pipeline_reads_resident)"""
+        check(lib().smash_pipeline_reads_resident(self.h, 1 if on else 0),
+              "smash_pipeline_reads_resident")
 
     @property
     def map_hints(self):

@@ -45,7 +45,9 @@ class OraclePhasePipeline:
         self.bins = np.asarray(bin_starts, np.int64)
         self.reset()
 
-    def reset(self):
+    def reset(self, keep_search=False):
+        # (keep_search: no look-ahead searches to keep here -- phase_map
+        # searches synchronously)
         self.seen = set()
         self.total = self.dups = self.kept = 0
         self.error = 0

@@ -566,6 +566,24 @@ def test_c4_real_driver_threads_equal_oracle(c4_run, W, per_rank, bits, ahead2, 
     assert np.array_equal(total, orc[0])
 
 
+@pytest.mark.parametrize("W,per_rank,bits,runs", [(3, 20_000, 0, 2), (8, 10_000, 18, 3)])
+def test_c4_back_to_back_runs_cross_search(c4_run, W, per_rank, bits, runs, monkeypatch):
+    """bench.py's sharded loop over back-to-back runs: each run's last batch
+    issues the next run's first two searches (next_reads / next2_reads), and
+    the next run's reset keeps them (smash_pipeline_reset_ex,
+    SMASH_RESET_KEEP_SEARCH) -- every run's counts and the last run's stats
+    == the oracle's (a fresh smashMEM.py + varbin.py run each time)."""
+    from thread_ranks import run_resident
+    dix, cs, starts, d_reads, single, orc = c4_run
+    if bits:
+        monkeypatch.setenv("SMASH_KEY_HASH_BITS", str(bits))
+    total, st, per_run = run_resident(dix, d_reads, W, per_rank, starts, cs, runs=runs,
+                                      cross=True)
+    assert st == orc[1], (st, orc[1])
+    for k, c in enumerate(per_run):
+        assert np.array_equal(c, orc[0]), k
+
+
 def test_c4_real_driver_variants(c4_run, monkeypatch):
     """The W = 8 driver, and one pipeline over 24 batches (the key records
     written by one launch and compared by later ones), with each kernel form

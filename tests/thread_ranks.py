@@ -114,22 +114,31 @@ def make_pipes(ix, world, cs, starts, L, batch, capacity):
     return pipes, counts
 
 
-def run_resident(ix, d_reads, world, per_rank, starts, cs, ahead2=True, capacity=None):
+def run_resident(ix, d_reads, world, per_rank, starts, cs, ahead2=True, capacity=None, runs=1,
+                 cross=False):
     """bench.py's sharded step loop, one thread per rank: rank r's pairs are
     d_reads' global pairs [b W B + r B, + B) of batch b (the bench's layout:
     each rank holds its own P pairs, here dealt from one tensor), with the
     next batch searched under this one's exchange and, with ahead2, the one
-    after that right after the export."""
+    after that right after the export.  runs: that many runs over the same
+    pairs back to back, each from a reset (a fresh run); cross: as bench.py
+    does, a run's last batch issues the next run's first searches and the
+    next run's reset keeps them, and the searches wait on no input event
+    (smash_pipeline_reads_resident).  Returns the last run's summary (with
+    runs > 1: and every run's counts)."""
     n = d_reads.shape[0] // 2
     nb = n // (world * per_rank)
     assert nb * world * per_rank == n
     pipes, counts = make_pipes(ix, world, cs, starts, d_reads.shape[1], per_rank,
                                capacity or n)
     dev = d_reads.device
+    per_run = [[None] * world for _ in range(runs)]
+    if cross:   # (as bench.py's sharded step: resident reads, no input event)
+        for p in pipes:
+            p.reads_resident(True)
 
     def body(r, comm):
         sc = ShardedCounter(pipes[r], r, world, dev, comm=comm)
-        sc.reset()
 
         def mine(b):   # rank r's batch b, or None past the end
             if b >= nb:
@@ -137,14 +146,27 @@ def run_resident(ix, d_reads, world, per_rank, starts, cs, ahead2=True, capacity
             lo = b * world * per_rank + r * per_rank
             return d_reads[2 * lo:2 * (lo + per_rank)]
 
-        for b in range(nb):
-            nxt, nxt2 = mine(b + 1), mine(b + 2) if ahead2 else None
-            sc.step(mine(b), per_rank, b * world * per_rank, counts[r],
-                    nxt, per_rank if nxt is not None else 0,
-                    next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
+        for run in range(runs):
+            sc.reset(keep_search=cross and run > 0)
+            counts[r].zero_()
+            for b in range(nb):
+                more = cross and run + 1 < runs
+                nxt = mine(b + 1) if b + 1 < nb else (mine(0) if more else None)
+                if not ahead2:
+                    nxt2 = None
+                elif b + 2 < nb:
+                    nxt2 = mine(b + 2)
+                else:   # (the next run's batch after nxt, when that is its first)
+                    nxt2 = mine(b + 2 - nb) if more and 0 < b + 2 - nb < nb else None
+                sc.step(mine(b), per_rank, b * world * per_rank, counts[r],
+                        nxt, per_rank if nxt is not None else 0,
+                        next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
+            per_run[run][r] = counts[r].cpu().numpy().astype(np.uint64)
 
     _run_threads(world, body)
-    return _summary(pipes, counts)
+    if runs == 1:
+        return _summary(pipes, counts)
+    return _summary(pipes, counts) + ([sum(x) for x in per_run],)
 
 
 def run_files(ix, paths, world, batch, starts, cs, capacity, shards=True):
