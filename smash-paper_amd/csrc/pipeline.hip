@@ -1688,12 +1688,30 @@ extern "C" int smash_pipeline_create(const smash_index *ix,
       SMASH_HIPX(hipMemcpy(p->d_sp_cell, cell.data(), 4 * (p->sp_ncell + 1), hipMemcpyHostToDevice));
     }
     p->rec_bytes = search_rec_bytes(2 * P, p->read_len);
+    int search_prio = 0;
+    if (const char *e = getenv("SMASH_SEARCH_PRIO")) {
+      int least = 0, greatest = 0;
+      SMASH_HIPX(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      if (!strcmp(e, "high")) search_prio = greatest;
+      else if (!strcmp(e, "low")) search_prio = least;
+    }
     for (int k = 0; k < 2; ++k) {
       p->d_match_s[k] = dalloc<uint64_t>(2 * P * p->slots);
       p->d_nmatch_s[k] = dalloc<uint32_t>(2 * P);
       // (the records: only for dense input, allocated by the first search that needs them)
       p->d_work_s[k] = dalloc<unsigned long long>(1);
-      SMASH_HIPX(hipStreamCreateWithFlags(&p->xs[k], hipStreamNonBlocking));
+      // SMASH_SEARCH_PRIO=high / low: the search streams at that priority.
+      // HIP shares a process's hardware queues among its streams once it
+      // has GPU_MAX_HW_QUEUES (4) of them, one pool per priority; with RCCL
+      // and gloo streams in the process (the sharded step) a search stream
+      // landed on the caller's stream's queue, so the next search waited
+      // behind every exchange kernel queued before it.  A stream of its own
+      // priority gets a queue from another pool.
+      if (search_prio) {
+        SMASH_HIPX(hipStreamCreateWithPriority(&p->xs[k], hipStreamNonBlocking, search_prio));
+      } else {
+        SMASH_HIPX(hipStreamCreateWithFlags(&p->xs[k], hipStreamNonBlocking));
+      }
       SMASH_HIPX(hipEventCreateWithFlags(&p->ev_found[k], hipEventDisableTiming));
       SMASH_HIPX(hipEventCreateWithFlags(&p->ev_free[k], hipEventDisableTiming));
     }

@@ -33,9 +33,9 @@
 // loads, its LDS placement and its run stores ran one after the other with
 // two blocks per CU.  Now each lane loads whole vectors (a pair of SA
 // elements + their LCP bytes, four E1 entries) and the next tile's loads
-// are issued before the current tile is placed; a pass-1 variant takes
-// tiles of 16 384 ranks in one block per CU (SMASH_UPART_NT=1024: runs twice
-// as long).
+// are issued before the current tile is placed; the tiles are 16 384
+// entries in one 1024-thread block per CU (runs twice as long as with
+// 8 192; SMASH_UPART_NT / _NT2=512 for the two-block form).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -212,30 +212,31 @@ __global__ __launch_bounds__(NT, 2048 / NT) void k_upart1(const IdxT *__restrict
 // pass 2: level-1 buckets [c0, c0 + nc) -> their windows of 2^S2 positions
 // (E2 chunk-local); entries read 4 per lane per load, the next tile's in
 // flight while this one is placed
-template <int S1, int S2>
-__global__ __launch_bounds__(kUT, 4) void k_upart2(const uint32_t *__restrict__ E1, uint64_t n,
+template <int S1, int S2, int NT>
+__global__ __launch_bounds__(NT, 2048 / NT) void k_upart2(const uint32_t *__restrict__ E1, uint64_t n,
                                                 uint32_t c0, uint32_t nc, unsigned int *cur,
                                                 uint32_t *E2) {
   static_assert(S1 - S2 == 8, "256 windows per level-1 bucket");
-  __shared__ TileLds<kUT> t;
-  const uint64_t tpb = (uint64_t(1) << S1) / kUTile;   // tiles per bucket
+  constexpr uint32_t kTile = NT * kUPer;
+  __shared__ TileLds<NT> t;
+  const uint64_t tpb = (uint64_t(1) << S1) / kTile;   // tiles per bucket
   const uint64_t ntiles = uint64_t(nc) * tpb;
-  for (uint32_t b = threadIdx.x; b < kNB2; b += kUT) t.cnt[b] = 0;
+  for (uint32_t b = threadIdx.x; b < kNB2; b += NT) t.cnt[b] = 0;
   __syncthreads();
   // a tile is live when it starts inside its bucket (block-uniform)
   auto live = [&](uint64_t tile, uint64_t &bbeg, uint64_t &bsize) {
     const uint64_t b = c0 + tile / tpb;
     bbeg = b << S1;
     bsize = umin64(uint64_t(1) << S1, n - bbeg);
-    return (tile % tpb) * kUTile < bsize;
+    return (tile % tpb) * kTile < bsize;
   };
   auto load = [&](uint64_t tile, uint4 (&v)[kUPer / 4]) {
     uint64_t bbeg, bsize;
     live(tile, bbeg, bsize);
-    const uint64_t e0 = (tile % tpb) * kUTile;
+    const uint64_t e0 = (tile % tpb) * kTile;
 #pragma unroll
     for (int k = 0; k < kUPer / 4; ++k) {
-      const uint64_t e = e0 + 4 * (uint64_t(k) * kUT + threadIdx.x);
+      const uint64_t e = e0 + 4 * (uint64_t(k) * NT + threadIdx.x);
       if (e + 4 <= bsize) {
         v[k] = *reinterpret_cast<const uint4 *>(E1 + bbeg + e);
       } else {
@@ -258,12 +259,12 @@ __global__ __launch_bounds__(kUT, 4) void k_upart2(const uint32_t *__restrict__ 
     uint64_t bbeg, bsize;
     live(tile, bbeg, bsize);
     const uint32_t bl = uint32_t(tile / tpb);   // chunk-local bucket
-    const uint64_t e0 = (tile % tpb) * kUTile;
+    const uint64_t e0 = (tile % tpb) * kTile;
     uint32_t ent[kUPer];
     uint32_t bk[kUPer];
 #pragma unroll
     for (int k = 0; k < kUPer / 4; ++k) {
-      const uint64_t e = e0 + 4 * (uint64_t(k) * kUT + threadIdx.x);
+      const uint64_t e = e0 + 4 * (uint64_t(k) * NT + threadIdx.x);
       const uint32_t q[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
@@ -343,10 +344,13 @@ void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   uint32_t *E2 = reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1);
   unsigned int *cur = reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + b_e2);
   SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * nb1, s));
-  // SMASH_UPART_NT=1024: pass-1 tiles of 16 384 ranks (one block per CU,
-  // runs twice as long) instead of 8 192 (two blocks per CU)
+  // SMASH_UPART_NT=512: pass-1 tiles of 8 192 ranks (two blocks per CU)
+  // instead of 16 384 (one block per CU, runs twice as long: 21.5 vs 23.5 ms
+  // at hg19, profiles/r06/upart2); SMASH_UPART_NT2 likewise for pass 2
   const char *nt = getenv("SMASH_UPART_NT");
-  if (nt && atoi(nt) == 1024) {
+  const char *nt2e = getenv("SMASH_UPART_NT2");
+  const int nt2 = nt2e ? atoi(nt2e) : 1024;
+  if (!(nt && atoi(nt) == 512)) {
     const uint64_t t1 = (N + 1024 * kUPer - 1) / (1024 * kUPer);
     k_upart1<IdxT, S1, 1024><<<unsigned(std::min<uint64_t>(t1, uint64_t(cus))), 1024, 0, s>>>(
         static_cast<const IdxT *>(ix->d_sa), ix->pos_mask, ix->d_lcp8, N, lo, hi, nb1, cur, E1);
@@ -360,9 +364,15 @@ void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   for (uint32_t c0 = 0; c0 < nb1; c0 += chunk) {
     const uint32_t nc = std::min(chunk, nb1 - c0);
     SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * uint64_t(nc) * kNB2, s));
-    const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << S1) / kUTile);
-    k_upart2<S1, S2><<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, s>>>(
-        E1, n, c0, nc, cur, E2);
+    if (nt2 == 1024) {
+      const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << S1) / (1024 * kUPer));
+      k_upart2<S1, S2, 1024><<<unsigned(std::min<uint64_t>(t2, uint64_t(cus))), 1024, 0, s>>>(
+          E1, n, c0, nc, cur, E2);
+    } else {
+      const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << S1) / kUTile);
+      k_upart2<S1, S2, kUT><<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, s>>>(
+          E1, n, c0, nc, cur, E2);
+    }
     k_upart3<S1, S2><<<unsigned(std::min<uint64_t>(uint64_t(nc) * kNB2, uint64_t(cus) * per_cu3)),
                        kU3, 0, s>>>(E2, n, c0, nc, lo, ix->d_uniq);
     SMASH_HIPX(hipGetLastError());

@@ -127,21 +127,23 @@ def host_uniq(oix):
     return np.maximum(L8[isa], Lp[isa]).astype(np.uint8)
 
 
-@pytest.mark.parametrize("form", ["partition", "partition_chunk1", "partition_nt1024", "gather"])
+@pytest.mark.parametrize("form", ["partition", "partition_chunk1", "partition_nt512", "gather"])
 def test_prepare_rebuilds_u_from_the_suffix_array(mid, form, monkeypatch):
     """smash_mappability_prepare (C5's preparation from SA + L8,
     csrc/uniq_build.hip): U poisoned on the device, rebuilt for the whole
     genome, equals the host's U from the oracle's ISA + LCP, and the scan over
     it equals the oracle's map.bin (longSA.cpp:612-690); SMASH_UNIQ_GATHER=1
     runs the gather form for A/B; partition_chunk1 the partition with one
-    level-1 bucket per pass-2/3 chunk; partition_nt1024 pass 1 in tiles of
-    16 384 ranks."""
+    level-1 bucket per pass-2/3 chunk; partition_nt512 passes 1 and 2 in
+    tiles of 8 192 entries."""
     oix, dix, off, starts = mid
     if form == "gather":
         monkeypatch.setenv("SMASH_UNIQ_GATHER", "1")
     if form == "partition_chunk1":
-        monkeypatch.setenv("SMASH_UPART_S1", "24")
         monkeypatch.setenv("SMASH_UPART_E2MB", "1")
+    if form == "partition_nt512":
+        monkeypatch.setenv("SMASH_UPART_NT", "512")
+        monkeypatch.setenv("SMASH_UPART_NT2", "512")
     N = dix.info.N
     U = S.device_view(dix.info.d_uniq, N + 64, torch.uint8)
     want = host_uniq(oix)
