@@ -336,17 +336,23 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
     U = S.device_view(dix.info.d_uniq, N + 64, torch.uint8)
     U[lo:hi].fill_(0x55)
 
+    host_ms = []   # per timed rep: host time in the prepare call, in the scan call
+
     def step(i, timed):
         bc.zero_()
         cc.zero_()
         if timed:
             ev[3 * i].record()
+        h0 = time.perf_counter()
         S.mappability_prepare(dix, g0, g1)
+        h1 = time.perf_counter()
         if timed:
             ev[3 * i + 1].record()
         S.mappability_scan(dix, g0, g1, k, out, off, d_bins, len(starts), bc, cc)
+        h2 = time.perf_counter()
         if timed:
             ev[3 * i + 2].record()
+            host_ms.append((round(1e3 * (h1 - h0), 2), round(1e3 * (h2 - h1), 2)))
         if world > 1:
             dist.all_reduce(bc)
             dist.all_reduce(cc)
@@ -389,6 +395,9 @@ def c5_scan(args, dix, contigs, cfg_bins, world, rank, dev, dist, oix=None, reps
            "value": value, "unit": "bases/s", "ms_per_scan": 1000.0 * el / reps,
            "scaling": "strong", "bases": total, "k": k, "bins": int(len(starts)),
            "prepare_ms": round(prep_ms, 3), "scan_ms": round(scan_ms, 3),
+           "reps_ms": [[round(ev[3 * i].elapsed_time(ev[3 * i + 1]), 2),
+                        round(ev[3 * i + 1].elapsed_time(ev[3 * i + 2]), 2)] for i in range(reps)],
+           "reps_host_ms": host_ms,
            "window_positions": int(nw),
            "roofline": {"bound": "hbm", "kernel": "smash_mappability_prepare (k_upart1-3, "
                                                   "k_nsdir) + k_mapscan + k_mapfix",

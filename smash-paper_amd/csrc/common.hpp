@@ -142,6 +142,8 @@ struct smash_index {
   mutable uint64_t *d_nsdir = nullptr;   // first U < 255 per 4096 positions (mappability.hip)
   uint8_t *d_uscratch = nullptr; // U's partition passes (uniq_build.hip), kept between
   uint64_t uscratch_bytes = 0;   // smash_mappability_prepare calls until released
+  hipStream_t uaux = nullptr;    // the partition passes' second stream (chunks alternate)
+  hipEvent_t uev[2] = {nullptr, nullptr};   // its start (after pass 1) and end events
   uint64_t *d_kmer = nullptr;    // per k-mer: {lo,hi} + (k+2)-mer presence bits (kt_filter)
   uint32_t kmer_k = 0;
   uint64_t *d_bitmap = nullptr;  // (none since round 3: the presence bits live in d_kmer)

@@ -44,7 +44,8 @@ void free_index(smash_index *ix) {
   dfree(ix->d_text); dfree(ix->d_sa); dfree(ix->d_isa); dfree(ix->d_lcp8);
   dfree(ix->d_ovf); dfree(ix->d_map); dfree(ix->d_startpos); dfree(ix->d_sizes);
   dfree(ix->d_uniq); dfree(ix->d_kmer); dfree(ix->d_bitmap); dfree(ix->d_work); dfree(ix->d_rec);
-  dfree(ix->d_nsdir); dfree(ix->d_uscratch);
+  dfree(ix->d_nsdir);
+  smash::release_uniq_scratch(ix);   // (its scratch and second stream)
   (void)hipSetDevice(cur);
   delete ix;
 }

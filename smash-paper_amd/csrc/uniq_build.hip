@@ -332,17 +332,35 @@ void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   if (const char *e = getenv("SMASH_UPART_E2MB")) e2mb = std::max<uint64_t>(1, strtoull(e, 0, 10));
   const uint32_t kc = uint32_t(std::max<uint64_t>(1, (e2mb << 18) >> S1));   // buckets per chunk
   const uint32_t chunk = std::min(kc, nb1);
+  // SMASH_UPART_2S=1: the chunks alternate between the caller's stream and
+  // a second one, each with its own E2 and cursors, so one chunk's pass 2
+  // runs beside the other's pass 3 (prepare 39.8-42.2 vs 41.4-43.5 ms at
+  // hg19 on two boxes, profiles/r06/upart4).  Off by default: two of its
+  // fourteen C5 lines there had one rep whose scan took ~1.2 s longer (the
+  // GPU idle between the scan's events), never seen with one stream.
+  const char *ts = getenv("SMASH_UPART_2S");
+  const bool two = ts && ts[0] == '1' && nb1 > chunk;
   const uint64_t b_e1 = (4 * n + 255) & ~uint64_t(255);
   const uint64_t b_e2 = 4 * (uint64_t(chunk) << S1);
-  const uint64_t need = b_e1 + b_e2 + 4 * uint64_t(std::max(chunk * kNB2, nb1));
+  const uint64_t b_cur = (4 * uint64_t(std::max(chunk * kNB2, nb1)) + 255) & ~uint64_t(255);
+  const uint64_t need = b_e1 + 2 * b_e2 + 2 * b_cur;
   if (ix->uscratch_bytes < need) {
     release_uniq_scratch(ix);
     ix->d_uscratch = dalloc<uint8_t>(need);
     ix->uscratch_bytes = need;
   }
+  if (two && !ix->uaux) {
+    SMASH_HIPX(hipStreamCreateWithFlags(&ix->uaux, hipStreamNonBlocking));
+    for (int q = 0; q < 2; ++q)
+      SMASH_HIPX(hipEventCreateWithFlags(&ix->uev[q], hipEventDisableTiming));
+  }
   uint32_t *E1 = reinterpret_cast<uint32_t *>(ix->d_uscratch);
-  uint32_t *E2 = reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1);
-  unsigned int *cur = reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + b_e2);
+  uint32_t *E2s[2] = {reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1),
+                      reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1 + b_e2)};
+  unsigned int *curs[2] = {
+      reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + 2 * b_e2),
+      reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + 2 * b_e2 + b_cur)};
+  unsigned int *cur = curs[0];
   SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * nb1, s));
   // SMASH_UPART_NT=512: pass-1 tiles of 8 192 ranks (two blocks per CU)
   // instead of 16 384 (one block per CU, runs twice as long: 21.5 vs 23.5 ms
@@ -361,26 +379,36 @@ void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   }
   SMASH_HIPX(hipGetLastError());
   const unsigned per_cu3 = (1u << S2) > 65536 ? 1u : 2u;   // LDS: one window per block
-  for (uint32_t c0 = 0; c0 < nb1; c0 += chunk) {
+  if (two) {   // the second stream starts after pass 1
+    SMASH_HIPX(hipEventRecord(ix->uev[0], s));
+    SMASH_HIPX(hipStreamWaitEvent(ix->uaux, ix->uev[0], 0));
+  }
+  for (uint32_t c0 = 0, ci = 0; c0 < nb1; c0 += chunk, ++ci) {
     const uint32_t nc = std::min(chunk, nb1 - c0);
-    SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * uint64_t(nc) * kNB2, s));
+    const int h = two ? int(ci & 1) : 0;
+    hipStream_t st = h ? ix->uaux : s;
+    uint32_t *E2 = E2s[h];
+    unsigned int *cc = curs[h];
+    SMASH_HIPX(hipMemsetAsync(cc, 0, 4 * uint64_t(nc) * kNB2, st));
     if (nt2 == 1024) {
       const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << S1) / (1024 * kUPer));
-      k_upart2<S1, S2, 1024><<<unsigned(std::min<uint64_t>(t2, uint64_t(cus))), 1024, 0, s>>>(
-          E1, n, c0, nc, cur, E2);
+      k_upart2<S1, S2, 1024><<<unsigned(std::min<uint64_t>(t2, uint64_t(cus))), 1024, 0, st>>>(
+          E1, n, c0, nc, cc, E2);
     } else {
       const uint64_t t2 = uint64_t(nc) * ((uint64_t(1) << S1) / kUTile);
-      k_upart2<S1, S2, kUT><<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, s>>>(
-          E1, n, c0, nc, cur, E2);
+      k_upart2<S1, S2, kUT><<<unsigned(std::min<uint64_t>(t2, 2 * uint64_t(cus))), kUT, 0, st>>>(
+          E1, n, c0, nc, cc, E2);
     }
     k_upart3<S1, S2><<<unsigned(std::min<uint64_t>(uint64_t(nc) * kNB2, uint64_t(cus) * per_cu3)),
-                       kU3, 0, s>>>(E2, n, c0, nc, lo, ix->d_uniq);
+                       kU3, 0, st>>>(E2, n, c0, nc, lo, ix->d_uniq);
     SMASH_HIPX(hipGetLastError());
+  }
+  if (two) {   // the caller's stream continues after both
+    SMASH_HIPX(hipEventRecord(ix->uev[1], ix->uaux));
+    SMASH_HIPX(hipStreamWaitEvent(s, ix->uev[1], 0));
   }
 }
 
-// (an entry is one u32: 24 position bits inside the level-1 bucket + the
-// 8-bit value, so level-1 buckets hold 2^24 positions)
 template <class IdxT>
 void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   const uint64_t n = hi - lo;
@@ -398,6 +426,15 @@ void uniq_range_t(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
 }  // namespace
 
 void release_uniq_scratch(smash_index *ix) {
+  if (ix->uaux) {
+    (void)hipStreamSynchronize(ix->uaux);
+    (void)hipStreamDestroy(ix->uaux);
+    ix->uaux = nullptr;
+    for (int q = 0; q < 2; ++q) {
+      (void)hipEventDestroy(ix->uev[q]);
+      ix->uev[q] = nullptr;
+    }
+  }
   if (ix->d_uscratch) (void)hipFree(ix->d_uscratch);
   ix->d_uscratch = nullptr;
   ix->uscratch_bytes = 0;

@@ -417,6 +417,13 @@ def test_c5_prepare_rebuilds_u_full_genome(hg19, hg19_oracle, monkeypatch):
     S.mappability_prepare(dix, 0, total)
     torch.cuda.synchronize()
     assert torch.equal(U[:N], gathered)
+    # (SMASH_UPART_2S=1: the pass-2/3 chunks alternating over two streams)
+    monkeypatch.setenv("SMASH_UPART_2S", "1")
+    U[:N].fill_(0x55)
+    S.mappability_prepare(dix, 0, total)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("SMASH_UPART_2S")
+    assert torch.equal(U[:N], gathered)
     del gathered
     out = torch.empty(2 * total, dtype=torch.uint8, device="cuda")
     S.mappability_scan(dix, 0, total, 36, out, None, None, 0, None, None)

@@ -37,6 +37,8 @@ def main():
             print("[c5_ab] %-10s round %d: prepare %.3f ms, scan %.3f ms, %.4e bases/s, map ok %s"
                   % (name, rnd, r["prepare_ms"], r["scan_ms"], r["value"],
                      r["map_identical_to_index_build"]), flush=True)
+            print("[c5_ab]   per rep (device prepare, scan ms): %s; host (prepare, scan call ms): %s"
+                  % (r["reps_ms"], r["reps_host_ms"]), flush=True)
 
 
 if __name__ == "__main__":
