@@ -343,7 +343,7 @@ void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
   const uint64_t b_e1 = (4 * n + 255) & ~uint64_t(255);
   const uint64_t b_e2 = 4 * (uint64_t(chunk) << S1);
   const uint64_t b_cur = (4 * uint64_t(std::max(chunk * kNB2, nb1)) + 255) & ~uint64_t(255);
-  const uint64_t need = b_e1 + 2 * b_e2 + 2 * b_cur;
+  const uint64_t need = b_e1 + (two ? 2 : 1) * (b_e2 + b_cur);
   if (ix->uscratch_bytes < need) {
     release_uniq_scratch(ix);
     ix->d_uscratch = dalloc<uint8_t>(need);
@@ -355,10 +355,11 @@ void uniq_range_g(smash_index *ix, uint64_t lo, uint64_t hi, hipStream_t s) {
       SMASH_HIPX(hipEventCreateWithFlags(&ix->uev[q], hipEventDisableTiming));
   }
   uint32_t *E1 = reinterpret_cast<uint32_t *>(ix->d_uscratch);
+  // [E1][E2 | cursors] (+ [E2 | cursors] of the second stream)
   uint32_t *E2s[2] = {reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1),
-                      reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1 + b_e2)};
+                      reinterpret_cast<uint32_t *>(ix->d_uscratch + b_e1 + b_e2 + b_cur)};
   unsigned int *curs[2] = {
-      reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + 2 * b_e2),
+      reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + b_e2),
       reinterpret_cast<unsigned int *>(ix->d_uscratch + b_e1 + 2 * b_e2 + b_cur)};
   unsigned int *cur = curs[0];
   SMASH_HIPX(hipMemsetAsync(cur, 0, 4 * nb1, s));
