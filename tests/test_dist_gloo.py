@@ -22,7 +22,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, per_rank, steps, out_q):
+def _worker(rank, world, port, per_rank, steps, out_q, runs=1):
     import sys
     for p in ("oracle", "tools", "tests", "smash-paper_amd"):
         sys.path.insert(0, os.path.join(ROOT, p))
@@ -44,26 +44,40 @@ def _worker(rank, world, port, per_rank, steps, out_q):
     sc = ShardedCounter(pipe, rank, world, torch.device("cpu"))
     reads = interleaved_reads("s100")
     counts = torch.zeros(len(starts), dtype=torch.int64)
-    sc.reset()
-    for s in range(steps):
-        base = s * world * per_rank
-        lo = base + rank * per_rank
-        d_reads = torch.from_numpy(reads[2 * lo:2 * (lo + per_rank)].copy())
-        if s + 1 < steps and s % 2 == 0:   # the look-ahead form (next batch's search issued now)
-            nlo = lo + world * per_rank
-            nxt = torch.from_numpy(reads[2 * nlo:2 * (nlo + per_rank)].copy())
-            n2lo = nlo + world * per_rank   # and the one after (smash_phase_search_ahead)
-            nxt2 = (torch.from_numpy(reads[2 * n2lo:2 * (n2lo + per_rank)].copy())
-                    if s + 2 < steps else None)
-            sc.step(d_reads, per_rank, base, counts, nxt, per_rank,
-                    next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
-        else:
-            sc.step(d_reads, per_rank, base, counts)
-    dist.all_reduce(counts)
-    st = torch.tensor([pipe.total, pipe.dups, pipe.kept], dtype=torch.int64)
-    dist.all_reduce(st)
+
+    def mine(s):
+        lo = s * world * per_rank + rank * per_rank
+        return torch.from_numpy(reads[2 * lo:2 * (lo + per_rank)].copy())
+
+    out = []
+    for run in range(runs):
+        # (runs > 1: bench.py's back-to-back runs -- a run's last step passes
+        # the next run's first batches as its look-ahead, and the next run's
+        # reset keeps them)
+        sc.reset(keep_search=run > 0)
+        counts.zero_()
+        for s in range(steps):
+            base = s * world * per_rank
+            d_reads = mine(s)
+            if s + 1 == steps and run + 1 < runs:
+                nxt2 = mine(1) if steps > 1 else None
+                sc.step(d_reads, per_rank, base, counts, mine(0), per_rank,
+                        next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
+            elif s + 1 < steps and s % 2 == 0:   # the look-ahead form (next batch's search issued now)
+                nxt = mine(s + 1)
+                # and the one after (smash_phase_search_ahead)
+                nxt2 = mine(s + 2) if s + 2 < steps else None
+                sc.step(d_reads, per_rank, base, counts, nxt, per_rank,
+                        next2_reads=nxt2, next2_pairs=per_rank if nxt2 is not None else 0)
+            else:
+                sc.step(d_reads, per_rank, base, counts)
+        c = counts.clone()
+        dist.all_reduce(c)
+        st = torch.tensor([pipe.total, pipe.dups, pipe.kept], dtype=torch.int64)
+        dist.all_reduce(st)
+        out.append((c.numpy().tolist(), st.tolist()))
     if rank == 0:
-        out_q.put((counts.numpy().tolist(), st.tolist()))
+        out_q.put(out[0] if runs == 1 else out)
     dist.destroy_process_group()
 
 
@@ -310,3 +324,45 @@ def test_key_set_sized_from_plan_and_first_batch_skew(tiny_ix):
     assert op.run(reads, threads=4) == 0
     assert counts == op.counts.tolist()
     assert st == [op.state.total, op.state.dups, op.state.kept]
+
+
+def test_two_rank_back_to_back_runs(tiny_ix):
+    """bench.py's sharded loop over back-to-back runs (the last step of a run
+    passes the next run's first batches as its look-ahead; the next run's
+    reset keeps them, dist.ShardedCounter.reset(keep_search=True)): every run
+    over gloo equals the single-process chain."""
+    import oracle as O
+    import queue as _queue
+    world, per_rank, steps, runs = 2, 97, 3, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, per_rank, steps, q, runs))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = None
+    for _ in range(600):
+        try:
+            res = q.get(timeout=1)
+            break
+        except _queue.Empty:
+            if any(p.exitcode not in (None, 0) for p in procs):
+                break
+    for p in procs:
+        if res is None:
+            p.terminate()
+    assert res is not None, [p.exitcode for p in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = world * per_rank * steps
+    reads = interleaved_reads("s100")[:2 * n]
+    _, starts = load_bins(gold("tiny_bins.txt"))
+    cs = load_chrom_sizes(gold("tiny_chrom_sizes.txt"))
+    op = O.Pipeline(tiny_ix, tiny_ix.mappability(), cs, starts)
+    assert op.run(reads, threads=4) == 0
+    assert len(res) == runs
+    for got_counts, got_stats in res:
+        assert got_counts == op.counts.tolist()
+        assert got_stats == [op.state.total, op.state.dups, op.state.kept]
