@@ -13,7 +13,7 @@
 // known in advance -- SA is a permutation, so every aligned window of 2^k
 // positions receives exactly 2^k entries:
 //
-//   pass 1 (k_upart1): ranks in tiles of 8 192; each entry {x mod 2^24, v}
+//   pass 1 (k_upart1): ranks in tiles (round 6: 16 384); each entry {x mod 2^24, v}
 //     (one u32) goes to the level-1 bucket of x >> 24; a tile is sorted by
 //     bucket in LDS and each bucket's run is stored contiguously at an
 //     atomically claimed offset inside the bucket's fixed slice of E1 (u32
@@ -45,7 +45,7 @@
 namespace smash {
 namespace {
 
-constexpr int kUT = 512;                         // threads per block (passes 1, 2)
+constexpr int kUT = 512;                         // threads per block of the 8 192-entry form
 constexpr int kUPer = 16;                        // entries per thread per tile
 constexpr uint32_t kUTile = uint32_t(kUT) * kUPer;   // 8 192: 54 KB of LDS, 2 blocks per CU
 constexpr int kU3 = 1024;                        // threads per block (pass 3)
